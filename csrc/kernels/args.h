@@ -1,0 +1,126 @@
+// Launch-argument structs shared by the device kernels and the native executor
+// (csrc/runtime/executor.cpp). Plain-old-data only: passed by value as kernel args.
+#pragma once
+#include <stdint.h>
+
+namespace ea {
+
+// ---------------------------------------------------------------- enums ----
+// Keep in sync with elephas_amd/ops/native.py
+enum Act : int {
+  ACT_LINEAR = 0, ACT_RELU = 1, ACT_SIGMOID = 2, ACT_TANH = 3, ACT_SOFTMAX = 4,
+  ACT_ELU = 5, ACT_SELU = 6, ACT_SOFTPLUS = 7, ACT_SOFTSIGN = 8, ACT_EXPONENTIAL = 9,
+  ACT_HARD_SIGMOID = 10, ACT_SWISH = 11, ACT_GELU = 12, ACT_RELU6 = 13
+};
+
+enum Loss : int {
+  LOSS_CCE = 0, LOSS_SPARSE_CCE = 1, LOSS_BCE = 2, LOSS_MSE = 3, LOSS_MAE = 4,
+  LOSS_MAPE = 5, LOSS_MSLE = 6, LOSS_LOGCOSH = 7, LOSS_HINGE = 8, LOSS_SQ_HINGE = 9,
+  LOSS_KLD = 10, LOSS_POISSON = 11, LOSS_COSINE = 12, LOSS_CAT_HINGE = 13
+};
+
+// Metrics: values < 100 reuse the Loss enum (a loss evaluated as a metric);
+// accuracies use the 100+ range.
+enum Metric : int {
+  MET_ACC_CAT = 100, MET_ACC_SPARSE = 101, MET_ACC_BIN = 102
+};
+
+enum Opt : int { OPT_SGD = 0, OPT_RMSPROP = 1, OPT_ADAM = 2, OPT_ADAGRAD = 3, OPT_ADAMAX = 4 };
+
+struct OptParams {
+  int opt; int nesterov; float lr, decay, mom, b1, b2, eps, rho, grad_scale;
+  long long s_plane;  // stride between optimizer state planes (elements)
+};
+
+enum ProbKind : int {
+  PK_PLAIN = 0,      // C (fp32) = A.BT
+  PK_FWD = 1,        // Z = A.BT + b ; D = dropout(act(Z)) ; D^T
+  PK_FWD_LOSS = 2,   // final layer: logits -> loss/metrics -> dZ, dZ^T (or predictions)
+  PK_DX = 3,         // dZ_{l-1} = (dZ_l.W_l^T) * act'(Z_{l-1}) * mask_{l-1}
+  PK_DW_UPDATE = 4,  // dW -> fused optimizer update of master params + bf16/f32 shadows
+  PK_DW_GRAD = 5,    // dW -> flat gradient buffer (all-reduce path)
+  PK_GATHER_T = 6,   // X^T batch (gathered through perm) for DW of layer 1
+  PK_LOSS_ROWS = 7   // wide final layer: one wave per row over fp32 logits Z
+};
+
+struct Prob {
+  int kind;
+  int M, N, K;             // K: padded reduction length (multiple of 8)
+  int R;                   // replicas
+  int tiles_m, tiles_n;
+  int block_begin;
+  // operands
+  const void* A; long long lda, sA;
+  const void* BT; long long ldb, sB;
+  int a_gather;            // 1: A rows come from the batch window (train: perm, eval: contiguous)
+  int ones_row;            // >= 0: index of a virtual all-ones A row (bias gradient)
+  int bt_shadow;           // 1: BT is a parity-double-buffered shadow (offset by par * bt_par)
+  long long bt_par;
+  // batch window
+  const int* perm; long long sPerm;
+  const int* ntrain;       // per replica number of training rows (0 => replica inactive)
+  const int* vstart;       // eval: per replica first row
+  const int* vcount;       // eval: per replica number of rows
+  int B;                   // rows per step
+  int eval_mode;
+  long long chunk;         // eval: chunk index (rows chunk*B ...)
+  // layer epilogue
+  int act; float rate; int layer; int row_valid_mask;
+  const float* bias; long long sBias;
+  float* Z; long long ldz, sZ;
+  void* D; long long ldd, sD;
+  void* DT; long long lddt, sDT;
+  // loss
+  int loss; int nmet; int met[4];
+  const float* Y; long long ldy, sY;
+  double* acc; int acc_stride;
+  float* pred; long long ldp, sPred;
+  // parameters / optimizer
+  float* P; long long sP; long long p_off;
+  float* G; long long sG;
+  float* S; long long sS;
+  void* Wsh; long long sWsh, ldwsh, wsh_par;
+  void* WTsh; long long sWTsh, ldwtsh, wtsh_par;
+  OptParams op;
+};
+
+struct GroupArgs {
+  Prob p[2];
+  int nprob;
+  int total_blocks;
+  long long* ctr;           // [0]=step in epoch, [1]=arrive counter, [2..2+R)=iter per replica
+  unsigned long long seed;
+  int advance;              // this launch ends the step: last block advances counters
+  int adv_R; int adv_B;     // replicas / batch for the advance
+  const int* adv_ntrain;
+};
+
+constexpr int MAX_SEG = 16;
+
+struct Seg {
+  long long p_off;   // offset of the kernel matrix [K][N] in the flat vector
+  int K, N;          // kernel shape; bias (if any) follows at p_off + K*N
+  int has_bias;
+  long long wsh_off, ldwsh;    // row-major shadow W  [K][ldwsh]
+  long long wtsh_off, ldwtsh;  // transposed shadow W^T [N][ldwtsh]
+};
+
+struct FlatArgs {
+  int R;
+  long long n;        // params per replica
+  float* P; long long sP;
+  const float* G; long long sG;
+  float* S; long long sS;
+  OptParams op;
+  int nseg;
+  Seg seg[MAX_SEG];
+  void* Wsh; long long sWsh, wsh_par;
+  void* WTsh; long long sWTsh, wtsh_par;
+  long long* ctr;
+  const int* ntrain; int B;
+  int advance;
+  int both_parities;  // refresh: write both shadow parities
+  int total_blocks;
+};
+
+}  // namespace ea

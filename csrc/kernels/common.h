@@ -1,0 +1,426 @@
+// Shared device-side definitions for the elephas_amd CDNA4 (gfx950) kernels.
+//
+// Design notes (MI355X-first, see docs/ARCHITECTURE.md):
+//  * wave64 everywhere; every block is 256 threads = 4 waves.
+//  * GEMM-shaped work runs on MFMA: bf16 operands use v_mfma_f32_16x16x32_bf16,
+//    fp32 operands use the exact-f32 v_mfma_f32_16x16x4_f32 (no xf32 on gfx950).
+//  * Activation / dropout / loss / optimizer math is fused into GEMM epilogues.
+//  * Dropout masks are counter-based (Philox4x32-10) so backward regenerates them
+//    instead of storing them.
+//
+// Semantics mirror tf.keras 2.10 as used by the reference
+// (reference: elephas/worker.py:41-42 model.fit, tests/conftest.py:8-40 layer set).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "args.h"
+
+namespace ea {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+
+constexpr float KERAS_EPS = 1e-7f;
+
+// -------------------------------------------------------------- bf16 I/O ----
+template <typename T> __device__ __forceinline__ float to_f(T v);
+template <> __device__ __forceinline__ float to_f<float>(float v) { return v; }
+template <> __device__ __forceinline__ float to_f<__bf16>(__bf16 v) { return (float)v; }
+template <typename T> __device__ __forceinline__ T from_f(float v);
+template <> __device__ __forceinline__ float from_f<float>(float v) { return v; }
+template <> __device__ __forceinline__ __bf16 from_f<__bf16>(float v) { return (__bf16)v; }
+
+// --------------------------------------------------------------- Philox ----
+// Philox4x32-10 (Salmon et al. 2011). Counter-based: mask(element) is a pure
+// function of (seed, replica, layer, iteration, element) -> bwd regenerates it.
+__device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint2 k) {
+  const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u;
+  const uint32_t W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    uint32_t hi0 = __umulhi(M0, c.x), lo0 = M0 * c.x;
+    uint32_t hi1 = __umulhi(M1, c.z), lo1 = M1 * c.z;
+    c = make_uint4(hi1 ^ c.y ^ k.x, lo1, hi0 ^ c.w ^ k.y, lo0);
+    k.x += W0; k.y += W1;
+  }
+  return c;
+}
+
+// Uniform in [0,1) for one element; keep iff u >= rate (tf.nn.dropout semantics).
+__device__ __forceinline__ float dropout_uniform(uint64_t seed, int replica, int layer,
+                                                 long long iter, long long elem) {
+  uint4 c = make_uint4((uint32_t)elem, (uint32_t)(elem >> 32),
+                       (uint32_t)iter, ((uint32_t)(iter >> 32) & 0xFFFFu) ^
+                                           ((uint32_t)layer << 16) ^ ((uint32_t)replica << 24));
+  uint2 k = make_uint2((uint32_t)seed ^ (uint32_t)replica * 0x85EBCA6Bu, (uint32_t)(seed >> 32));
+  uint4 r = philox4x32_10(c, k);
+  return (float)(r.x >> 8) * (1.0f / 16777216.0f);
+}
+
+// ----------------------------------------------------------- activations ----
+__device__ __forceinline__ float sigmoidf_(float x) { return 1.f / (1.f + __expf(-x)); }
+__device__ __forceinline__ float softplusf_(float x) {
+  // log(1+exp(x)), stable
+  return fmaxf(x, 0.f) + log1pf(__expf(-fabsf(x)));
+}
+
+__device__ __forceinline__ float act_fwd(int act, float z) {
+  switch (act) {
+    case ACT_RELU: return fmaxf(z, 0.f);
+    case ACT_SIGMOID: return sigmoidf_(z);
+    case ACT_TANH: return tanhf(z);
+    case ACT_ELU: return z > 0.f ? z : expm1f(z);
+    case ACT_SELU: return 1.0507009873554805f * (z > 0.f ? z : 1.6732632423543772f * expm1f(z));
+    case ACT_SOFTPLUS: return softplusf_(z);
+    case ACT_SOFTSIGN: return z / (fabsf(z) + 1.f);
+    case ACT_EXPONENTIAL: return __expf(z);
+    case ACT_HARD_SIGMOID: return fminf(fmaxf(0.2f * z + 0.5f, 0.f), 1.f);
+    case ACT_SWISH: return z * sigmoidf_(z);
+    case ACT_GELU: return 0.5f * z * (1.f + erff(z * 0.7071067811865476f));
+    case ACT_RELU6: return fminf(fmaxf(z, 0.f), 6.f);
+    default: return z;  // linear (softmax handled row-wise)
+  }
+}
+
+// d act / d z evaluated at z
+__device__ __forceinline__ float act_grad(int act, float z) {
+  switch (act) {
+    case ACT_RELU: return z > 0.f ? 1.f : 0.f;
+    case ACT_SIGMOID: { float s = sigmoidf_(z); return s * (1.f - s); }
+    case ACT_TANH: { float t = tanhf(z); return 1.f - t * t; }
+    case ACT_ELU: return z > 0.f ? 1.f : __expf(z);
+    case ACT_SELU: return 1.0507009873554805f * (z > 0.f ? 1.f : 1.6732632423543772f * __expf(z));
+    case ACT_SOFTPLUS: return sigmoidf_(z);
+    case ACT_SOFTSIGN: { float d = fabsf(z) + 1.f; return 1.f / (d * d); }
+    case ACT_EXPONENTIAL: return __expf(z);
+    case ACT_HARD_SIGMOID: return (z > -2.5f && z < 2.5f) ? 0.2f : 0.f;
+    case ACT_SWISH: { float s = sigmoidf_(z); return s + z * s * (1.f - s); }
+    case ACT_GELU: {
+      const float c = 0.3989422804014327f;  // 1/sqrt(2pi)
+      return 0.5f * (1.f + erff(z * 0.7071067811865476f)) + z * c * __expf(-0.5f * z * z);
+    }
+    case ACT_RELU6: return (z > 0.f && z < 6.f) ? 1.f : 0.f;
+    default: return 1.f;
+  }
+}
+
+// --------------------------------------------------------- row reductions ----
+// W = 1: a single thread owns the row.  W = 64: a whole wave owns the row.
+template <int W> __device__ __forceinline__ float row_sum(float v) {
+  if constexpr (W == 1) return v;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+template <int W> __device__ __forceinline__ float row_max(float v) {
+  if constexpr (W == 1) return v;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+// argmax with first-index tie-break (np.argmax / tf.argmax semantics)
+template <int W> __device__ __forceinline__ void row_argmax(float& v, int& i) {
+  if constexpr (W == 1) return;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    float ov = __shfl_xor(v, o, 64);
+    int oi = __shfl_xor(i, o, 64);
+    if (ov > v || (ov == v && oi < i)) { v = ov; i = oi; }
+  }
+}
+
+// ------------------------------------------------- per-row loss & metrics ----
+// Computes, for one row of logits z[0..N) with targets y, the per-row loss value
+// (keras per-sample loss, before the batch mean), optional per-row metric
+// values, and optionally dL/dz (per-row, NOT yet divided by batch size) and/or
+// the activated prediction p.
+//
+// z:  pointer to the row's pre-activation values (fp32) (read-only)
+// y:  pointer to the row's targets (fp32); sparse labels: y[0] = class id
+// Softmax+CCE and sigmoid+BCE take tf.keras's logits path
+// (keras/backend.py categorical_crossentropy: output._keras_logits); every other
+// pairing uses the clipped probability formula and a chain rule through act.
+struct RowOut {
+  float loss;
+  float metric[4];
+};
+
+template <int W>
+__device__ __forceinline__ float loss_elem_value(int loss, float p, float y, float z, bool logit_path) {
+  const float eps = KERAS_EPS;
+  switch (loss) {
+    case LOSS_MSE: { float d = p - y; return d * d; }
+    case LOSS_MAE: return fabsf(p - y);
+    case LOSS_MAPE: return 100.f * fabsf((y - p) / fmaxf(fabsf(y), eps));
+    case LOSS_MSLE: { float a = log1pf(fmaxf(p, eps)) - log1pf(fmaxf(y, eps)); return a * a; }
+    case LOSS_LOGCOSH: { float x = p - y; return x + softplusf_(-2.f * x) - 0.6931471805599453f; }
+    case LOSS_HINGE: return fmaxf(1.f - y * p, 0.f);
+    case LOSS_SQ_HINGE: { float h = fmaxf(1.f - y * p, 0.f); return h * h; }
+    case LOSS_POISSON: return p - y * logf(p + eps);
+    case LOSS_BCE: {
+      if (logit_path) return fmaxf(z, 0.f) - z * y + log1pf(__expf(-fabsf(z)));
+      float pc = fminf(fmaxf(p, eps), 1.f - eps);
+      return -(y * logf(pc + eps) + (1.f - y) * logf(1.f - pc + eps));
+    }
+    case LOSS_KLD: {
+      float yt = fminf(fmaxf(y, eps), 1.f), pp = fminf(fmaxf(p, eps), 1.f);
+      return yt * logf(yt / pp);
+    }
+    default: return 0.f;
+  }
+}
+
+// derivative of the elementwise loss term wrt p
+__device__ __forceinline__ float loss_elem_grad(int loss, float p, float y) {
+  const float eps = KERAS_EPS;
+  switch (loss) {
+    case LOSS_MSE: return 2.f * (p - y);
+    case LOSS_MAE: return (p > y) ? 1.f : ((p < y) ? -1.f : 0.f);
+    case LOSS_MAPE: { float s = (p > y) ? 1.f : ((p < y) ? -1.f : 0.f); return 100.f * s / fmaxf(fabsf(y), eps); }
+    case LOSS_MSLE: {
+      float a = log1pf(fmaxf(p, eps)) - log1pf(fmaxf(y, eps));
+      return (p > eps) ? 2.f * a / (1.f + p) : 0.f;
+    }
+    case LOSS_LOGCOSH: return tanhf(p - y);
+    case LOSS_HINGE: return (1.f - y * p > 0.f) ? -y : 0.f;
+    case LOSS_SQ_HINGE: { float h = 1.f - y * p; return h > 0.f ? -2.f * y * h : 0.f; }
+    case LOSS_POISSON: return 1.f - y / (p + eps);
+    case LOSS_BCE: {
+      if (p <= eps || p >= 1.f - eps) return 0.f;  // clip_by_value grad
+      return -(y / (p + eps)) + (1.f - y) / (1.f - p + eps);
+    }
+    case LOSS_KLD: { float yt = fminf(fmaxf(y, eps), 1.f); return (p > eps && p < 1.f) ? -yt / p : 0.f; }
+    default: return 0.f;
+  }
+}
+
+__device__ __forceinline__ bool loss_is_mean_over_last_axis(int loss) {
+  return !(loss == LOSS_CCE || loss == LOSS_SPARSE_CCE || loss == LOSS_KLD || loss == LOSS_COSINE ||
+           loss == LOSS_CAT_HINGE);
+}
+
+// Generic per-row evaluation. Element j is visited by lane `lane` for j = lane, lane+W, ...
+//   dz_out(j, v) is called with the per-row gradient dL_row/dz_j (if want_grad)
+//   p_out(j, v) is called with the prediction p_j (if want_pred)
+template <int W, typename ZF, typename YF, typename GF, typename PF>
+__device__ void row_loss(int lane, int N, int act, int loss, const int* metrics, int nmetrics,
+                         ZF zat, YF yat, bool want_grad, GF dz_out, bool want_pred, PF p_out,
+                         RowOut& out) {
+  const bool sparse = (loss == LOSS_SPARSE_CCE);
+  const int ycls = sparse ? (int)yat(0) : -1;
+  auto Y = [&](int j) -> float { return sparse ? (j == ycls ? 1.f : 0.f) : yat(j); };
+  // softmax statistics
+  float zmax = -INFINITY, sumexp = 0.f;
+  if (act == ACT_SOFTMAX) {
+    for (int j = lane; j < N; j += W) zmax = fmaxf(zmax, zat(j));
+    zmax = row_max<W>(zmax);
+    for (int j = lane; j < N; j += W) sumexp += __expf(zat(j) - zmax);
+    sumexp = row_sum<W>(sumexp);
+  }
+  const float lse = zmax + logf(sumexp);
+  auto P = [&](int j) -> float {
+    float z = zat(j);
+    return act == ACT_SOFTMAX ? __expf(z - lse) : act_fwd(act, z);
+  };
+  const bool cce_like = (loss == LOSS_CCE || loss == LOSS_SPARSE_CCE);
+  const bool logit_cce = cce_like && act == ACT_SOFTMAX;
+  const bool logit_bce = (loss == LOSS_BCE) && act == ACT_SIGMOID;
+  const float invN = 1.f / (float)N;
+
+  // ---- loss value
+  float lsum = 0.f, psum = 0.f, ysum = 0.f;
+  if (cce_like && !logit_cce) {
+    for (int j = lane; j < N; j += W) psum += P(j);
+    psum = row_sum<W>(psum);
+  }
+  float ynorm = 0.f, pnorm = 0.f, yp = 0.f;  // cosine
+  float cat_pos = 0.f, cat_neg = -INFINITY;  // categorical hinge
+  for (int j = lane; j < N; j += W) {
+    float z = zat(j), y = Y(j), p = P(j);
+    if (logit_cce) lsum += -y * (z - lse);
+    else if (cce_like) {
+      float pn = fminf(fmaxf(p / psum, KERAS_EPS), 1.f - KERAS_EPS);
+      lsum += -y * logf(pn);
+    } else if (loss == LOSS_COSINE) { ynorm += y * y; pnorm += p * p; yp += y * p; }
+    else if (loss == LOSS_CAT_HINGE) { cat_pos += y * p; cat_neg = fmaxf(cat_neg, (1.f - y) * p); }
+    else lsum += loss_elem_value<W>(loss, p, y, z, logit_bce);
+    ysum += y;
+  }
+  lsum = row_sum<W>(lsum);
+  ysum = row_sum<W>(ysum);
+  float rl;
+  if (loss == LOSS_COSINE) {
+    ynorm = row_sum<W>(ynorm); pnorm = row_sum<W>(pnorm); yp = row_sum<W>(yp);
+    float ny = rsqrtf(fmaxf(ynorm, 1e-12f)), np_ = rsqrtf(fmaxf(pnorm, 1e-12f));
+    rl = -yp * ny * np_;
+  } else if (loss == LOSS_CAT_HINGE) {
+    cat_pos = row_sum<W>(cat_pos); cat_neg = row_max<W>(cat_neg);
+    rl = fmaxf(cat_neg - cat_pos + 1.f, 0.f);
+  } else {
+    rl = loss_is_mean_over_last_axis(loss) ? lsum * invN : lsum;
+  }
+  out.loss = rl;
+
+  // ---- metrics
+  for (int mi = 0; mi < nmetrics; ++mi) {
+    int m = metrics[mi];
+    float mv = 0.f;
+    if (m == MET_ACC_CAT || m == MET_ACC_SPARSE) {
+      float bp = -INFINITY; int ip = 0x7fffffff;
+      float by = -INFINITY; int iy = 0x7fffffff;
+      for (int j = lane; j < N; j += W) {
+        float p = P(j);
+        if (p > bp) { bp = p; ip = j; }
+        float yv = Y(j);
+        if (yv > by) { by = yv; iy = j; }
+      }
+      row_argmax<W>(bp, ip);
+      row_argmax<W>(by, iy);
+      if (m == MET_ACC_SPARSE) iy = ycls;
+      mv = (ip == iy) ? 1.f : 0.f;
+    } else if (m == MET_ACC_BIN) {
+      float s = 0.f;
+      for (int j = lane; j < N; j += W) s += ((P(j) > 0.5f ? 1.f : 0.f) == Y(j)) ? 1.f : 0.f;
+      mv = row_sum<W>(s) * invN;
+    } else if (m == LOSS_CCE || m == LOSS_SPARSE_CCE) {
+      float s = 0.f;
+      for (int j = lane; j < N; j += W) s += (act == ACT_SOFTMAX) ? -Y(j) * (zat(j) - lse)
+                                                                  : -Y(j) * logf(fminf(fmaxf(P(j), KERAS_EPS), 1.f - KERAS_EPS));
+      mv = row_sum<W>(s);
+    } else if (m == LOSS_COSINE) {
+      float a = 0.f, b = 0.f, c = 0.f;
+      for (int j = lane; j < N; j += W) { float p = P(j), y = Y(j); a += y * y; b += p * p; c += y * p; }
+      a = row_sum<W>(a); b = row_sum<W>(b); c = row_sum<W>(c);
+      mv = c * rsqrtf(fmaxf(a, 1e-12f)) * rsqrtf(fmaxf(b, 1e-12f));  // keras metric: +cos
+    } else {
+      float s = 0.f;
+      for (int j = lane; j < N; j += W) s += loss_elem_value<W>(m, P(j), Y(j), zat(j), m == LOSS_BCE && act == ACT_SIGMOID);
+      s = row_sum<W>(s);
+      mv = loss_is_mean_over_last_axis(m) ? s * invN : s;
+    }
+    out.metric[mi] = mv;
+  }
+
+  // ---- prediction
+  if (want_pred)
+    for (int j = lane; j < N; j += W) p_out(j, P(j));
+
+  // ---- gradient wrt z (per row)
+  if (want_grad) {
+    if (logit_cce) {
+      for (int j = lane; j < N; j += W) dz_out(j, __expf(zat(j) - lse) * ysum - Y(j));
+    } else if (logit_bce) {
+      for (int j = lane; j < N; j += W) dz_out(j, (sigmoidf_(zat(j)) - Y(j)) * invN);
+    } else {
+      // g_j = dL/dp_j
+      auto G = [&](int j) -> float {
+        float p = P(j), y = Y(j);
+        if (cce_like) {
+          float pn = p / psum;
+          if (pn <= KERAS_EPS || pn >= 1.f - KERAS_EPS) return 0.f;
+          // d/dp_j of -sum_k y_k log(p_k/psum) = -y_j/p_j + ysum/psum
+          return -y / p + ysum / psum;
+        }
+        if (loss == LOSS_COSINE) {
+          float ny = rsqrtf(fmaxf(ynorm, 1e-12f)), np_ = rsqrtf(fmaxf(pnorm, 1e-12f));
+          // d/dp (-(y.p) ny np)
+          return -(y * ny * np_ - yp * ny * np_ * np_ * np_ * p);
+        }
+        if (loss == LOSS_CAT_HINGE) {
+          float h = cat_neg - cat_pos + 1.f;
+          if (h <= 0.f) return 0.f;
+          float g = -y;
+          if ((1.f - y) * p == cat_neg) g += (1.f - y);
+          return g;
+        }
+        float g = loss_elem_grad(loss, p, y);
+        return loss_is_mean_over_last_axis(loss) ? g * invN : g;
+      };
+      if (act == ACT_SOFTMAX) {
+        float gp = 0.f;
+        for (int j = lane; j < N; j += W) gp += G(j) * P(j);
+        gp = row_sum<W>(gp);
+        for (int j = lane; j < N; j += W) dz_out(j, P(j) * (G(j) - gp));
+      } else {
+        for (int j = lane; j < N; j += W) dz_out(j, G(j) * act_grad(act, zat(j)));
+      }
+    }
+  }
+}
+
+
+// ---------------------------------------------------------- optimizer math
+// Keras 2.10 optimizer_v2 update rules (keras/optimizers/optimizer_v2/{gradient_descent,
+// rmsprop,adam,adagrad,adamax}.py); decayed lr = lr / (1 + decay * iterations).
+__device__ __forceinline__ float opt_update(const OptParams& p, float w, float g, float* S, long long si,
+                                            long long iter) {
+  const float lr = p.lr / (1.f + p.decay * (float)iter);
+  switch (p.opt) {
+    case OPT_SGD: {
+      if (p.mom == 0.f) return w - lr * g;
+      float v = p.mom * S[si] - lr * g;
+      S[si] = v;
+      return p.nesterov ? w + p.mom * v - lr * g : w + v;
+    }
+    case OPT_RMSPROP: {
+      float ms = p.rho * S[si] + (1.f - p.rho) * g * g;
+      S[si] = ms;
+      float upd = lr * g / (sqrtf(ms) + p.eps);
+      if (p.mom > 0.f) {
+        float m = p.mom * S[si + p.s_plane] + upd;
+        S[si + p.s_plane] = m;
+        return w - m;
+      }
+      return w - upd;
+    }
+    case OPT_ADAM: {
+      const float t = (float)(iter + 1);
+      const float b1t = powf(p.b1, t), b2t = powf(p.b2, t);
+      const float lrt = lr * sqrtf(1.f - b2t) / (1.f - b1t);
+      float m = p.b1 * S[si] + (1.f - p.b1) * g;
+      float v = p.b2 * S[si + p.s_plane] + (1.f - p.b2) * g * g;
+      S[si] = m;
+      S[si + p.s_plane] = v;
+      return w - lrt * m / (sqrtf(v) + p.eps);
+    }
+    case OPT_ADAGRAD: {
+      float a = S[si] + g * g;
+      S[si] = a;
+      return w - lr * g / (sqrtf(a) + p.eps);
+    }
+    case OPT_ADAMAX: {
+      const float t = (float)(iter + 1);
+      const float lrt = lr / (1.f - powf(p.b1, t));
+      float m = p.b1 * S[si] + (1.f - p.b1) * g;
+      float u = fmaxf(p.b2 * S[si + p.s_plane], fabsf(g));
+      S[si] = m;
+      S[si + p.s_plane] = u;
+      return w - lrt * m / (u + p.eps);
+    }
+  }
+  return w;
+}
+
+template <int W, typename ZF, typename PF>
+__device__ void row_predict(int lane, int N, int act, ZF zat, PF p_out) {
+  if (act == ACT_SOFTMAX) {
+    float zmax = -INFINITY, s = 0.f;
+    for (int j = lane; j < N; j += W) zmax = fmaxf(zmax, zat(j));
+    zmax = row_max<W>(zmax);
+    for (int j = lane; j < N; j += W) s += __expf(zat(j) - zmax);
+    s = row_sum<W>(s);
+    const float inv = 1.f / s;
+    for (int j = lane; j < N; j += W) p_out(j, __expf(zat(j) - zmax) * inv);
+  } else {
+    for (int j = lane; j < N; j += W) p_out(j, act_fwd(act, zat(j)));
+  }
+}
+
+// ------------------------------------------------------- shared structs ----
+// Step counters, one block per executor:  [0]=step-in-epoch, [1]=arrive, [2..2+R)=iter[r]
+struct Counters {
+  long long* base;
+  __device__ long long step() const { return base[0]; }
+};
+
+}  // namespace ea

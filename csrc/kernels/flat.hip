@@ -1,0 +1,182 @@
+// Flat-buffer kernels over the packed parameter vector (Keras weight order,
+// reference utils/functional_utils.py:6-43 and spark_model.py:221-227):
+//   * fused optimizer apply after a gradient all-reduce (sync per-step DP path)
+//   * shadow refresh (fp32 master -> compute-dtype W and W^T images)
+//   * replica averaging (reference sync mode: theta <- theta0 - mean(delta_i))
+//   * parameter-server updates (theta <- theta - delta; lock-free hogwild variant
+//     with fp32 global atomics) and generic axpby.
+// All loads/stores are 16-byte vectorised where the layout allows.
+#include "common.h"
+
+namespace ea {
+
+__device__ __forceinline__ int find_seg(const FlatArgs& a, long long i) {
+  int s = 0;
+  for (int q = 1; q < a.nseg; ++q)
+    if (i >= a.seg[q].p_off) s = q;
+  return s;
+}
+
+template <typename T>
+__device__ __forceinline__ void write_shadow(const FlatArgs& a, int r, long long i, float w, long long par) {
+  const int s = find_seg(a, i);
+  const Seg& g = a.seg[s];
+  const long long rel = i - g.p_off;
+  if (rel < 0 || rel >= (long long)g.K * g.N) return;  // bias: no shadow
+  const long long k = rel / g.N, nn = rel % g.N;
+  if (a.Wsh)
+    reinterpret_cast<T*>(a.Wsh)[(long long)r * a.sWsh + par * a.wsh_par + g.wsh_off + k * g.ldwsh + nn] = from_f<T>(w);
+  if (a.WTsh)
+    reinterpret_cast<T*>(a.WTsh)[(long long)r * a.sWTsh + par * a.wtsh_par + g.wtsh_off + nn * g.ldwtsh + k] = from_f<T>(w);
+}
+
+__device__ __forceinline__ void arrive_and_advance(const FlatArgs& a) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();
+    unsigned long long prev = atomicAdd(reinterpret_cast<unsigned long long*>(a.ctr + 1), 1ull);
+    if (prev == (unsigned long long)(a.total_blocks - 1)) {
+      const long long s = a.ctr[0];
+      for (int r = 0; r < a.R; ++r)
+        if ((long long)a.ntrain[r] - s * a.B > 0) a.ctr[2 + r] += 1;
+      a.ctr[0] = s + 1;
+      a.ctr[1] = 0;
+      __threadfence();
+    }
+  }
+}
+
+// grid: total_blocks over R*n elements
+template <typename T>
+__global__ __launch_bounds__(256) void apply_update_kernel(FlatArgs a) {
+  const long long total = (long long)a.R * a.n;
+  const long long step = a.ctr[0];
+  for (long long e = (long long)blockIdx.x * 256 + threadIdx.x; e < total; e += (long long)gridDim.x * 256) {
+    const int r = (int)(e / a.n);
+    const long long i = e % a.n;
+    if ((long long)a.ntrain[r] - step * a.B <= 0) continue;  // replica has no batch this step
+    const long long iter = a.ctr[2 + r];
+    const float g = a.G[(long long)r * a.sG + i] * a.op.grad_scale;
+    float* S = a.S ? a.S + (long long)r * a.sS : nullptr;
+    const float w = opt_update(a.op, a.P[(long long)r * a.sP + i], g, S, i, iter);
+    a.P[(long long)r * a.sP + i] = w;
+    write_shadow<T>(a, r, i, w, (iter + 1) & 1);
+  }
+  if (a.advance) arrive_and_advance(a);
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void refresh_shadows_kernel(FlatArgs a) {
+  const long long total = (long long)a.R * a.n;
+  for (long long e = (long long)blockIdx.x * 256 + threadIdx.x; e < total; e += (long long)gridDim.x * 256) {
+    const int r = (int)(e / a.n);
+    const long long i = e % a.n;
+    const float w = a.P[(long long)r * a.sP + i];
+    if (a.both_parities) {
+      write_shadow<T>(a, r, i, w, 0);
+      write_shadow<T>(a, r, i, w, 1);
+    } else {
+      write_shadow<T>(a, r, i, w, a.ctr[2 + r] & 1);
+    }
+  }
+}
+
+// mean over R replicas of P[r][i]; result written to every replica (and to out if given)
+__global__ __launch_bounds__(256) void replica_average_kernel(float* P, long long sP, int R, long long n,
+                                                              float* out, int write_back) {
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+    double s = 0.0;
+    for (int r = 0; r < R; ++r) s += P[(long long)r * sP + i];
+    const float m = (float)(s / R);
+    if (out) out[i] = m;
+    if (write_back)
+      for (int r = 0; r < R; ++r) P[(long long)r * sP + i] = m;
+  }
+}
+
+// y = alpha*x + beta*y   (vectorised, n multiple handled with tail)
+__global__ __launch_bounds__(256) void axpby_kernel(const float* x, float* y, long long n, float alpha, float beta) {
+  const long long n4 = n / 4;
+  const float4* x4 = reinterpret_cast<const float4*>(x);
+  float4* y4 = reinterpret_cast<float4*>(y);
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long long)gridDim.x * 256) {
+    float4 a = x4[i], b = y4[i];
+    y4[i] = make_float4(alpha * a.x + beta * b.x, alpha * a.y + beta * b.y, alpha * a.z + beta * b.z,
+                        alpha * a.w + beta * b.w);
+  }
+  for (long long i = n4 * 4 + (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256)
+    y[i] = alpha * x[i] + beta * y[i];
+}
+
+// parameter server apply: p -= scale * delta  (plain RMW: serialised by the
+// caller's lock in 'asynchronous' mode, racy by design in 'hogwild' mode)
+__global__ __launch_bounds__(256) void ps_sub_kernel(float* p, const float* d, long long n, float scale) {
+  const long long n4 = n / 4;
+  float4* p4 = reinterpret_cast<float4*>(p);
+  const float4* d4 = reinterpret_cast<const float4*>(d);
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long long)gridDim.x * 256) {
+    float4 a = p4[i], b = d4[i];
+    p4[i] = make_float4(a.x - scale * b.x, a.y - scale * b.y, a.z - scale * b.z, a.w - scale * b.w);
+  }
+  for (long long i = n4 * 4 + (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256)
+    p[i] -= scale * d[i];
+}
+
+// lock-free hogwild apply with fp32 global atomics: no update is lost, order is arbitrary
+__global__ __launch_bounds__(256) void ps_sub_atomic_kernel(float* p, const float* d, long long n, float scale) {
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256)
+    atomicAdd(p + i, -scale * d[i]);
+}
+
+// delta = a - b
+__global__ __launch_bounds__(256) void sub_kernel(const float* a, const float* b, float* out, long long n) {
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256)
+    out[i] = a[i] - b[i];
+}
+
+static inline int grid_for(long long n) {
+  long long g = (n + 255) / 256;
+  if (g > 4096) g = 4096;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+}  // namespace ea
+
+using namespace ea;
+
+extern "C" hipError_t ea_apply_update(FlatArgs* a, int bf16, hipStream_t s) {
+  a->total_blocks = grid_for((long long)a->R * a->n);
+  if (bf16) hipLaunchKernelGGL(apply_update_kernel<__bf16>, dim3(a->total_blocks), dim3(256), 0, s, *a);
+  else hipLaunchKernelGGL(apply_update_kernel<float>, dim3(a->total_blocks), dim3(256), 0, s, *a);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t ea_refresh_shadows(FlatArgs* a, int bf16, hipStream_t s) {
+  a->total_blocks = grid_for((long long)a->R * a->n);
+  if (bf16) hipLaunchKernelGGL(refresh_shadows_kernel<__bf16>, dim3(a->total_blocks), dim3(256), 0, s, *a);
+  else hipLaunchKernelGGL(refresh_shadows_kernel<float>, dim3(a->total_blocks), dim3(256), 0, s, *a);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t ea_replica_average(float* P, long long sP, int R, long long n, float* out, int write_back,
+                                         hipStream_t s) {
+  hipLaunchKernelGGL(replica_average_kernel, dim3(grid_for(n)), dim3(256), 0, s, P, sP, R, n, out, write_back);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t ea_axpby(const float* x, float* y, long long n, float alpha, float beta, hipStream_t s) {
+  hipLaunchKernelGGL(axpby_kernel, dim3(grid_for((n + 3) / 4)), dim3(256), 0, s, x, y, n, alpha, beta);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t ea_ps_sub(float* p, const float* d, long long n, float scale, int atomic, hipStream_t s) {
+  if (atomic) hipLaunchKernelGGL(ps_sub_atomic_kernel, dim3(grid_for(n)), dim3(256), 0, s, p, d, n, scale);
+  else hipLaunchKernelGGL(ps_sub_kernel, dim3(grid_for((n + 3) / 4)), dim3(256), 0, s, p, d, n, scale);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t ea_sub(const float* a, const float* b, float* out, long long n, hipStream_t s) {
+  hipLaunchKernelGGL(sub_kernel, dim3(grid_for(n)), dim3(256), 0, s, a, b, out, n);
+  return hipGetLastError();
+}

@@ -1,0 +1,263 @@
+// pybind11 bindings for the elephas_amd native runtime (_C).
+//
+// Tensors cross the boundary as raw device pointers + strides (the Python side
+// owns storage through torch's caching allocator) and streams as raw
+// hipStream_t handles (torch.cuda.current_stream().cuda_stream), so no torch
+// headers or ABI are involved and every launch lands on the caller's stream.
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <cstring>
+
+#include "executor.h"
+#include "param_server.h"
+#include "host_loader.h"
+
+namespace py = pybind11;
+using namespace ea;
+
+extern "C" hipError_t ea_gemm_grouped(const ea::GroupArgs* ga, int bf16, int cfg, hipStream_t s);
+extern "C" int ea_gemm_tile_m(int cfg);
+extern "C" int ea_gemm_tile_n(int cfg);
+extern "C" void ea_gemm_init();
+extern "C" hipError_t ea_replica_average(float* P, long long sP, int R, long long n, float* out, int write_back,
+                                         hipStream_t s);
+extern "C" hipError_t ea_axpby(const float* x, float* y, long long n, float alpha, float beta, hipStream_t s);
+extern "C" hipError_t ea_ps_sub(float* p, const float* d, long long n, float scale, int atomic, hipStream_t s);
+extern "C" hipError_t ea_sub(const float* a, const float* b, float* out, long long n, hipStream_t s);
+
+static void chk(hipError_t e, const char* w) {
+  if (e != hipSuccess) throw std::runtime_error(std::string("HIP error in ") + w + ": " + hipGetErrorString(e));
+}
+
+template <typename T>
+static T get(const py::dict& d, const char* k, T def) {
+  if (!d.contains(k)) return def;
+  py::object o = d[k];
+  if (o.is_none()) return def;
+  return o.cast<T>();
+}
+
+static hipStream_t S(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
+
+static OptParams parse_opt(const py::dict& d) {
+  OptParams o{};
+  o.opt = get<int>(d, "opt", 0);
+  o.nesterov = get<int>(d, "nesterov", 0);
+  o.lr = get<float>(d, "lr", 0.01f);
+  o.decay = get<float>(d, "decay", 0.f);
+  o.mom = get<float>(d, "momentum", 0.f);
+  o.b1 = get<float>(d, "beta_1", 0.9f);
+  o.b2 = get<float>(d, "beta_2", 0.999f);
+  o.eps = get<float>(d, "epsilon", 1e-7f);
+  o.rho = get<float>(d, "rho", 0.9f);
+  o.grad_scale = get<float>(d, "grad_scale", 1.f);
+  o.s_plane = get<long long>(d, "s_plane", 0);
+  return o;
+}
+
+static ExecCfg parse_cfg(const py::dict& d) {
+  ExecCfg c;
+  c.R = get<int>(d, "R", 1);
+  c.B = get<int>(d, "B", 32);
+  c.Bp = get<int>(d, "Bp", 32);
+  c.bf16 = get<int>(d, "bf16", 1);
+  c.seed = get<unsigned long long>(d, "seed", 0);
+  c.force_cfg = get<int>(d, "force_cfg", -1);
+  for (auto item : d["layers"].cast<py::list>()) {
+    py::dict l = item.cast<py::dict>();
+    LayerCfg lc;
+    lc.K = get<int>(l, "K", 0);
+    lc.N = get<int>(l, "N", 0);
+    lc.Kp = get<int>(l, "Kp", 0);
+    lc.Np = get<int>(l, "Np", 0);
+    lc.act = get<int>(l, "act", 0);
+    lc.has_bias = get<int>(l, "has_bias", 1);
+    lc.rate = get<float>(l, "rate", 0.f);
+    lc.p_off = get<long long>(l, "p_off", 0);
+    lc.Z = get<uintptr_t>(l, "Z", 0);
+    lc.D = get<uintptr_t>(l, "D", 0);
+    lc.DT = get<uintptr_t>(l, "DT", 0);
+    lc.dZ = get<uintptr_t>(l, "dZ", 0);
+    lc.dZT = get<uintptr_t>(l, "dZT", 0);
+    lc.wsh_off = get<long long>(l, "wsh_off", 0);
+    lc.wtsh_off = get<long long>(l, "wtsh_off", 0);
+    c.layers.push_back(lc);
+  }
+  c.X = get<uintptr_t>(d, "X", 0);
+  c.sX = get<long long>(d, "sX", 0);
+  c.ldx = get<long long>(d, "ldx", 0);
+  c.Y = get<uintptr_t>(d, "Y", 0);
+  c.sY = get<long long>(d, "sY", 0);
+  c.ldy = get<long long>(d, "ldy", 0);
+  c.perm = get<uintptr_t>(d, "perm", 0);
+  c.sPerm = get<long long>(d, "sPerm", 0);
+  c.ntrain = get<uintptr_t>(d, "ntrain", 0);
+  c.vstart = get<uintptr_t>(d, "vstart", 0);
+  c.vcount = get<uintptr_t>(d, "vcount", 0);
+  c.XT = get<uintptr_t>(d, "XT", 0);
+  c.P = get<uintptr_t>(d, "P", 0);
+  c.sP = get<long long>(d, "sP", 0);
+  c.nparams = get<long long>(d, "nparams", 0);
+  c.G = get<uintptr_t>(d, "G", 0);
+  c.sG = get<long long>(d, "sG", 0);
+  c.S = get<uintptr_t>(d, "S", 0);
+  c.sS = get<long long>(d, "sS", 0);
+  c.Wsh = get<uintptr_t>(d, "Wsh", 0);
+  c.sWsh = get<long long>(d, "sWsh", 0);
+  c.wsh_par = get<long long>(d, "wsh_par", 0);
+  c.WTsh = get<uintptr_t>(d, "WTsh", 0);
+  c.sWTsh = get<long long>(d, "sWTsh", 0);
+  c.wtsh_par = get<long long>(d, "wtsh_par", 0);
+  c.op = parse_opt(d["opt"].cast<py::dict>());
+  c.loss = get<int>(d, "loss", 0);
+  auto mets = get<std::vector<int>>(d, "metrics", {});
+  if (mets.size() > 4) throw std::invalid_argument("at most 4 fused metrics");
+  c.nmet = (int)mets.size();
+  for (size_t i = 0; i < mets.size(); ++i) c.met[i] = mets[i];
+  c.acc = get<uintptr_t>(d, "acc", 0);
+  c.acc_stride = get<int>(d, "acc_stride", 6);
+  c.ctr = get<uintptr_t>(d, "ctr", 0);
+  return c;
+}
+
+static EvalSource parse_src(const py::dict& d) {
+  EvalSource e;
+  e.X = get<uintptr_t>(d, "X", 0);
+  e.sX = get<long long>(d, "sX", 0);
+  e.ldx = get<long long>(d, "ldx", 0);
+  e.Y = get<uintptr_t>(d, "Y", 0);
+  e.sY = get<long long>(d, "sY", 0);
+  e.ldy = get<long long>(d, "ldy", 0);
+  e.vstart = get<uintptr_t>(d, "vstart", 0);
+  e.vcount = get<uintptr_t>(d, "vcount", 0);
+  e.acc = get<uintptr_t>(d, "acc", 0);
+  e.pred = get<uintptr_t>(d, "pred", 0);
+  e.sPred = get<long long>(d, "sPred", 0);
+  e.ldp = get<long long>(d, "ldp", 0);
+  return e;
+}
+
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "elephas_amd native runtime: CDNA4 (gfx950) HIP kernels + executor";
+
+  py::class_<Executor>(m, "Executor")
+      .def(py::init([](py::dict cfg) { return new Executor(parse_cfg(cfg)); }))
+      .def("train_step", [](Executor& e, uintptr_t s) { e.train_step(S(s)); })
+      .def("forward_backward", [](Executor& e, uintptr_t s) { e.forward_backward(S(s)); })
+      .def("apply", [](Executor& e, uintptr_t s) { e.apply(S(s)); })
+      .def("eval_chunk", [](Executor& e, long long chunk, py::dict src, uintptr_t s) {
+        e.eval_chunk(chunk, parse_src(src), S(s));
+      })
+      .def("refresh_shadows", [](Executor& e, bool both, uintptr_t s) { e.refresh_shadows(both, S(s)); })
+      .def("reset_epoch", [](Executor& e, uintptr_t s) { e.reset_epoch(S(s)); })
+      .def("capture", [](Executor& e, int n, int mode, uintptr_t s) { return e.capture(n, mode, S(s)); })
+      .def("replay", [](Executor& e, int id, uintptr_t s) {
+        py::gil_scoped_release rel;
+        e.replay(id, S(s));
+      })
+      .def("replay_n", [](Executor& e, int id, int times, uintptr_t s) {
+        py::gil_scoped_release rel;
+        for (int i = 0; i < times; ++i) e.replay(id, S(s));
+      })
+      .def("destroy_graphs", &Executor::destroy_graphs)
+      .def("launches_per_step", &Executor::launches_per_step)
+      .def("launch_cfgs", &Executor::launch_cfgs);
+
+  // single PLAIN GEMM (C fp32 = A . BT^T) for kernel tests / generic matmul
+  m.def("gemm_nt", [](uintptr_t A, uintptr_t BT, uintptr_t C, int M, int N, int K, long long lda, long long ldb,
+                      long long ldc, int bf16, int cfg, uintptr_t s) {
+    ea_gemm_init();
+    GroupArgs ga;
+    std::memset(&ga, 0, sizeof(ga));
+    Prob& p = ga.p[0];
+    p.kind = PK_PLAIN;
+    p.M = M; p.N = N; p.K = K; p.R = 1;
+    p.A = reinterpret_cast<const void*>(A); p.lda = lda;
+    p.BT = reinterpret_cast<const void*>(BT); p.ldb = ldb;
+    p.D = reinterpret_cast<void*>(C); p.ldd = ldc;
+    p.ones_row = -1;
+    p.B = M;
+    p.tiles_m = (M + ea_gemm_tile_m(cfg) - 1) / ea_gemm_tile_m(cfg);
+    p.tiles_n = (N + ea_gemm_tile_n(cfg) - 1) / ea_gemm_tile_n(cfg);
+    ga.nprob = 1;
+    ga.total_blocks = p.tiles_m * p.tiles_n;
+    static long long* dctr = nullptr;
+    if (!dctr) {
+      chk(hipMalloc(&dctr, 64 * sizeof(long long)), "hipMalloc");
+      chk(hipMemset(dctr, 0, 64 * sizeof(long long)), "hipMemset");
+    }
+    ga.ctr = dctr;
+    chk(ea_gemm_grouped(&ga, bf16, cfg, S(s)), "gemm_nt");
+  });
+  m.def("tile_shape", [](int cfg) { return py::make_tuple(ea_gemm_tile_m(cfg), ea_gemm_tile_n(cfg)); });
+
+  m.def("replica_average", [](uintptr_t P, long long sP, int R, long long n, uintptr_t out, int write_back,
+                              uintptr_t s) {
+    chk(ea_replica_average(reinterpret_cast<float*>(P), sP, R, n, reinterpret_cast<float*>(out), write_back, S(s)),
+        "replica_average");
+  });
+  m.def("axpby", [](uintptr_t x, uintptr_t y, long long n, float a, float b, uintptr_t s) {
+    chk(ea_axpby(reinterpret_cast<const float*>(x), reinterpret_cast<float*>(y), n, a, b, S(s)), "axpby");
+  });
+  m.def("ps_sub", [](uintptr_t p, uintptr_t d, long long n, float scale, int atomic, uintptr_t s) {
+    chk(ea_ps_sub(reinterpret_cast<float*>(p), reinterpret_cast<const float*>(d), n, scale, atomic, S(s)), "ps_sub");
+  });
+  m.def("sub", [](uintptr_t a, uintptr_t b, uintptr_t out, long long n, uintptr_t s) {
+    chk(ea_sub(reinterpret_cast<const float*>(a), reinterpret_cast<const float*>(b), reinterpret_cast<float*>(out), n,
+               S(s)),
+        "sub");
+  });
+
+  // ---- device parameter server (async / hogwild), see param_server.h
+  py::class_<DeviceParameterServer>(m, "DeviceParameterServer")
+      .def(py::init<long long, int, int, const std::string&>(), py::arg("n"), py::arg("locked"), py::arg("device"),
+           py::arg("lock_name") = "")
+      .def("pull", [](DeviceParameterServer& ps, uintptr_t dst, uintptr_t s) {
+        py::gil_scoped_release rel;
+        ps.pull(reinterpret_cast<float*>(dst), S(s));
+      })
+      .def("push", [](DeviceParameterServer& ps, uintptr_t delta, uintptr_t s) {
+        py::gil_scoped_release rel;
+        ps.push(reinterpret_cast<const float*>(delta), S(s));
+      })
+      .def("set", [](DeviceParameterServer& ps, uintptr_t src, uintptr_t s) {
+        py::gil_scoped_release rel;
+        ps.set(reinterpret_cast<const float*>(src), S(s));
+      })
+      .def("ipc_handle", [](DeviceParameterServer& ps) { return py::bytes(ps.ipc_handle()); })
+      .def("data_ptr", [](DeviceParameterServer& ps) { return reinterpret_cast<uintptr_t>(ps.data()); })
+      .def_property_readonly("n", &DeviceParameterServer::size)
+      .def_property_readonly("pushes", &DeviceParameterServer::pushes)
+      .def_property_readonly("pulls", &DeviceParameterServer::pulls);
+  py::class_<RemoteParameterServer>(m, "RemoteParameterServer")
+      .def(py::init([](py::bytes h, long long n, int locked, std::string lock_name) {
+             return new RemoteParameterServer(std::string(h), n, locked, lock_name);
+           }),
+           py::arg("handle"), py::arg("n"), py::arg("locked"), py::arg("lock_name"))
+      .def("pull", [](RemoteParameterServer& ps, uintptr_t dst, uintptr_t s) {
+        py::gil_scoped_release rel;
+        ps.pull(reinterpret_cast<float*>(dst), S(s));
+      })
+      .def("push", [](RemoteParameterServer& ps, uintptr_t delta, uintptr_t s) {
+        py::gil_scoped_release rel;
+        ps.push(reinterpret_cast<const float*>(delta), S(s));
+      });
+  m.def("shm_rwlock_create", &shm_rwlock_create);
+  m.def("shm_rwlock_destroy", &shm_rwlock_destroy);
+
+  // ---- host loader (pinned, double-buffered H2D)
+  py::class_<HostLoader>(m, "HostLoader")
+      .def(py::init<long long, int>(), py::arg("chunk_bytes"), py::arg("nbuf") = 2)
+      .def("upload", [](HostLoader& L, uintptr_t host, uintptr_t dev, long long nbytes, uintptr_t s) {
+        py::gil_scoped_release rel;
+        L.upload(reinterpret_cast<const void*>(host), reinterpret_cast<void*>(dev), nbytes, S(s));
+      })
+      .def("upload_rows", [](HostLoader& L, uintptr_t host, long long host_ld, uintptr_t dev, long long dev_ld,
+                             long long nrows, long long row_bytes, uintptr_t s) {
+        py::gil_scoped_release rel;
+        L.upload_rows(reinterpret_cast<const char*>(host), host_ld, reinterpret_cast<char*>(dev), dev_ld, nrows,
+                      row_bytes, S(s));
+      })
+      .def_property_readonly("bytes_uploaded", &HostLoader::bytes_uploaded);
+}

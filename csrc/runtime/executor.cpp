@@ -1,0 +1,435 @@
+// Native MLP executor: plan -> grouped MFMA launches -> hipGraph.
+// See executor.h for the step structure.
+#include "executor.h"
+
+#include <algorithm>
+#include <cstring>
+
+extern "C" hipError_t ea_gemm_grouped(const ea::GroupArgs* ga, int bf16, int cfg, hipStream_t s);
+extern "C" int ea_gemm_tile_m(int cfg);
+extern "C" int ea_gemm_tile_n(int cfg);
+extern "C" void ea_gemm_init();
+extern "C" hipError_t ea_apply_update(ea::FlatArgs* a, int bf16, hipStream_t s);
+extern "C" hipError_t ea_refresh_shadows(ea::FlatArgs* a, int bf16, hipStream_t s);
+
+namespace ea {
+
+static void check(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw std::runtime_error(std::string("HIP error in ") + what + ": " + hipGetErrorString(e));
+}
+
+static inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
+
+Executor::Executor(const ExecCfg& cfg) : c_(cfg) {
+  if (c_.layers.empty()) throw std::invalid_argument("executor needs at least one Dense layer");
+  if (c_.B <= 0 || c_.Bp < c_.B || (c_.Bp % 8) != 0) throw std::invalid_argument("bad batch padding");
+  for (auto& l : c_.layers) {
+    if (l.Kp % 8 || l.Np % 8 || l.Kp < l.K || l.Np < l.N) throw std::invalid_argument("layer dims must be padded to 8");
+  }
+  ea_gemm_init();
+  build();
+}
+
+Executor::~Executor() { destroy_graphs(); }
+
+void Executor::destroy_graphs() {
+  for (auto& g : graphs_) {
+    if (g.second) (void)hipGraphExecDestroy(g.second);
+    if (g.first) (void)hipGraphDestroy(g.first);
+  }
+  graphs_.clear();
+}
+
+int Executor::pick_cfg(long long M, long long N, long long K) const {
+  if (c_.force_cfg >= 0) return c_.force_cfg;
+  return (M >= 256 && N >= 256 && K >= 256) ? 1 : 0;
+}
+
+Prob Executor::base_prob() const {
+  Prob p;
+  std::memset(&p, 0, sizeof(p));
+  p.R = c_.R;
+  p.B = c_.B;
+  p.perm = reinterpret_cast<const int*>(c_.perm);
+  p.sPerm = c_.sPerm;
+  p.ntrain = reinterpret_cast<const int*>(c_.ntrain);
+  p.vstart = reinterpret_cast<const int*>(c_.vstart);
+  p.vcount = reinterpret_cast<const int*>(c_.vcount);
+  p.ones_row = -1;
+  p.op = c_.op;
+  p.loss = c_.loss;
+  p.nmet = c_.nmet;
+  for (int i = 0; i < 4; ++i) p.met[i] = c_.met[i];
+  p.acc_stride = c_.acc_stride;
+  return p;
+}
+
+void Executor::finalize(Launch& L) const {
+  const int bm = ea_gemm_tile_m(L.cfg), bn = ea_gemm_tile_n(L.cfg);
+  int begin = 0;
+  for (int i = 0; i < L.ga.nprob; ++i) {
+    Prob& p = L.ga.p[i];
+    if (p.kind == PK_GATHER_T) {
+      p.tiles_m = cdiv(p.B, 64);
+      p.tiles_n = cdiv(p.K, 64);
+    } else if (p.kind == PK_LOSS_ROWS) {
+      p.tiles_m = cdiv(p.M, 4);
+      p.tiles_n = 1;
+    } else {
+      p.tiles_m = cdiv(p.M, bm);
+      p.tiles_n = cdiv(p.N, bn);
+    }
+    p.block_begin = begin;
+    begin += p.R * p.tiles_m * p.tiles_n;
+  }
+  L.ga.total_blocks = begin;
+  L.ga.ctr = reinterpret_cast<long long*>(c_.ctr);
+  L.ga.seed = c_.seed;
+  L.ga.adv_R = c_.R;
+  L.ga.adv_B = c_.B;
+  L.ga.adv_ntrain = reinterpret_cast<const int*>(c_.ntrain);
+}
+
+std::vector<Executor::Launch> Executor::build_forward(bool eval, long long chunk, const EvalSource* src) const {
+  const size_t esz = c_.bf16 ? 2 : 4;
+  const int L = (int)c_.layers.size();
+  std::vector<Launch> out;
+  for (int l = 0; l < L; ++l) {
+    const LayerCfg& ly = c_.layers[l];
+    const bool last = l == L - 1;
+    Prob p = base_prob();
+    p.eval_mode = eval ? 1 : 0;
+    p.chunk = chunk;
+    if (eval) {
+      p.vstart = reinterpret_cast<const int*>(src->vstart);
+      p.vcount = reinterpret_cast<const int*>(src->vcount);
+    }
+    p.M = c_.B;
+    p.N = ly.N;
+    p.K = ly.Kp;
+    if (l == 0) {
+      p.A = reinterpret_cast<const void*>(eval ? src->X : c_.X);
+      p.lda = eval ? src->ldx : c_.ldx;
+      p.sA = eval ? src->sX : c_.sX;
+      p.a_gather = 1;
+    } else {
+      const LayerCfg& pv = c_.layers[l - 1];
+      p.A = reinterpret_cast<const void*>(pv.D);
+      p.lda = pv.Np;
+      p.sA = (long long)c_.B * pv.Np;
+    }
+    p.BT = reinterpret_cast<const void*>(c_.WTsh + ly.wtsh_off * esz);
+    p.ldb = ly.Kp;
+    p.sB = c_.sWTsh;
+    p.bt_shadow = 1;
+    p.bt_par = c_.wtsh_par;
+    p.bias = ly.has_bias ? reinterpret_cast<const float*>(c_.P) + ly.p_off + (long long)ly.K * ly.N : nullptr;
+    p.sBias = c_.sP;
+    p.layer = l;
+    p.act = ly.act;
+    p.rate = ly.rate;
+    const int cfg = pick_cfg(c_.B, ly.N, ly.Kp);
+    Launch La;
+    std::memset(&La, 0, sizeof(La));
+    La.cfg = cfg;
+    if (!last) {
+      p.kind = PK_FWD;
+      p.Z = reinterpret_cast<float*>(ly.Z);
+      p.ldz = ly.N;
+      p.sZ = (long long)c_.B * ly.N;
+      p.D = reinterpret_cast<void*>(ly.D);
+      p.ldd = ly.Np;
+      p.sD = (long long)c_.B * ly.Np;
+      if (!eval) {
+        p.DT = reinterpret_cast<void*>(ly.DT);
+        p.lddt = c_.Bp;
+        p.sDT = (long long)ly.N * c_.Bp;
+      }
+      La.ga.p[0] = p;
+      La.ga.nprob = 1;
+    } else {
+      // loss / prediction plumbing
+      p.Y = reinterpret_cast<const float*>(eval ? src->Y : c_.Y);
+      p.ldy = eval ? src->ldy : c_.ldy;
+      p.sY = eval ? src->sY : c_.sY;
+      p.acc = reinterpret_cast<double*>(eval ? src->acc : c_.acc);
+      if (eval) {
+        p.pred = reinterpret_cast<float*>(src->pred);
+        p.ldp = src->ldp;
+        p.sPred = src->sPred;
+      }
+      const bool fused = ly.N <= ea_gemm_tile_n(cfg);
+      if (fused) {
+        p.kind = PK_FWD_LOSS;
+        if (!eval) {
+          p.D = reinterpret_cast<void*>(ly.dZ);
+          p.ldd = ly.Np;
+          p.sD = (long long)c_.B * ly.Np;
+          p.DT = reinterpret_cast<void*>(ly.dZT);
+          p.lddt = c_.Bp;
+          p.sDT = (long long)ly.N * c_.Bp;
+        }
+        La.ga.p[0] = p;
+        La.ga.nprob = 1;
+      } else {
+        Prob g = p;
+        g.kind = PK_FWD;
+        g.act = ACT_LINEAR;
+        g.rate = 0.f;
+        g.Z = reinterpret_cast<float*>(ly.Z);
+        g.ldz = ly.N;
+        g.sZ = (long long)c_.B * ly.N;
+        g.D = nullptr;
+        g.DT = nullptr;
+        g.acc = nullptr;
+        g.pred = nullptr;
+        La.ga.p[0] = g;
+        La.ga.nprob = 1;
+        finalize(La);
+        out.push_back(La);
+        // wave-per-row loss over the logits
+        Prob q = p;
+        q.kind = PK_LOSS_ROWS;
+        q.Z = reinterpret_cast<float*>(ly.Z);
+        q.ldz = ly.N;
+        q.sZ = (long long)c_.B * ly.N;
+        if (!eval) {
+          q.D = reinterpret_cast<void*>(ly.dZ);
+          q.ldd = ly.Np;
+          q.sD = (long long)c_.B * ly.Np;
+          q.DT = reinterpret_cast<void*>(ly.dZT);
+          q.lddt = c_.Bp;
+          q.sDT = (long long)ly.N * c_.Bp;
+        }
+        std::memset(&La, 0, sizeof(La));
+        La.cfg = cfg;
+        La.ga.p[0] = q;
+        La.ga.nprob = 1;
+      }
+    }
+    if (l == 0 && !eval && L > 0) {
+      // X^T of the batch for the layer-0 weight gradient, in the same launch
+      Prob t = base_prob();
+      t.kind = PK_GATHER_T;
+      t.A = reinterpret_cast<const void*>(c_.X);
+      t.lda = c_.ldx;
+      t.sA = c_.sX;
+      t.K = ly.Kp;
+      t.DT = reinterpret_cast<void*>(c_.XT);
+      t.lddt = c_.Bp;
+      t.sDT = (long long)ly.Kp * c_.Bp;
+      if (La.ga.nprob == 1 && La.ga.p[0].kind != PK_LOSS_ROWS) {
+        La.ga.p[1] = t;
+        La.ga.nprob = 2;
+      } else {
+        Launch Lt;
+        std::memset(&Lt, 0, sizeof(Lt));
+        Lt.cfg = 0;
+        Lt.ga.p[0] = t;
+        Lt.ga.nprob = 1;
+        finalize(Lt);
+        out.push_back(Lt);
+      }
+    }
+    finalize(La);
+    out.push_back(La);
+  }
+  return out;
+}
+
+void Executor::build() {
+  fwd_ = build_forward(false, 0, nullptr);
+  bwd_.clear();
+  const size_t esz = c_.bf16 ? 2 : 4;
+  const int L = (int)c_.layers.size();
+  for (int l = L - 1; l >= 0; --l) {
+    const LayerCfg& ly = c_.layers[l];
+    Prob w = base_prob();
+    w.kind = PK_DW_UPDATE;
+    if (l == 0) {
+      w.A = reinterpret_cast<const void*>(c_.XT);
+      w.sA = (long long)ly.Kp * c_.Bp;
+    } else {
+      const LayerCfg& pv = c_.layers[l - 1];
+      w.A = reinterpret_cast<const void*>(pv.DT);
+      w.sA = (long long)pv.N * c_.Bp;
+    }
+    w.lda = c_.Bp;
+    w.M = ly.K + (ly.has_bias ? 1 : 0);
+    w.ones_row = ly.has_bias ? ly.K : -1;
+    w.N = ly.N;
+    w.K = c_.Bp;
+    w.BT = reinterpret_cast<const void*>(ly.dZT);
+    w.ldb = c_.Bp;
+    w.sB = (long long)ly.N * c_.Bp;
+    w.P = reinterpret_cast<float*>(c_.P);
+    w.sP = c_.sP;
+    w.p_off = ly.p_off;
+    w.S = reinterpret_cast<float*>(c_.S);
+    w.sS = c_.sS;
+    w.G = reinterpret_cast<float*>(c_.G);
+    w.sG = c_.sG;
+    w.Wsh = reinterpret_cast<void*>(c_.Wsh + ly.wsh_off * esz);
+    w.sWsh = c_.sWsh;
+    w.ldwsh = ly.Np;
+    w.wsh_par = c_.wsh_par;
+    w.WTsh = reinterpret_cast<void*>(c_.WTsh + ly.wtsh_off * esz);
+    w.sWTsh = c_.sWTsh;
+    w.ldwtsh = ly.Kp;
+    w.wtsh_par = c_.wtsh_par;
+    Launch La;
+    std::memset(&La, 0, sizeof(La));
+    long long work = (long long)w.M * w.N * w.K;
+    La.ga.p[0] = w;
+    La.ga.nprob = 1;
+    int cm = (int)w.M, cn = w.N, ck = w.K;
+    if (l >= 1) {
+      const LayerCfg& pv = c_.layers[l - 1];
+      Prob x = base_prob();
+      x.kind = PK_DX;
+      x.A = reinterpret_cast<const void*>(ly.dZ);
+      x.lda = ly.Np;
+      x.sA = (long long)c_.B * ly.Np;
+      x.BT = reinterpret_cast<const void*>(c_.Wsh + ly.wsh_off * esz);
+      x.ldb = ly.Np;
+      x.sB = c_.sWsh;
+      x.bt_shadow = 1;
+      x.bt_par = c_.wsh_par;
+      x.M = c_.B;
+      x.N = ly.K;
+      x.K = ly.Np;
+      x.act = pv.act;
+      x.rate = pv.rate;
+      x.layer = l - 1;
+      x.Z = reinterpret_cast<float*>(pv.Z);
+      x.ldz = pv.N;
+      x.sZ = (long long)c_.B * pv.N;
+      x.D = reinterpret_cast<void*>(pv.dZ);
+      x.ldd = pv.Np;
+      x.sD = (long long)c_.B * pv.Np;
+      x.DT = reinterpret_cast<void*>(pv.dZT);
+      x.lddt = c_.Bp;
+      x.sDT = (long long)pv.N * c_.Bp;
+      La.ga.p[1] = x;
+      La.ga.nprob = 2;
+      long long xw = (long long)x.M * x.N * x.K;
+      if (xw > work) { cm = x.M; cn = x.N; ck = x.K; }
+    }
+    La.cfg = pick_cfg(cm, cn, ck);
+    La.ga.advance = (l == 0) ? 1 : 0;
+    finalize(La);
+    bwd_.push_back(La);
+  }
+}
+
+void Executor::run(const std::vector<Launch>& ls, hipStream_t s) const {
+  for (const auto& L : ls) check(ea_gemm_grouped(&L.ga, c_.bf16, L.cfg, s), "gemm_grouped");
+}
+
+std::vector<int> Executor::launch_cfgs() const {
+  std::vector<int> v;
+  for (auto& L : fwd_) v.push_back(L.cfg);
+  for (auto& L : bwd_) v.push_back(L.cfg);
+  return v;
+}
+
+void Executor::train_step(hipStream_t s) {
+  run(fwd_, s);
+  run(bwd_, s);
+}
+
+void Executor::forward_backward(hipStream_t s) {
+  run(fwd_, s);
+  for (auto L : bwd_) {
+    for (int i = 0; i < L.ga.nprob; ++i)
+      if (L.ga.p[i].kind == PK_DW_UPDATE) L.ga.p[i].kind = PK_DW_GRAD;
+    L.ga.advance = 0;
+    check(ea_gemm_grouped(&L.ga, c_.bf16, L.cfg, s), "gemm_grouped(grad)");
+  }
+}
+
+FlatArgs Executor::flat_args() const {
+  FlatArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.R = c_.R;
+  a.n = c_.nparams;
+  a.P = reinterpret_cast<float*>(c_.P);
+  a.sP = c_.sP;
+  a.G = reinterpret_cast<const float*>(c_.G);
+  a.sG = c_.sG;
+  a.S = reinterpret_cast<float*>(c_.S);
+  a.sS = c_.sS;
+  a.op = c_.op;
+  a.nseg = (int)c_.layers.size();
+  if (a.nseg > MAX_SEG) throw std::invalid_argument("too many layers for the flat kernels");
+  for (int i = 0; i < a.nseg; ++i) {
+    const LayerCfg& l = c_.layers[i];
+    a.seg[i].p_off = l.p_off;
+    a.seg[i].K = l.K;
+    a.seg[i].N = l.N;
+    a.seg[i].has_bias = l.has_bias;
+    a.seg[i].wsh_off = l.wsh_off;
+    a.seg[i].ldwsh = l.Np;
+    a.seg[i].wtsh_off = l.wtsh_off;
+    a.seg[i].ldwtsh = l.Kp;
+  }
+  a.Wsh = reinterpret_cast<void*>(c_.Wsh);
+  a.sWsh = c_.sWsh;
+  a.wsh_par = c_.wsh_par;
+  a.WTsh = reinterpret_cast<void*>(c_.WTsh);
+  a.sWTsh = c_.sWTsh;
+  a.wtsh_par = c_.wtsh_par;
+  a.ctr = reinterpret_cast<long long*>(c_.ctr);
+  a.ntrain = reinterpret_cast<const int*>(c_.ntrain);
+  a.B = c_.B;
+  return a;
+}
+
+void Executor::apply(hipStream_t s) {
+  FlatArgs a = flat_args();
+  a.advance = 1;
+  check(ea_apply_update(&a, c_.bf16, s), "apply_update");
+}
+
+void Executor::refresh_shadows(bool both, hipStream_t s) {
+  FlatArgs a = flat_args();
+  a.both_parities = both ? 1 : 0;
+  check(ea_refresh_shadows(&a, c_.bf16, s), "refresh_shadows");
+}
+
+void Executor::reset_epoch(hipStream_t s) {
+  check(hipMemsetAsync(reinterpret_cast<void*>(c_.ctr), 0, 2 * sizeof(long long), s), "reset_epoch");
+}
+
+void Executor::eval_chunk(long long chunk, const EvalSource& src, hipStream_t s) {
+  auto ls = build_forward(true, chunk, &src);
+  run(ls, s);
+}
+
+int Executor::capture(int nsteps, int mode, hipStream_t s) {
+  hipGraph_t g = nullptr;
+  hipGraphExec_t e = nullptr;
+  check(hipStreamBeginCapture(s, hipStreamCaptureModeRelaxed), "hipStreamBeginCapture");
+  try {
+    for (int i = 0; i < nsteps; ++i) {
+      if (mode == 0) train_step(s);
+      else if (mode == 1) forward_backward(s);
+      else apply(s);
+    }
+  } catch (...) {
+    hipGraph_t dummy;
+    (void)hipStreamEndCapture(s, &dummy);
+    throw;
+  }
+  check(hipStreamEndCapture(s, &g), "hipStreamEndCapture");
+  check(hipGraphInstantiate(&e, g, nullptr, nullptr, 0), "hipGraphInstantiate");
+  graphs_.push_back({g, e});
+  return (int)graphs_.size() - 1;
+}
+
+void Executor::replay(int id, hipStream_t s) {
+  if (id < 0 || id >= (int)graphs_.size()) throw std::out_of_range("graph id");
+  check(hipGraphLaunch(graphs_[id].second, s), "hipGraphLaunch");
+}
+
+}  // namespace ea

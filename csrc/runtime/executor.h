@@ -1,0 +1,107 @@
+// Native MLP training executor (MI355X / HIP).
+//
+// Replaces the reference's per-partition Keras `model.fit` hot loop
+// (reference elephas/worker.py:26-49 SparkWorker.train, :76-131
+// AsynchronousSparkWorker.train) with a plan of grouped MFMA launches:
+//
+//   step = [FWD_0 + gather X^T] [FWD_1] ... [FWD_{L-1} + loss]   (L launches)
+//          [DW_{L-1} + DX_{L-1}] ... [DW_0 (+ counter advance)]  (L launches)
+//
+// The step reads its batch index, dropout counter and optimizer iteration from
+// device counters, so one captured hipGraph of a step is replayed for every
+// step of every epoch (no host round-trip, no per-step launch cost beyond the
+// graph's kernel boundaries). R independent replicas ("logical workers" in the
+// reference's sense, one per Spark partition) are batched into every launch.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <map>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../kernels/args.h"
+
+namespace ea {
+
+struct LayerCfg {
+  int K = 0, N = 0, Kp = 0, Np = 0, act = 0, has_bias = 1;
+  float rate = 0.f;
+  long long p_off = 0;
+  uintptr_t Z = 0, D = 0, DT = 0, dZ = 0, dZT = 0;
+  long long wsh_off = 0, wtsh_off = 0;
+};
+
+struct ExecCfg {
+  int R = 1, B = 32, Bp = 32, bf16 = 1;
+  unsigned long long seed = 0;
+  std::vector<LayerCfg> layers;
+  // training data (device)
+  uintptr_t X = 0; long long sX = 0, ldx = 0;
+  uintptr_t Y = 0; long long sY = 0, ldy = 0;
+  uintptr_t perm = 0; long long sPerm = 0;
+  uintptr_t ntrain = 0, vstart = 0, vcount = 0;
+  uintptr_t XT = 0;
+  // parameters
+  uintptr_t P = 0; long long sP = 0, nparams = 0;
+  uintptr_t G = 0; long long sG = 0;
+  uintptr_t S = 0; long long sS = 0;
+  uintptr_t Wsh = 0; long long sWsh = 0, wsh_par = 0;
+  uintptr_t WTsh = 0; long long sWTsh = 0, wtsh_par = 0;
+  OptParams op{};
+  int loss = 0, nmet = 0, met[4] = {0, 0, 0, 0};
+  uintptr_t acc = 0; int acc_stride = 6;
+  uintptr_t ctr = 0;
+  int force_cfg = -1;  // -1 auto, 0 LAT, 1 THR
+};
+
+struct EvalSource {
+  uintptr_t X = 0; long long sX = 0, ldx = 0;
+  uintptr_t Y = 0; long long sY = 0, ldy = 0;
+  uintptr_t vstart = 0, vcount = 0;
+  uintptr_t acc = 0;
+  uintptr_t pred = 0; long long sPred = 0, ldp = 0;
+};
+
+class Executor {
+ public:
+  explicit Executor(const ExecCfg& cfg);
+  ~Executor();
+
+  // eager launches on `stream`
+  void train_step(hipStream_t s);          // fused-update path (+ counter advance)
+  void forward_backward(hipStream_t s);    // gradient path: writes G (no update)
+  void apply(hipStream_t s);               // gradient path: optimizer apply + advance
+  void eval_chunk(long long chunk, const EvalSource& src, hipStream_t s);
+  void refresh_shadows(bool both, hipStream_t s);
+  void reset_epoch(hipStream_t s);
+
+  // hipGraph capture / replay of `nsteps` training steps (mode 0: train_step,
+  // mode 1: forward_backward only, mode 2: apply only)
+  int capture(int nsteps, int mode, hipStream_t s);
+  void replay(int graph_id, hipStream_t s);
+  void destroy_graphs();
+
+  int launches_per_step() const { return (int)fwd_.size() + (int)bwd_.size(); }
+  std::vector<int> launch_cfgs() const;
+
+ private:
+  struct Launch {
+    GroupArgs ga;
+    int cfg;
+  };
+  ExecCfg c_;
+  std::vector<Launch> fwd_, bwd_;
+  std::vector<std::pair<hipGraph_t, hipGraphExec_t>> graphs_;
+
+  Prob base_prob() const;
+  void finalize(Launch& L) const;
+  int pick_cfg(long long M, long long N, long long K) const;
+  std::vector<Launch> build_forward(bool eval, long long chunk, const EvalSource* src) const;
+  void build();
+  void run(const std::vector<Launch>& ls, hipStream_t s) const;
+  FlatArgs flat_args() const;
+};
+
+}  // namespace ea

@@ -1,0 +1,77 @@
+#include "host_loader.h"
+
+#include <algorithm>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+
+namespace ea {
+
+static void chk(hipError_t e, const char* w) {
+  if (e != hipSuccess) throw std::runtime_error(std::string("HIP error in ") + w + ": " + hipGetErrorString(e));
+}
+
+HostLoader::HostLoader(long long chunk_bytes, int nbuf) : chunk_(chunk_bytes) {
+  if (chunk_bytes <= 0 || nbuf < 1) throw std::invalid_argument("HostLoader: bad sizes");
+  for (int i = 0; i < nbuf; ++i) {
+    void* p = nullptr;
+    chk(hipHostMalloc(&p, (size_t)chunk_bytes, hipHostMallocDefault), "hipHostMalloc");
+    bufs_.push_back(reinterpret_cast<char*>(p));
+    hipEvent_t e;
+    chk(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
+    evs_.push_back(e);
+    busy_.push_back(false);
+  }
+}
+
+HostLoader::~HostLoader() {
+  for (size_t i = 0; i < bufs_.size(); ++i) {
+    if (busy_[i]) (void)hipEventSynchronize(evs_[i]);
+    (void)hipEventDestroy(evs_[i]);
+    (void)hipHostFree(bufs_[i]);
+  }
+}
+
+char* HostLoader::acquire(hipStream_t) {
+  const int i = next_;
+  if (busy_[i]) chk(hipEventSynchronize(evs_[i]), "loader wait");  // DMA of this buffer finished
+  busy_[i] = false;
+  return bufs_[i];
+}
+
+void HostLoader::release(hipStream_t s) {
+  chk(hipEventRecord(evs_[next_], s), "loader record");
+  busy_[next_] = true;
+  next_ = (next_ + 1) % (int)bufs_.size();
+}
+
+void HostLoader::upload(const void* host, void* dev, long long nbytes, hipStream_t s) {
+  const char* h = reinterpret_cast<const char*>(host);
+  char* d = reinterpret_cast<char*>(dev);
+  for (long long off = 0; off < nbytes; off += chunk_) {
+    const long long n = std::min(chunk_, nbytes - off);
+    char* buf = acquire(s);
+    std::memcpy(buf, h + off, (size_t)n);
+    chk(hipMemcpyAsync(d + off, buf, (size_t)n, hipMemcpyHostToDevice, s), "loader H2D");
+    release(s);
+    bytes_ += n;
+  }
+}
+
+void HostLoader::upload_rows(const char* host, long long host_ld, char* dev, long long dev_ld, long long nrows,
+                             long long row_bytes, hipStream_t s) {
+  if (row_bytes > chunk_) throw std::invalid_argument("row larger than loader chunk");
+  const long long rows_per_chunk = std::max<long long>(1, chunk_ / row_bytes);
+  for (long long r0 = 0; r0 < nrows; r0 += rows_per_chunk) {
+    const long long nr = std::min(rows_per_chunk, nrows - r0);
+    char* buf = acquire(s);
+    for (long long r = 0; r < nr; ++r) std::memcpy(buf + r * row_bytes, host + (r0 + r) * host_ld, (size_t)row_bytes);
+    chk(hipMemcpy2DAsync(dev + r0 * dev_ld, (size_t)dev_ld, buf, (size_t)row_bytes, (size_t)row_bytes, (size_t)nr,
+                         hipMemcpyHostToDevice, s),
+        "loader H2D 2D");
+    release(s);
+    bytes_ += nr * row_bytes;
+  }
+}
+
+}  // namespace ea

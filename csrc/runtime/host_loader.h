@@ -1,0 +1,37 @@
+// Host -> device data loader with pinned, double-buffered staging.
+//
+// Replaces Spark's parallelize/repartition data shipping (reference
+// utils/rdd_utils.py:10-20, spark_model.py:182-183): a rank's partition
+// (contiguous rows of the host dataset) is streamed into HBM through `nbuf`
+// pinned chunks; the CPU packs chunk i+1 while the DMA engine moves chunk i.
+// Sized for 288 GB HBM: whole shards stay resident on the device afterwards.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <vector>
+
+namespace ea {
+
+class HostLoader {
+ public:
+  HostLoader(long long chunk_bytes, int nbuf = 2);
+  ~HostLoader();
+  // contiguous copy
+  void upload(const void* host, void* dev, long long nbytes, hipStream_t s);
+  // row-strided copy (e.g. pad rows to a 16-byte multiple on the device)
+  void upload_rows(const char* host, long long host_ld, char* dev, long long dev_ld, long long nrows,
+                   long long row_bytes, hipStream_t s);
+  long long bytes_uploaded() const { return bytes_; }
+
+ private:
+  long long chunk_;
+  std::vector<char*> bufs_;
+  std::vector<hipEvent_t> evs_;
+  std::vector<bool> busy_;
+  long long bytes_ = 0;
+  int next_ = 0;
+  char* acquire(hipStream_t s);
+  void release(hipStream_t s);
+};
+
+}  // namespace ea

@@ -1,0 +1,176 @@
+#include "param_server.h"
+
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <cstring>
+#include <stdexcept>
+
+extern "C" hipError_t ea_ps_sub(float* p, const float* d, long long n, float scale, int atomic, hipStream_t s);
+
+namespace ea {
+
+static void chk(hipError_t e, const char* w) {
+  if (e != hipSuccess) throw std::runtime_error(std::string("HIP error in ") + w + ": " + hipGetErrorString(e));
+}
+
+// ------------------------------------------------------------------ locks
+class LocalLock : public RWLockBase {
+ public:
+  void lock_shared() override { m_.lock_shared(); }
+  void unlock_shared() override { m_.unlock_shared(); }
+  void lock() override { m_.lock(); }
+  void unlock() override { m_.unlock(); }
+
+ private:
+  std::shared_mutex m_;
+};
+
+static std::string shm_path(const std::string& name) { return name[0] == '/' ? name : "/" + name; }
+
+class ShmLock : public RWLockBase {
+ public:
+  explicit ShmLock(const std::string& name) {
+    int fd = shm_open(shm_path(name).c_str(), O_RDWR, 0600);
+    if (fd < 0) throw std::runtime_error("shm_open failed for lock " + name);
+    void* p = mmap(nullptr, sizeof(pthread_rwlock_t), PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+    close(fd);
+    if (p == MAP_FAILED) throw std::runtime_error("mmap failed for lock " + name);
+    l_ = reinterpret_cast<pthread_rwlock_t*>(p);
+  }
+  ~ShmLock() override { munmap(l_, sizeof(pthread_rwlock_t)); }
+  void lock_shared() override { pthread_rwlock_rdlock(l_); }
+  void unlock_shared() override { pthread_rwlock_unlock(l_); }
+  void lock() override { pthread_rwlock_wrlock(l_); }
+  void unlock() override { pthread_rwlock_unlock(l_); }
+
+ private:
+  pthread_rwlock_t* l_;
+};
+
+void shm_rwlock_create(const std::string& name) {
+  int fd = shm_open(shm_path(name).c_str(), O_CREAT | O_RDWR | O_TRUNC, 0600);
+  if (fd < 0) throw std::runtime_error("shm_open(create) failed for " + name);
+  if (ftruncate(fd, sizeof(pthread_rwlock_t)) != 0) {
+    close(fd);
+    throw std::runtime_error("ftruncate failed for " + name);
+  }
+  void* p = mmap(nullptr, sizeof(pthread_rwlock_t), PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+  close(fd);
+  if (p == MAP_FAILED) throw std::runtime_error("mmap failed for " + name);
+  pthread_rwlockattr_t a;
+  pthread_rwlockattr_init(&a);
+  pthread_rwlockattr_setpshared(&a, PTHREAD_PROCESS_SHARED);
+  // writer priority, as the reference RWLock (utils/rwlock.py:24-46)
+  pthread_rwlockattr_setkind_np(&a, PTHREAD_RWLOCK_PREFER_WRITER_NONRECURSIVE_NP);
+  pthread_rwlock_init(reinterpret_cast<pthread_rwlock_t*>(p), &a);
+  pthread_rwlockattr_destroy(&a);
+  munmap(p, sizeof(pthread_rwlock_t));
+}
+
+void shm_rwlock_destroy(const std::string& name) { shm_unlink(shm_path(name).c_str()); }
+
+std::unique_ptr<RWLockBase> make_lock(const std::string& shm_name) {
+  if (shm_name.empty()) return std::make_unique<LocalLock>();
+  return std::make_unique<ShmLock>(shm_name);
+}
+
+// ------------------------------------------------------------ local owner
+DeviceParameterServer::DeviceParameterServer(long long n, int locked, int device, const std::string& lock_name)
+    : n_(n), locked_(locked), device_(device), lock_(make_lock(lock_name)) {
+  chk(hipSetDevice(device), "hipSetDevice");
+  chk(hipMalloc(&p_, (size_t)n * sizeof(float)), "hipMalloc(ps)");
+  chk(hipMemset(p_, 0, (size_t)n * sizeof(float)), "hipMemset(ps)");
+}
+
+DeviceParameterServer::~DeviceParameterServer() {
+  if (p_) (void)hipFree(p_);
+}
+
+void DeviceParameterServer::pull(float* dst, hipStream_t s) {
+  if (locked_) lock_->lock_shared();
+  try {
+    chk(hipMemcpyAsync(dst, p_, (size_t)n_ * sizeof(float), hipMemcpyDeviceToDevice, s), "ps.pull");
+    if (locked_) chk(hipStreamSynchronize(s), "ps.pull sync");
+  } catch (...) {
+    if (locked_) lock_->unlock_shared();
+    throw;
+  }
+  if (locked_) lock_->unlock_shared();
+  pulls_++;
+}
+
+void DeviceParameterServer::push(const float* delta, hipStream_t s) {
+  if (locked_) lock_->lock();
+  try {
+    chk(ea_ps_sub(p_, delta, n_, 1.f, 0, s), "ps.push");
+    if (locked_) chk(hipStreamSynchronize(s), "ps.push sync");
+  } catch (...) {
+    if (locked_) lock_->unlock();
+    throw;
+  }
+  if (locked_) lock_->unlock();
+  pushes_++;
+}
+
+void DeviceParameterServer::set(const float* src, hipStream_t s) {
+  lock_->lock();
+  try {
+    chk(hipMemcpyAsync(p_, src, (size_t)n_ * sizeof(float), hipMemcpyDeviceToDevice, s), "ps.set");
+    chk(hipStreamSynchronize(s), "ps.set sync");
+  } catch (...) {
+    lock_->unlock();
+    throw;
+  }
+  lock_->unlock();
+}
+
+std::string DeviceParameterServer::ipc_handle() const {
+  hipIpcMemHandle_t h;
+  chk(hipIpcGetMemHandle(&h, p_), "hipIpcGetMemHandle");
+  return std::string(reinterpret_cast<const char*>(&h), sizeof(h));
+}
+
+// ----------------------------------------------------------- remote (xGMI)
+RemoteParameterServer::RemoteParameterServer(const std::string& handle, long long n, int locked,
+                                             const std::string& lock_name)
+    : n_(n), locked_(locked), lock_(make_lock(lock_name)) {
+  if (handle.size() != sizeof(hipIpcMemHandle_t)) throw std::invalid_argument("bad IPC handle size");
+  hipIpcMemHandle_t h;
+  std::memcpy(&h, handle.data(), sizeof(h));
+  void* p = nullptr;
+  chk(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle");
+  p_ = reinterpret_cast<float*>(p);
+}
+
+RemoteParameterServer::~RemoteParameterServer() {
+  if (p_) (void)hipIpcCloseMemHandle(p_);
+}
+
+void RemoteParameterServer::pull(float* dst, hipStream_t s) {
+  if (locked_) lock_->lock_shared();
+  try {
+    chk(hipMemcpyAsync(dst, p_, (size_t)n_ * sizeof(float), hipMemcpyDeviceToDevice, s), "remote.pull");
+    chk(hipStreamSynchronize(s), "remote.pull sync");
+  } catch (...) {
+    if (locked_) lock_->unlock_shared();
+    throw;
+  }
+  if (locked_) lock_->unlock_shared();
+}
+
+void RemoteParameterServer::push(const float* delta, hipStream_t s) {
+  if (locked_) lock_->lock();
+  try {
+    chk(ea_ps_sub(p_, delta, n_, 1.f, 0, s), "remote.push");
+    chk(hipStreamSynchronize(s), "remote.push sync");
+  } catch (...) {
+    if (locked_) lock_->unlock();
+    throw;
+  }
+  if (locked_) lock_->unlock();
+}
+
+}  // namespace ea

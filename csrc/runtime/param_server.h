@@ -1,0 +1,73 @@
+// Device-resident parameter server for the asynchronous / hogwild modes.
+//
+// Replaces the reference's Flask/socket parameter servers
+// (reference elephas/parameter/server.py:42-233, client.py:41-91): the master
+// parameters live in HBM of the owning GPU as one flat fp32 vector.
+//   pull  = device-to-device copy (peer copy over xGMI for a remote owner)
+//   push  = remote-subtract kernel  theta <- theta - delta  run by the pusher
+//           directly on the owner's memory (peer RMW over xGMI)
+// 'asynchronous' mode serialises pushes and pulls with a writer-priority
+// reader/writer lock (reference utils/rwlock.py:10-67 semantics), in-process or
+// shared between processes through POSIX shared memory; 'hogwild' takes no lock
+// and lets concurrent updates race (reference server.py:109-131 guards).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <pthread.h>
+
+#include <atomic>
+#include <memory>
+#include <shared_mutex>
+#include <string>
+
+namespace ea {
+
+class RWLockBase {
+ public:
+  virtual ~RWLockBase() = default;
+  virtual void lock_shared() = 0;
+  virtual void unlock_shared() = 0;
+  virtual void lock() = 0;
+  virtual void unlock() = 0;
+};
+
+std::unique_ptr<RWLockBase> make_lock(const std::string& shm_name);  // "" -> in-process
+void shm_rwlock_create(const std::string& name);
+void shm_rwlock_destroy(const std::string& name);
+
+class DeviceParameterServer {
+ public:
+  DeviceParameterServer(long long n, int locked, int device, const std::string& lock_name = "");
+  ~DeviceParameterServer();
+  void pull(float* dst, hipStream_t s);
+  void push(const float* delta, hipStream_t s);
+  void set(const float* src, hipStream_t s);
+  std::string ipc_handle() const;
+  float* data() const { return p_; }
+  long long size() const { return n_; }
+  long long pushes() const { return pushes_.load(); }
+  long long pulls() const { return pulls_.load(); }
+
+ private:
+  long long n_;
+  int locked_;
+  int device_;
+  float* p_ = nullptr;
+  std::unique_ptr<RWLockBase> lock_;
+  std::atomic<long long> pushes_{0}, pulls_{0};
+};
+
+class RemoteParameterServer {
+ public:
+  RemoteParameterServer(const std::string& handle, long long n, int locked, const std::string& lock_name);
+  ~RemoteParameterServer();
+  void pull(float* dst, hipStream_t s);
+  void push(const float* delta, hipStream_t s);
+
+ private:
+  long long n_;
+  int locked_;
+  float* p_ = nullptr;
+  std::unique_ptr<RWLockBase> lock_;
+};
+
+}  // namespace ea

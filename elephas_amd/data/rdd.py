@@ -1,0 +1,298 @@
+"""In-process, eager stand-in for Spark's SparkContext / RDD / Broadcast.
+
+There is no JVM: an RDD is a list of partitions (lists) held in host memory,
+and partition i is what one logical worker trains on.  The operations keep
+Spark's observable semantics that the reference relies on
+(SURVEY.md §2.7 'Spark partitioning'):
+  * ``parallelize`` cuts the data into ``numSlices`` CONTIGUOUS slices
+    (``defaultParallelism`` = N of ``local[N]``);
+  * ``repartition(n)`` redistributes round-robin (order is not preserved,
+    which is why the reference index-tags predictions: spark_model.py:257-266);
+  * ``zipWithIndex`` numbers elements in partition order; ``sortBy`` sorts.
+Training never iterates these Python lists on the hot path: partitions are
+stacked into device-resident shards (elephas_amd/parallel/workers.py).
+"""
+from __future__ import annotations
+
+import itertools
+import os
+import re
+from functools import reduce as _reduce
+from typing import Any, Callable, Iterable, List, Optional
+
+
+class SparkConf:
+    def __init__(self, loadDefaults=True):
+        self._conf = {}
+
+    def setAppName(self, name):
+        self._conf["spark.app.name"] = name
+        return self
+
+    def setMaster(self, master):
+        self._conf["spark.master"] = master
+        return self
+
+    def set(self, key, value):
+        self._conf[key] = value
+        return self
+
+    def get(self, key, default=None):
+        return self._conf.get(key, default)
+
+    def getAll(self):
+        return list(self._conf.items())
+
+
+class Broadcast:
+    def __init__(self, value):
+        self._value = value
+
+    @property
+    def value(self):
+        return self._value
+
+    def unpersist(self, blocking=False):
+        pass
+
+    def destroy(self, blocking=False):
+        self._value = None
+
+
+def _parallelism_from_master(master: str) -> int:
+    m = re.match(r"local\[(\d+|\*)\]", master or "")
+    if m:
+        if m.group(1) == "*":
+            return max(1, min(os.cpu_count() or 1, 8))
+        return int(m.group(1))
+    if master == "local":
+        return 1
+    return max(1, min(os.cpu_count() or 1, 8))
+
+
+class SparkContext:
+    _active: Optional["SparkContext"] = None
+
+    def __init__(self, master: Optional[str] = None, appName: Optional[str] = None, conf: Optional[SparkConf] = None,
+                 **kwargs):
+        conf = conf or SparkConf()
+        self._conf = conf
+        self.master = master or conf.get("spark.master", os.environ.get("ELEPHAS_AMD_MASTER", "local[*]"))
+        self.appName = appName or conf.get("spark.app.name", "elephas_amd")
+        self.defaultParallelism = _parallelism_from_master(self.master)
+        SparkContext._active = self
+
+    @classmethod
+    def getOrCreate(cls, conf: Optional[SparkConf] = None) -> "SparkContext":
+        if cls._active is None:
+            cls._active = SparkContext(conf=conf)
+        return cls._active
+
+    def getConf(self):
+        return self._conf
+
+    def stop(self):
+        if SparkContext._active is self:
+            SparkContext._active = None
+
+    def parallelize(self, data: Iterable, numSlices: Optional[int] = None) -> "RDD":
+        items = list(data)
+        n = numSlices or self.defaultParallelism
+        n = max(1, int(n))
+        parts = [items[i * len(items) // n:(i + 1) * len(items) // n] for i in range(n)]
+        return RDD(parts, self)
+
+    def broadcast(self, value) -> Broadcast:
+        return Broadcast(value)
+
+    def emptyRDD(self) -> "RDD":
+        return RDD([[]], self)
+
+    def textFile(self, path: str, minPartitions: Optional[int] = None) -> "RDD":
+        with open(path, "r") as f:
+            lines = [l.rstrip("\n") for l in f]
+        return self.parallelize(lines, minPartitions)
+
+    def union(self, rdds):
+        parts = []
+        for r in rdds:
+            parts.extend(r._parts)
+        return RDD(parts, self)
+
+    def setLogLevel(self, level):
+        pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.stop()
+
+
+class RDD:
+    def __init__(self, partitions: List[list], ctx: Optional[SparkContext] = None):
+        self._parts = [list(p) for p in partitions]
+        self.ctx = ctx or SparkContext.getOrCreate()
+
+    # ---- structure
+    @property
+    def context(self):
+        return self.ctx
+
+    def getNumPartitions(self) -> int:
+        return len(self._parts)
+
+    def glom(self) -> "RDD":
+        return RDD([[list(p)] for p in self._parts], self.ctx)
+
+    def partitions(self) -> List[list]:
+        return [list(p) for p in self._parts]
+
+    def cache(self):
+        return self
+
+    persist = cache
+
+    def unpersist(self, blocking=False):
+        return self
+
+    # ---- transformations
+    def map(self, f, preservesPartitioning=False) -> "RDD":
+        return RDD([[f(x) for x in p] for p in self._parts], self.ctx)
+
+    def flatMap(self, f, preservesPartitioning=False) -> "RDD":
+        return RDD([[y for x in p for y in f(x)] for p in self._parts], self.ctx)
+
+    def filter(self, f) -> "RDD":
+        return RDD([[x for x in p if f(x)] for p in self._parts], self.ctx)
+
+    def mapPartitions(self, f, preservesPartitioning=False) -> "RDD":
+        out = []
+        for p in self._parts:
+            r = f(iter(p))
+            out.append(list(r) if r is not None else [])
+        return RDD(out, self.ctx)
+
+    def mapPartitionsWithIndex(self, f, preservesPartitioning=False) -> "RDD":
+        out = []
+        for i, p in enumerate(self._parts):
+            r = f(i, iter(p))
+            out.append(list(r) if r is not None else [])
+        return RDD(out, self.ctx)
+
+    def repartition(self, numPartitions: int) -> "RDD":
+        n = max(1, int(numPartitions))
+        parts = [[] for _ in range(n)]
+        for i, x in enumerate(itertools.chain.from_iterable(self._parts)):
+            parts[i % n].append(x)
+        return RDD(parts, self.ctx)
+
+    def coalesce(self, numPartitions: int, shuffle: bool = False) -> "RDD":
+        if shuffle:
+            return self.repartition(numPartitions)
+        n = max(1, min(int(numPartitions), len(self._parts)))
+        groups = [self._parts[i * len(self._parts) // n:(i + 1) * len(self._parts) // n] for i in range(n)]
+        return RDD([[x for p in g for x in p] for g in groups], self.ctx)
+
+    def zipWithIndex(self) -> "RDD":
+        out, k = [], 0
+        for p in self._parts:
+            q = []
+            for x in p:
+                q.append((x, k))
+                k += 1
+            out.append(q)
+        return RDD(out, self.ctx)
+
+    def zip(self, other: "RDD") -> "RDD":
+        if [len(p) for p in self._parts] != [len(p) for p in other._parts]:
+            raise ValueError("Can only zip RDDs with the same number of elements in each partition")
+        return RDD([list(zip(a, b)) for a, b in zip(self._parts, other._parts)], self.ctx)
+
+    def sortBy(self, keyfunc, ascending=True, numPartitions=None) -> "RDD":
+        items = sorted(self.collect(), key=keyfunc, reverse=not ascending)
+        n = numPartitions or len(self._parts)
+        return self.ctx.parallelize(items, n)
+
+    def distinct(self, numPartitions=None) -> "RDD":
+        seen, out = set(), []
+        for x in self.collect():
+            k = x if not hasattr(x, "toArray") else x.toArray().tobytes()
+            try:
+                if k in seen:
+                    continue
+                seen.add(k)
+            except TypeError:
+                pass
+            out.append(x)
+        return self.ctx.parallelize(out, numPartitions or len(self._parts))
+
+    def keys(self):
+        return self.map(lambda kv: kv[0])
+
+    def values(self):
+        return self.map(lambda kv: kv[1])
+
+    def union(self, other):
+        return RDD(self._parts + other._parts, self.ctx)
+
+    def sample(self, withReplacement, fraction, seed=None):
+        import random
+        rnd = random.Random(seed)
+        return RDD([[x for x in p if rnd.random() < fraction] for p in self._parts], self.ctx)
+
+    # ---- actions
+    def collect(self) -> list:
+        return [x for p in self._parts for x in p]
+
+    def count(self) -> int:
+        return sum(len(p) for p in self._parts)
+
+    def first(self):
+        for p in self._parts:
+            if p:
+                return p[0]
+        raise ValueError("RDD is empty")
+
+    def take(self, n: int) -> list:
+        return list(itertools.islice(itertools.chain.from_iterable(self._parts), n))
+
+    def reduce(self, f):
+        items = self.collect()
+        if not items:
+            raise ValueError("Can not reduce() empty RDD")
+        return _reduce(f, items)
+
+    def fold(self, zeroValue, op):
+        return _reduce(op, self.collect(), zeroValue)
+
+    def sum(self):
+        return sum(self.collect())
+
+    def max(self, key=None):
+        return max(self.collect(), key=key) if key else max(self.collect())
+
+    def min(self, key=None):
+        return min(self.collect(), key=key) if key else min(self.collect())
+
+    def mean(self):
+        items = self.collect()
+        return sum(items) / len(items)
+
+    def foreach(self, f):
+        for x in self.collect():
+            f(x)
+
+    def foreachPartition(self, f):
+        for p in self._parts:
+            f(iter(p))
+
+    def isEmpty(self) -> bool:
+        return self.count() == 0
+
+    def toDF(self, schema=None):
+        from .sql import SparkSession
+        return SparkSession.builder.getOrCreate().createDataFrame(self, schema)
+
+    def __repr__(self):
+        return f"RDD[{self.getNumPartitions()} partitions, {self.count()} elements]"

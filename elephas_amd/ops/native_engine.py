@@ -1,0 +1,442 @@
+"""Native MI355X training engine: device buffers + the C++ ``Executor``.
+
+Memory layout (per replica r; everything stays resident in HBM):
+  P    fp32 [R, n]            master weights, Keras flat order (all-reduce / PS payload)
+  S    fp32 [R, k, n]         optimizer state planes
+  G    fp32 [R, n]            gradients (per-step all-reduce path only)
+  Wsh  T    [R, 2, sum K*Np]  row-major weight image, 2 parities (read by DX GEMMs)
+  WTsh T    [R, 2, sum N*Kp]  transposed weight image, 2 parities (read by FWD GEMMs)
+  X    T    [R, nmax, Kp0]    the replica's data shard (padded rows), Y fp32 [R, nmax, ldy]
+  per layer workspaces Z/D/D^T/dZ/dZ^T for one batch
+T is bf16 under the 'mixed_bfloat16' policy and fp32 otherwise.  The fused
+update epilogue writes the next step's shadow parity while this step's DX
+GEMMs still read the current one, so DW and DX of a layer share one launch.
+
+One training step is 2L grouped launches; the step is captured once as a
+hipGraph (natively, in csrc/runtime/executor.cpp) and replayed for every step
+of every epoch because batch index, dropout counter and optimizer iteration are
+read from device counters.
+"""
+from __future__ import annotations
+
+import math
+import os
+from typing import Dict, List, Optional
+
+import numpy as np
+import torch
+
+from .. import config
+from ..models import optimizers as O
+from . import native
+from .plan import flatten_weights
+from .trainer import TrainerBase, prepare_features, prepare_targets, split_point
+
+
+def pad8(n: int) -> int:
+    return (int(n) + 7) // 8 * 8
+
+
+class NativeTrainer(TrainerBase):
+    GRAPH_CHUNK = 16
+
+    def __init__(self, model, plan, R: int = 1, batch_size: int = 32, device=None, seed: Optional[int] = None,
+                 policy: Optional[str] = None, eval_batch: int = 2048):
+        super().__init__(model, plan, R, batch_size)
+        self.C = native.require()
+        if not plan.native_ok:
+            raise ValueError(f"model is not supported by the native engine: {plan.reason}")
+        self.dev = torch.device(device) if device is not None else config.get_device()
+        if self.dev.type != "cuda":
+            raise ValueError("NativeTrainer needs a GPU device")
+        policy = policy or config.get_policy()
+        self.bf16 = policy == "mixed_bfloat16"
+        self.T = torch.bfloat16 if self.bf16 else torch.float32
+        self.seed = int(seed) if seed is not None else int(np.random.randint(1, 2**62))
+        self.eval_B = max(int(eval_batch), self.B)
+        self.stream = torch.cuda.Stream(device=self.dev)
+        self.loader = self.C.HostLoader(8 << 20, 2)
+        # optimizer
+        opt = model.optimizer
+        nat = opt.native() if opt is not None else None
+        if nat is None:
+            raise ValueError(f"optimizer {type(opt).__name__} is not supported by the native engine")
+        self.opt_id, self.opt_hp, self.nstate = nat
+        if self.loss.native is None:
+            raise ValueError(f"loss {self.loss.name} is not supported by the native engine")
+        if any(m.native is None for m in self.metrics) or len(self.metrics) > 4:
+            raise ValueError("metrics not supported by the native engine")
+
+        L = plan.layers
+        self.dims = []
+        wsh, wtsh = 0, 0
+        for s in L:
+            K, N = s.in_dim, s.units
+            d = dict(K=K, N=N, Kp=pad8(K), Np=pad8(N), wsh_off=wsh, wtsh_off=wtsh)
+            wsh += K * d["Np"]
+            wtsh += N * d["Kp"]
+            self.dims.append(d)
+        self.wsh_total, self.wtsh_total = wsh, wtsh
+        self.n = plan.n_params
+        self.Kp0 = self.dims[0]["Kp"]
+        self.ldy = 1 if self.loss.name == "sparse_categorical_crossentropy" else self.n_out
+        dev, R = self.dev, self.R
+        with torch.cuda.device(dev):
+            self.P = torch.zeros(R, self.n, dtype=torch.float32, device=dev)
+            self.S = torch.zeros(R, max(self.nstate, 1), self.n, dtype=torch.float32, device=dev)
+            if "state_init" in self.opt_hp:
+                self.S.fill_(float(self.opt_hp["state_init"]))
+            self.G = torch.zeros(R, self.n, dtype=torch.float32, device=dev)
+            self.Wsh = torch.zeros(R, 2, max(wsh, 1), dtype=self.T, device=dev)
+            self.WTsh = torch.zeros(R, 2, max(wtsh, 1), dtype=self.T, device=dev)
+            self.ctr = torch.zeros(2 + R, dtype=torch.int64, device=dev)
+            self.acc = torch.zeros(R, 6, dtype=torch.float64, device=dev)
+            self.acc_val = torch.zeros(R, 6, dtype=torch.float64, device=dev)
+            self.ws = self._alloc_workspace(self.B)
+            self.ws_eval = None
+            # empty data shard until set_data
+            self.nmax = 1
+            self.X = torch.zeros(R, 1, self.Kp0, dtype=self.T, device=dev)
+            self.Y = torch.zeros(R, 1, self.ldy, dtype=torch.float32, device=dev)
+            self.perm = torch.zeros(R, 1, dtype=torch.int32, device=dev)
+            self.ntrain = torch.zeros(R, dtype=torch.int32, device=dev)
+            self.vstart = torch.zeros(R, dtype=torch.int32, device=dev)
+            self.vcount = torch.zeros(R, dtype=torch.int32, device=dev)
+        self.ntrain_h = [0] * R
+        self.vcount_h = [0] * R
+        self.active = [True] * R
+        self.shuffle = True
+        self.exe = None
+        self.exe_eval = None
+        self._graphs: Dict[tuple, int] = {}
+        self._build_executor()
+        self.set_weights_flat(flatten_weights(model.get_weights()))
+
+    # ------------------------------------------------------------ workspaces
+    def _alloc_workspace(self, B: int) -> dict:
+        Bp = pad8(B)
+        R, dev, T = self.R, self.dev, self.T
+        layers = []
+        for d in self.dims:
+            N, Np = d["N"], d["Np"]
+            layers.append(dict(
+                Z=torch.zeros(R, B, N, dtype=torch.float32, device=dev),
+                D=torch.zeros(R, B, Np, dtype=T, device=dev),
+                DT=torch.zeros(R, N, Bp, dtype=T, device=dev),
+                dZ=torch.zeros(R, B, Np, dtype=T, device=dev),
+                dZT=torch.zeros(R, N, Bp, dtype=T, device=dev)))
+        XT = torch.zeros(R, self.Kp0, Bp, dtype=T, device=dev)
+        return dict(B=B, Bp=Bp, layers=layers, XT=XT)
+
+    def _cfg(self, ws: dict) -> dict:
+        layers = []
+        for s, d, w in zip(self.plan.layers, self.dims, ws["layers"]):
+            layers.append(dict(K=d["K"], N=d["N"], Kp=d["Kp"], Np=d["Np"], act=s.act_id,
+                               has_bias=int(s.use_bias), rate=float(s.dropout), p_off=s.p_off,
+                               Z=w["Z"].data_ptr(), D=w["D"].data_ptr(), DT=w["DT"].data_ptr(),
+                               dZ=w["dZ"].data_ptr(), dZT=w["dZT"].data_ptr(),
+                               wsh_off=d["wsh_off"], wtsh_off=d["wtsh_off"]))
+        opt = dict(opt=self.opt_id, s_plane=self.n, grad_scale=1.0)
+        opt.update({k: v for k, v in self.opt_hp.items() if k != "state_init"})
+        return dict(
+            R=self.R, B=ws["B"], Bp=ws["Bp"], bf16=int(self.bf16), seed=self.seed,
+            force_cfg=int(os.environ.get("ELEPHAS_AMD_GEMM_CFG", "-1")),
+            layers=layers,
+            X=self.X.data_ptr(), sX=self.nmax * self.Kp0, ldx=self.Kp0,
+            Y=self.Y.data_ptr(), sY=self.nmax * self.ldy, ldy=self.ldy,
+            perm=self.perm.data_ptr(), sPerm=self.nmax,
+            ntrain=self.ntrain.data_ptr(), vstart=self.vstart.data_ptr(), vcount=self.vcount.data_ptr(),
+            XT=ws["XT"].data_ptr(),
+            P=self.P.data_ptr(), sP=self.n, nparams=self.n,
+            G=self.G.data_ptr(), sG=self.n,
+            S=self.S.data_ptr(), sS=self.S.shape[1] * self.n,
+            Wsh=self.Wsh.data_ptr(), sWsh=2 * self.Wsh.shape[2], wsh_par=self.Wsh.shape[2],
+            WTsh=self.WTsh.data_ptr(), sWTsh=2 * self.WTsh.shape[2], wtsh_par=self.WTsh.shape[2],
+            opt=opt, loss=self.loss.native, metrics=[m.native for m in self.metrics],
+            acc=self.acc.data_ptr(), acc_stride=6, ctr=self.ctr.data_ptr())
+
+    def _build_executor(self):
+        if self.exe is not None:
+            self.exe.destroy_graphs()
+        self._graphs = {}
+        self.exe = self.C.Executor(self._cfg(self.ws))
+
+    def _eval_exe(self):
+        if self.exe_eval is None:
+            with torch.cuda.device(self.dev):
+                self.ws_eval = self._alloc_workspace(self.eval_B)
+            self.exe_eval = self.C.Executor(self._cfg(self.ws_eval))
+        return self.exe_eval
+
+    @property
+    def s(self) -> int:
+        return int(self.stream.cuda_stream)
+
+    def _enter(self):
+        self.stream.wait_stream(torch.cuda.current_stream(self.dev))
+
+    def _exit(self):
+        torch.cuda.current_stream(self.dev).wait_stream(self.stream)
+
+    # ---------------------------------------------------------------- weights
+    def set_weights_flat(self, flat):
+        flat = np.asarray(flat, np.float32)
+        if flat.ndim == 1:
+            flat = np.broadcast_to(flat, (self.R, flat.size))
+        self._enter()
+        with torch.cuda.stream(self.stream):
+            self.P.copy_(torch.from_numpy(np.array(flat, dtype=np.float32, copy=True)).to(self.dev))
+            self.exe.refresh_shadows(True, self.s)
+        self._exit()
+
+    def sync_shadows(self):
+        """Rebuild the weight images after P was modified on device (all-reduce, PS pull)."""
+        with torch.cuda.stream(self.stream):
+            self.exe.refresh_shadows(True, self.s)
+
+    def get_weights_flat(self):
+        return self._host(self.P)
+
+    def reset_optimizer_state(self):
+        with torch.cuda.stream(self.stream):
+            self.S.fill_(float(self.opt_hp.get("state_init", 0.0)))
+            self.ctr.zero_()
+            self.exe.refresh_shadows(True, self.s)
+
+    def iterations(self) -> np.ndarray:
+        return self._host(self.ctr[2:])
+
+    # ------------------------------------------------------------------- data
+    def _upload_rows(self, dst: torch.Tensor, x: np.ndarray):
+        """Stream host rows into a device tensor through the native pinned loader."""
+        x = np.ascontiguousarray(x, dtype=np.float32)
+        n, k = x.shape
+        if n == 0:
+            return
+        if dst.dtype == torch.float32 and dst.shape[-1] >= k:
+            self.loader.upload_rows(x.ctypes.data, k * 4, dst.data_ptr(), dst.stride(0) * 4, n, k * 4, self.s)
+            torch.cuda.current_stream(self.dev)  # keep ordering explicit: loader ran on self.stream
+        else:
+            stage = torch.empty(n, k, dtype=torch.float32, device=self.dev)
+            self.loader.upload_rows(x.ctypes.data, k * 4, stage.data_ptr(), k * 4, n, k * 4, self.s)
+            dst[:n, :k].copy_(stage)
+        self.stream.synchronize()  # host buffer must stay alive until the DMA is done
+
+    def set_data(self, xs, ys, validation_split=0.0, active=None, shuffle=True):
+        assert len(xs) == self.R and len(ys) == self.R
+        xs = [prepare_features(x, self.in_dim) if len(x) else np.zeros((0, self.in_dim), np.float32) for x in xs]
+        ys = [prepare_targets(y, self.n_out, self.loss) if len(y) else np.zeros((0, self.ldy), np.float32)
+              for y in ys]
+        nmax = max(1, max(len(x) for x in xs))
+        self._enter()
+        with torch.cuda.stream(self.stream):
+            if nmax != self.nmax:
+                self.nmax = nmax
+                self.X = torch.zeros(self.R, nmax, self.Kp0, dtype=self.T, device=self.dev)
+                self.Y = torch.zeros(self.R, nmax, self.ldy, dtype=torch.float32, device=self.dev)
+                self.perm = torch.zeros(self.R, nmax, dtype=torch.int32, device=self.dev)
+                rebuild = True
+            else:
+                self.X.zero_()
+                self.Y.zero_()
+                rebuild = False
+            for r in range(self.R):
+                self._upload_rows(self.X[r], xs[r])
+                self._upload_rows(self.Y[r], ys[r])
+        self.active = [True if active is None else bool(active[r]) for r in range(self.R)]
+        nt, vs, vc = [], [], []
+        for r in range(self.R):
+            n = len(xs[r])
+            sp = split_point(n, validation_split)
+            nt.append(sp if self.active[r] else 0)
+            vs.append(sp)
+            vc.append(n - sp if self.active[r] else 0)
+        self.ntrain_h, self.vcount_h = nt, vc
+        with torch.cuda.stream(self.stream):
+            self.ntrain.copy_(torch.tensor(nt, dtype=torch.int32))
+            self.vstart.copy_(torch.tensor(vs, dtype=torch.int32))
+            self.vcount.copy_(torch.tensor(vc, dtype=torch.int32))
+        self.shuffle = shuffle
+        if rebuild:
+            self._build_executor()
+            if self.exe_eval is not None:
+                self.exe_eval = None
+        self._exit()
+
+    def _new_perm(self, gen: Optional[torch.Generator] = None):
+        R, nmax = self.R, self.nmax
+        with torch.cuda.stream(self.stream):
+            if self.shuffle:
+                keys = torch.rand(R, nmax, device=self.dev, generator=gen)
+                nt = self.ntrain.to(torch.int64).view(R, 1)
+                ar = torch.arange(nmax, device=self.dev).view(1, nmax)
+                keys = torch.where(ar < nt, keys, torch.full_like(keys, 2.0))
+                self.perm.copy_(torch.argsort(keys, dim=1).to(torch.int32))
+            else:
+                self.perm.copy_(torch.arange(nmax, device=self.dev, dtype=torch.int32).expand(R, nmax))
+
+    # ------------------------------------------------------------------ train
+    def steps_per_epoch(self) -> int:
+        return int(math.ceil(max(self.ntrain_h) / self.B)) if max(self.ntrain_h) > 0 else 0
+
+    def _graph(self, nsteps: int, mode: int) -> int:
+        key = (nsteps, mode)
+        if key not in self._graphs:
+            self._graphs[key] = self.exe.capture(nsteps, mode, self.s)
+        return self._graphs[key]
+
+    def run_steps(self, nsteps: int, use_graph: bool = True):
+        """Launch nsteps fused training steps on self.stream (asynchronous)."""
+        if nsteps <= 0:
+            return
+        if not use_graph:
+            for _ in range(nsteps):
+                self.exe.train_step(self.s)
+            return
+        g = min(self.GRAPH_CHUNK, nsteps)
+        full, rest = divmod(nsteps, g)
+        if full:
+            self.exe.replay_n(self._graph(g, 0), full, self.s)
+        if rest:
+            self.exe.replay_n(self._graph(1, 0), rest, self.s)
+
+    def run_steps_allreduce(self, nsteps: int, allreduce, use_graph: bool = True):
+        """Per-step gradient all-reduce path: [fwd+bwd -> G] -> allreduce(G) -> [apply]."""
+        for _ in range(nsteps):
+            if use_graph:
+                self.exe.replay(self._graph(1, 1), self.s)
+            else:
+                self.exe.forward_backward(self.s)
+            with torch.cuda.stream(self.stream):
+                allreduce(self.G)
+            if use_graph:
+                self.exe.replay(self._graph(1, 2), self.s)
+            else:
+                self.exe.apply(self.s)
+
+    def begin_epoch(self, gen=None):
+        with torch.cuda.stream(self.stream):
+            self.exe.reset_epoch(self.s)
+            self.acc.zero_()
+        self._new_perm(gen)
+
+    def set_grad_scale(self, scale: float):
+        if abs(scale - 1.0) > 0:
+            cfg = self._cfg(self.ws)
+            cfg["opt"]["grad_scale"] = float(scale)
+            self.exe.destroy_graphs()
+            self._graphs = {}
+            self.exe = self.C.Executor(cfg)
+
+    def fit(self, epochs, verbose=0, allreduce=None):
+        hist = [dict() if self.active[r] else None for r in range(self.R)]
+        self._enter()
+        steps = self.steps_per_epoch()
+        for epoch in range(int(epochs)):
+            self.begin_epoch()
+            if allreduce is None:
+                self.run_steps(steps)
+            else:
+                self.run_steps_allreduce(steps, allreduce)
+            sums = self._host(self.acc) if steps > 0 else np.zeros((self.R, 6))
+            val = self._val_sums() if max(self.vcount_h) > 0 else None
+            for r in range(self.R):
+                if not self.active[r]:
+                    continue
+                h = self._history_from_sums(sums[r]) if self.ntrain_h[r] > 0 else {}
+                if val is not None and self.vcount_h[r] > 0:
+                    h.update(self._history_from_sums(val[r], "val_"))
+                for k, v in h.items():
+                    hist[r].setdefault(k, []).append(v)
+                if verbose:
+                    self.print_epoch(epoch, epochs, h, r)
+        self._exit()
+        return hist
+
+    def _val_sums(self):
+        """Validation tails of the training shards (per replica), dropout off."""
+        exe = self._eval_exe()
+        with torch.cuda.stream(self.stream):
+            self.acc_val.zero_()
+            nch = int(math.ceil(max(self.vcount_h) / self.eval_B))
+            src = dict(X=self.X.data_ptr(), sX=self.nmax * self.Kp0, ldx=self.Kp0,
+                       Y=self.Y.data_ptr(), sY=self.nmax * self.ldy, ldy=self.ldy,
+                       vstart=self.vstart.data_ptr(), vcount=self.vcount.data_ptr(),
+                       acc=self.acc_val.data_ptr())
+            for c in range(nch):
+                exe.eval_chunk(c, src, self.s)
+        return self._host(self.acc_val)
+
+    def _host(self, t: torch.Tensor) -> np.ndarray:
+        """Device -> host read ordered after everything queued on the executor stream."""
+        self.stream.synchronize()
+        return t.detach().cpu().numpy().copy()
+
+    # ------------------------------------------------------------------- eval
+    def _eval_src(self, x: np.ndarray, y: Optional[np.ndarray], want_pred: bool):
+        n = len(x)
+        with torch.cuda.stream(self.stream):
+            Xe = torch.zeros(1, max(n, 1), self.Kp0, dtype=self.T, device=self.dev)
+            self._upload_rows(Xe[0], x)
+            src = dict(X=Xe.data_ptr(), sX=0, ldx=self.Kp0,
+                       vstart=torch.zeros(self.R, dtype=torch.int32, device=self.dev),
+                       vcount=torch.full((self.R,), n, dtype=torch.int32, device=self.dev))
+            keep = [Xe, src["vstart"], src["vcount"]]
+            src["vstart"], src["vcount"] = src["vstart"].data_ptr(), src["vcount"].data_ptr()
+            if y is not None:
+                Ye = torch.zeros(1, max(n, 1), self.ldy, dtype=torch.float32, device=self.dev)
+                self._upload_rows(Ye[0], y)
+                keep.append(Ye)
+                src.update(Y=Ye.data_ptr(), sY=0, ldy=self.ldy)
+            if want_pred:
+                pred = torch.zeros(self.R, max(n, 1), self.n_out, dtype=torch.float32, device=self.dev)
+                keep.append(pred)
+                src.update(pred=pred.data_ptr(), sPred=max(n, 1) * self.n_out, ldp=self.n_out)
+        return src, keep
+
+    def evaluate_sums(self, x, y, batch_size=None, r: int = 0) -> np.ndarray:
+        x = prepare_features(x, self.in_dim)
+        y = prepare_targets(y, self.n_out, self.loss)
+        self._enter()
+        exe = self._eval_exe()
+        src, keep = self._eval_src(x, y, False)
+        with torch.cuda.stream(self.stream):
+            self.acc_val.zero_()
+            src["acc"] = self.acc_val.data_ptr()
+            for c in range(int(math.ceil(len(x) / self.eval_B))):
+                exe.eval_chunk(c, src, self.s)
+        out = self._host(self.acc_val[r])
+        self._exit()
+        return out
+
+    def evaluate(self, x, y, batch_size=None, r: int = 0):
+        s = self.evaluate_sums(x, y, batch_size, r)
+        cnt = max(s[1], 1.0)
+        return [float(s[0] / cnt)] + [float(s[2 + i] / cnt) for i in range(len(self.metrics))]
+
+    def predict(self, x, batch_size=None, r: int = 0):
+        x = prepare_features(x, self.in_dim)
+        if len(x) == 0:
+            return np.zeros((0, self.n_out), np.float32)
+        self._enter()
+        exe = self._eval_exe()
+        src, keep = self._eval_src(x, None, True)
+        with torch.cuda.stream(self.stream):
+            for c in range(int(math.ceil(len(x) / self.eval_B))):
+                exe.eval_chunk(c, src, self.s)
+        out = self._host(keep[-1][r, :len(x)])
+        self._exit()
+        return out
+
+    def train_on_batch(self, x, y, r: int = 0):
+        """One optimizer step on exactly this batch (rows in order), keras semantics."""
+        x = prepare_features(x, self.in_dim)
+        self.set_data([x] * self.R, [y] * self.R, 0.0, shuffle=False)
+        self.begin_epoch()
+        self.run_steps(1, use_graph=False)
+        s = self._host(self.acc[r])
+        cnt = max(s[1], 1.0)
+        return [float(s[0] / cnt)] + [float(s[2 + i] / cnt) for i in range(len(self.metrics))]
+
+    def launch_count(self) -> int:
+        return self.exe.launches_per_step()

@@ -1,0 +1,204 @@
+"""Reference training engine on torch tensors (CPU, or GPU for custom ops).
+
+This is the semantic anchor of the framework: it runs
+the model's layer chain op by op with autograd, applies the Keras 2.10
+optimizer rules from ``models/optimizers.py`` and the loss/metric formulas from
+``models/losses.py``/``metrics.py``.  It handles everything the native
+executor does not fuse (custom activation/loss/metric callables, stacked
+activations, Adadelta/Nadam, ...), and the HIP kernels are tested against it.
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from ..models import activations as A
+from ..models import optimizers as O
+from ..models.layers import Activation, Dense, Dropout, Flatten
+from .plan import flatten_weights, unflatten_weights
+from .trainer import TrainerBase, prepare_features, prepare_targets, split_point
+
+
+class TorchTrainer(TrainerBase):
+    def __init__(self, model, plan, R: int = 1, batch_size: int = 32, device=None, seed: Optional[int] = None):
+        super().__init__(model, plan, R, batch_size)
+        self.device = torch.device(device) if device is not None else torch.device("cpu")
+        self.like = model.get_weights()
+        self.gen = torch.Generator(device="cpu")
+        self.gen.manual_seed(int(seed) if seed is not None else int(np.random.randint(0, 2**31 - 1)))
+        self.opts = [O.clone(model.optimizer) for _ in range(self.R)]
+        self.params: List[List[torch.Tensor]] = []
+        self.state = []
+        self.iters = [0] * self.R
+        self.set_weights_flat(flatten_weights(self.like))
+        self.xs = self.ys = None
+
+    # ---------------------------------------------------------------- weights
+    def set_weights_flat(self, flat):
+        flat = np.asarray(flat, np.float32)
+        if flat.ndim == 1:
+            flat = np.broadcast_to(flat, (self.R, flat.size))
+        self.params = []
+        for r in range(self.R):
+            ws = unflatten_weights(flat[r], self.like)
+            self.params.append([torch.tensor(w, device=self.device) for w in ws])
+        self.state = [opt.init_state(p) for opt, p in zip(self.opts, self.params)]
+
+    def get_weights_flat(self):
+        return np.stack([np.concatenate([p.detach().cpu().numpy().reshape(-1) for p in ps]) for ps in self.params])
+
+    def reset_optimizer_state(self):
+        self.state = [opt.init_state(p) for opt, p in zip(self.opts, self.params)]
+        self.iters = [0] * self.R
+
+    # ---------------------------------------------------------------- forward
+    def forward(self, r: int, x: torch.Tensor, training: bool):
+        h = x
+        wi = 0
+        pre, last_act = None, None
+        ps = self.params[r]
+        for op in self.plan.ops:
+            if isinstance(op, Dense):
+                h = h @ ps[wi]
+                wi += 1
+                if op.use_bias:
+                    h = h + ps[wi]
+                    wi += 1
+                pre, last_act = h, op.activation
+                h = op.activation(h)
+            elif isinstance(op, Activation):
+                pre, last_act = h, op.activation
+                h = op.activation(h)
+            elif isinstance(op, Dropout):
+                if training and op.rate > 0:
+                    keep = torch.rand(h.shape, generator=self.gen).to(h.device) >= op.rate
+                    h = h * keep.to(h.dtype) / (1.0 - op.rate)
+            elif isinstance(op, Flatten):
+                h = h.reshape(h.shape[0], -1)
+        logits = None
+        if last_act is A.softmax and self.loss.name in ("categorical_crossentropy", "sparse_categorical_crossentropy"):
+            logits = pre
+        elif last_act is A.sigmoid and self.loss.name == "binary_crossentropy":
+            logits = pre
+        return h, logits
+
+    def _metric_logits(self, m, last_logits):
+        return last_logits
+
+    def _loss_and_metrics(self, y, pred, logits):
+        per = self.loss(y, pred, logits)
+        if per.dim() > 1:
+            per = per.reshape(per.shape[0], -1).mean(-1)
+        mvals = []
+        for m in self.metrics:
+            v = m(y, pred, logits)
+            if v.dim() > 1:
+                v = v.reshape(v.shape[0], -1).mean(-1)
+            mvals.append(v)
+        return per, mvals
+
+    # ------------------------------------------------------------------- data
+    def set_data(self, xs, ys, validation_split=0.0, active=None, shuffle=True):
+        assert len(xs) == self.R and len(ys) == self.R
+        self.xs, self.ys, self.split, self.active = [], [], [], []
+        self.shuffle = shuffle
+        for r in range(self.R):
+            x = prepare_features(xs[r], self.in_dim) if len(xs[r]) else np.zeros((0, self.in_dim), np.float32)
+            y = prepare_targets(ys[r], self.n_out, self.loss) if len(ys[r]) else np.zeros((0, 1), np.float32)
+            self.xs.append(torch.tensor(x, device=self.device))
+            self.ys.append(torch.tensor(y, device=self.device))
+            self.split.append(split_point(len(x), validation_split))
+            self.active.append(True if active is None else bool(active[r]))
+
+    # ------------------------------------------------------------------ train
+    def train_batch(self, r: int, xb: torch.Tensor, yb: torch.Tensor):
+        ps = self.params[r]
+        for p in ps:
+            p.requires_grad_(True)
+        pred, logits = self.forward(r, xb, True)
+        per, mvals = self._loss_and_metrics(yb, pred, logits)
+        loss = per.mean()
+        grads = torch.autograd.grad(loss, ps, allow_unused=True)
+        grads = [g if g is not None else torch.zeros_like(p) for g, p in zip(grads, ps)]
+        for p in ps:
+            p.requires_grad_(False)
+        self.opts[r].apply_torch(ps, grads, self.state[r], self.iters[r])
+        self.iters[r] += 1
+        return per.detach(), [m.detach() for m in mvals]
+
+    def fit(self, epochs, verbose=0):
+        hist = [dict() if self.active[r] else None for r in range(self.R)]
+        for epoch in range(int(epochs)):
+            for r in range(self.R):
+                if not self.active[r]:
+                    continue
+                n = self.split[r]
+                idx = torch.randperm(n, generator=self.gen) if self.shuffle else torch.arange(n)
+                sums = np.zeros(2 + len(self.metrics))
+                for b0 in range(0, n, self.B):
+                    bi = idx[b0:b0 + self.B].to(self.device)
+                    per, mvals = self.train_batch(r, self.xs[r][bi], self.ys[r][bi])
+                    sums[0] += float(per.sum())
+                    sums[1] += per.numel()
+                    for i, v in enumerate(mvals):
+                        sums[2 + i] += float(v.sum())
+                h = self._history_from_sums(sums) if n > 0 else {}
+                nval = len(self.xs[r]) - n
+                if nval > 0:
+                    ev = self._eval_tensors(r, self.xs[r][n:], self.ys[r][n:])
+                    h.update(self._history_from_sums(ev, "val_"))
+                for k, v in h.items():
+                    hist[r].setdefault(k, []).append(v)
+                if verbose:
+                    self.print_epoch(epoch, epochs, h, r)
+        return hist
+
+    def train_steps(self, nsteps: int):
+        """Bench helper: nsteps batches per replica over the (shuffled) shard."""
+        for r in range(self.R):
+            n = self.split[r]
+            for s in range(nsteps):
+                b0 = (s * self.B) % max(n, 1)
+                self.train_batch(r, self.xs[r][b0:b0 + self.B], self.ys[r][b0:b0 + self.B])
+
+    # ------------------------------------------------------------------- eval
+    @torch.no_grad()
+    def _eval_tensors(self, r, x, y, bs=None):
+        bs = bs or max(self.B, 1024)
+        sums = np.zeros(2 + len(self.metrics))
+        for b0 in range(0, len(x), bs):
+            pred, logits = self.forward(r, x[b0:b0 + bs], False)
+            per, mvals = self._loss_and_metrics(y[b0:b0 + bs], pred, logits)
+            sums[0] += float(per.sum())
+            sums[1] += per.numel()
+            for i, v in enumerate(mvals):
+                sums[2 + i] += float(v.sum())
+        return sums
+
+    def evaluate_sums(self, x, y, batch_size=None, r: int = 0) -> np.ndarray:
+        xt = torch.tensor(prepare_features(x, self.in_dim), device=self.device)
+        yt = torch.tensor(prepare_targets(y, self.n_out, self.loss), device=self.device)
+        return self._eval_tensors(r, xt, yt, batch_size)
+
+    def evaluate(self, x, y, batch_size=None, r: int = 0):
+        s = self.evaluate_sums(x, y, batch_size, r)
+        cnt = max(s[1], 1.0)
+        return [float(s[0] / cnt)] + [float(v / cnt) for v in s[2:]]
+
+    @torch.no_grad()
+    def predict(self, x, batch_size=None, r: int = 0):
+        xt = torch.tensor(prepare_features(x, self.in_dim), device=self.device)
+        bs = batch_size or 4096
+        outs = [self.forward(r, xt[b0:b0 + bs], False)[0] for b0 in range(0, len(xt), bs)]
+        if not outs:
+            return np.zeros((0, self.n_out), np.float32)
+        return torch.cat(outs).float().cpu().numpy()
+
+    def train_on_batch(self, x, y, r: int = 0):
+        xt = torch.tensor(prepare_features(x, self.in_dim), device=self.device)
+        yt = torch.tensor(prepare_targets(y, self.n_out, self.loss), device=self.device)
+        per, mvals = self.train_batch(r, xt, yt)
+        return [float(per.mean())] + [float(v.mean()) for v in mvals]

@@ -1,0 +1,118 @@
+"""Process-group helpers: one process per GPU, torch.distributed over RCCL.
+
+``init_from_env`` joins the job started by ``torchrun`` (RANK / WORLD_SIZE /
+MASTER_ADDR / MASTER_PORT); backend 'nccl' (= RCCL over xGMI on ROCm) when the
+process owns a GPU, 'gloo' on CPU.  Without a launcher everything degrades to
+rank 0 of a world of 1, so the same SparkModel code runs single-process.
+
+Collectives used by the engine (SURVEY.md §2.6 call sites C1-C13):
+  * ``all_reduce_sum_``  -- sync averaging of the flat parameter/delta vector
+                            (C2/C3) and of evaluation sums (C10)
+  * ``broadcast_``       -- initial weights / final PS weights (C1/C8)
+  * ``all_gather_object``-- histories, predictions (C9/C11)
+"""
+from __future__ import annotations
+
+import os
+from datetime import timedelta
+from typing import Any, List
+
+import torch
+import torch.distributed as dist
+
+
+def is_initialized() -> bool:
+    return dist.is_available() and dist.is_initialized()
+
+
+def init_from_env(backend: str = None, timeout_s: int = 600) -> bool:
+    """Join a torchrun-style job if the environment describes one."""
+    if is_initialized():
+        return True
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    if ws <= 1:
+        return False
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    if backend is None:
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+    if backend == "nccl":
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
+    dist.init_process_group(backend=backend, timeout=timedelta(seconds=timeout_s))
+    return True
+
+
+def rank() -> int:
+    return dist.get_rank() if is_initialized() else 0
+
+
+def world_size() -> int:
+    return dist.get_world_size() if is_initialized() else 1
+
+
+def backend() -> str:
+    return dist.get_backend() if is_initialized() else "none"
+
+
+def _comm_device() -> torch.device:
+    if is_initialized() and dist.get_backend() == "nccl":
+        return torch.device("cuda", torch.cuda.current_device())
+    return torch.device("cpu")
+
+
+def all_reduce_sum_(t: torch.Tensor) -> torch.Tensor:
+    """In-place sum across ranks; moves through the backend's device if needed."""
+    if not is_initialized() or world_size() == 1:
+        return t
+    dev = _comm_device()
+    if t.device == dev or (t.device.type == dev.type == "cuda"):
+        dist.all_reduce(t)
+        return t
+    tmp = t.to(dev)
+    dist.all_reduce(tmp)
+    t.copy_(tmp.to(t.device))
+    return t
+
+
+def broadcast_(t: torch.Tensor, src: int = 0) -> torch.Tensor:
+    if not is_initialized() or world_size() == 1:
+        return t
+    dev = _comm_device()
+    if t.device.type == dev.type:
+        dist.broadcast(t, src)
+        return t
+    tmp = t.to(dev)
+    dist.broadcast(tmp, src)
+    t.copy_(tmp.to(t.device))
+    return t
+
+
+def all_gather_object(obj: Any) -> List[Any]:
+    if not is_initialized() or world_size() == 1:
+        return [obj]
+    out = [None] * world_size()
+    dist.all_gather_object(out, obj)
+    return out
+
+
+def broadcast_object(obj: Any, src: int = 0) -> Any:
+    if not is_initialized() or world_size() == 1:
+        return obj
+    box = [obj]
+    dist.broadcast_object_list(box, src)
+    return box[0]
+
+
+def barrier() -> None:
+    if is_initialized() and world_size() > 1:
+        if dist.get_backend() == "nccl":
+            dist.barrier(device_ids=[torch.cuda.current_device()])
+        else:
+            dist.barrier()
+
+
+def block_range(n: int, r: int = None, w: int = None):
+    """Contiguous block [lo, hi) of n items owned by rank r of w."""
+    r = rank() if r is None else r
+    w = world_size() if w is None else w
+    return r * n // w, (r + 1) * n // w

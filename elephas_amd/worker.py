@@ -1,0 +1,191 @@
+"""Workers: what runs per partition (reference elephas/worker.py:11-131).
+
+``SparkWorker``           synchronous mode: train the partition for all epochs
+                          with a fresh optimizer, report (weights_before -
+                          weights_after, history); skip when n <= batch_size.
+``AsynchronousSparkWorker`` asynchronous / hogwild: per epoch (or per batch)
+                          pull -> train -> push delta to the parameter server.
+
+Both keep the reference's per-partition ``train(iterator)`` generator API.  On
+the MI355X path ``SparkWorker.train_partitions`` trains ALL of a rank's
+partitions at once as replicas of one native executor (every grouped launch
+covers every local worker), and the async worker moves parameters
+device-to-device with the DeviceClient (no host round trip).
+"""
+from __future__ import annotations
+
+import math
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+from .models import optimizers as O
+from .models import model_from_json
+from .ops.plan import flatten_weights, unflatten_weights
+from .parameter.client import BaseParameterClient, DeviceClient
+from .utils.functional_utils import subtract_params
+
+
+def _value(parameters):
+    return parameters.value if hasattr(parameters, "value") else parameters
+
+
+def partition_to_numpy(data):
+    items = list(data)
+    if not items:
+        return np.zeros((0,)), np.zeros((0,))
+    x = np.asarray([xy[0] for xy in items])
+    y = np.asarray([xy[1] for xy in items])
+    return x, y
+
+
+def _build_model(json_str, custom_objects, optimizer, loss, metrics, weights):
+    model = model_from_json(json_str, custom_objects)
+    opt = O.deserialize(optimizer, custom_objects) if isinstance(optimizer, dict) else O.clone(optimizer)
+    model.compile(optimizer=opt, loss=loss, metrics=metrics, custom_objects=custom_objects)
+    model.set_weights(weights)
+    return model
+
+
+class SparkWorker:
+    """Synchronous worker (reference worker.py:11-49)."""
+
+    def __init__(self, json, parameters, train_config, master_optimizer, master_loss, master_metrics,
+                 custom_objects):
+        self.json = json
+        self.parameters = parameters
+        self.train_config = dict(train_config)
+        self.master_optimizer = master_optimizer
+        self.master_loss = master_loss
+        self.master_metrics = master_metrics
+        self.custom_objects = custom_objects or {}
+        self.model = None
+
+    def _cfg(self):
+        tc = self.train_config
+        return (int(tc.get("batch_size", 32)), int(tc.get("epochs", 1)), int(tc.get("verbose", 0)),
+                float(tc.get("validation_split", 0.0)), bool(tc.get("shuffle", True)))
+
+    def train(self, data_iterator):
+        """Single-partition generator, as the reference's mapPartitions function."""
+        self.model = _build_model(self.json, self.custom_objects, self.master_optimizer, self.master_loss,
+                                  self.master_metrics, _value(self.parameters))
+        x_train, y_train = partition_to_numpy(data_iterator)
+        bs, epochs, verbose, vs, shuffle = self._cfg()
+        before = self.model.get_weights()
+        history = None
+        if x_train.shape[0] > bs:
+            h = self.model.fit(x_train, y_train, batch_size=bs, epochs=epochs, verbose=verbose,
+                               validation_split=vs, shuffle=shuffle)
+            history = h.history
+        after = self.model.get_weights()
+        yield [subtract_params(before, after), history]
+
+    def train_partitions(self, partitions: Sequence[list], engine: Optional[str] = None, seed: Optional[int] = None):
+        """Batched: train every partition as one replica of a shared executor.
+
+        Returns (trainer, histories, active); the trainer's per-replica weights
+        are the workers' final weights (theta_i); delta_i = theta_0 - theta_i.
+        """
+        from .ops.engine import make_trainer
+        self.model = _build_model(self.json, self.custom_objects, self.master_optimizer, self.master_loss,
+                                  self.master_metrics, _value(self.parameters))
+        bs, epochs, verbose, vs, shuffle = self._cfg()
+        xs, ys = [], []
+        for p in partitions:
+            x, y = partition_to_numpy(p)
+            xs.append(x)
+            ys.append(y)
+        active = [len(x) > bs for x in xs]   # reference worker.py:41 (`if n > batch_size: fit`)
+        R = max(1, len(partitions))
+        trainer = make_trainer(self.model, R, bs, engine=engine, seed=seed)
+        if not partitions:
+            return trainer, [], []
+        trainer.set_data(xs, ys, vs, active=active, shuffle=shuffle)
+        hist = trainer.fit(epochs, verbose=verbose) if any(active) else [None] * R
+        hist = [h if a else None for h, a in zip(hist, active)]
+        return trainer, hist, active
+
+
+class AsynchronousSparkWorker:
+    """Asynchronous / hogwild worker (reference worker.py:52-131)."""
+
+    def __init__(self, json, parameters, client, train_config, frequency, master_optimizer, master_loss,
+                 master_metrics, custom_objects):
+        if isinstance(client, BaseParameterClient):
+            self.client = client
+        else:
+            self.client = BaseParameterClient.get_client(client)
+        self.train_config = dict(train_config)
+        self.frequency = frequency
+        self.master_optimizer = master_optimizer
+        self.master_loss = master_loss
+        self.master_metrics = master_metrics
+        self.json = json
+        self.parameters = parameters
+        self.custom_objects = custom_objects or {}
+        self.model = None
+
+    def train(self, data_iterator):
+        x_train, y_train = partition_to_numpy(data_iterator)
+        if x_train.size == 0:
+            return
+        self.model = _build_model(self.json, self.custom_objects, self.master_optimizer, self.master_loss,
+                                  self.master_metrics, _value(self.parameters))
+        epochs = int(self.train_config.get("epochs", 1))
+        batch_size = int(self.train_config.get("batch_size", 32))
+        verbose = int(self.train_config.get("verbose", 0))
+        vs = float(self.train_config.get("validation_split", 0.0))
+        if self.frequency not in ("epoch", "batch"):
+            raise ValueError("frequency parameter can be `epoch` or `batch, got {}".format(self.frequency))
+        from .ops.engine import make_trainer
+        trainer = make_trainer(self.model, 1, batch_size)
+        native = hasattr(trainer, "exe") and isinstance(self.client, DeviceClient)
+        if self.frequency == "epoch":
+            trainer.set_data([x_train], [y_train], vs, shuffle=True)
+            for _ in range(epochs):
+                self._pull(trainer, native)
+                if x_train.shape[0] > batch_size:
+                    trainer.fit(1, verbose=verbose)
+                self._push(trainer, native)
+        else:
+            if x_train.shape[0] > batch_size:
+                trainer.set_data([x_train], [y_train], 0.0, shuffle=False)
+                nb = int(math.ceil(x_train.shape[0] / batch_size))
+                for _ in range(epochs):
+                    if native:
+                        trainer.begin_epoch()
+                    for b in range(nb):
+                        self._pull(trainer, native)
+                        if native:
+                            trainer.run_steps(1, use_graph=True)
+                        else:
+                            trainer.train_batch(0, trainer.xs[0][b * batch_size:(b + 1) * batch_size],
+                                                trainer.ys[0][b * batch_size:(b + 1) * batch_size])
+                        self._push(trainer, native)
+        self.model.set_weights(unflatten_weights(trainer.get_weights_flat()[0], self.model.get_weights()))
+        yield []
+
+    # --- parameter-server exchange
+    def _pull(self, trainer, native):
+        if native:
+            import torch
+            with torch.cuda.stream(trainer.stream):
+                self.client.pull_into(trainer.P.data_ptr(), trainer.s)
+                trainer.sync_shadows()
+                self._before = trainer.P.clone()
+        else:
+            w = self.client.get_parameters()
+            self._before = flatten_weights(list(w))
+            trainer.set_weights_flat(self._before)
+
+    def _push(self, trainer, native):
+        if native:
+            import torch
+            with torch.cuda.stream(trainer.stream):
+                delta = self._before - trainer.P   # theta_pulled - theta_after
+                self.client.push_from(delta.data_ptr(), trainer.s)
+        else:
+            after = trainer.get_weights_flat()[0]
+            delta = self._before - after
+            self.client.update_parameters(unflatten_weights(delta, self.model.get_weights()))

@@ -1,0 +1,180 @@
+"""Native HIP executor vs. the torch fp32 reference (GPU only).
+
+The native engine must reproduce the reference engine's math: with dropout off
+and shuffling off, one optimizer step on the same batch gives the same weights
+(fp32 policy: exact-f32 MFMA, tight tolerance; bf16 policy: loose tolerance).
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _mlp(in_dim, hidden, out, act="relu", out_act="softmax", dropout=0.0, bias=True):
+    from elephas_amd.models import Sequential, Dense, Dropout, Activation
+    m = Sequential()
+    m.add(Dense(hidden[0], input_dim=in_dim, use_bias=bias))
+    m.add(Activation(act))
+    if dropout:
+        m.add(Dropout(dropout))
+    for h in hidden[1:]:
+        m.add(Dense(h, activation=act, use_bias=bias))
+        if dropout:
+            m.add(Dropout(dropout))
+    m.add(Dense(out, activation=out_act))
+    return m
+
+
+def _data(n, d, k, seed=0, onehot=True):
+    rng = np.random.default_rng(seed)
+    x = rng.normal(size=(n, d)).astype(np.float32)
+    y = rng.integers(0, k, n)
+    if onehot:
+        y = np.eye(k, dtype=np.float32)[y]
+    return x, y
+
+
+def _engines(model, B, policy):
+    from elephas_amd import config
+    from elephas_amd.ops.plan import build_plan
+    from elephas_amd.ops.native_engine import NativeTrainer
+    from elephas_amd.ops.torch_engine import TorchTrainer
+    plan = build_plan(model)
+    config.set_policy(policy)
+    nat = NativeTrainer(model, plan, 1, B, torch.device("cuda"))
+    ref = TorchTrainer(model, plan, 1, B, torch.device("cuda"))
+    return nat, ref
+
+
+@pytest.mark.parametrize("policy,tol", [("float32", 2e-5), ("mixed_bfloat16", 3e-2)])
+@pytest.mark.parametrize("opt", ["sgd", "sgd_mom", "adam", "rmsprop", "adagrad"])
+def test_one_step_matches_reference(policy, tol, opt):
+    from elephas_amd.models import optimizers as O
+    model = _mlp(784, [128, 128], 10)
+    optim = {"sgd": O.SGD(0.1), "sgd_mom": O.SGD(0.01, momentum=0.9, nesterov=True, decay=1e-6),
+             "adam": O.Adam(0.001), "rmsprop": O.RMSprop(), "adagrad": O.Adagrad(0.01)}[opt]
+    model.compile(optim, "categorical_crossentropy", ["acc"])
+    x, y = _data(64, 784, 10)
+    nat, ref = _engines(model, 64, policy)
+    for t in (nat, ref):
+        t.set_data([x], [y], 0.0, shuffle=False)
+        t.fit(2)
+    wn, wr = nat.get_weights_flat()[0], ref.get_weights_flat()[0]
+    w0 = np.concatenate([w.reshape(-1) for w in model.get_weights()])
+    step = np.abs(wr - w0).max()
+    assert step > 0
+    if policy == "float32":
+        err = np.abs(wn - wr).max() / step
+        assert err < 1e-3, err
+    else:
+        # bf16 operands: adaptive optimizers amplify near-zero-gradient noise
+        # (Adam step ~ lr*sign(g)), so compare on average
+        err = np.abs(wn - wr).mean() / np.abs(wr - w0).mean()
+        assert err < 0.15, err
+
+
+@pytest.mark.parametrize("loss,act,metrics,out", [
+    ("categorical_crossentropy", "softmax", ["acc"], 10),
+    ("binary_crossentropy", "sigmoid", ["acc"], 1),
+    ("mse", "linear", ["mae", "mean_absolute_percentage_error"], 1),
+    ("mae", "linear", ["mse"], 3),
+    ("sparse_categorical_crossentropy", "softmax", ["acc"], 7),
+    ("logcosh", "tanh", ["mae"], 4),
+    ("kld", "softmax", ["acc"], 5),
+])
+def test_evaluate_predict_match_reference(loss, act, metrics, out):
+    from elephas_amd import config
+    model = _mlp(20, [32, 16], out, act="tanh", out_act=act)
+    model.compile("sgd", loss, metrics)
+    x, y = _data(300, 20, out, seed=1, onehot=loss != "sparse_categorical_crossentropy")
+    if loss in ("mse", "mae", "logcosh"):
+        y = np.random.default_rng(2).normal(size=(300, out)).astype(np.float32)
+    if loss == "binary_crossentropy":
+        y = (np.random.default_rng(3).random((300, 1)) > 0.5).astype(np.float32)
+    nat, ref = _engines(model, 32, "float32")
+    en, er = nat.evaluate(x, y), ref.evaluate(x, y)
+    assert np.allclose(en, er, rtol=1e-4, atol=1e-5), (en, er)
+    pn, pr = nat.predict(x), ref.predict(x)
+    assert np.allclose(pn, pr, rtol=1e-4, atol=1e-5)
+
+
+def test_wide_output_loss_rows_path():
+    # 200 classes > GEMM tile width: wave-per-row loss kernel
+    model = _mlp(64, [96], 200)
+    model.compile("sgd", "categorical_crossentropy", ["acc"])
+    x, y = _data(128, 64, 200)
+    nat, ref = _engines(model, 64, "float32")
+    for t in (nat, ref):
+        t.set_data([x], [y], 0.0, shuffle=False)
+        t.fit(1)
+    assert np.allclose(nat.get_weights_flat(), ref.get_weights_flat(), atol=1e-5)
+    assert np.allclose(nat.evaluate(x, y), ref.evaluate(x, y), rtol=1e-4)
+
+
+def test_partial_batches_and_validation():
+    model = _mlp(30, [40], 4, dropout=0.0)
+    model.compile("sgd", "categorical_crossentropy", ["acc"])
+    x, y = _data(203, 30, 4)
+    nat, ref = _engines(model, 32, "float32")
+    hs = []
+    for t in (nat, ref):
+        t.set_data([x], [y], 0.2, shuffle=False)
+        hs.append(t.fit(3)[0])
+    assert np.allclose(nat.get_weights_flat(), ref.get_weights_flat(), atol=2e-5)
+    for k in ("loss", "acc", "val_loss", "val_acc"):
+        assert np.allclose(hs[0][k], hs[1][k], rtol=1e-4, atol=1e-5), k
+
+
+def test_replicas_independent_and_dropout_trains():
+    # R replicas with different shards == R separate single-replica runs (no dropout)
+    from elephas_amd import config
+    from elephas_amd.ops.plan import build_plan
+    from elephas_amd.ops.native_engine import NativeTrainer
+    config.set_policy("float32")
+    model = _mlp(50, [64], 6)
+    model.compile("adam", "categorical_crossentropy", ["acc"])
+    plan = build_plan(model)
+    shards = [_data(n, 50, 6, seed=n) for n in (100, 37, 64, 10)]
+    multi = NativeTrainer(model, plan, 4, 16, torch.device("cuda"))
+    multi.set_data([s[0] for s in shards], [s[1] for s in shards], 0.0, shuffle=False,
+                   active=[True, True, True, False])
+    multi.fit(2)
+    wm = multi.get_weights_flat()
+    w0 = np.concatenate([w.reshape(-1) for w in model.get_weights()])
+    assert np.array_equal(wm[3], w0)  # inactive replica untouched
+    for r in range(3):
+        single = NativeTrainer(model, plan, 1, 16, torch.device("cuda"))
+        single.set_data([shards[r][0]], [shards[r][1]], 0.0, shuffle=False)
+        single.fit(2)
+        assert np.allclose(single.get_weights_flat()[0], wm[r], atol=1e-6)
+    # dropout + shuffle + bf16: loss goes down
+    config.set_policy("mixed_bfloat16")
+    model2 = _mlp(784, [128, 128], 10, dropout=0.2)
+    model2.compile("sgd", "categorical_crossentropy", ["acc"])
+    from elephas_amd.models.datasets import synthetic_classification
+    xx, yy = synthetic_classification(4096, 784, 10, seed=5)
+    t = NativeTrainer(model2, build_plan(model2), 1, 64, torch.device("cuda"))
+    t.set_data([xx / 10], [np.eye(10, dtype=np.float32)[yy]], 0.1)
+    h = t.fit(3)[0]
+    assert h["loss"][-1] < h["loss"][0]
+    config.set_policy("float32")
+
+
+def test_graph_replay_equals_eager():
+    from elephas_amd import config
+    from elephas_amd.ops.plan import build_plan
+    from elephas_amd.ops.native_engine import NativeTrainer
+    config.set_policy("float32")
+    model = _mlp(100, [64, 32], 5, dropout=0.3)
+    model.compile("sgd", "categorical_crossentropy")
+    x, y = _data(640, 100, 5)
+    ws = []
+    for graph in (True, False):
+        t = NativeTrainer(model, build_plan(model), 2, 32, torch.device("cuda"), seed=7)
+        t.set_data([x, x], [y, y], 0.0, shuffle=False)
+        t.begin_epoch()
+        t.run_steps(20, use_graph=graph)
+        ws.append(t.get_weights_flat())
+    assert np.array_equal(ws[0], ws[1])
+    assert not np.array_equal(ws[0][0], ws[0][1])  # replicas draw different dropout masks
