@@ -27,6 +27,12 @@ class DenseVector(Vector):
     def toArray(self) -> np.ndarray:
         return self.array
 
+    def __getattr__(self, item):
+        # pyspark's DenseVector delegates unknown attributes (shape, ...) to the array
+        if item == "array" or item.startswith("__"):
+            raise AttributeError(item)
+        return getattr(self.array, item)
+
     @property
     def values(self):
         return self.array
@@ -140,7 +146,7 @@ class LabeledPoint:
     __slots__ = ("label", "features")
 
     def __init__(self, label, features):
-        self.label = float(label)
+        self.label = float(np.asarray(label, dtype=np.float64).reshape(-1)[0])
         self.features = features if isinstance(features, Vector) else DenseVector(features)
 
     def __repr__(self):

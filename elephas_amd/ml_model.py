@@ -1,0 +1,214 @@
+"""Spark-ML Estimator / Transformer (reference elephas/ml_model.py:25-269).
+
+``ElephasEstimator._fit`` turns a DataFrame into a (features, label) RDD,
+compiles the Keras-compatible model from its JSON config and trains it with a
+``SparkModel`` (MI355X native engine); the result is an ``ElephasTransformer``
+holding the trained weights.  ``_transform`` appends a prediction column:
+``DoubleType`` for regression losses, ``ArrayType(DoubleType)`` of class
+probabilities for classification (reference :243-249).  ``inference_batch_size``
+chunks the prediction exactly like the reference's ``batched_prediction``
+(chunked and unchunked results are identical: tests/test_ml_model.py:345-354).
+"""
+from __future__ import annotations
+
+import copy
+import json
+import warnings
+from typing import Optional
+
+import numpy as np
+
+from .data.ml import (DefaultParamsReadable, DefaultParamsWritable, Estimator, HasFeaturesCol, HasLabelCol,
+                      HasOutputCol, Model, keyword_only)
+from .data.sql import ArrayType, DataFrame, DoubleType, Row, SparkSession, StructField, StructType
+from .io import h5lite
+from .ml.adapter import df_to_simple_rdd
+from .ml.params import *  # noqa: F401,F403
+from .ml.params import (HasBatchSize, HasCategoricalLabels, HasCustomObjects, HasEpochs, HasFrequency,
+                        HasInferenceBatchSize, HasKerasModelConfig, HasKerasOptimizerConfig, HasLoss, HasMetrics,
+                        HasMode, HasNumberOfClasses, HasNumberOfWorkers, HasValidationSplit, HasVerbosity)
+from .mllib.adapter import from_vector
+from .models import model_from_json
+from .models import optimizers as O
+from .spark_model import SparkModel
+from .utils.model_utils import LossModelTypeMapper, ModelType, ModelTypeEncoder, as_enum
+
+
+def _attr_json(raw):
+    if isinstance(raw, (bytes, np.bytes_)):
+        return bytes(raw).decode("utf8")
+    return str(raw)
+
+
+class ElephasEstimator(Estimator, HasCategoricalLabels, HasValidationSplit, HasKerasModelConfig, HasFeaturesCol,
+                       HasLabelCol, HasMode, HasEpochs, HasBatchSize, HasFrequency, HasVerbosity, HasNumberOfClasses,
+                       HasNumberOfWorkers, HasOutputCol, HasLoss, HasMetrics, HasKerasOptimizerConfig,
+                       HasCustomObjects, DefaultParamsReadable, DefaultParamsWritable):
+    """Spark-ML Estimator wrapping a Keras-compatible model config."""
+
+    @keyword_only
+    def __init__(self, **kwargs):
+        super(ElephasEstimator, self).__init__()
+        self._defaultParamMap[self.outputCol] = "prediction"
+        self.set_params(**kwargs)
+
+    def get_config(self):
+        return {"keras_model_config": self.get_keras_model_config(),
+                "mode": self.get_mode(),
+                "frequency": self.get_frequency(),
+                "num_workers": self.get_num_workers(),
+                "categorical": self.get_categorical_labels(),
+                "loss": self.get_loss(),
+                "metrics": self.get_metrics(),
+                "validation_split": self.get_validation_split(),
+                "featuresCol": self.getFeaturesCol(),
+                "labelCol": self.getLabelCol(),
+                "epochs": self.get_epochs(),
+                "batch_size": self.get_batch_size(),
+                "verbose": self.get_verbosity(),
+                "nb_classes": self.get_nb_classes(),
+                "outputCol": self.getOutputCol()}
+
+    def save(self, file_name: str):
+        """HDF5 holding only the ``distributed_config`` attribute (reference :61-70)."""
+        f = h5lite.File(file_name, mode="w")
+        f.attrs["distributed_config"] = json.dumps({
+            "class_name": self.__class__.__name__,
+            "config": self.get_config()
+        }).encode("utf8")
+        f.flush()
+        f.close()
+
+    @keyword_only
+    def set_params(self, **kwargs):
+        return self._set(**kwargs)
+
+    def get_model(self):
+        return model_from_json(self.get_keras_model_config(), self.get_custom_objects())
+
+    def _fit(self, df: DataFrame):
+        simple_rdd = df_to_simple_rdd(df, categorical=self.get_categorical_labels(), nb_classes=self.get_nb_classes(),
+                                      features_col=self.getFeaturesCol(), label_col=self.getLabelCol())
+        simple_rdd = simple_rdd.repartition(self.get_num_workers())
+        keras_model = model_from_json(self.get_keras_model_config(), self.get_custom_objects())
+        metrics = self.get_metrics()
+        loss = self.get_loss()
+        optimizer = O.get(self.get_optimizer_config())
+        keras_model.compile(loss=loss, optimizer=optimizer, metrics=metrics,
+                            custom_objects=self.get_custom_objects())
+        spark_model = SparkModel(model=keras_model, mode=self.get_mode(), frequency=self.get_frequency(),
+                                 num_workers=self.get_num_workers(), custom_objects=self.get_custom_objects())
+        spark_model.fit(simple_rdd, epochs=self.get_epochs(), batch_size=self.get_batch_size(),
+                        verbose=self.get_verbosity(), validation_split=self.get_validation_split())
+        model_weights = spark_model.master_network.get_weights()
+        return ElephasTransformer(labelCol=self.getLabelCol(),
+                                  outputCol=self.getOutputCol(),
+                                  featuresCol=self.getFeaturesCol(),
+                                  keras_model_config=spark_model.master_network.to_json(),
+                                  weights=model_weights,
+                                  custom_objects=self.get_custom_objects(),
+                                  model_type=LossModelTypeMapper().get_model_type(loss),
+                                  history=spark_model.training_histories)
+
+    def setFeaturesCol(self, value):
+        warnings.warn("setFeaturesCol is deprecated in Spark 3.0.x+ - please supply featuresCol in the constructor "
+                      "i.e; ElephasEstimator(featuresCol='foo')", DeprecationWarning)
+        return self._set(featuresCol=value)
+
+    def setLabelCol(self, value):
+        warnings.warn("setLabelCol is deprecated in Spark 3.0.x+ - please supply labelCol in the constructor i.e;"
+                      " ElephasEstimator(labelCol='foo')", DeprecationWarning)
+        return self._set(labelCol=value)
+
+    def setOutputCol(self, value):
+        warnings.warn("setOutputCol is deprecated in Spark 3.0.x+ - please supply outputCol in the constructor i.e;"
+                      " ElephasEstimator(outputCol='foo')", DeprecationWarning)
+        return self._set(outputCol=value)
+
+
+def load_ml_estimator(file_name: str) -> ElephasEstimator:
+    f = h5lite.File(file_name, mode="r")
+    elephas_conf = json.loads(_attr_json(f.attrs.get("distributed_config")))
+    config = elephas_conf.get("config")
+    return ElephasEstimator(**config)
+
+
+class ElephasTransformer(Model, HasKerasModelConfig, HasLabelCol, HasOutputCol, HasFeaturesCol, HasCustomObjects,
+                         HasInferenceBatchSize):
+    """Spark-ML Model holding a trained network; ``transform`` appends predictions."""
+
+    @keyword_only
+    def __init__(self, **kwargs):
+        super(ElephasTransformer, self).__init__()
+        if "weights" in kwargs.keys():
+            self.weights = kwargs.pop("weights")
+        if "model_type" in kwargs.keys():
+            self.model_type = kwargs.pop("model_type")
+        self._history = kwargs.pop("history", [])
+        self.set_params(**kwargs)
+
+    @property
+    def history(self):
+        return self._history
+
+    @keyword_only
+    def set_params(self, **kwargs):
+        return self._set(**kwargs)
+
+    def get_config(self):
+        return {"keras_model_config": self.get_keras_model_config(),
+                "labelCol": self.getLabelCol(),
+                "featuresCol": self.getFeaturesCol(),
+                "outputCol": self.getOutputCol(),
+                "weights": [weight.tolist() for weight in getattr(self, "weights", [])],
+                "model_type": getattr(self, "model_type", None)}
+
+    def save(self, file_name: str):
+        f = h5lite.File(file_name, mode="w")
+        f.attrs["distributed_config"] = json.dumps({
+            "class_name": self.__class__.__name__,
+            "config": self.get_config()
+        }, cls=ModelTypeEncoder).encode("utf8")
+        f.flush()
+        f.close()
+
+    def get_model(self):
+        return model_from_json(self.get_keras_model_config(), self.get_custom_objects())
+
+    def _predict_fn(self):
+        model = self.get_model()
+        model.set_weights(self.weights)
+        return model.predict
+
+    def _transform(self, df: DataFrame) -> DataFrame:
+        output_col = self.getOutputCol()
+        new_schema = copy.deepcopy(df.schema)
+        rows = df.collect()
+        predict = self._predict_fn()
+        features_col = self.getFeaturesCol()
+        feats = np.array([from_vector(r[features_col]) for r in rows]) if rows else np.zeros((0, 1))
+        bs = self.get_inference_batch_size()
+        if len(feats) == 0:
+            preds = np.zeros((0, 1))
+        elif bs is not None and bs > 0:
+            preds = np.vstack([predict(feats[i:i + bs]) for i in range(0, len(feats), bs)])
+        else:
+            preds = predict(feats)
+        if getattr(self, "model_type", None) == ModelType.REGRESSION:
+            values = [float(np.asarray(p).reshape(-1)[0]) for p in preds]
+            output_col_field = StructField(output_col, DoubleType(), True)
+        else:
+            values = [np.asarray(p, dtype=np.float64).tolist() for p in preds]
+            output_col_field = StructField(output_col, ArrayType(DoubleType()), True)
+        new_schema.add(output_col_field)
+        names = new_schema.names
+        out_rows = [Row.from_pairs(names, tuple(r) + (v,)) for r, v in zip(rows, values)]
+        return DataFrame(out_rows, new_schema, df._nparts)
+
+
+def load_ml_transformer(file_name: str) -> ElephasTransformer:
+    f = h5lite.File(file_name, mode="r")
+    elephas_conf = json.loads(_attr_json(f.attrs.get("distributed_config")), object_hook=as_enum)
+    config = elephas_conf.get("config")
+    config["weights"] = [np.array(weight) for weight in config["weights"]]
+    return ElephasTransformer(**config)

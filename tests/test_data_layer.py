@@ -1,0 +1,102 @@
+"""Spark-local semantics of the host data layer (reference tests/utils/test_rdd_utils.py,
+tests/ml/test_adapter.py) plus RDD/DataFrame/ML-pipeline behaviour the API relies on."""
+import numpy as np
+import pytest
+
+from elephas_amd.data import LabeledPoint, SparkContext, SparkSession, Vectors
+from elephas_amd.ml import adapter
+from elephas_amd.utils import rdd_utils
+
+
+def test_to_simple_rdd(spark_context):
+    rdd = rdd_utils.to_simple_rdd(spark_context, np.ones((5, 10)), np.ones((5,)))
+    assert rdd.count() == 5
+    first = rdd.first()
+    assert first[0].shape == (10,) and first[1] == 1.0
+
+
+def test_labeled_point_roundtrips(spark_context):
+    features = np.ones((2, 10))
+    cat = np.asarray([[0, 0, 1.0], [0, 1.0, 0]])
+    lp = rdd_utils.to_labeled_point(spark_context, features, cat, True)
+    assert lp.count() == 2 and lp.first().label == 2.0 and lp.first().features.shape == (10,)
+    x, y = rdd_utils.from_labeled_point(lp, True, 3)
+    assert x.shape == features.shape and y.shape == cat.shape
+    lp2 = rdd_utils.to_labeled_point(spark_context, features, np.asarray([2.0, 1.0]), False)
+    x, y = rdd_utils.from_labeled_point(lp2, False, None)
+    assert y.shape == (2,)
+    r = rdd_utils.lp_to_simple_rdd(lp, categorical=True)  # nb_classes inferred
+    assert r.first()[1].shape == (3,)
+    r2 = rdd_utils.lp_to_simple_rdd(lp2, categorical=False, nb_classes=3)
+    assert r2.first()[1] == 2.0
+
+
+def test_encode_label():
+    e = rdd_utils.encode_label(3, 10)
+    assert len(e) == 10 and e[3] == 1 and e.sum() == 1
+
+
+def test_data_frame_adapters(spark_context):
+    features = np.ones((2, 10))
+    df = adapter.to_data_frame(spark_context, features, np.asarray([[2.0], [1.0]]), categorical=False)
+    assert df.count() == 2
+    df2 = adapter.to_data_frame(spark_context, features, np.asarray([[0, 0, 1.0], [0, 1.0, 0]]), categorical=True)
+    x, y = adapter.from_data_frame(df2, categorical=True, nb_classes=3)
+    assert x.shape == (2, 10) and y.shape == (2, 3)
+    rdd = adapter.df_to_simple_rdd(adapter.to_data_frame(spark_context, features, np.asarray([2.0, 1.0])), False)
+    assert rdd.count() == 2
+    renamed = df.withColumnRenamed("features", "f").withColumnRenamed("label", "l")
+    r = adapter.df_to_simple_rdd(renamed, False, features_col="f", label_col="l")
+    assert r.first()[0].shape == (10,)
+
+
+def test_parallelize_contiguous_and_repartition(spark_context):
+    sc = SparkContext(master="local[4]")
+    rdd = sc.parallelize(range(10))
+    assert rdd.getNumPartitions() == 4
+    assert rdd.glom().collect() == [[0, 1], [2, 3, 4], [5, 6], [7, 8, 9]]
+    rp = rdd.repartition(3)
+    assert rp.getNumPartitions() == 3 and sorted(rp.collect()) == list(range(10))
+    z = rdd.zipWithIndex().collect()
+    assert z[3] == (3, 3)
+    assert rdd.map(lambda v: v * 2).reduce(lambda a, b: a + b) == 90
+    assert rdd.sortBy(lambda v: -v).collect()[0] == 9
+    assert sc.parallelize([1, 2]).zip(sc.parallelize([3, 4])).collect() == [(1, 3), (2, 4)]
+    assert rdd.mapPartitions(lambda it: [sum(it)]).collect() == [1, 9, 11, 24]
+
+
+def test_dataframe_sql_and_show(spark_context, capsys):
+    spark = SparkSession.builder.getOrCreate()
+    df = spark.createDataFrame([(Vectors.dense([1.0, 2.0]), "a"), (Vectors.dense([3.0, 4.0]), "b")],
+                               ["features", "category"])
+    df.createOrReplaceTempView("t1")
+    s = spark.sql("SELECT features AS f, category as c from t1")
+    assert s.columns == ["f", "c"] and s.first().c == "a"
+    df.show()
+    assert "category" in capsys.readouterr().out
+    assert df.select("category").distinct().count() == 2
+
+
+def test_string_indexer_and_scaler_pipeline(spark_context):
+    from elephas_amd.data.ml import Pipeline, StandardScaler, StringIndexer, PipelineModel
+    spark = SparkSession.builder.getOrCreate()
+    rows = [(Vectors.dense([float(i), 2.0 * i]), c) for i, c in enumerate("aabbbc")]
+    df = spark.createDataFrame(rows, ["features", "category"])
+    si = StringIndexer(inputCol="category", outputCol="idx")
+    sc_ = StandardScaler(inputCol="features", outputCol="scaled", withStd=True, withMean=True)
+    pm = Pipeline(stages=[si, sc_]).fit(df)
+    out = pm.transform(df)
+    idx = [r.idx for r in out.collect()]
+    assert idx == [1.0, 1.0, 0.0, 0.0, 0.0, 2.0]     # frequency-descending
+    sc_vals = np.stack([r.scaled.toArray() for r in out.collect()])
+    assert np.allclose(sc_vals.mean(0), 0) and np.allclose(sc_vals.std(0, ddof=1), 1)
+
+
+def test_metrics():
+    from elephas_amd.data.ml import MulticlassMetrics, RegressionMetrics
+    sc = SparkContext.getOrCreate()
+    m = MulticlassMetrics(sc.parallelize([(0.0, 0.0), (1.0, 1.0), (1.0, 0.0), (2.0, 2.0)]))
+    assert m.accuracy == 0.75 and m.precision(1.0) == 0.5 and m.recall(0.0) == 0.5
+    assert 0 < m.weightedPrecision <= 1
+    r = RegressionMetrics(sc.parallelize([(1.0, 1.0), (2.0, 2.5), (3.0, 2.5)]))
+    assert abs(r.meanAbsoluteError - 1 / 3) < 1e-9 and r.r2 < 1
