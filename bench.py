@@ -1,0 +1,241 @@
+#!/usr/bin/env python
+"""Headline benchmark: MNIST-MLP 784-128-128-10 synchronous data-parallel
+training throughput (samples/sec, whole node) on MI355X.
+
+Config (BASELINE.json / BASELINE.md, reference examples/mnist_mlp_spark_synchronous.py):
+  model 784-128(relu, dropout .2)-128(relu, dropout .2)-10(softmax), SGD lr .1,
+  categorical cross-entropy + accuracy, batch 64 per worker, validation_split .1,
+  8 workers per node-slot (the reference's ``local[8]``), mode='synchronous'.
+Data: synthetic MNIST-shaped (784 features in [0,1], 10 one-hot classes),
+  random-init weights (no network access for datasets/checkpoints).
+
+Semantics (``--granularity``):
+  fit   (default, the reference's 'synchronous' mode, spark_model.py:217-228):
+        every worker trains its own partition; the timed region is K optimizer
+        steps of EVERY worker followed by the synchronous parameter averaging
+        (device replica sum + RCCL all-reduce over xGMI + divide).
+  batch (per-step sync DP): the gradients of all workers are averaged every step
+        (local batch 64*workers, RCCL all-reduce of the flat gradient per step).
+A "step" = one optimizer step on one batch of 64 rows by every worker; epoch
+rollover (reshuffle) happens inside the timed region as it does in fit().
+
+Usage: python bench.py --gpus N --steps K --warmup W   (N>1 via torch.distributed.run)
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+MODELS = {
+    # name: (layers, dropout, classes, rows per worker, lr)
+    "mnist": ([784, 128, 128], 0.2, 10, 7500, 0.1),
+    "otto": ([93, 512, 512, 512], 0.5, 9, 7735, 0.01),
+    "wide": ([4096, 4096, 4096], 0.0, 1000, 4096, 0.01),
+}
+
+
+def build_model(name):
+    from elephas_amd.models import Sequential, Dense, Activation, Dropout
+    from elephas_amd.models.optimizers import SGD
+    dims, drop, classes, _, lr = MODELS[name]
+    m = Sequential()
+    m.add(Dense(dims[1], input_dim=dims[0]))
+    m.add(Activation("relu"))
+    if drop:
+        m.add(Dropout(drop))
+    for d in dims[2:]:
+        m.add(Dense(d))
+        m.add(Activation("relu"))
+        if drop:
+            m.add(Dropout(drop))
+    m.add(Dense(classes))
+    m.add(Activation("softmax"))
+    m.compile(SGD(learning_rate=lr), "categorical_crossentropy", ["acc"])
+    return m
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=500)
+    ap.add_argument("--warmup", type=int, default=50)
+    ap.add_argument("--model", default="mnist", choices=sorted(MODELS))
+    ap.add_argument("--workers-per-gpu", type=int, default=8)
+    ap.add_argument("--batch", type=int, default=64)
+    ap.add_argument("--policy", default="mixed_bfloat16", choices=["mixed_bfloat16", "float32"])
+    ap.add_argument("--granularity", default="fit", choices=["fit", "batch"])
+    ap.add_argument("--validation-split", type=float, default=0.1)
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--dropout", type=float, default=None, help="override the model's dropout (diagnostics)")
+    ap.add_argument("--out", default=None, help="also append the JSON line to this file")
+    args = ap.parse_args()
+
+    import torch
+    from elephas_amd import config
+    from elephas_amd.parallel import dist
+    from elephas_amd.ops.plan import build_plan
+
+    dist.init_from_env()
+    rank, world = dist.rank(), dist.world_size()
+    if world != args.gpus and rank == 0:
+        print(f"warning: --gpus {args.gpus} but world size {world}", file=sys.stderr)
+    gpu = torch.cuda.is_available()
+    dev = torch.device("cuda", torch.cuda.current_device()) if gpu else torch.device("cpu")
+    config.set_device(dev)
+    config.set_policy(args.policy)
+    np.random.seed(1234 + rank)
+
+    if args.dropout is not None:
+        d, dr, c, r, lr = MODELS[args.model]
+        MODELS[args.model] = (d, args.dropout, c, r, lr)
+    model = build_model(args.model)
+    plan = build_plan(model)
+    dims, drop, classes, rows, _ = MODELS[args.model]
+    W = args.workers_per_gpu
+    B = args.batch
+    batch_mode = args.granularity == "batch"
+    R = 1 if batch_mode else W
+    Bloc = B * W if batch_mode else B
+
+    # synthetic MNIST-shaped shards, one per worker
+    rng = np.random.default_rng(1000 + rank)
+    centers = rng.normal(0, 1, size=(classes, dims[0])).astype(np.float32)
+    xs, ys = [], []
+    for r in range(R):
+        n = rows * (W if batch_mode else 1)
+        y = rng.integers(0, classes, n)
+        x = centers[y] + rng.normal(0, 2.0, size=(n, dims[0])).astype(np.float32)
+        x = (x - x.min()) / (x.max() - x.min())
+        xs.append(x.astype(np.float32))
+        ys.append(np.eye(classes, dtype=np.float32)[y])
+
+    if gpu:
+        from elephas_amd.ops.native_engine import NativeTrainer
+        t = NativeTrainer(model, plan, R, Bloc, dev, seed=4321 + rank)
+    else:
+        from elephas_amd.ops.torch_engine import TorchTrainer
+        t = TorchTrainer(model, plan, R, Bloc, dev, seed=4321 + rank)
+    t.set_data(xs, ys, args.validation_split, shuffle=True)
+    ntrain = t.ntrain_h[0] if gpu else t.split[0]
+    steps_per_epoch = int(math.ceil(ntrain / Bloc))
+
+    def allreduce_grads(G):
+        dist.all_reduce_sum_(G)
+
+    if batch_mode and gpu and world > 1:
+        t.set_grad_scale(1.0 / world)   # mean of the ranks' gradients after the sum all-reduce
+
+    state = {"step_in_epoch": steps_per_epoch, "rows": 0}
+
+    def run(k):
+        """k optimizer steps with epoch rollover; returns rows processed per worker."""
+        done_rows = 0
+        while k > 0:
+            if state["step_in_epoch"] >= steps_per_epoch:
+                if gpu:
+                    t.begin_epoch()
+                state["step_in_epoch"] = 0
+            n = min(k, steps_per_epoch - state["step_in_epoch"])
+            if gpu:
+                if batch_mode and world > 1:
+                    t.run_steps_allreduce(n, allreduce_grads, use_graph=not args.no_graph)
+                else:
+                    t.run_steps(n, use_graph=not args.no_graph)
+            else:
+                t.train_steps(n)
+            s0 = state["step_in_epoch"]
+            for s in range(s0, s0 + n):
+                done_rows += min(Bloc, ntrain - s * Bloc)
+            state["step_in_epoch"] += n
+            k -= n
+        return done_rows
+
+    def average():
+        """Reference sync mode: theta <- mean_i theta_i over all workers of the job."""
+        if batch_mode:
+            return
+        if gpu:
+            with torch.cuda.stream(t.stream):
+                tot = t.P.sum(0)
+                dist.all_reduce_sum_(tot)
+                t.P.copy_((tot / float(R * world)).expand_as(t.P))
+                t.sync_shadows()
+        else:
+            w = t.get_weights_flat().sum(0)
+            tt = torch.from_numpy(w)
+            dist.all_reduce_sum_(tt)
+            t.set_weights_flat(tt.numpy() / float(R * world))
+
+    def sync():
+        if gpu:
+            t.stream.synchronize()
+            torch.cuda.synchronize()
+        dist.barrier()
+
+    # warmup (includes hipGraph capture)
+    run(args.warmup)
+    average()
+    sync()
+    t0 = time.perf_counter()
+    rows_done = run(args.steps)
+    average()
+    sync()
+    dt = time.perf_counter() - t0
+
+    dts = dist.all_gather_object(dt)
+    dt_max = max(dts)
+    samples = rows_done * (R if not batch_mode else 1) * world
+    if rank == 0:
+        value = samples / dt_max
+        launches = t.launch_count() if gpu else None
+        line = {
+            "metric": "samples/sec (whole node) MNIST-MLP 784-128-128-10 sync DP at 1/2/4/8 MI355X",
+            "value": round(value, 1),
+            "unit": "samples/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(dt_max / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16" if args.policy == "mixed_bfloat16" else "fp32",
+            "data": "synthetic MNIST-shaped (784 features, 10 classes), random-init weights",
+            "config": {
+                "model": {"mnist": "MNIST-MLP 784-128-128-10", "otto": "Otto-MLP 93-512-512-512-9",
+                          "wide": "Wide-MLP 4096-4096-4096-1000"}[args.model],
+                "global_batch": B * W * world,
+                "seq_len": None,
+                "parallelism": f"dp{world}",
+                "workers_per_gpu": W,
+                "batch_per_worker": B,
+                "sync": "reference (one-shot averaging per fit)" if not batch_mode else "per-step gradient all-reduce",
+                "optimizer": "SGD(lr=%g)" % MODELS[args.model][4],
+                "engine": "native HIP executor + hipGraph" if gpu else "torch CPU reference",
+                "launches_per_step": launches,
+                "policy": args.policy,
+            },
+        }
+        s = json.dumps(line)
+        print(s, flush=True)
+        if args.out:
+            with open(args.out, "a") as f:
+                f.write(s + "\n")
+    if dist.is_initialized():
+        dist.barrier()
+        import torch.distributed as tdist
+        tdist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -93,6 +93,7 @@ struct GroupArgs {
   int advance;              // this launch ends the step: last block advances counters
   int adv_R; int adv_B;     // replicas / batch for the advance
   const int* adv_ntrain;
+  long long* stamps;        // diagnostics: [block][16] s_memrealtime stamps (null = off)
 };
 
 constexpr int MAX_SEG = 16;

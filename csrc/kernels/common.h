@@ -33,11 +33,12 @@ template <> __device__ __forceinline__ __bf16 from_f<__bf16>(float v) { return (
 // --------------------------------------------------------------- Philox ----
 // Philox4x32-10 (Salmon et al. 2011). Counter-based: mask(element) is a pure
 // function of (seed, replica, layer, iteration, element) -> bwd regenerates it.
-__device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint2 k) {
+template <int ROUNDS>
+__device__ __forceinline__ uint4 philox4x32_r(uint4 c, uint2 k) {
   const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u;
   const uint32_t W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
 #pragma unroll
-  for (int i = 0; i < 10; ++i) {
+  for (int i = 0; i < ROUNDS; ++i) {
     uint32_t hi0 = __umulhi(M0, c.x), lo0 = M0 * c.x;
     uint32_t hi1 = __umulhi(M1, c.z), lo1 = M1 * c.z;
     c = make_uint4(hi1 ^ c.y ^ k.x, lo1, hi0 ^ c.w ^ k.y, lo0);
@@ -47,14 +48,18 @@ __device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint2 k) {
 }
 
 // Uniform in [0,1) for one element; keep iff u >= rate (tf.nn.dropout semantics).
-__device__ __forceinline__ float dropout_uniform(uint64_t seed, int replica, int layer,
-                                                 long long iter, long long elem) {
-  uint4 c = make_uint4((uint32_t)elem, (uint32_t)(elem >> 32),
-                       (uint32_t)iter, ((uint32_t)(iter >> 32) & 0xFFFFu) ^
-                                           ((uint32_t)layer << 16) ^ ((uint32_t)replica << 24));
+// Dropout uniforms for the 4 columns [4*cg, 4*cg+4) of row `row`: one
+// Philox4x32-7 call (counter = (cg, row, iter, layer/replica), key = seed ^
+// replica) yields all four. Forward and backward regenerate the same mask
+// from the same counters, so no mask is stored.
+__device__ __forceinline__ float4 dropout_u4(uint64_t seed, int replica, int layer, long long iter,
+                                             long long row, long long cg) {
+  uint4 c = make_uint4((uint32_t)cg, (uint32_t)row, (uint32_t)iter,
+                       ((uint32_t)(iter >> 32) & 0xFFFFu) ^ ((uint32_t)layer << 16) ^ ((uint32_t)replica << 24));
   uint2 k = make_uint2((uint32_t)seed ^ (uint32_t)replica * 0x85EBCA6Bu, (uint32_t)(seed >> 32));
-  uint4 r = philox4x32_10(c, k);
-  return (float)(r.x >> 8) * (1.0f / 16777216.0f);
+  const uint4 r = philox4x32_r<7>(c, k);
+  constexpr float s = 1.0f / 16777216.0f;
+  return make_float4((float)(r.x >> 8) * s, (float)(r.y >> 8) * s, (float)(r.z >> 8) * s, (float)(r.w >> 8) * s);
 }
 
 // ----------------------------------------------------------- activations ----
@@ -106,25 +111,45 @@ __device__ __forceinline__ float act_grad(int act, float z) {
 
 // --------------------------------------------------------- row reductions ----
 // W = 1: a single thread owns the row.  W = 64: a whole wave owns the row.
+// lane-group reductions. W == 4 (quads) uses DPP quad_perm moves (no LDS
+// round trip); wider groups use ds_bpermute via __shfl_xor.
+__device__ __forceinline__ float quad_xor1(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float quad_xor2(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, false));
+}
+__device__ __forceinline__ int quad_xor1(int v) { return __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, false); }
+__device__ __forceinline__ int quad_xor2(int v) { return __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, false); }
+
 template <int W> __device__ __forceinline__ float row_sum(float v) {
   if constexpr (W == 1) return v;
+  if constexpr (W == 4) { v += quad_xor1(v); return v + quad_xor2(v); }
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  for (int o = W / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, W);
   return v;
 }
 template <int W> __device__ __forceinline__ float row_max(float v) {
   if constexpr (W == 1) return v;
+  if constexpr (W == 4) { v = fmaxf(v, quad_xor1(v)); return fmaxf(v, quad_xor2(v)); }
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  for (int o = W / 2; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, W));
   return v;
 }
 // argmax with first-index tie-break (np.argmax / tf.argmax semantics)
 template <int W> __device__ __forceinline__ void row_argmax(float& v, int& i) {
   if constexpr (W == 1) return;
+  if constexpr (W == 4) {
+    float ov = quad_xor1(v); int oi = quad_xor1(i);
+    if (ov > v || (ov == v && oi < i)) { v = ov; i = oi; }
+    ov = quad_xor2(v); oi = quad_xor2(i);
+    if (ov > v || (ov == v && oi < i)) { v = ov; i = oi; }
+    return;
+  }
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    float ov = __shfl_xor(v, o, 64);
-    int oi = __shfl_xor(i, o, 64);
+  for (int o = W / 2; o > 0; o >>= 1) {
+    float ov = __shfl_xor(v, o, W);
+    int oi = __shfl_xor(i, o, W);
     if (ov > v || (ov == v && oi < i)) { v = ov; i = oi; }
   }
 }
@@ -202,24 +227,38 @@ __device__ __forceinline__ bool loss_is_mean_over_last_axis(int loss) {
 // Generic per-row evaluation. Element j is visited by lane `lane` for j = lane, lane+W, ...
 //   dz_out(j, v) is called with the per-row gradient dL_row/dz_j (if want_grad)
 //   p_out(j, v) is called with the prediction p_j (if want_pred)
-template <int W, typename ZF, typename YF, typename GF, typename PF>
-__device__ void row_loss(int lane, int N, int act, int loss, const int* metrics, int nmetrics,
-                         ZF zat, YF yat, bool want_grad, GF dz_out, bool want_pred, PF p_out,
+// Column loop over this lane's elements j = lane, lane+W, ... (< N).
+// NV > 0: fully unrolled over NV register slots (i_ is a compile-time index, so
+// accessors may index register arrays); NV == 0: runtime loop (wide rows).
+#define EA_FORJ(...)                                                         \
+  if constexpr (NV > 0) {                                                    \
+    _Pragma("unroll") for (int i_ = 0; i_ < (NV > 0 ? NV : 1); ++i_) {       \
+      const int j = lane + i_ * W;                                           \
+      if (j < N) { __VA_ARGS__ }                                             \
+    }                                                                        \
+  } else {                                                                   \
+    for (int j = lane, i_ = 0; j < N; j += W, ++i_) { __VA_ARGS__ }          \
+  }
+
+template <int W, int NV, typename ZF, typename YF, typename GF, typename PF>
+__device__ __forceinline__ void row_loss(int lane, int N, int act, int loss, const int* metrics, int nmetrics,
+                         ZF zat, YF yat, float y0, bool want_grad, GF dz_out, bool want_pred, PF p_out,
                          RowOut& out) {
+  // y0: the row's first target value (the class id for sparse labels)
   const bool sparse = (loss == LOSS_SPARSE_CCE);
-  const int ycls = sparse ? (int)yat(0) : -1;
-  auto Y = [&](int j) -> float { return sparse ? (j == ycls ? 1.f : 0.f) : yat(j); };
+  const int ycls = sparse ? (int)y0 : -1;
+  auto Y = [&](int i, int j) -> float { return sparse ? (j == ycls ? 1.f : 0.f) : yat(i, j); };
   // softmax statistics
   float zmax = -INFINITY, sumexp = 0.f;
   if (act == ACT_SOFTMAX) {
-    for (int j = lane; j < N; j += W) zmax = fmaxf(zmax, zat(j));
+    EA_FORJ(zmax = fmaxf(zmax, zat(i_, j));)
     zmax = row_max<W>(zmax);
-    for (int j = lane; j < N; j += W) sumexp += __expf(zat(j) - zmax);
+    EA_FORJ(sumexp += __expf(zat(i_, j) - zmax);)
     sumexp = row_sum<W>(sumexp);
   }
   const float lse = zmax + logf(sumexp);
-  auto P = [&](int j) -> float {
-    float z = zat(j);
+  auto P = [&](int i, int j) -> float {
+    float z = zat(i, j);
     return act == ACT_SOFTMAX ? __expf(z - lse) : act_fwd(act, z);
   };
   const bool cce_like = (loss == LOSS_CCE || loss == LOSS_SPARSE_CCE);
@@ -230,13 +269,12 @@ __device__ void row_loss(int lane, int N, int act, int loss, const int* metrics,
   // ---- loss value
   float lsum = 0.f, psum = 0.f, ysum = 0.f;
   if (cce_like && !logit_cce) {
-    for (int j = lane; j < N; j += W) psum += P(j);
+    EA_FORJ(psum += P(i_, j);)
     psum = row_sum<W>(psum);
   }
   float ynorm = 0.f, pnorm = 0.f, yp = 0.f;  // cosine
   float cat_pos = 0.f, cat_neg = -INFINITY;  // categorical hinge
-  for (int j = lane; j < N; j += W) {
-    float z = zat(j), y = Y(j), p = P(j);
+  EA_FORJ(float z = zat(i_, j), y = Y(i_, j), p = P(i_, j);
     if (logit_cce) lsum += -y * (z - lse);
     else if (cce_like) {
       float pn = fminf(fmaxf(p / psum, KERAS_EPS), 1.f - KERAS_EPS);
@@ -244,8 +282,7 @@ __device__ void row_loss(int lane, int N, int act, int loss, const int* metrics,
     } else if (loss == LOSS_COSINE) { ynorm += y * y; pnorm += p * p; yp += y * p; }
     else if (loss == LOSS_CAT_HINGE) { cat_pos += y * p; cat_neg = fmaxf(cat_neg, (1.f - y) * p); }
     else lsum += loss_elem_value<W>(loss, p, y, z, logit_bce);
-    ysum += y;
-  }
+    ysum += y;)
   lsum = row_sum<W>(lsum);
   ysum = row_sum<W>(ysum);
   float rl;
@@ -261,40 +298,40 @@ __device__ void row_loss(int lane, int N, int act, int loss, const int* metrics,
   }
   out.loss = rl;
 
-  // ---- metrics
-  for (int mi = 0; mi < nmetrics; ++mi) {
-    int m = metrics[mi];
+  // ---- metrics (static indices only: no scratch copies of the metric list)
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi) {
+    if (mi >= nmetrics) break;
+    const int m = metrics[mi];
     float mv = 0.f;
     if (m == MET_ACC_CAT || m == MET_ACC_SPARSE) {
       float bp = -INFINITY; int ip = 0x7fffffff;
       float by = -INFINITY; int iy = 0x7fffffff;
-      for (int j = lane; j < N; j += W) {
-        float p = P(j);
+      EA_FORJ(float p = P(i_, j);
         if (p > bp) { bp = p; ip = j; }
-        float yv = Y(j);
-        if (yv > by) { by = yv; iy = j; }
-      }
+        float yv = Y(i_, j);
+        if (yv > by) { by = yv; iy = j; })
       row_argmax<W>(bp, ip);
       row_argmax<W>(by, iy);
       if (m == MET_ACC_SPARSE) iy = ycls;
       mv = (ip == iy) ? 1.f : 0.f;
     } else if (m == MET_ACC_BIN) {
       float s = 0.f;
-      for (int j = lane; j < N; j += W) s += ((P(j) > 0.5f ? 1.f : 0.f) == Y(j)) ? 1.f : 0.f;
+      EA_FORJ(s += ((P(i_, j) > 0.5f ? 1.f : 0.f) == Y(i_, j)) ? 1.f : 0.f;)
       mv = row_sum<W>(s) * invN;
     } else if (m == LOSS_CCE || m == LOSS_SPARSE_CCE) {
       float s = 0.f;
-      for (int j = lane; j < N; j += W) s += (act == ACT_SOFTMAX) ? -Y(j) * (zat(j) - lse)
-                                                                  : -Y(j) * logf(fminf(fmaxf(P(j), KERAS_EPS), 1.f - KERAS_EPS));
+      EA_FORJ(s += (act == ACT_SOFTMAX) ? -Y(i_, j) * (zat(i_, j) - lse)
+                                                                  : -Y(i_, j) * logf(fminf(fmaxf(P(i_, j), KERAS_EPS), 1.f - KERAS_EPS));)
       mv = row_sum<W>(s);
     } else if (m == LOSS_COSINE) {
       float a = 0.f, b = 0.f, c = 0.f;
-      for (int j = lane; j < N; j += W) { float p = P(j), y = Y(j); a += y * y; b += p * p; c += y * p; }
+      EA_FORJ(float p = P(i_, j), y = Y(i_, j); a += y * y; b += p * p; c += y * p;)
       a = row_sum<W>(a); b = row_sum<W>(b); c = row_sum<W>(c);
       mv = c * rsqrtf(fmaxf(a, 1e-12f)) * rsqrtf(fmaxf(b, 1e-12f));  // keras metric: +cos
     } else {
       float s = 0.f;
-      for (int j = lane; j < N; j += W) s += loss_elem_value<W>(m, P(j), Y(j), zat(j), m == LOSS_BCE && act == ACT_SIGMOID);
+      EA_FORJ(s += loss_elem_value<W>(m, P(i_, j), Y(i_, j), zat(i_, j), m == LOSS_BCE && act == ACT_SIGMOID);)
       s = row_sum<W>(s);
       mv = loss_is_mean_over_last_axis(m) ? s * invN : s;
     }
@@ -303,18 +340,18 @@ __device__ void row_loss(int lane, int N, int act, int loss, const int* metrics,
 
   // ---- prediction
   if (want_pred)
-    for (int j = lane; j < N; j += W) p_out(j, P(j));
+    EA_FORJ(p_out(i_, j, P(i_, j));)
 
   // ---- gradient wrt z (per row)
   if (want_grad) {
     if (logit_cce) {
-      for (int j = lane; j < N; j += W) dz_out(j, __expf(zat(j) - lse) * ysum - Y(j));
+      EA_FORJ(dz_out(i_, j, __expf(zat(i_, j) - lse) * ysum - Y(i_, j));)
     } else if (logit_bce) {
-      for (int j = lane; j < N; j += W) dz_out(j, (sigmoidf_(zat(j)) - Y(j)) * invN);
+      EA_FORJ(dz_out(i_, j, (sigmoidf_(zat(i_, j)) - Y(i_, j)) * invN);)
     } else {
       // g_j = dL/dp_j
-      auto G = [&](int j) -> float {
-        float p = P(j), y = Y(j);
+      auto G = [&](int i, int j) -> float {
+        float p = P(i, j), y = Y(i, j);
         if (cce_like) {
           float pn = p / psum;
           if (pn <= KERAS_EPS || pn >= 1.f - KERAS_EPS) return 0.f;
@@ -338,11 +375,11 @@ __device__ void row_loss(int lane, int N, int act, int loss, const int* metrics,
       };
       if (act == ACT_SOFTMAX) {
         float gp = 0.f;
-        for (int j = lane; j < N; j += W) gp += G(j) * P(j);
+        EA_FORJ(gp += G(i_, j) * P(i_, j);)
         gp = row_sum<W>(gp);
-        for (int j = lane; j < N; j += W) dz_out(j, P(j) * (G(j) - gp));
+        EA_FORJ(dz_out(i_, j, P(i_, j) * (G(i_, j) - gp));)
       } else {
-        for (int j = lane; j < N; j += W) dz_out(j, G(j) * act_grad(act, zat(j)));
+        EA_FORJ(dz_out(i_, j, G(i_, j) * act_grad(act, zat(i_, j)));)
       }
     }
   }
@@ -401,19 +438,78 @@ __device__ __forceinline__ float opt_update(const OptParams& p, float w, float g
   return w;
 }
 
-template <int W, typename ZF, typename PF>
-__device__ void row_predict(int lane, int N, int act, ZF zat, PF p_out) {
+template <int W, int NV, typename ZF, typename PF>
+__device__ __forceinline__ void row_predict(int lane, int N, int act, ZF zat, PF p_out) {
   if (act == ACT_SOFTMAX) {
     float zmax = -INFINITY, s = 0.f;
-    for (int j = lane; j < N; j += W) zmax = fmaxf(zmax, zat(j));
+    EA_FORJ(zmax = fmaxf(zmax, zat(i_, j));)
     zmax = row_max<W>(zmax);
-    for (int j = lane; j < N; j += W) s += __expf(zat(j) - zmax);
+    EA_FORJ(s += __expf(zat(i_, j) - zmax);)
     s = row_sum<W>(s);
     const float inv = 1.f / s;
-    for (int j = lane; j < N; j += W) p_out(j, __expf(zat(j) - zmax) * inv);
+    EA_FORJ(p_out(i_, j, __expf(zat(i_, j) - zmax) * inv);)
   } else {
-    for (int j = lane; j < N; j += W) p_out(j, act_fwd(act, zat(j)));
+    EA_FORJ(p_out(i_, j, act_fwd(act, zat(i_, j)));)
   }
+}
+
+// number of optimizer state planes a rule reads/writes
+__device__ __forceinline__ int opt_planes(const OptParams& p) {
+  switch (p.opt) {
+    case OPT_SGD: return p.mom != 0.f ? 1 : 0;
+    case OPT_RMSPROP: return p.mom > 0.f ? 2 : 1;
+    case OPT_ADAGRAD: return 1;
+    default: return 2;  // adam, adamax
+  }
+}
+
+// same rules as opt_update with the state held in registers
+__device__ __forceinline__ float opt_update_reg(const OptParams& p, float w, float g, float& s0, float& s1,
+                                                long long iter) {
+  const float lr = p.lr / (1.f + p.decay * (float)iter);
+  switch (p.opt) {
+    case OPT_SGD: {
+      if (p.mom == 0.f) return w - lr * g;
+      const float v = p.mom * s0 - lr * g;
+      s0 = v;
+      return p.nesterov ? w + p.mom * v - lr * g : w + v;
+    }
+    case OPT_RMSPROP: {
+      const float ms = p.rho * s0 + (1.f - p.rho) * g * g;
+      s0 = ms;
+      const float upd = lr * g / (sqrtf(ms) + p.eps);
+      if (p.mom > 0.f) {
+        const float m = p.mom * s1 + upd;
+        s1 = m;
+        return w - m;
+      }
+      return w - upd;
+    }
+    case OPT_ADAM: {
+      const float t = (float)(iter + 1);
+      const float lrt = lr * sqrtf(1.f - powf(p.b2, t)) / (1.f - powf(p.b1, t));
+      const float m = p.b1 * s0 + (1.f - p.b1) * g;
+      const float v = p.b2 * s1 + (1.f - p.b2) * g * g;
+      s0 = m;
+      s1 = v;
+      return w - lrt * m / (sqrtf(v) + p.eps);
+    }
+    case OPT_ADAGRAD: {
+      const float a = s0 + g * g;
+      s0 = a;
+      return w - lr * g / (sqrtf(a) + p.eps);
+    }
+    case OPT_ADAMAX: {
+      const float t = (float)(iter + 1);
+      const float lrt = lr / (1.f - powf(p.b1, t));
+      const float m = p.b1 * s0 + (1.f - p.b1) * g;
+      const float u = fmaxf(p.b2 * s1, fabsf(g));
+      s0 = m;
+      s1 = u;
+      return w - lrt * m / (u + p.eps);
+    }
+  }
+  return w;
 }
 
 // ------------------------------------------------------- shared structs ----

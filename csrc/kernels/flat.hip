@@ -10,17 +10,28 @@
 
 namespace ea {
 
-__device__ __forceinline__ int find_seg(const FlatArgs& a, long long i) {
-  int s = 0;
-  for (int q = 1; q < a.nseg; ++q)
-    if (i >= a.seg[q].p_off) s = q;
-  return s;
+// Segment lookup with compile-time indices only (dynamic indexing of the
+// kernarg segment table would make hipcc copy FlatArgs to scratch per lane).
+struct SegV {
+  long long p_off, wsh_off, ldwsh, wtsh_off, ldwtsh;
+  int K, N;
+};
+
+__device__ __forceinline__ SegV find_seg(const FlatArgs& a, long long i) {
+  SegV v{a.seg[0].p_off, a.seg[0].wsh_off, a.seg[0].ldwsh, a.seg[0].wtsh_off, a.seg[0].ldwtsh, a.seg[0].K, a.seg[0].N};
+#pragma unroll
+  for (int q = 1; q < MAX_SEG; ++q) {
+    if (q < a.nseg && i >= a.seg[q].p_off) {
+      v = SegV{a.seg[q].p_off, a.seg[q].wsh_off, a.seg[q].ldwsh, a.seg[q].wtsh_off, a.seg[q].ldwtsh, a.seg[q].K,
+               a.seg[q].N};
+    }
+  }
+  return v;
 }
 
 template <typename T>
 __device__ __forceinline__ void write_shadow(const FlatArgs& a, int r, long long i, float w, long long par) {
-  const int s = find_seg(a, i);
-  const Seg& g = a.seg[s];
+  const SegV g = find_seg(a, i);
   const long long rel = i - g.p_off;
   if (rel < 0 || rel >= (long long)g.K * g.N) return;  // bias: no shadow
   const long long k = rel / g.N, nn = rel % g.N;

@@ -23,6 +23,8 @@
 // grouped launch; blockIdx.x selects the problem.
 #include "common.h"
 
+#include <algorithm>
+
 namespace ea {
 
 // ------------------------------------------------------------------ helpers
@@ -75,7 +77,7 @@ template <typename T> __device__ __forceinline__ void st(void* base, long long i
 
 // ------------------------------------------------------- gather-transpose
 template <typename T>
-__device__ void gather_transpose_block(const GroupArgs& ga, const Prob& p, int lb, float* sm) {
+__device__ __forceinline__ void gather_transpose_block(const GroupArgs& ga, const Prob& p, int lb, float* sm) {
   // one block = 64 batch rows x 64 features; output XT[k][m] (ld = lddt)
   // tiles_m: batch blocks, tiles_n: feature blocks
   const int per_r = p.tiles_m * p.tiles_n;
@@ -109,7 +111,7 @@ __device__ void gather_transpose_block(const GroupArgs& ga, const Prob& p, int l
 // the logits Z, then one wave per row runs the same row_loss math as the fused
 // epilogue with wave-wide reductions.
 template <typename T>
-__device__ void loss_rows_block(const GroupArgs& ga, const Prob& p, int lb) {
+__device__ __forceinline__ void loss_rows_block(const GroupArgs& ga, const Prob& p, int lb) {
   const int r = lb / p.tiles_m;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int row = (lb % p.tiles_m) * 4 + wave;
@@ -130,46 +132,201 @@ __device__ void loss_rows_block(const GroupArgs& ga, const Prob& p, int lb) {
   const float* zrow = p.Z + (long long)r * p.sZ + (long long)row * p.ldz;
   float* prow = p.pred ? p.pred + (long long)r * p.sPred + (p.chunk * p.B + row) * p.ldp : nullptr;
   if (!p.Y) {  // predict only
-    if (prow) row_predict<64>(lane, p.N, p.act, [&](int j) { return zrow[j]; }, [&](int j, float v) { prow[j] = v; });
+    if (prow) row_predict<64, 0>(lane, p.N, p.act, [&](int, int j) { return zrow[j]; }, [&](int, int j, float v) { prow[j] = v; });
     return;
   }
   const long long drow = batch_row(p, r, step, row);
   const float* yrow = p.Y + (long long)r * p.sY + drow * p.ldy;
   RowOut ro;
   ro.loss = 0.f;
+#pragma unroll
   for (int q = 0; q < 4; ++q) ro.metric[q] = 0.f;
-  row_loss<64>(lane, p.N, p.act, p.loss, p.met, p.nmet,
-               [&](int j) { return zrow[j]; },
-               [&](int j) { return yrow[j]; },
+  row_loss<64, 0>(lane, p.N, p.act, p.loss, p.met, p.nmet,
+               [&](int, int j) { return zrow[j]; },
+               [&](int, int j) { return yrow[j]; }, yrow[0],
                train,
-               [&](int j, float v) {
+               [&](int, int j, float v) {
                  st<T>(p.D, (long long)r * p.sD + (long long)row * p.ldd + j, v * inv_valid);
                  if (p.DT) st<T>(p.DT, (long long)r * p.sDT + (long long)j * p.lddt + row, v * inv_valid);
                },
-               prow != nullptr, [&](int j, float v) { prow[j] = v; }, ro);
+               prow != nullptr, [&](int, int j, float v) { prow[j] = v; }, ro);
   if (p.acc && lane == 0) {
     double* a = p.acc + (long long)r * p.acc_stride;
     atomicAdd(a + 0, (double)ro.loss);
     atomicAdd(a + 1, 1.0);
-    for (int q = 0; q < p.nmet; ++q) atomicAdd(a + 2 + q, (double)ro.metric[q]);
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if (q < p.nmet) atomicAdd(a + 2 + q, (double)ro.metric[q]);
   }
+}
+
+
+// 8 contiguous outputs -> one 16-byte (bf16) or two 16-byte (fp32) stores.
+// Callers guarantee 16-byte alignment (row strides and column chunks are multiples of 8).
+template <typename T>
+__device__ __forceinline__ void st8(void* base, long long idx, const float (&v)[8]) {
+  if constexpr (sizeof(T) == 2) {
+    auto pk2 = [](float a, float b) -> unsigned {
+      const unsigned lo = __builtin_bit_cast(unsigned short, (__bf16)a);
+      const unsigned hi = __builtin_bit_cast(unsigned short, (__bf16)b);
+      return lo | (hi << 16);
+    };
+    *reinterpret_cast<uint4*>(reinterpret_cast<__bf16*>(base) + idx) =
+        make_uint4(pk2(v[0], v[1]), pk2(v[2], v[3]), pk2(v[4], v[5]), pk2(v[6], v[7]));
+  } else {
+    float* f = reinterpret_cast<float*>(base) + idx;
+    *reinterpret_cast<float4*>(f) = make_float4(v[0], v[1], v[2], v[3]);
+    *reinterpret_cast<float4*>(f + 4) = make_float4(v[4], v[5], v[6], v[7]);
+  }
+}
+
+// Fused loss over the tile's rows: groups of W lanes own one row each
+// (W = 16/32/64 by output width), reductions are W-lane shuffles.
+// Fused softmax + (sparse) categorical cross-entropy over a GEMM tile holding
+// whole rows (N <= 32): one quad (4 lanes) per row, the row's logits/targets in
+// registers (NV = ceil(N/4) statically unrolled slots per lane) and DPP quad
+// reductions -- no LDS round trips inside the row math, 64 rows per pass.
+// Same math as row_loss's logits path (keras backend.categorical_crossentropy
+// with from_logits): loss = -sum y (z - lse), dL/dz = softmax(z) * sum(y) - y.
+// Other loss/activation/metric combinations use loss_tile_lds.
+__device__ __forceinline__ bool softmax_cce_fast(const Prob& p) {
+  if (p.act != ACT_SOFTMAX || !(p.loss == LOSS_CCE || p.loss == LOSS_SPARSE_CCE) || !p.Y || p.N > 32) return false;
+  bool ok = true;
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    if (q < p.nmet)
+      ok = ok && (p.met[q] == MET_ACC_CAT || p.met[q] == MET_ACC_SPARSE || p.met[q] == LOSS_CCE ||
+                  p.met[q] == LOSS_SPARSE_CCE);
+  return ok;
+}
+
+template <int NV, int BM, int LDC, int BN>
+__device__ __forceinline__ void loss_tile_cce(const Prob& p, int r, int m0, float* C, const float* Ys, const int* srow,
+                                              bool train, float inv_valid, float (&sums)[6]) {
+  constexpr int W = 4;
+  const int lane = threadIdx.x & 3, grp = threadIdx.x >> 2;
+  const int N = p.N;
+  const bool sparse = p.loss == LOSS_SPARSE_CCE;
+  for (int row = grp; row < BM; row += 64) {
+    float* zrow = C + row * LDC;
+    const float* yrow = Ys + row * BN;
+    float z[NV], y[NV];
+    const int ycls = sparse ? (int)yrow[0] : -1;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {  // in-bounds of the LDS tile even past N
+      const int j = lane + i * W;
+      z[i] = zrow[j];
+      y[i] = sparse ? (j == ycls ? 1.f : 0.f) : yrow[j];
+    }
+    if (srow[row] < 0) {
+      if (train) {
+#pragma unroll
+        for (int i = 0; i < NV; ++i)
+          if (lane + i * W < N) zrow[lane + i * W] = 0.f;
+      }
+      continue;
+    }
+    float zmax = -INFINITY;
+#pragma unroll
+    for (int i = 0; i < NV; ++i)
+      if (lane + i * W < N) zmax = fmaxf(zmax, z[i]);
+    zmax = row_max<W>(zmax);
+    float se = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i)
+      if (lane + i * W < N) se += __expf(z[i] - zmax);
+    se = row_sum<W>(se);
+    const float lse = zmax + logf(se);
+    float l = 0.f, ysum = 0.f, bp = -INFINITY, by = -INFINITY, pr[NV];
+    int ip = 0x7fffffff, iy = 0x7fffffff;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int j = lane + i * W;
+      pr[i] = __expf(z[i] - lse);
+      if (j < N) {
+        l += -y[i] * (z[i] - lse);
+        ysum += y[i];
+        if (pr[i] > bp) { bp = pr[i]; ip = j; }
+        if (y[i] > by) { by = y[i]; iy = j; }
+      }
+    }
+    l = row_sum<W>(l);
+    ysum = row_sum<W>(ysum);
+    row_argmax<W>(bp, ip);
+    row_argmax<W>(by, iy);
+    if (sparse) iy = ycls;
+    const float acc = ip == iy ? 1.f : 0.f;
+    if (p.pred) {
+      float* prow = p.pred + (long long)r * p.sPred + (p.chunk * p.B + m0 + row) * p.ldp;
+#pragma unroll
+      for (int i = 0; i < NV; ++i)
+        if (lane + i * W < N) prow[lane + i * W] = pr[i];
+    }
+    if (train) {
+#pragma unroll
+      for (int i = 0; i < NV; ++i)
+        if (lane + i * W < N) zrow[lane + i * W] = (pr[i] * ysum - y[i]) * inv_valid;
+    }
+    if (lane == 0) {
+      sums[0] += l;
+      sums[1] += 1.f;
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (q < p.nmet) sums[2 + q] += (p.met[q] == MET_ACC_CAT || p.met[q] == MET_ACC_SPARSE) ? acc : l;
+    }
+  }
+}
+
+// Generic fused loss (any loss/activation/metrics): 16 lanes per row, values
+// read from the LDS tile in runtime loops (keeps code size bounded).
+template <int BM, int LDC, int BN>
+__device__ __forceinline__ void loss_tile_lds(const Prob& p, int r, int m0, float* C, const float* Ys, const int* srow,
+                                              bool train, float inv_valid, float (&sums)[6]) {
+  constexpr int W = 16;
+  const int lane = threadIdx.x % W, grp = threadIdx.x / W;
+  for (int row = grp; row < BM; row += 256 / W) {
+    float* zrow = C + row * LDC;
+    const float* yrow = Ys + row * BN;
+    if (srow[row] < 0) {
+      if (train)
+        for (int j = lane; j < p.N; j += W) zrow[j] = 0.f;
+      continue;
+    }
+    float* prow = p.pred ? p.pred + (long long)r * p.sPred + (p.chunk * p.B + m0 + row) * p.ldp : nullptr;
+    auto zat = [&](int, int j) { return zrow[j]; };
+    auto pout = [&](int, int j, float v) { prow[j] = v; };
+    if (!p.Y) {
+      if (prow) row_predict<W, 0>(lane, p.N, p.act, zat, pout);
+      continue;
+    }
+    RowOut ro;
+    ro.loss = 0.f;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) ro.metric[q] = 0.f;
+    row_loss<W, 0>(lane, p.N, p.act, p.loss, p.met, p.nmet, zat, [&](int, int j) { return yrow[j]; }, yrow[0],
+                   train, [&](int, int j, float v) { zrow[j] = v * inv_valid; }, prow != nullptr, pout, ro);
+    if (lane == 0) {
+      sums[0] += ro.loss;
+      sums[1] += 1.f;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) sums[2 + q] += ro.metric[q];
+    }
+  }
+}
+
+// diagnostics: wall-clock stamps (100 MHz s_memrealtime) of block-relative phases
+__device__ __forceinline__ void stamp(const GroupArgs& ga, int k) {
+  if (ga.stamps && threadIdx.x == 0) ga.stamps[(long long)blockIdx.x * 16 + k] = (long long)__builtin_amdgcn_s_memrealtime();
 }
 
 // --------------------------------------------------------------- the kernel
 template <typename T, int WM, int WN, int WAVES_M, int WAVES_N, int KSPLIT>
-__global__ __launch_bounds__(256) void gemm_grouped(GroupArgs ga) {
+__device__ __forceinline__ void run_prob(const GroupArgs& ga, const Prob& p, const int lb, float* smem) {
   static_assert(WAVES_M * WAVES_N * KSPLIT == 4, "4 waves per block");
   constexpr int BM = WAVES_M * WM * 16;
   constexpr int BN = WAVES_N * WN * 16;
-  constexpr int LDC = BN + 1;
+  constexpr int LDC = BN + 4;  // 16-byte aligned rows for float4 LDS access
   constexpr int EPL = KT<T>::EPL, KC = KT<T>::KC;
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-
-  int bid = blockIdx.x;
-  const int pi = (ga.nprob > 1 && bid >= ga.p[1].block_begin) ? 1 : 0;
-  const Prob& p = ga.p[pi];
-  const int lb = bid - p.block_begin;
-
   if (p.kind == PK_GATHER_T) {
     gather_transpose_block<T>(ga, p, lb, smem);
   } else if (p.kind == PK_LOSS_ROWS) {
@@ -184,6 +341,7 @@ __global__ __launch_bounds__(256) void gemm_grouped(GroupArgs ga) {
     const long long iter = ga.ctr[2 + r];
     const int valid = (p.kind == PK_PLAIN) ? p.M : batch_valid(p, r, step);
     const bool skip_update = (p.kind == PK_DW_UPDATE) && valid == 0;
+    stamp(ga, 1);
 
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int wk = wave % KSPLIT;
@@ -201,38 +359,60 @@ __global__ __launch_bounds__(256) void gemm_grouped(GroupArgs ga) {
       const T* A = reinterpret_cast<const T*>(p.A) + (long long)r * p.sA;
       const T* BTp = reinterpret_cast<const T*>(p.BT) + (long long)r * p.sB +
                      (p.bt_shadow ? (iter & 1) * p.bt_par : 0);
+      // Every fragment load is an unconditional, in-bounds 16-byte global load
+      // (invalid rows read row 0, k past the end reads k=0) followed by a value
+      // select, so hipcc emits global_load_dwordx4 and never a pointer select
+      // into a stack constant (which would become flat loads + scratch).
       const T* arow[WM];
-      bool aones[WM];
+      unsigned amask = 0, aones_m = 0;  // bit i: row i valid / row i is the ones row
 #pragma unroll
       for (int i = 0; i < WM; ++i) {
         const int m = m0 + wm * WM * 16 + i * 16 + i16;
-        aones[i] = (m == p.ones_row);
-        arow[i] = nullptr;
-        if (m < p.M && !aones[i]) {
+        arow[i] = A;
+        if (m == p.ones_row) {
+          aones_m |= 1u << i;
+        } else if (m < p.M) {
           if (p.a_gather) {
-            if (m < valid) arow[i] = A + batch_row(p, r, step, m) * p.lda;
+            if (m < valid) {
+              arow[i] = A + batch_row(p, r, step, m) * p.lda;
+              amask |= 1u << i;
+            }
           } else {
             arow[i] = A + (long long)m * p.lda;
+            amask |= 1u << i;
           }
         }
       }
       const T* bcol[WN];
+      unsigned bmask = 0;
 #pragma unroll
       for (int j = 0; j < WN; ++j) {
         const int n = n0 + wn * WN * 16 + j * 16 + i16;
-        bcol[j] = (n < p.N) ? BTp + (long long)n * p.ldb : nullptr;
+        bcol[j] = BTp;
+        if (n < p.N) {
+          bcol[j] = BTp + (long long)n * p.ldb;
+          bmask |= 1u << j;
+        }
       }
       const uint4 zero = make_uint4(0u, 0u, 0u, 0u);
       const uint4 one = ones_frag<T>();
+      auto sel = [](bool c, const uint4& a, const uint4& b) {
+        return make_uint4(c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z, c ? a.w : b.w);
+      };
       auto load_frags = [&](int kc, uint4 (&a)[WM], uint4 (&b)[WN]) {
         const int kk = kc + g * EPL;
         const bool kin = kk < p.K;
+        const int kq = kin ? kk : 0;
 #pragma unroll
-        for (int i = 0; i < WM; ++i)
-          a[i] = (kin && arow[i]) ? *reinterpret_cast<const uint4*>(arow[i] + kk) : ((kin && aones[i]) ? one : zero);
+        for (int i = 0; i < WM; ++i) {
+          const uint4 v = *reinterpret_cast<const uint4*>(arow[i] + kq);
+          a[i] = sel(kin && ((amask >> i) & 1u), v, sel(kin && ((aones_m >> i) & 1u), one, zero));
+        }
 #pragma unroll
-        for (int j = 0; j < WN; ++j)
-          b[j] = (kin && bcol[j]) ? *reinterpret_cast<const uint4*>(bcol[j] + kk) : zero;
+        for (int j = 0; j < WN; ++j) {
+          const uint4 v = *reinterpret_cast<const uint4*>(bcol[j] + kq);
+          b[j] = sel(kin && ((bmask >> j) & 1u), v, zero);
+        }
       };
       constexpr int KSTEP = KSPLIT * KC;
       int kc = wk * KC;
@@ -256,6 +436,7 @@ __global__ __launch_bounds__(256) void gemm_grouped(GroupArgs ga) {
       }
     }
 
+    stamp(ga, 2);
     // ---- accumulators -> LDS (one region per k-split wave)
     float* region = smem + wk * BM * LDC;
 #pragma unroll
@@ -270,125 +451,191 @@ __global__ __launch_bounds__(256) void gemm_grouped(GroupArgs ga) {
         }
     __syncthreads();
     if constexpr (KSPLIT > 1) {
-      for (int e = threadIdx.x; e < BM * BN; e += 256) {
-        const int row = e / BN, col = e % BN;
-        float s = smem[row * LDC + col];
+      for (int e = threadIdx.x; e < BM * BN / 4; e += 256) {
+        const int row = e / (BN / 4), c4 = (e % (BN / 4)) * 4;
+        float4 s = *reinterpret_cast<const float4*>(smem + row * LDC + c4);
 #pragma unroll
-        for (int w = 1; w < KSPLIT; ++w) s += smem[w * BM * LDC + row * LDC + col];
-        smem[row * LDC + col] = s;
+        for (int w = 1; w < KSPLIT; ++w) {
+          const float4 o = *reinterpret_cast<const float4*>(smem + w * BM * LDC + row * LDC + c4);
+          s.x += o.x; s.y += o.y; s.z += o.z; s.w += o.w;
+        }
+        *reinterpret_cast<float4*>(smem + row * LDC + c4) = s;
       }
       __syncthreads();
     }
     float* C = smem;  // final tile [BM][LDC]
+    stamp(ga, 3);
 
-    // ---- epilogues
+    // Epilogue thread mapping: each thread owns 8 contiguous columns of one row
+    // per pass and issues all of its global loads before any store, so the
+    // loads of a pass overlap instead of serialising behind possibly-aliasing
+    // stores.
+    constexpr int CPR = BN / 8;          // 8-column chunks per row
+    constexpr int RPP = 256 / CPR;       // rows per pass
+    constexpr int PASSES = BM / RPP;
+    const int t_row = threadIdx.x / CPR, t_c0 = (threadIdx.x % CPR) * 8;
+    auto lds8 = [&](int row, int c0, float (&v)[8]) {
+      const float4 a = *reinterpret_cast<const float4*>(C + row * LDC + c0);
+      const float4 b = *reinterpret_cast<const float4*>(C + row * LDC + c0 + 4);
+      v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+    };
+    auto sts8 = [&](int row, int c0, const float (&v)[8]) {
+      *reinterpret_cast<float4*>(C + row * LDC + c0) = make_float4(v[0], v[1], v[2], v[3]);
+      *reinterpret_cast<float4*>(C + row * LDC + c0 + 4) = make_float4(v[4], v[5], v[6], v[7]);
+    };
+    // transposed store of the tile (D^T, dZ^T, W^T): consecutive threads -> consecutive rows
+    auto store_transposed = [&](void* base, long long off, long long ld, int nrows) {
+      for (int e = threadIdx.x; e < BM * BN; e += 256) {
+        const int col = e / BM, row = e % BM, gm = m0 + row, gn = n0 + col;
+        if (gm < nrows && gn < p.N) st<T>(base, off + (long long)gn * ld + gm, C[row * LDC + col]);
+      }
+    };
+
     switch (p.kind) {
       case PK_PLAIN: {
         float* out = reinterpret_cast<float*>(p.D) + (long long)r * p.sD;
-        for (int e = threadIdx.x; e < BM * BN; e += 256) {
-          const int row = e / BN, col = e % BN, gm = m0 + row, gn = n0 + col;
-          if (gm < p.M && gn < p.N) out[(long long)gm * p.ldd + gn] = C[row * LDC + col];
+#pragma unroll
+        for (int ps = 0; ps < PASSES; ++ps) {
+          const int row = ps * RPP + t_row, gm = m0 + row, gn0 = n0 + t_c0;
+          if (gm >= p.M) continue;
+          float v[8];
+          lds8(row, t_c0, v);
+#pragma unroll
+          for (int q = 0; q < 8; ++q)
+            if (gn0 + q < p.N) out[(long long)gm * p.ldd + gn0 + q] = v[q];
         }
         break;
       }
       case PK_FWD:
       case PK_DX: {
         const bool fwd = p.kind == PK_FWD;
-        const float* bias = fwd && p.bias ? p.bias + (long long)r * p.sBias : nullptr;
-        float* Z = p.Z ? p.Z + (long long)r * p.sZ : nullptr;
+        const float* __restrict__ bias = fwd && p.bias ? p.bias + (long long)r * p.sBias : nullptr;
+        float* __restrict__ Z = p.Z ? p.Z + (long long)r * p.sZ : nullptr;
         const float keep_scale = p.rate > 0.f ? 1.f / (1.f - p.rate) : 1.f;
         const bool drop = p.rate > 0.f && !p.eval_mode;
-        for (int e = threadIdx.x; e < BM * BN; e += 256) {
-          const int row = e / BN, col = e % BN, gm = m0 + row, gn = n0 + col;
-          if (gm >= p.M || gn >= p.N) continue;
-          float v = C[row * LDC + col];
-          float out = 0.f;
-          if (gm < valid) {
-            bool keep = true;
-            if (drop) keep = dropout_uniform(ga.seed, r, p.layer, iter, (long long)gm * p.N + gn) >= p.rate;
-            if (fwd) {
-              const float z = v + (bias ? bias[gn] : 0.f);
-              if (Z) Z[(long long)gm * p.ldz + gn] = z;
-              out = keep ? act_fwd(p.act, z) * keep_scale : 0.f;
-            } else {
-              const float z = Z[(long long)gm * p.ldz + gn];
-              out = keep ? v * act_grad(p.act, z) * keep_scale : 0.f;
-            }
-          } else if (fwd && Z) {
-            Z[(long long)gm * p.ldz + gn] = 0.f;
+#pragma unroll
+        for (int ps = 0; ps < PASSES; ++ps) {
+          const int row = ps * RPP + t_row, gm = m0 + row, gn0 = n0 + t_c0;
+          if (gm >= p.M || gn0 >= p.N) continue;
+          const bool rv = gm < valid;
+          float v[8], aux[8], zv[8], out[8], u[8];
+          lds8(row, t_c0, v);
+          if (drop) {  // t_c0 is a multiple of 8: two 4-column Philox groups
+            const float4 u0 = dropout_u4(ga.seed, r, p.layer, iter, gm, gn0 >> 2);
+            const float4 u1 = dropout_u4(ga.seed, r, p.layer, iter, gm, (gn0 >> 2) + 1);
+            u[0] = u0.x; u[1] = u0.y; u[2] = u0.z; u[3] = u0.w;
+            u[4] = u1.x; u[5] = u1.y; u[6] = u1.z; u[7] = u1.w;
+          } else {
+#pragma unroll
+            for (int q = 0; q < 8; ++q) u[q] = 1.f;
           }
-          if (p.D) st<T>(p.D, (long long)r * p.sD + (long long)gm * p.ldd + gn, out);
-          C[row * LDC + col] = out;
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {  // loads first
+            const bool in = gn0 + q < p.N;
+            if (fwd) aux[q] = (bias && in) ? bias[gn0 + q] : 0.f;
+            else aux[q] = (in && rv) ? Z[(long long)gm * p.ldz + gn0 + q] : 0.f;
+          }
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            const int gn = gn0 + q;
+            zv[q] = 0.f;
+            out[q] = 0.f;
+            if (gn < p.N && rv) {
+              const bool keep = u[q] >= p.rate;
+              if (fwd) {
+                zv[q] = v[q] + aux[q];
+                out[q] = keep ? act_fwd(p.act, zv[q]) * keep_scale : 0.f;
+              } else {
+                out[q] = keep ? v[q] * act_grad(p.act, aux[q]) * keep_scale : 0.f;
+              }
+            }
+          }
+          if (ps == 0) stamp(ga, 5);
+          if (fwd && Z) {
+#pragma unroll
+            for (int q = 0; q < 8; ++q)
+              if (gn0 + q < p.N) Z[(long long)gm * p.ldz + gn0 + q] = zv[q];
+          }
+          if (p.D) st8<T>(p.D, (long long)r * p.sD + (long long)gm * p.ldd + gn0, out);
+          sts8(row, t_c0, out);
         }
+        stamp(ga, 6);
         if (p.DT) {
           __syncthreads();
-          for (int e = threadIdx.x; e < BM * BN; e += 256) {
-            const int col = e / BM, row = e % BM, gm = m0 + row, gn = n0 + col;
-            if (gm < p.M && gn < p.N) st<T>(p.DT, (long long)r * p.sDT + (long long)gn * p.lddt + gm, C[row * LDC + col]);
-          }
+          stamp(ga, 7);
+          store_transposed(p.DT, (long long)r * p.sDT, p.lddt, p.M);
         }
         break;
       }
       case PK_FWD_LOSS: {
         // whole rows live in this tile (N <= BN, tiles_n == 1)
-        const float* bias = p.bias ? p.bias + (long long)r * p.sBias : nullptr;
-        for (int e = threadIdx.x; e < BM * BN; e += 256) {
-          const int row = e / BN, col = e % BN;
-          if (col < p.N) C[row * LDC + col] += bias ? bias[col] : 0.f;
+        const float* __restrict__ bias = p.bias ? p.bias + (long long)r * p.sBias : nullptr;
+        int* srow = reinterpret_cast<int*>(smem + BM * LDC);   // data row of each tile row
+        float* Ys = smem + BM * LDC + BM;                       // staged targets [BM][BN]
+#pragma unroll
+        for (int ps = 0; ps < PASSES; ++ps) {
+          const int row = ps * RPP + t_row, gn0 = t_c0;
+          if (gn0 >= p.N) continue;
+          float v[8], b[8];
+          lds8(row, t_c0, v);
+#pragma unroll
+          for (int q = 0; q < 8; ++q) b[q] = (bias && gn0 + q < p.N) ? bias[gn0 + q] : 0.f;
+#pragma unroll
+          for (int q = 0; q < 8; ++q) v[q] += b[q];
+          sts8(row, t_c0, v);
+        }
+        stamp(ga, 5);
+        const int ldy = p.Y ? (int)p.ldy : 0;
+        for (int row = threadIdx.x; row < BM; row += 256) {
+          const int gm = m0 + row;
+          srow[row] = (gm < p.M && gm < valid) ? (int)batch_row(p, r, step, gm) : -1;
         }
         __syncthreads();
-        const int row = threadIdx.x;  // rows 0..BM-1 handled by the first BM threads
-        RowOut ro;
-        ro.loss = 0.f;
-        for (int q = 0; q < 4; ++q) ro.metric[q] = 0.f;
-        const int gm = m0 + row;
-        const bool rvalid = row < BM && gm < p.M && gm < valid;
+        if (p.Y) {
+          const float* Yb = p.Y + (long long)r * p.sY;
+          for (int e = threadIdx.x; e < BM * ldy; e += 256) {
+            const int row = e / ldy, j = e % ldy;
+            const int dr = srow[row];
+            Ys[row * BN + j] = dr >= 0 ? Yb[(long long)dr * ldy + j] : 0.f;
+          }
+        }
+        __syncthreads();
+        stamp(ga, 6);
         const bool train = !p.eval_mode && p.D;
         const float inv_valid = valid > 0 ? 1.f / (float)valid : 0.f;
-        if (rvalid && !p.Y) {  // predict only
-          float* zrow = C + row * LDC;
-          float* prow = p.pred ? p.pred + (long long)r * p.sPred + (p.chunk * p.B + gm) * p.ldp : nullptr;
-          if (prow) row_predict<1>(0, p.N, p.act, [&](int j) { return zrow[j]; }, [&](int j, float v) { prow[j] = v; });
-        } else if (rvalid) {
-          const long long drow = batch_row(p, r, step, gm);
-          const float* yrow = p.Y + (long long)r * p.sY + drow * p.ldy;
-          float* zrow = C + row * LDC;
-          float* prow = p.pred ? p.pred + (long long)r * p.sPred + (p.chunk * p.B + gm) * p.ldp : nullptr;
-          // The gradient pass is row_loss's last pass and, for every j, reads z_j before
-          // it writes dz_j, so dz can overwrite the logits in place in LDS.
-          row_loss<1>(0, p.N, p.act, p.loss, p.met, p.nmet,
-                      [&](int j) { return zrow[j]; },
-                      [&](int j) { return yrow[j]; },
-                      train, [&](int j, float v) { zrow[j] = v * inv_valid; },
-                      prow != nullptr, [&](int j, float v) { prow[j] = v; }, ro);
-        } else if (row < BM) {
-          for (int j = 0; j < p.N; ++j) C[row * LDC + j] = 0.f;
+        float sums[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        if (softmax_cce_fast(p)) {
+          if (p.N <= 16) loss_tile_cce<4, BM, LDC, BN>(p, r, m0, C, Ys, srow, train, inv_valid, sums);
+          else loss_tile_cce<8, BM, LDC, BN>(p, r, m0, C, Ys, srow, train, inv_valid, sums);
+        } else {
+          loss_tile_lds<BM, LDC, BN>(p, r, m0, C, Ys, srow, train, inv_valid, sums);
         }
-        // accumulate loss / metrics (wave 0 holds rows 0..63)
-        if (p.acc && p.Y && threadIdx.x < 64 * ((BM + 63) / 64)) {
-          float vals[6];
-          vals[0] = rvalid ? ro.loss : 0.f;
-          vals[1] = rvalid ? 1.f : 0.f;
-          for (int q = 0; q < 4; ++q) vals[2 + q] = rvalid ? ro.metric[q] : 0.f;
-          for (int q = 0; q < 2 + p.nmet; ++q) {
-            float s = row_sum<64>(vals[q]);
-            if ((threadIdx.x & 63) == 0 && s != 0.f)
-              atomicAdd(p.acc + (long long)r * p.acc_stride + q, (double)s);
-          }
-        }
-        if (train) {
-          __syncthreads();  // dz rows were produced by one thread per row
-          for (int e = threadIdx.x; e < BM * BN; e += 256) {
-            const int rr = e / BN, col = e % BN, gmm = m0 + rr;
-            if (gmm < p.M && col < p.N) st<T>(p.D, (long long)r * p.sD + (long long)gmm * p.ldd + col, C[rr * LDC + col]);
-          }
-          if (p.DT) {
-            for (int e = threadIdx.x; e < BM * BN; e += 256) {
-              const int col = e / BM, rr = e % BM, gmm = m0 + rr;
-              if (gmm < p.M && col < p.N)
-                st<T>(p.DT, (long long)r * p.sDT + (long long)col * p.lddt + gmm, C[rr * LDC + col]);
+        stamp(ga, 7);
+        if (p.acc && p.Y) {
+#pragma unroll
+          for (int q = 0; q < 6; ++q) {
+            if (q < 2 + p.nmet) {
+              const float s = row_sum<64>(sums[q]);
+              if ((threadIdx.x & 63) == 0 && s != 0.f)
+                atomicAdd(p.acc + (long long)r * p.acc_stride + q, (double)s);
             }
           }
+        }
+        stamp(ga, 8);
+        if (train) {
+          __syncthreads();  // dz rows were produced by lane groups
+#pragma unroll
+          for (int ps = 0; ps < PASSES; ++ps) {
+            const int row = ps * RPP + t_row, gm = m0 + row, gn0 = t_c0;
+            if (gm >= p.M || gn0 >= p.N) continue;
+            float v[8];
+            lds8(row, t_c0, v);
+#pragma unroll
+            for (int q = 0; q < 8; ++q)
+              if (gn0 + q >= p.N) v[q] = 0.f;
+            st8<T>(p.D, (long long)r * p.sD + (long long)gm * p.ldd + gn0, v);
+          }
+          if (p.DT) store_transposed(p.DT, (long long)r * p.sDT, p.lddt, p.M);
         }
         break;
       }
@@ -396,40 +643,75 @@ __global__ __launch_bounds__(256) void gemm_grouped(GroupArgs ga) {
       case PK_DW_GRAD: {
         if (skip_update) break;
         const bool upd = p.kind == PK_DW_UPDATE;
-        float* P = p.P + (long long)r * p.sP;
-        float* S = p.S ? p.S + (long long)r * p.sS : nullptr;
-        float* G = p.G ? p.G + (long long)r * p.sG : nullptr;
+        float* __restrict__ P = p.P + (long long)r * p.sP;
+        float* __restrict__ S = p.S ? p.S + (long long)r * p.sS : nullptr;
+        float* __restrict__ G = p.G ? p.G + (long long)r * p.sG : nullptr;
         const long long wpar = ((iter + 1) & 1);
-        for (int e = threadIdx.x; e < BM * BN; e += 256) {
-          const int row = e / BN, col = e % BN, gm = m0 + row, gn = n0 + col;
-          if (gm >= p.M || gn >= p.N) continue;
-          const float gval = C[row * LDC + col] * p.op.grad_scale;
-          const long long pidx = p.p_off + (long long)gm * p.N + gn;
+        const int krows = p.ones_row >= 0 ? p.ones_row : p.M;
+        const int np = S ? opt_planes(p.op) : 0;
+#pragma unroll
+        for (int ps = 0; ps < PASSES; ++ps) {
+          const int row = ps * RPP + t_row, gm = m0 + row, gn0 = n0 + t_c0;
+          if (gm >= p.M || gn0 >= p.N) continue;
+          float v[8];
+          lds8(row, t_c0, v);
+          const long long pidx = p.p_off + (long long)gm * p.N + gn0;
           if (!upd) {
-            if (valid > 0) G[pidx] = gval; else G[pidx] = 0.f;
+#pragma unroll
+            for (int q = 0; q < 8; ++q)
+              if (gn0 + q < p.N) G[pidx + q] = valid > 0 ? v[q] * p.op.grad_scale : 0.f;
             continue;
           }
-          const float w = opt_update(p.op, P[pidx], gval, S, pidx, iter);
-          P[pidx] = w;
-          C[row * LDC + col] = w;
-          if (gm < p.ones_row || p.ones_row < 0) {  // kernel row (not bias): refresh shadows
-            if (p.Wsh) st<T>(p.Wsh, (long long)r * p.sWsh + wpar * p.wsh_par + (long long)gm * p.ldwsh + gn, w);
+          float w[8], s0[8], s1[8];
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {  // loads first
+            const bool in = gn0 + q < p.N;
+            w[q] = in ? P[pidx + q] : 0.f;
+            s0[q] = (in && np > 0) ? S[pidx + q] : 0.f;
+            s1[q] = (in && np > 1) ? S[p.op.s_plane + pidx + q] : 0.f;
           }
+#pragma unroll
+          for (int q = 0; q < 8; ++q)
+            if (gn0 + q < p.N) w[q] = opt_update_reg(p.op, w[q], v[q] * p.op.grad_scale, s0[q], s1[q], iter);
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            if (gn0 + q < p.N) {
+              P[pidx + q] = w[q];
+              if (np > 0) S[pidx + q] = s0[q];
+              if (np > 1) S[p.op.s_plane + pidx + q] = s1[q];
+            } else {
+              w[q] = 0.f;
+            }
+          }
+          if (p.Wsh && gm < krows)
+            st8<T>(p.Wsh, (long long)r * p.sWsh + wpar * p.wsh_par + (long long)gm * p.ldwsh + gn0, w);
+          sts8(row, t_c0, w);
         }
         if (upd && p.WTsh) {
           __syncthreads();
-          for (int e = threadIdx.x; e < BM * BN; e += 256) {
-            const int col = e / BM, row = e % BM, gm = m0 + row, gn = n0 + col;
-            const int krows = p.ones_row >= 0 ? p.ones_row : p.M;
-            if (gm < krows && gn < p.N)
-              st<T>(p.WTsh, (long long)r * p.sWTsh + wpar * p.wtsh_par + (long long)gn * p.ldwtsh + gm, C[row * LDC + col]);
-          }
+          store_transposed(p.WTsh, (long long)r * p.sWTsh + wpar * p.wtsh_par, p.ldwtsh, krows);
         }
         break;
       }
     }
   }
 
+}
+
+// Kernel arguments are only ever indexed with compile-time constants (the
+// problem is picked by a wave-uniform branch), so hipcc keeps every Prob field
+// in the kernarg segment (scalar loads) instead of copying the struct to scratch.
+template <typename T, int WM, int WN, int WAVES_M, int WAVES_N, int KSPLIT>
+__global__ __launch_bounds__(256) void gemm_grouped(GroupArgs ga) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  stamp(ga, 0);
+  const int bid = blockIdx.x;
+  if (ga.nprob > 1 && bid >= ga.p[1].block_begin)
+    run_prob<T, WM, WN, WAVES_M, WAVES_N, KSPLIT>(ga, ga.p[1], bid - ga.p[1].block_begin, smem);
+  else
+    run_prob<T, WM, WN, WAVES_M, WAVES_N, KSPLIT>(ga, ga.p[0], bid - ga.p[0].block_begin, smem);
+
+  stamp(ga, 4);
   // ---- end-of-step counter advance (last arriving block)
   if (ga.advance) {
     __syncthreads();
@@ -452,12 +734,14 @@ __global__ __launch_bounds__(256) void gemm_grouped(GroupArgs ga) {
 
 // ------------------------------------------------------------- host side
 template <typename T, int WM, int WN, int WAVES_M, int WAVES_N, int KSPLIT>
-static size_t lds_bytes() {
+static size_t lds_bytes(bool loss = true) {
   constexpr int BM = WAVES_M * WM * 16;
   constexpr int BN = WAVES_N * WN * 16;
-  size_t lds = (size_t)KSPLIT * BM * (BN + 1) * sizeof(float);
-  if (lds < 64 * 65 * sizeof(float)) lds = 64 * 65 * sizeof(float);  // gather-transpose
-  return lds;
+  const size_t tile = (size_t)BM * (BN + 4);
+  size_t floats = (size_t)KSPLIT * tile;
+  if (loss) floats = std::max(floats, tile + BM + (size_t)BM * BN);  // + row map + staged targets
+  floats = std::max(floats, (size_t)64 * 65);                       // gather-transpose
+  return floats * sizeof(float);
 }
 
 template <typename T, int WM, int WN, int WAVES_M, int WAVES_N, int KSPLIT>
@@ -470,7 +754,9 @@ static void set_attr() {
 template <typename T, int WM, int WN, int WAVES_M, int WAVES_N, int KSPLIT>
 static hipError_t launch_cfg(const GroupArgs& ga, hipStream_t s) {
   if (ga.total_blocks <= 0) return hipSuccess;
-  const size_t lds = lds_bytes<T, WM, WN, WAVES_M, WAVES_N, KSPLIT>();
+  bool loss = false;
+  for (int i = 0; i < ga.nprob; ++i) loss |= ga.p[i].kind == PK_FWD_LOSS;
+  const size_t lds = lds_bytes<T, WM, WN, WAVES_M, WAVES_N, KSPLIT>(loss);
   hipLaunchKernelGGL((gemm_grouped<T, WM, WN, WAVES_M, WAVES_N, KSPLIT>), dim3(ga.total_blocks), dim3(256), lds, s,
                      ga);
   return hipGetLastError();

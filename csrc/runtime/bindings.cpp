@@ -162,7 +162,10 @@ PYBIND11_MODULE(_C, m) {
       })
       .def("destroy_graphs", &Executor::destroy_graphs)
       .def("launches_per_step", &Executor::launches_per_step)
-      .def("launch_cfgs", &Executor::launch_cfgs);
+      .def("launch_cfgs", &Executor::launch_cfgs)
+      .def("launch_blocks", &Executor::launch_blocks)
+      .def("set_stamps", &Executor::set_stamps)
+      .def("train_launch", [](Executor& e, int idx, uintptr_t s) { e.train_launch(idx, S(s)); });
 
   // single PLAIN GEMM (C fp32 = A . BT^T) for kernel tests / generic matmul
   m.def("gemm_nt", [](uintptr_t A, uintptr_t BT, uintptr_t C, int M, int N, int K, long long lda, long long ldb,

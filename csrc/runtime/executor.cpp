@@ -326,6 +326,24 @@ void Executor::run(const std::vector<Launch>& ls, hipStream_t s) const {
   for (const auto& L : ls) check(ea_gemm_grouped(&L.ga, c_.bf16, L.cfg, s), "gemm_grouped");
 }
 
+void Executor::train_launch(int idx, hipStream_t s) {
+  const int nf = (int)fwd_.size();
+  const Launch& L = idx < nf ? fwd_[idx] : bwd_[idx - nf];
+  check(ea_gemm_grouped(&L.ga, c_.bf16, L.cfg, s), "train_launch");
+}
+
+void Executor::set_stamps(uintptr_t buf) {
+  for (auto& L : fwd_) L.ga.stamps = reinterpret_cast<long long*>(buf);
+  for (auto& L : bwd_) L.ga.stamps = reinterpret_cast<long long*>(buf);
+}
+
+std::vector<int> Executor::launch_blocks() const {
+  std::vector<int> v;
+  for (auto& L : fwd_) v.push_back(L.ga.total_blocks);
+  for (auto& L : bwd_) v.push_back(L.ga.total_blocks);
+  return v;
+}
+
 std::vector<int> Executor::launch_cfgs() const {
   std::vector<int> v;
   for (auto& L : fwd_) v.push_back(L.cfg);

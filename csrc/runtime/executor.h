@@ -85,6 +85,10 @@ class Executor {
 
   int launches_per_step() const { return (int)fwd_.size() + (int)bwd_.size(); }
   std::vector<int> launch_cfgs() const;
+  // diagnostics: bind a [blocks_max][16] int64 buffer for in-kernel stamps (0 = off)
+  void set_stamps(uintptr_t buf);
+  void train_launch(int idx, hipStream_t s);
+  std::vector<int> launch_blocks() const;
 
  private:
   struct Launch {

@@ -105,6 +105,11 @@ class Optimizer:
 class SGD(Optimizer):
     _defaults = {"learning_rate": 0.01, "momentum": 0.0, "nesterov": False}
 
+    def __init__(self, learning_rate=0.01, momentum=0.0, nesterov=False, name="SGD", **kwargs):
+        if "lr" in kwargs:  # legacy keras argument
+            learning_rate = kwargs.pop("lr")
+        super().__init__(name=name, learning_rate=learning_rate, momentum=momentum, nesterov=nesterov, **kwargs)
+
     def native(self):
         h = self._hyper
         return OPT_SGD, {"lr": h["learning_rate"], "momentum": h["momentum"], "nesterov": int(bool(h["nesterov"])),
@@ -131,6 +136,11 @@ class SGD(Optimizer):
 
 class RMSprop(Optimizer):
     _defaults = {"learning_rate": 0.001, "rho": 0.9, "momentum": 0.0, "epsilon": 1e-7, "centered": False}
+
+    def __init__(self, learning_rate=0.001, rho=0.9, momentum=0.0, epsilon=1e-07, centered=False, name="RMSprop", **kwargs):
+        if "lr" in kwargs:  # legacy keras argument
+            learning_rate = kwargs.pop("lr")
+        super().__init__(name=name, learning_rate=learning_rate, rho=rho, momentum=momentum, epsilon=epsilon, centered=centered, **kwargs)
 
     def native(self):
         h = self._hyper
@@ -169,6 +179,11 @@ class RMSprop(Optimizer):
 class Adam(Optimizer):
     _defaults = {"learning_rate": 0.001, "beta_1": 0.9, "beta_2": 0.999, "epsilon": 1e-7, "amsgrad": False}
 
+    def __init__(self, learning_rate=0.001, beta_1=0.9, beta_2=0.999, epsilon=1e-07, amsgrad=False, name="Adam", **kwargs):
+        if "lr" in kwargs:  # legacy keras argument
+            learning_rate = kwargs.pop("lr")
+        super().__init__(name=name, learning_rate=learning_rate, beta_1=beta_1, beta_2=beta_2, epsilon=epsilon, amsgrad=amsgrad, **kwargs)
+
     def native(self):
         h = self._hyper
         if h["amsgrad"]:
@@ -200,6 +215,11 @@ class Adam(Optimizer):
 class Adagrad(Optimizer):
     _defaults = {"learning_rate": 0.001, "initial_accumulator_value": 0.1, "epsilon": 1e-7}
 
+    def __init__(self, learning_rate=0.001, initial_accumulator_value=0.1, epsilon=1e-07, name="Adagrad", **kwargs):
+        if "lr" in kwargs:  # legacy keras argument
+            learning_rate = kwargs.pop("lr")
+        super().__init__(name=name, learning_rate=learning_rate, initial_accumulator_value=initial_accumulator_value, epsilon=epsilon, **kwargs)
+
     def native(self):
         h = self._hyper
         return OPT_ADAGRAD, {"lr": h["learning_rate"], "epsilon": h["epsilon"], "decay": h["decay"],
@@ -221,6 +241,11 @@ class Adagrad(Optimizer):
 
 class Adamax(Optimizer):
     _defaults = {"learning_rate": 0.001, "beta_1": 0.9, "beta_2": 0.999, "epsilon": 1e-7}
+
+    def __init__(self, learning_rate=0.001, beta_1=0.9, beta_2=0.999, epsilon=1e-07, name="Adamax", **kwargs):
+        if "lr" in kwargs:  # legacy keras argument
+            learning_rate = kwargs.pop("lr")
+        super().__init__(name=name, learning_rate=learning_rate, beta_1=beta_1, beta_2=beta_2, epsilon=epsilon, **kwargs)
 
     def native(self):
         h = self._hyper
@@ -245,6 +270,11 @@ class Adamax(Optimizer):
 class Adadelta(Optimizer):
     _defaults = {"learning_rate": 0.001, "rho": 0.95, "epsilon": 1e-7}
 
+    def __init__(self, learning_rate=0.001, rho=0.95, epsilon=1e-07, name="Adadelta", **kwargs):
+        if "lr" in kwargs:  # legacy keras argument
+            learning_rate = kwargs.pop("lr")
+        super().__init__(name=name, learning_rate=learning_rate, rho=rho, epsilon=epsilon, **kwargs)
+
     def n_state(self):
         return 2
 
@@ -262,6 +292,11 @@ class Adadelta(Optimizer):
 
 class Nadam(Optimizer):
     _defaults = {"learning_rate": 0.001, "beta_1": 0.9, "beta_2": 0.999, "epsilon": 1e-7}
+
+    def __init__(self, learning_rate=0.001, beta_1=0.9, beta_2=0.999, epsilon=1e-07, name="Nadam", **kwargs):
+        if "lr" in kwargs:  # legacy keras argument
+            learning_rate = kwargs.pop("lr")
+        super().__init__(name=name, learning_rate=learning_rate, beta_1=beta_1, beta_2=beta_2, epsilon=epsilon, **kwargs)
 
     def n_state(self):
         return 2

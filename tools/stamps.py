@@ -1,0 +1,36 @@
+"""In-kernel phase stamps for each launch of one training step (diagnostics)."""
+import os, sys, numpy as np, torch
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bench
+from elephas_amd import config
+from elephas_amd.ops.plan import build_plan
+from elephas_amd.ops.native_engine import NativeTrainer
+config.set_policy("mixed_bfloat16")
+m = bench.build_model("mnist")
+R = int(sys.argv[1]) if len(sys.argv) > 1 else 8
+t = NativeTrainer(m, build_plan(m), R, 64, torch.device("cuda"))
+rng = np.random.default_rng(0)
+xs = [rng.random((7500, 784), dtype=np.float32) for _ in range(R)]
+ys = [np.eye(10, dtype=np.float32)[rng.integers(0, 10, 7500)] for _ in range(R)]
+t.set_data(xs, ys, 0.1)
+t.begin_epoch()
+t.run_steps(30)
+blocks = t.exe.launch_blocks()
+buf = torch.zeros(max(blocks) * 16, dtype=torch.int64, device="cuda")
+t.exe.set_stamps(buf.data_ptr())
+names = ["start", "setup", "mainloop", "reduce", "end", "e5", "e6", "e7", "e8"]
+for rep in range(2):
+    for i, nb in enumerate(blocks):
+        buf.zero_()
+        torch.cuda.synchronize()
+        t.exe.train_launch(i, t.s)
+        t.stream.synchronize()
+        st = buf[:nb * 16].view(nb, 16)[:, :9].cpu().numpy().astype(np.int64)
+        t0 = st[:, 0].min()
+        rel = np.where(st > 0, (st - t0) * 10.0, np.nan)  # ns
+        med = np.nanmedian(rel, axis=0)
+        mx = np.nanmax(rel, axis=0)
+        if rep == 1:
+            print(f"launch {i} blocks {nb}: median(ns) " + " ".join(f"{n}={v:.0f}" for n, v in zip(names, med)) +
+                  f" | max end {mx[4]:.0f} | start spread {mx[0]:.0f}", flush=True)
+t.exe.set_stamps(0)
