@@ -90,9 +90,13 @@ struct GroupArgs {
   int total_blocks;
   long long* ctr;           // [0]=step in epoch, [1]=arrive counter, [2..2+R)=iter per replica
   unsigned long long seed;
-  int advance;              // this launch ends the step: last block advances counters
-  int adv_R; int adv_B;     // replicas / batch for the advance
-  const int* adv_ntrain;
+  // Step counters: ctr[0] = base step-in-epoch, ctr[2 + r] = base optimizer
+  // iteration of replica r. Kernels only READ them: a launch at position
+  // `step_off` of a captured chunk uses step = ctr[0] + step_off and
+  // iter_r = ctr[2+r] + clamp(nb_r - ctr[0], 0, step_off) (nb_r = batches of
+  // replica r per epoch); one 1-block advance kernel per chunk moves the base.
+  // (No same-address atomics in the step: those serialise at ~60 ns each.)
+  int step_off;
   long long* stamps;        // diagnostics: [block][16] s_memrealtime stamps (null = off)
 };
 
@@ -119,7 +123,6 @@ struct FlatArgs {
   void* WTsh; long long sWTsh, wtsh_par;
   long long* ctr;
   const int* ntrain; int B;
-  int advance;
   int both_parities;  // refresh: write both shadow parities
   int total_blocks;
 };

@@ -519,4 +519,14 @@ struct Counters {
   __device__ long long step() const { return base[0]; }
 };
 
+// ------------------------------------------------------------ step counters
+// see GroupArgs::step_off (args.h)
+__device__ __forceinline__ long long iter_at(const long long* ctr, const int* ntrain, int B, int r, long long s0,
+                                             int off) {
+  const long long nb = ((long long)ntrain[r] + B - 1) / B;
+  long long d = nb - s0;
+  d = d < 0 ? 0 : (d > off ? off : d);
+  return ctr[2 + r] + d;
+}
+
 }  // namespace ea

@@ -41,20 +41,16 @@ __device__ __forceinline__ void write_shadow(const FlatArgs& a, int r, long long
     reinterpret_cast<T*>(a.WTsh)[(long long)r * a.sWTsh + par * a.wtsh_par + g.wtsh_off + nn * g.ldwtsh + k] = from_f<T>(w);
 }
 
-__device__ __forceinline__ void arrive_and_advance(const FlatArgs& a) {
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __threadfence();
-    unsigned long long prev = atomicAdd(reinterpret_cast<unsigned long long*>(a.ctr + 1), 1ull);
-    if (prev == (unsigned long long)(a.total_blocks - 1)) {
-      const long long s = a.ctr[0];
-      for (int r = 0; r < a.R; ++r)
-        if ((long long)a.ntrain[r] - s * a.B > 0) a.ctr[2 + r] += 1;
-      a.ctr[0] = s + 1;
-      a.ctr[1] = 0;
-      __threadfence();
-    }
+// Move the step-counter base by n steps (one block; see GroupArgs::step_off).
+__global__ __launch_bounds__(64) void advance_kernel(long long* ctr, const int* ntrain, int R, int B, int n) {
+  const long long s0 = ctr[0];
+  for (int r = threadIdx.x; r < R; r += 64) {
+    const long long nb = ((long long)ntrain[r] + B - 1) / B;
+    long long d = nb - s0;
+    ctr[2 + r] += d < 0 ? 0 : (d > n ? n : d);
   }
+  __syncthreads();
+  if (threadIdx.x == 0) ctr[0] = s0 + n;
 }
 
 // grid: total_blocks over R*n elements
@@ -73,7 +69,6 @@ __global__ __launch_bounds__(256) void apply_update_kernel(FlatArgs a) {
     a.P[(long long)r * a.sP + i] = w;
     write_shadow<T>(a, r, i, w, (iter + 1) & 1);
   }
-  if (a.advance) arrive_and_advance(a);
 }
 
 template <typename T>
@@ -160,6 +155,11 @@ extern "C" hipError_t ea_apply_update(FlatArgs* a, int bf16, hipStream_t s) {
   a->total_blocks = grid_for((long long)a->R * a->n);
   if (bf16) hipLaunchKernelGGL(apply_update_kernel<__bf16>, dim3(a->total_blocks), dim3(256), 0, s, *a);
   else hipLaunchKernelGGL(apply_update_kernel<float>, dim3(a->total_blocks), dim3(256), 0, s, *a);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t ea_advance(long long* ctr, const int* ntrain, int R, int B, int n, hipStream_t s) {
+  hipLaunchKernelGGL(advance_kernel, dim3(1), dim3(64), 0, s, ctr, ntrain, R, B, n);
   return hipGetLastError();
 }
 

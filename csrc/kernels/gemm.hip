@@ -85,7 +85,7 @@ __device__ __forceinline__ void gather_transpose_block(const GroupArgs& ga, cons
   const int t = lb % per_r;
   const int b0 = (t / p.tiles_n) * 64;
   const int k0 = (t % p.tiles_n) * 64;
-  const long long step = ga.ctr[0];
+  const long long step = ga.ctr[0] + ga.step_off;
   const int valid = batch_valid(p, r, step);
   const T* A = reinterpret_cast<const T*>(p.A) + (long long)r * p.sA;
   T* XT = reinterpret_cast<T*>(p.DT) + (long long)r * p.sDT;
@@ -116,7 +116,7 @@ __device__ __forceinline__ void loss_rows_block(const GroupArgs& ga, const Prob&
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int row = (lb % p.tiles_m) * 4 + wave;
   if (row >= p.M) return;
-  const long long step = ga.ctr[0];
+  const long long step = ga.ctr[0] + ga.step_off;
   const int valid = batch_valid(p, r, step);
   const bool train = !p.eval_mode && p.D;
   const float inv_valid = valid > 0 ? 1.f / (float)valid : 0.f;
@@ -318,6 +318,10 @@ __device__ __forceinline__ void loss_tile_lds(const Prob& p, int r, int m0, floa
 __device__ __forceinline__ void stamp(const GroupArgs& ga, int k) {
   if (ga.stamps && threadIdx.x == 0) ga.stamps[(long long)blockIdx.x * 16 + k] = (long long)__builtin_amdgcn_s_memrealtime();
 }
+// shader-clock counter (slots 10..15) to estimate the SCLK the kernel runs at
+__device__ __forceinline__ void stamp_clk(const GroupArgs& ga, int k) {
+  if (ga.stamps && threadIdx.x == 0) ga.stamps[(long long)blockIdx.x * 16 + k] = (long long)__builtin_amdgcn_s_memtime();
+}
 
 // --------------------------------------------------------------- the kernel
 template <typename T, int WM, int WN, int WAVES_M, int WAVES_N, int KSPLIT>
@@ -337,8 +341,8 @@ __device__ __forceinline__ void run_prob(const GroupArgs& ga, const Prob& p, con
     const int t = lb % per_r;
     const int tm = t / p.tiles_n, tn = t % p.tiles_n;
     const int m0 = tm * BM, n0 = tn * BN;
-    const long long step = ga.ctr[0];
-    const long long iter = ga.ctr[2 + r];
+    const long long step = ga.ctr[0] + ga.step_off;
+    const long long iter = iter_at(ga.ctr, p.ntrain, p.B, r, ga.ctr[0], ga.step_off);
     const int valid = (p.kind == PK_PLAIN) ? p.M : batch_valid(p, r, step);
     const bool skip_update = (p.kind == PK_DW_UPDATE) && valid == 0;
     stamp(ga, 1);
@@ -673,6 +677,7 @@ __device__ __forceinline__ void run_prob(const GroupArgs& ga, const Prob& p, con
 #pragma unroll
           for (int q = 0; q < 8; ++q)
             if (gn0 + q < p.N) w[q] = opt_update_reg(p.op, w[q], v[q] * p.op.grad_scale, s0[q], s1[q], iter);
+          if (ps == 0) stamp(ga, 5);
 #pragma unroll
           for (int q = 0; q < 8; ++q) {
             if (gn0 + q < p.N) {
@@ -687,9 +692,12 @@ __device__ __forceinline__ void run_prob(const GroupArgs& ga, const Prob& p, con
             st8<T>(p.Wsh, (long long)r * p.sWsh + wpar * p.wsh_par + (long long)gm * p.ldwsh + gn0, w);
           sts8(row, t_c0, w);
         }
+        stamp(ga, 6);
         if (upd && p.WTsh) {
           __syncthreads();
+          stamp(ga, 7);
           store_transposed(p.WTsh, (long long)r * p.sWTsh + wpar * p.wtsh_par, p.ldwtsh, krows);
+          stamp(ga, 8);
         }
         break;
       }
@@ -705,6 +713,7 @@ template <typename T, int WM, int WN, int WAVES_M, int WAVES_N, int KSPLIT>
 __global__ __launch_bounds__(256) void gemm_grouped(GroupArgs ga) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   stamp(ga, 0);
+  stamp_clk(ga, 10);
   const int bid = blockIdx.x;
   if (ga.nprob > 1 && bid >= ga.p[1].block_begin)
     run_prob<T, WM, WN, WAVES_M, WAVES_N, KSPLIT>(ga, ga.p[1], bid - ga.p[1].block_begin, smem);
@@ -712,24 +721,7 @@ __global__ __launch_bounds__(256) void gemm_grouped(GroupArgs ga) {
     run_prob<T, WM, WN, WAVES_M, WAVES_N, KSPLIT>(ga, ga.p[0], bid - ga.p[0].block_begin, smem);
 
   stamp(ga, 4);
-  // ---- end-of-step counter advance (last arriving block)
-  if (ga.advance) {
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      __threadfence();
-      unsigned long long prev = atomicAdd(reinterpret_cast<unsigned long long*>(ga.ctr + 1), 1ull);
-      if (prev == (unsigned long long)(ga.total_blocks - 1)) {
-        const long long s = ga.ctr[0];
-        for (int r = 0; r < ga.adv_R; ++r) {
-          long long c = (long long)ga.adv_ntrain[r] - s * ga.adv_B;
-          if (c > 0) ga.ctr[2 + r] += 1;
-        }
-        ga.ctr[0] = s + 1;
-        ga.ctr[1] = 0;
-        __threadfence();
-      }
-    }
-  }
+  stamp_clk(ga, 11);
 }
 
 // ------------------------------------------------------------- host side

@@ -11,6 +11,7 @@ extern "C" int ea_gemm_tile_n(int cfg);
 extern "C" void ea_gemm_init();
 extern "C" hipError_t ea_apply_update(ea::FlatArgs* a, int bf16, hipStream_t s);
 extern "C" hipError_t ea_refresh_shadows(ea::FlatArgs* a, int bf16, hipStream_t s);
+extern "C" hipError_t ea_advance(long long* ctr, const int* ntrain, int R, int B, int n, hipStream_t s);
 
 namespace ea {
 
@@ -85,9 +86,6 @@ void Executor::finalize(Launch& L) const {
   L.ga.total_blocks = begin;
   L.ga.ctr = reinterpret_cast<long long*>(c_.ctr);
   L.ga.seed = c_.seed;
-  L.ga.adv_R = c_.R;
-  L.ga.adv_B = c_.B;
-  L.ga.adv_ntrain = reinterpret_cast<const int*>(c_.ntrain);
 }
 
 std::vector<Executor::Launch> Executor::build_forward(bool eval, long long chunk, const EvalSource* src) const {
@@ -316,20 +314,28 @@ void Executor::build() {
       if (xw > work) { cm = x.M; cn = x.N; ck = x.K; }
     }
     La.cfg = pick_cfg(cm, cn, ck);
-    La.ga.advance = (l == 0) ? 1 : 0;
     finalize(La);
     bwd_.push_back(La);
   }
 }
 
-void Executor::run(const std::vector<Launch>& ls, hipStream_t s) const {
-  for (const auto& L : ls) check(ea_gemm_grouped(&L.ga, c_.bf16, L.cfg, s), "gemm_grouped");
+void Executor::run(const std::vector<Launch>& ls, hipStream_t s, int step_off) const {
+  for (const auto& L : ls) {
+    GroupArgs ga = L.ga;
+    ga.step_off = step_off;
+    check(ea_gemm_grouped(&ga, c_.bf16, L.cfg, s), "gemm_grouped");
+  }
+}
+
+void Executor::advance(int nsteps, hipStream_t s) const {
+  check(ea_advance(reinterpret_cast<long long*>(c_.ctr), reinterpret_cast<const int*>(c_.ntrain), c_.R, c_.B, nsteps, s),
+        "advance");
 }
 
 void Executor::train_launch(int idx, hipStream_t s) {
   const int nf = (int)fwd_.size();
   const Launch& L = idx < nf ? fwd_[idx] : bwd_[idx - nf];
-  check(ea_gemm_grouped(&L.ga, c_.bf16, L.cfg, s), "train_launch");
+  check(ea_gemm_grouped(&L.ga, c_.bf16, L.cfg, s), "train_launch");  // step_off 0, no advance
 }
 
 void Executor::set_stamps(uintptr_t buf) {
@@ -352,16 +358,17 @@ std::vector<int> Executor::launch_cfgs() const {
 }
 
 void Executor::train_step(hipStream_t s) {
-  run(fwd_, s);
-  run(bwd_, s);
+  run(fwd_, s, 0);
+  run(bwd_, s, 0);
+  advance(1, s);
 }
 
 void Executor::forward_backward(hipStream_t s) {
-  run(fwd_, s);
+  run(fwd_, s, 0);
   for (auto L : bwd_) {
     for (int i = 0; i < L.ga.nprob; ++i)
       if (L.ga.p[i].kind == PK_DW_UPDATE) L.ga.p[i].kind = PK_DW_GRAD;
-    L.ga.advance = 0;
+    L.ga.step_off = 0;
     check(ea_gemm_grouped(&L.ga, c_.bf16, L.cfg, s), "gemm_grouped(grad)");
   }
 }
@@ -405,8 +412,8 @@ FlatArgs Executor::flat_args() const {
 
 void Executor::apply(hipStream_t s) {
   FlatArgs a = flat_args();
-  a.advance = 1;
   check(ea_apply_update(&a, c_.bf16, s), "apply_update");
+  advance(1, s);
 }
 
 void Executor::refresh_shadows(bool both, hipStream_t s) {
@@ -421,7 +428,7 @@ void Executor::reset_epoch(hipStream_t s) {
 
 void Executor::eval_chunk(long long chunk, const EvalSource& src, hipStream_t s) {
   auto ls = build_forward(true, chunk, &src);
-  run(ls, s);
+  run(ls, s, 0);
 }
 
 int Executor::capture(int nsteps, int mode, hipStream_t s) {
@@ -429,10 +436,18 @@ int Executor::capture(int nsteps, int mode, hipStream_t s) {
   hipGraphExec_t e = nullptr;
   check(hipStreamBeginCapture(s, hipStreamCaptureModeRelaxed), "hipStreamBeginCapture");
   try {
-    for (int i = 0; i < nsteps; ++i) {
-      if (mode == 0) train_step(s);
-      else if (mode == 1) forward_backward(s);
-      else apply(s);
+    if (mode == 0) {
+      // one chunk: steps at offsets 0..nsteps-1 from the counter base, then one advance
+      for (int i = 0; i < nsteps; ++i) {
+        run(fwd_, s, i);
+        run(bwd_, s, i);
+      }
+      advance(nsteps, s);
+    } else {
+      for (int i = 0; i < nsteps; ++i) {
+        if (mode == 1) forward_backward(s);
+        else apply(s);
+      }
     }
   } catch (...) {
     hipGraph_t dummy;

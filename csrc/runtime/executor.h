@@ -83,6 +83,7 @@ class Executor {
   void replay(int graph_id, hipStream_t s);
   void destroy_graphs();
 
+  // GEMM launches per step (a captured chunk adds one 1-block counter advance)
   int launches_per_step() const { return (int)fwd_.size() + (int)bwd_.size(); }
   std::vector<int> launch_cfgs() const;
   // diagnostics: bind a [blocks_max][16] int64 buffer for in-kernel stamps (0 = off)
@@ -104,7 +105,8 @@ class Executor {
   int pick_cfg(long long M, long long N, long long K) const;
   std::vector<Launch> build_forward(bool eval, long long chunk, const EvalSource* src) const;
   void build();
-  void run(const std::vector<Launch>& ls, hipStream_t s) const;
+  void run(const std::vector<Launch>& ls, hipStream_t s, int step_off) const;
+  void advance(int nsteps, hipStream_t s) const;
   FlatArgs flat_args() const;
 };
 

@@ -30,7 +30,11 @@ for rep in range(2):
         rel = np.where(st > 0, (st - t0) * 10.0, np.nan)  # ns
         med = np.nanmedian(rel, axis=0)
         mx = np.nanmax(rel, axis=0)
+        clk = buf[:nb * 16].view(nb, 16).cpu().numpy().astype(np.int64)
+        ok = (clk[:, 11] > 0) & (clk[:, 10] > 0)
+        mhz = np.median((clk[ok, 11] - clk[ok, 10]) / ((clk[ok, 4] - clk[ok, 0]) * 10e-3))
         if rep == 1:
+            print(f"  est. s_memtime MHz {mhz:.0f}", flush=True)
             print(f"launch {i} blocks {nb}: median(ns) " + " ".join(f"{n}={v:.0f}" for n, v in zip(names, med)) +
                   f" | max end {mx[4]:.0f} | start spread {mx[0]:.0f}", flush=True)
 t.exe.set_stamps(0)
