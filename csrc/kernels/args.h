@@ -127,4 +127,57 @@ struct FlatArgs {
   int total_blocks;
 };
 
+// ------------------------------------------------------------ fused MLP tail
+// One workgroup per replica runs, for layers 1..L-1 of a small MLP, the
+// forward pass, the loss, and the backward pass with every weight update, with
+// all activations resident in LDS (see fused.hip). Layer 0's forward (wide K)
+// and weight update (many tiles) stay on the grouped GEMM kernel.
+constexpr int FUSED_MAX_L = 8;
+
+struct FusedLayer {
+  int K, N, Kp, Np;        // dims; Kp/Np padded to 8
+  int act, has_bias;
+  float rate;
+  int ldA;                 // LDS row stride (elements) of this layer's output D_l / dZ_l tiles
+  int offD;                // LDS byte offset of D_l (compute dtype, [64][ldA]) (l < L-1)
+  int offG;                // LDS byte offset of G_l (fp32 [64][ldG]): z, then act'(z)*dropout (l < L-1)
+  int ldG;
+  int pvec;                // P/S rows of this layer allow float4 access (N % 4 == 0, p_off % 4 == 0)
+  long long p_off;         // flat parameter offset (kernel K*N, then bias N)
+  long long wsh_off, wtsh_off;
+};
+
+struct FusedArgs {
+  int L;
+  int nsplit;              // workgroups per replica (each owns 1/nsplit of the update tiles)
+  const FusedLayer* ly;    // device array [L] (uniform loads)
+  int R, B, Bp;
+  // layer-0 outputs of the grouped forward launch
+  const void* D0; long long sD0;   // [B][Np0] compute dtype
+  const float* Z0; long long sZ0;  // [B][N0]  fp32
+  // targets
+  const float* Y; long long sY, ldy;
+  const int* perm; long long sPerm;
+  const int* ntrain;
+  // out: dZ_0^T [N0][Bp] (B^T operand of the layer-0 weight update)
+  void* dZ0T; long long sdZ0T;
+  // parameters
+  float* P; long long sP;
+  float* S; long long sS;
+  OptParams op;
+  void* Wsh; long long sWsh, wsh_par;
+  void* WTsh; long long sWTsh, wtsh_par;
+  int loss, nmet, met[4];
+  double* acc; int acc_stride;
+  long long* ctr; int step_off;
+  unsigned long long seed;
+  // LDS layout
+  int offLg, ldLg;         // logits / dZ_{L-1} fp32 [64][ldLg]
+  int offdZ0, offdZ1;      // dZ ping-pong (compute dtype [64][lddZ])
+  int lddZ;
+  int offY, offSrow;       // targets fp32 [64][32], row flags int[64]
+  int lds_bytes;
+  long long* stamps;
+};
+
 }  // namespace ea

@@ -5,8 +5,8 @@
 //  * GEMM-shaped work runs on MFMA: bf16 operands use v_mfma_f32_16x16x32_bf16,
 //    fp32 operands use the exact-f32 v_mfma_f32_16x16x4_f32 (no xf32 on gfx950).
 //  * Activation / dropout / loss / optimizer math is fused into GEMM epilogues.
-//  * Dropout masks are counter-based (Philox4x32-10) so backward regenerates them
-//    instead of storing them.
+//  * Dropout masks are counter-based (a hash of seed/replica/layer/iteration/
+//    row/column) so backward regenerates them instead of storing them.
 //
 // Semantics mirror tf.keras 2.10 as used by the reference
 // (reference: elephas/worker.py:41-42 model.fit, tests/conftest.py:8-40 layer set).
@@ -30,36 +30,36 @@ template <typename T> __device__ __forceinline__ T from_f(float v);
 template <> __device__ __forceinline__ float from_f<float>(float v) { return v; }
 template <> __device__ __forceinline__ __bf16 from_f<__bf16>(float v) { return (__bf16)v; }
 
-// --------------------------------------------------------------- Philox ----
-// Philox4x32-10 (Salmon et al. 2011). Counter-based: mask(element) is a pure
-// function of (seed, replica, layer, iteration, element) -> bwd regenerates it.
-template <int ROUNDS>
-__device__ __forceinline__ uint4 philox4x32_r(uint4 c, uint2 k) {
-  const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u;
-  const uint32_t W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
-#pragma unroll
-  for (int i = 0; i < ROUNDS; ++i) {
-    uint32_t hi0 = __umulhi(M0, c.x), lo0 = M0 * c.x;
-    uint32_t hi1 = __umulhi(M1, c.z), lo1 = M1 * c.z;
-    c = make_uint4(hi1 ^ c.y ^ k.x, lo1, hi0 ^ c.w ^ k.y, lo0);
-    k.x += W0; k.y += W1;
-  }
-  return c;
+// ---------------------------------------------------------------- dropout
+// keep iff u >= rate (tf.nn.dropout semantics), kept values scaled by 1/(1-rate).
+// Dropout keep-uniforms as a pure function of (seed, replica, layer, iteration,
+// batch row, column), so forward and backward (and the grouped and fused
+// kernels) regenerate identical masks without storing them. One murmur3 fmix32
+// (2 quarter-rate multiplies) per column PAIR yields two 16-bit uniforms --
+// ~6x cheaper than a Philox4x32-7 call per 4 columns; keep-probability error
+// < 2^-16. The per-(replica, layer, iteration) base is hoisted by the caller.
+__device__ __forceinline__ uint32_t fmix32(uint32_t h) {
+  h ^= h >> 16;
+  h *= 0x85EBCA6Bu;
+  h ^= h >> 13;
+  h *= 0xC2B2AE35u;
+  h ^= h >> 16;
+  return h;
 }
-
-// Uniform in [0,1) for one element; keep iff u >= rate (tf.nn.dropout semantics).
-// Dropout uniforms for the 4 columns [4*cg, 4*cg+4) of row `row`: one
-// Philox4x32-7 call (counter = (cg, row, iter, layer/replica), key = seed ^
-// replica) yields all four. Forward and backward regenerate the same mask
-// from the same counters, so no mask is stored.
-__device__ __forceinline__ float4 dropout_u4(uint64_t seed, int replica, int layer, long long iter,
-                                             long long row, long long cg) {
-  uint4 c = make_uint4((uint32_t)cg, (uint32_t)row, (uint32_t)iter,
-                       ((uint32_t)(iter >> 32) & 0xFFFFu) ^ ((uint32_t)layer << 16) ^ ((uint32_t)replica << 24));
-  uint2 k = make_uint2((uint32_t)seed ^ (uint32_t)replica * 0x85EBCA6Bu, (uint32_t)(seed >> 32));
-  const uint4 r = philox4x32_r<7>(c, k);
-  constexpr float s = 1.0f / 16777216.0f;
-  return make_float4((float)(r.x >> 8) * s, (float)(r.y >> 8) * s, (float)(r.z >> 8) * s, (float)(r.w >> 8) * s);
+__device__ __forceinline__ uint32_t dropout_base(uint64_t seed, int replica, int layer, long long iter) {
+  return fmix32((uint32_t)seed ^ fmix32((uint32_t)iter * 0x9E3779B1u ^ (uint32_t)((unsigned long long)iter >> 32) ^
+                                        ((uint32_t)layer << 24) ^ (uint32_t)replica * 0x27D4EB2Fu ^
+                                        (uint32_t)(seed >> 32)));
+}
+// uniforms for columns c0 .. c0+7 (c0 % 8 == 0) of batch row `row` (< 65536)
+__device__ __forceinline__ void dropout_u8(uint32_t base, int row, int c0, float (&u)[8]) {
+  constexpr float s = 1.0f / 65536.0f;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const uint32_t h = fmix32(base ^ (((uint32_t)row << 16) | (uint32_t)((c0 >> 1) + j)));
+    u[2 * j] = (float)(h & 0xFFFFu) * s;
+    u[2 * j + 1] = (float)(h >> 16) * s;
+  }
 }
 
 // ----------------------------------------------------------- activations ----
@@ -107,6 +107,62 @@ __device__ __forceinline__ float act_grad(int act, float z) {
     case ACT_RELU6: return (z > 0.f && z < 6.f) ? 1.f : 0.f;
     default: return 1.f;
   }
+}
+
+// Vector forms: the activation is uniform per layer, so dispatch ONCE and run a
+// compact per-case loop. Inlining the scalar switch per element (8-32 copies)
+// made kernels 0.3-1.3 MB and their executed path instruction-fetch bound.
+#define EA_ACTS(X)                                                                                   \
+  X(ACT_RELU, fmaxf(x, 0.f), (x > 0.f ? 1.f : 0.f))                                                  \
+  X(ACT_SIGMOID, sigmoidf_(x), (sigmoidf_(x) * (1.f - sigmoidf_(x))))                                \
+  X(ACT_TANH, tanhf(x), (1.f - tanhf(x) * tanhf(x)))                                                 \
+  X(ACT_ELU, (x > 0.f ? x : expm1f(x)), (x > 0.f ? 1.f : __expf(x)))                                 \
+  X(ACT_SELU, 1.0507009873554805f * (x > 0.f ? x : 1.6732632423543772f * expm1f(x)),                  \
+    1.0507009873554805f * (x > 0.f ? 1.f : 1.6732632423543772f * __expf(x)))                          \
+  X(ACT_SOFTPLUS, softplusf_(x), sigmoidf_(x))                                                       \
+  X(ACT_SOFTSIGN, x / (fabsf(x) + 1.f), 1.f / ((fabsf(x) + 1.f) * (fabsf(x) + 1.f)))                 \
+  X(ACT_EXPONENTIAL, __expf(x), __expf(x))                                                            \
+  X(ACT_HARD_SIGMOID, fminf(fmaxf(0.2f * x + 0.5f, 0.f), 1.f), ((x > -2.5f && x < 2.5f) ? 0.2f : 0.f)) \
+  X(ACT_SWISH, x * sigmoidf_(x), (sigmoidf_(x) + x * sigmoidf_(x) * (1.f - sigmoidf_(x))))          \
+  X(ACT_GELU, 0.5f * x * (1.f + erff(x * 0.7071067811865476f)),                                       \
+    0.5f * (1.f + erff(x * 0.7071067811865476f)) + x * 0.3989422804014327f * __expf(-0.5f * x * x))   \
+  X(ACT_RELU6, fminf(fmaxf(x, 0.f), 6.f), ((x > 0.f && x < 6.f) ? 1.f : 0.f))
+
+template <int NV>
+__device__ __forceinline__ void act_fg_v(int act, const float (&z)[NV], float (&o)[NV], float (&g)[NV]) {
+#define EA_CASE_FG(ID, F, G) \
+  case ID:                   \
+    _Pragma("unroll") for (int q = 0; q < NV; ++q) { const float x = z[q]; o[q] = (F); g[q] = (G); } break;
+  switch (act) {
+    EA_ACTS(EA_CASE_FG)
+    default:
+      _Pragma("unroll") for (int q = 0; q < NV; ++q) { o[q] = z[q]; g[q] = 1.f; }
+  }
+#undef EA_CASE_FG
+}
+template <int NV>
+__device__ __forceinline__ void act_f_v(int act, const float (&z)[NV], float (&o)[NV]) {
+#define EA_CASE_F(ID, F, G) \
+  case ID:                  \
+    _Pragma("unroll") for (int q = 0; q < NV; ++q) { const float x = z[q]; o[q] = (F); } break;
+  switch (act) {
+    EA_ACTS(EA_CASE_F)
+    default:
+      _Pragma("unroll") for (int q = 0; q < NV; ++q) o[q] = z[q];
+  }
+#undef EA_CASE_F
+}
+template <int NV>
+__device__ __forceinline__ void act_g_v(int act, const float (&z)[NV], float (&g)[NV]) {
+#define EA_CASE_G(ID, F, G) \
+  case ID:                  \
+    _Pragma("unroll") for (int q = 0; q < NV; ++q) { const float x = z[q]; g[q] = (G); } break;
+  switch (act) {
+    EA_ACTS(EA_CASE_G)
+    default:
+      _Pragma("unroll") for (int q = 0; q < NV; ++q) g[q] = 1.f;
+  }
+#undef EA_CASE_G
 }
 
 // --------------------------------------------------------- row reductions ----
@@ -464,60 +520,71 @@ __device__ __forceinline__ int opt_planes(const OptParams& p) {
 }
 
 // same rules as opt_update with the state held in registers
-__device__ __forceinline__ float opt_update_reg(const OptParams& p, float w, float g, float& s0, float& s1,
-                                                long long iter) {
+
+// Vector form: one dispatch on the optimizer, per-step scalars (decayed lr,
+// Adam/Adamax bias corrections) computed once, compact per-case loops.
+template <int NV>
+__device__ __forceinline__ void opt_update_v(const OptParams& p, float (&w)[NV], const float (&g)[NV],
+                                             float (&s0)[NV], float (&s1)[NV], long long iter) {
   const float lr = p.lr / (1.f + p.decay * (float)iter);
   switch (p.opt) {
-    case OPT_SGD: {
-      if (p.mom == 0.f) return w - lr * g;
-      const float v = p.mom * s0 - lr * g;
-      s0 = v;
-      return p.nesterov ? w + p.mom * v - lr * g : w + v;
-    }
-    case OPT_RMSPROP: {
-      const float ms = p.rho * s0 + (1.f - p.rho) * g * g;
-      s0 = ms;
-      const float upd = lr * g / (sqrtf(ms) + p.eps);
-      if (p.mom > 0.f) {
-        const float m = p.mom * s1 + upd;
-        s1 = m;
-        return w - m;
+    case OPT_SGD:
+      if (p.mom == 0.f) {
+        _Pragma("unroll") for (int q = 0; q < NV; ++q) w[q] -= lr * g[q];
+      } else {
+        _Pragma("unroll") for (int q = 0; q < NV; ++q) {
+          const float v = p.mom * s0[q] - lr * g[q];
+          s0[q] = v;
+          w[q] = p.nesterov ? w[q] + p.mom * v - lr * g[q] : w[q] + v;
+        }
       }
-      return w - upd;
-    }
+      break;
+    case OPT_RMSPROP:
+      _Pragma("unroll") for (int q = 0; q < NV; ++q) {
+        const float ms = p.rho * s0[q] + (1.f - p.rho) * g[q] * g[q];
+        s0[q] = ms;
+        const float upd = lr * g[q] / (sqrtf(ms) + p.eps);
+        if (p.mom > 0.f) {
+          const float m = p.mom * s1[q] + upd;
+          s1[q] = m;
+          w[q] -= m;
+        } else {
+          w[q] -= upd;
+        }
+      }
+      break;
     case OPT_ADAM: {
       const float t = (float)(iter + 1);
       const float lrt = lr * sqrtf(1.f - powf(p.b2, t)) / (1.f - powf(p.b1, t));
-      const float m = p.b1 * s0 + (1.f - p.b1) * g;
-      const float v = p.b2 * s1 + (1.f - p.b2) * g * g;
-      s0 = m;
-      s1 = v;
-      return w - lrt * m / (sqrtf(v) + p.eps);
+      _Pragma("unroll") for (int q = 0; q < NV; ++q) {
+        const float m = p.b1 * s0[q] + (1.f - p.b1) * g[q];
+        const float v = p.b2 * s1[q] + (1.f - p.b2) * g[q] * g[q];
+        s0[q] = m;
+        s1[q] = v;
+        w[q] -= lrt * m / (sqrtf(v) + p.eps);
+      }
+      break;
     }
-    case OPT_ADAGRAD: {
-      const float a = s0 + g * g;
-      s0 = a;
-      return w - lr * g / (sqrtf(a) + p.eps);
-    }
+    case OPT_ADAGRAD:
+      _Pragma("unroll") for (int q = 0; q < NV; ++q) {
+        const float a = s0[q] + g[q] * g[q];
+        s0[q] = a;
+        w[q] -= lr * g[q] / (sqrtf(a) + p.eps);
+      }
+      break;
     case OPT_ADAMAX: {
-      const float t = (float)(iter + 1);
-      const float lrt = lr / (1.f - powf(p.b1, t));
-      const float m = p.b1 * s0 + (1.f - p.b1) * g;
-      const float u = fmaxf(p.b2 * s1, fabsf(g));
-      s0 = m;
-      s1 = u;
-      return w - lrt * m / (u + p.eps);
+      const float lrt = lr / (1.f - powf(p.b1, (float)(iter + 1)));
+      _Pragma("unroll") for (int q = 0; q < NV; ++q) {
+        const float m = p.b1 * s0[q] + (1.f - p.b1) * g[q];
+        const float u = fmaxf(p.b2 * s1[q], fabsf(g[q]));
+        s0[q] = m;
+        s1[q] = u;
+        w[q] -= lrt * m / (u + p.eps);
+      }
+      break;
     }
   }
-  return w;
 }
-
-// ------------------------------------------------------- shared structs ----
-// Step counters, one block per executor:  [0]=step-in-epoch, [1]=arrive, [2..2+R)=iter[r]
-struct Counters {
-  long long* base;
-  __device__ long long step() const { return base[0]; }
-};
 
 // ------------------------------------------------------------ step counters
 // see GroupArgs::step_off (args.h)

@@ -22,6 +22,8 @@
 // Several independent problems (e.g. DW_l and DX_l of the same layer) run in one
 // grouped launch; blockIdx.x selects the problem.
 #include "common.h"
+#include "mfma.h"
+#include "loss_tile.h"
 
 #include <algorithm>
 
@@ -41,34 +43,6 @@ __device__ __forceinline__ int batch_valid(const Prob& p, int r, long long step)
 __device__ __forceinline__ long long batch_row(const Prob& p, int r, long long step, int m) {
   if (p.eval_mode) return (long long)p.vstart[r] + p.chunk * p.B + m;
   return (long long)p.perm[(long long)r * p.sPerm + step * p.B + m];
-}
-
-template <typename T> struct KT;
-template <> struct KT<__bf16> { static constexpr int EPL = 8, KC = 32; };
-template <> struct KT<float> { static constexpr int EPL = 4, KC = 16; };
-
-template <typename T>
-__device__ __forceinline__ void mma16(f32x4& acc, const uint4& a, const uint4& b) {
-  if constexpr (sizeof(T) == 2) {
-    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a),
-                                                  __builtin_bit_cast(bf16x8, b), acc, 0, 0, 0);
-  } else {
-    // lane group g holds k = 4g..4g+3 of this 16-deep chunk; MFMA t consumes element t.
-    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.x), __uint_as_float(b.x), acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.y), __uint_as_float(b.y), acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.z), __uint_as_float(b.z), acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.w), __uint_as_float(b.w), acc, 0, 0, 0);
-  }
-}
-
-template <typename T> __device__ __forceinline__ uint4 ones_frag() {
-  if constexpr (sizeof(T) == 2) {
-    const unsigned o = 0x3F803F80u;  // two bf16 1.0
-    return make_uint4(o, o, o, o);
-  } else {
-    const unsigned o = 0x3F800000u;
-    return make_uint4(o, o, o, o);
-  }
 }
 
 template <typename T> __device__ __forceinline__ void st(void* base, long long idx, float v) {
@@ -182,138 +156,6 @@ __device__ __forceinline__ void st8(void* base, long long idx, const float (&v)[
 
 // Fused loss over the tile's rows: groups of W lanes own one row each
 // (W = 16/32/64 by output width), reductions are W-lane shuffles.
-// Fused softmax + (sparse) categorical cross-entropy over a GEMM tile holding
-// whole rows (N <= 32): one quad (4 lanes) per row, the row's logits/targets in
-// registers (NV = ceil(N/4) statically unrolled slots per lane) and DPP quad
-// reductions -- no LDS round trips inside the row math, 64 rows per pass.
-// Same math as row_loss's logits path (keras backend.categorical_crossentropy
-// with from_logits): loss = -sum y (z - lse), dL/dz = softmax(z) * sum(y) - y.
-// Other loss/activation/metric combinations use loss_tile_lds.
-__device__ __forceinline__ bool softmax_cce_fast(const Prob& p) {
-  if (p.act != ACT_SOFTMAX || !(p.loss == LOSS_CCE || p.loss == LOSS_SPARSE_CCE) || !p.Y || p.N > 32) return false;
-  bool ok = true;
-#pragma unroll
-  for (int q = 0; q < 4; ++q)
-    if (q < p.nmet)
-      ok = ok && (p.met[q] == MET_ACC_CAT || p.met[q] == MET_ACC_SPARSE || p.met[q] == LOSS_CCE ||
-                  p.met[q] == LOSS_SPARSE_CCE);
-  return ok;
-}
-
-template <int NV, int BM, int LDC, int BN>
-__device__ __forceinline__ void loss_tile_cce(const Prob& p, int r, int m0, float* C, const float* Ys, const int* srow,
-                                              bool train, float inv_valid, float (&sums)[6]) {
-  constexpr int W = 4;
-  const int lane = threadIdx.x & 3, grp = threadIdx.x >> 2;
-  const int N = p.N;
-  const bool sparse = p.loss == LOSS_SPARSE_CCE;
-  for (int row = grp; row < BM; row += 64) {
-    float* zrow = C + row * LDC;
-    const float* yrow = Ys + row * BN;
-    float z[NV], y[NV];
-    const int ycls = sparse ? (int)yrow[0] : -1;
-#pragma unroll
-    for (int i = 0; i < NV; ++i) {  // in-bounds of the LDS tile even past N
-      const int j = lane + i * W;
-      z[i] = zrow[j];
-      y[i] = sparse ? (j == ycls ? 1.f : 0.f) : yrow[j];
-    }
-    if (srow[row] < 0) {
-      if (train) {
-#pragma unroll
-        for (int i = 0; i < NV; ++i)
-          if (lane + i * W < N) zrow[lane + i * W] = 0.f;
-      }
-      continue;
-    }
-    float zmax = -INFINITY;
-#pragma unroll
-    for (int i = 0; i < NV; ++i)
-      if (lane + i * W < N) zmax = fmaxf(zmax, z[i]);
-    zmax = row_max<W>(zmax);
-    float se = 0.f;
-#pragma unroll
-    for (int i = 0; i < NV; ++i)
-      if (lane + i * W < N) se += __expf(z[i] - zmax);
-    se = row_sum<W>(se);
-    const float lse = zmax + logf(se);
-    float l = 0.f, ysum = 0.f, bp = -INFINITY, by = -INFINITY, pr[NV];
-    int ip = 0x7fffffff, iy = 0x7fffffff;
-#pragma unroll
-    for (int i = 0; i < NV; ++i) {
-      const int j = lane + i * W;
-      pr[i] = __expf(z[i] - lse);
-      if (j < N) {
-        l += -y[i] * (z[i] - lse);
-        ysum += y[i];
-        if (pr[i] > bp) { bp = pr[i]; ip = j; }
-        if (y[i] > by) { by = y[i]; iy = j; }
-      }
-    }
-    l = row_sum<W>(l);
-    ysum = row_sum<W>(ysum);
-    row_argmax<W>(bp, ip);
-    row_argmax<W>(by, iy);
-    if (sparse) iy = ycls;
-    const float acc = ip == iy ? 1.f : 0.f;
-    if (p.pred) {
-      float* prow = p.pred + (long long)r * p.sPred + (p.chunk * p.B + m0 + row) * p.ldp;
-#pragma unroll
-      for (int i = 0; i < NV; ++i)
-        if (lane + i * W < N) prow[lane + i * W] = pr[i];
-    }
-    if (train) {
-#pragma unroll
-      for (int i = 0; i < NV; ++i)
-        if (lane + i * W < N) zrow[lane + i * W] = (pr[i] * ysum - y[i]) * inv_valid;
-    }
-    if (lane == 0) {
-      sums[0] += l;
-      sums[1] += 1.f;
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-        if (q < p.nmet) sums[2 + q] += (p.met[q] == MET_ACC_CAT || p.met[q] == MET_ACC_SPARSE) ? acc : l;
-    }
-  }
-}
-
-// Generic fused loss (any loss/activation/metrics): 16 lanes per row, values
-// read from the LDS tile in runtime loops (keeps code size bounded).
-template <int BM, int LDC, int BN>
-__device__ __forceinline__ void loss_tile_lds(const Prob& p, int r, int m0, float* C, const float* Ys, const int* srow,
-                                              bool train, float inv_valid, float (&sums)[6]) {
-  constexpr int W = 16;
-  const int lane = threadIdx.x % W, grp = threadIdx.x / W;
-  for (int row = grp; row < BM; row += 256 / W) {
-    float* zrow = C + row * LDC;
-    const float* yrow = Ys + row * BN;
-    if (srow[row] < 0) {
-      if (train)
-        for (int j = lane; j < p.N; j += W) zrow[j] = 0.f;
-      continue;
-    }
-    float* prow = p.pred ? p.pred + (long long)r * p.sPred + (p.chunk * p.B + m0 + row) * p.ldp : nullptr;
-    auto zat = [&](int, int j) { return zrow[j]; };
-    auto pout = [&](int, int j, float v) { prow[j] = v; };
-    if (!p.Y) {
-      if (prow) row_predict<W, 0>(lane, p.N, p.act, zat, pout);
-      continue;
-    }
-    RowOut ro;
-    ro.loss = 0.f;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) ro.metric[q] = 0.f;
-    row_loss<W, 0>(lane, p.N, p.act, p.loss, p.met, p.nmet, zat, [&](int, int j) { return yrow[j]; }, yrow[0],
-                   train, [&](int, int j, float v) { zrow[j] = v * inv_valid; }, prow != nullptr, pout, ro);
-    if (lane == 0) {
-      sums[0] += ro.loss;
-      sums[1] += 1.f;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) sums[2 + q] += ro.metric[q];
-    }
-  }
-}
-
 // diagnostics: wall-clock stamps (100 MHz s_memrealtime) of block-relative phases
 __device__ __forceinline__ void stamp(const GroupArgs& ga, int k) {
   if (ga.stamps && threadIdx.x == 0) ga.stamps[(long long)blockIdx.x * 16 + k] = (long long)__builtin_amdgcn_s_memrealtime();
@@ -418,25 +260,33 @@ __device__ __forceinline__ void run_prob(const GroupArgs& ga, const Prob& p, con
           b[j] = sel(kin && ((bmask >> j) & 1u), v, zero);
         }
       };
+      // PF-deep register ring: PF k-steps of fragments in flight per wave, so a
+      // K = 784 layer waits on ~2 load round trips instead of one per step.
       constexpr int KSTEP = KSPLIT * KC;
-      int kc = wk * KC;
-      uint4 a0[WM], b0[WN], a1[WM], b1[WN];
-      if (kc < p.K) load_frags(kc, a0, b0);
-      while (kc < p.K) {
-        const int kn = kc + KSTEP;
-        if (kn < p.K) load_frags(kn, a1, b1);
+      constexpr int PF = (WM * WN >= 16) ? 3 : 4;
+      const int kbeg = wk * KC;
+      const int nsteps = kbeg < p.K ? (p.K - kbeg + KSTEP - 1) / KSTEP : 0;
+      uint4 ra[PF][WM], rb[PF][WN];
 #pragma unroll
-        for (int i = 0; i < WM; ++i)
+      for (int u = 0; u < PF; ++u)
+        if (u < nsteps) load_frags(kbeg + u * KSTEP, ra[u], rb[u]);
+      for (int s0 = 0; s0 < nsteps; s0 += PF) {
 #pragma unroll
-          for (int j = 0; j < WN; ++j) mma16<T>(acc[i][j], a0[i], b0[j]);
-        if (kn >= p.K) break;
-        const int kn2 = kn + KSTEP;
-        if (kn2 < p.K) load_frags(kn2, a0, b0);
+        for (int u = 0; u < PF; ++u) {
+          const int st_ = s0 + u;
+          if (st_ < nsteps) {
+            uint4 a[WM], b[WN];
 #pragma unroll
-        for (int i = 0; i < WM; ++i)
+            for (int i = 0; i < WM; ++i) a[i] = ra[u][i];
 #pragma unroll
-          for (int j = 0; j < WN; ++j) mma16<T>(acc[i][j], a1[i], b1[j]);
-        kc = kn2;
+            for (int j = 0; j < WN; ++j) b[j] = rb[u][j];
+            if (st_ + PF < nsteps) load_frags(kbeg + (st_ + PF) * KSTEP, ra[u], rb[u]);
+#pragma unroll
+            for (int i = 0; i < WM; ++i)
+#pragma unroll
+              for (int j = 0; j < WN; ++j) mma16<T>(acc[i][j], a[i], b[j]);
+          }
+        }
       }
     }
 
@@ -524,11 +374,8 @@ __device__ __forceinline__ void run_prob(const GroupArgs& ga, const Prob& p, con
           const bool rv = gm < valid;
           float v[8], aux[8], zv[8], out[8], u[8];
           lds8(row, t_c0, v);
-          if (drop) {  // t_c0 is a multiple of 8: two 4-column Philox groups
-            const float4 u0 = dropout_u4(ga.seed, r, p.layer, iter, gm, gn0 >> 2);
-            const float4 u1 = dropout_u4(ga.seed, r, p.layer, iter, gm, (gn0 >> 2) + 1);
-            u[0] = u0.x; u[1] = u0.y; u[2] = u0.z; u[3] = u0.w;
-            u[4] = u1.x; u[5] = u1.y; u[6] = u1.z; u[7] = u1.w;
+          if (drop) {  // t_c0 is a multiple of 8
+            dropout_u8(dropout_base(ga.seed, r, p.layer, iter), gm, gn0, u);
           } else {
 #pragma unroll
             for (int q = 0; q < 8; ++q) u[q] = 1.f;
@@ -539,20 +386,20 @@ __device__ __forceinline__ void run_prob(const GroupArgs& ga, const Prob& p, con
             if (fwd) aux[q] = (bias && in) ? bias[gn0 + q] : 0.f;
             else aux[q] = (in && rv) ? Z[(long long)gm * p.ldz + gn0 + q] : 0.f;
           }
+          float av[8];
+          if (fwd) {
+#pragma unroll
+            for (int q = 0; q < 8; ++q) zv[q] = v[q] + aux[q];
+            act_f_v<8>(p.act, zv, av);
+          } else {
+            act_g_v<8>(p.act, aux, av);
+          }
 #pragma unroll
           for (int q = 0; q < 8; ++q) {
-            const int gn = gn0 + q;
-            zv[q] = 0.f;
-            out[q] = 0.f;
-            if (gn < p.N && rv) {
-              const bool keep = u[q] >= p.rate;
-              if (fwd) {
-                zv[q] = v[q] + aux[q];
-                out[q] = keep ? act_fwd(p.act, zv[q]) * keep_scale : 0.f;
-              } else {
-                out[q] = keep ? v[q] * act_grad(p.act, aux[q]) * keep_scale : 0.f;
-              }
-            }
+            const bool live = gn0 + q < p.N && rv;
+            const bool keep = live && u[q] >= p.rate;
+            if (!live) zv[q] = 0.f;
+            out[q] = keep ? (fwd ? av[q] : v[q] * av[q]) * keep_scale : 0.f;
           }
           if (ps == 0) stamp(ga, 5);
           if (fwd && Z) {
@@ -674,9 +521,12 @@ __device__ __forceinline__ void run_prob(const GroupArgs& ga, const Prob& p, con
             s0[q] = (in && np > 0) ? S[pidx + q] : 0.f;
             s1[q] = (in && np > 1) ? S[p.op.s_plane + pidx + q] : 0.f;
           }
+          {
+            float gq[8];
 #pragma unroll
-          for (int q = 0; q < 8; ++q)
-            if (gn0 + q < p.N) w[q] = opt_update_reg(p.op, w[q], v[q] * p.op.grad_scale, s0[q], s1[q], iter);
+            for (int q = 0; q < 8; ++q) gq[q] = v[q] * p.op.grad_scale;
+            opt_update_v<8>(p.op, w, gq, s0, s1, iter);  // lanes past N are discarded below
+          }
           if (ps == 0) stamp(ga, 5);
 #pragma unroll
           for (int q = 0; q < 8; ++q) {

@@ -64,6 +64,8 @@ static ExecCfg parse_cfg(const py::dict& d) {
   c.bf16 = get<int>(d, "bf16", 1);
   c.seed = get<unsigned long long>(d, "seed", 0);
   c.force_cfg = get<int>(d, "force_cfg", -1);
+  c.fused = get<int>(d, "fused", -1);
+  c.fused_split = get<int>(d, "fused_split", 16);
   for (auto item : d["layers"].cast<py::list>()) {
     py::dict l = item.cast<py::dict>();
     LayerCfg lc;
@@ -164,6 +166,8 @@ PYBIND11_MODULE(_C, m) {
       .def("launches_per_step", &Executor::launches_per_step)
       .def("launch_cfgs", &Executor::launch_cfgs)
       .def("launch_blocks", &Executor::launch_blocks)
+      .def("fused", &Executor::fused)
+      .def("fused_lds_bytes", &Executor::fused_lds_bytes)
       .def("set_stamps", &Executor::set_stamps)
       .def("train_launch", [](Executor& e, int idx, uintptr_t s) { e.train_launch(idx, S(s)); });
 

@@ -9,6 +9,8 @@ extern "C" hipError_t ea_gemm_grouped(const ea::GroupArgs* ga, int bf16, int cfg
 extern "C" int ea_gemm_tile_m(int cfg);
 extern "C" int ea_gemm_tile_n(int cfg);
 extern "C" void ea_gemm_init();
+extern "C" void ea_fused_init();
+extern "C" hipError_t ea_fused_tail(const ea::FusedArgs* a, int bf16, hipStream_t s);
 extern "C" hipError_t ea_apply_update(ea::FlatArgs* a, int bf16, hipStream_t s);
 extern "C" hipError_t ea_refresh_shadows(ea::FlatArgs* a, int bf16, hipStream_t s);
 extern "C" hipError_t ea_advance(long long* ctr, const int* ntrain, int R, int B, int n, hipStream_t s);
@@ -28,10 +30,107 @@ Executor::Executor(const ExecCfg& cfg) : c_(cfg) {
     if (l.Kp % 8 || l.Np % 8 || l.Kp < l.K || l.Np < l.N) throw std::invalid_argument("layer dims must be padded to 8");
   }
   ea_gemm_init();
+  ea_fused_init();
   build();
+  fused_ = c_.fused != 0 && build_fused();
+  if (c_.fused == 1 && !fused_) throw std::invalid_argument("fused MLP tail requested but the model is not eligible");
 }
 
-Executor::~Executor() { destroy_graphs(); }
+Executor::~Executor() {
+  destroy_graphs();
+  if (d_fly_) (void)hipFree(d_fly_);
+}
+
+// Eligibility + LDS layout of the fused tail (fused.hip): batch <= 64, every
+// layer width <= 256, a final layer of <= 32 units, everything in 160 KB of LDS.
+bool Executor::build_fused() {
+  const int L = (int)c_.layers.size();
+  if (L < 2 || L > FUSED_MAX_L || c_.B > 64 || c_.Bp > 64) return false;
+  if (c_.layers[0].N > 256) return false;
+  for (int l = 1; l < L; ++l)
+    if (c_.layers[l].K > 256 || c_.layers[l].N > 256) return false;
+  if (c_.layers[L - 1].N > 32) return false;
+  if (fwd_.empty() || fwd_[0].ga.nprob != 2 || fwd_[0].ga.p[0].kind != PK_FWD || fwd_[0].ga.p[1].kind != PK_GATHER_T)
+    return false;
+  const int esz = c_.bf16 ? 2 : 4, padA = c_.bf16 ? 8 : 4;
+  auto r16 = [](int x) { return (x + 15) / 16 * 16; };
+  std::vector<FusedLayer> fl(L);
+  long long off = 0;
+  int maxN = 0;
+  for (int l = 0; l < L; ++l) {
+    const LayerCfg& ly = c_.layers[l];
+    FusedLayer& f = fl[l];
+    std::memset(&f, 0, sizeof(f));
+    f.K = ly.K; f.N = ly.N; f.Kp = ly.Kp; f.Np = ly.Np;
+    f.act = ly.act; f.has_bias = ly.has_bias; f.rate = ly.rate;
+    f.p_off = ly.p_off; f.wsh_off = ly.wsh_off; f.wtsh_off = ly.wtsh_off;
+    f.pvec = (ly.N % 4 == 0 && ly.p_off % 4 == 0) ? 1 : 0;
+    if (l < L - 1) {
+      f.ldA = r16(ly.Np + 1) + padA;  // + the ones column (bias row of the next layer's update)
+      f.offD = (int)off;
+      off += 64LL * f.ldA * esz;
+      f.ldG = r16(ly.Np) + 4;
+      f.offG = (int)off;
+      off += 64LL * f.ldG * 4;
+    }
+    if (l >= 1) maxN = std::max(maxN, ly.N);
+  }
+  FusedArgs& a = fa_;
+  std::memset(&a, 0, sizeof(a));
+  a.offLg = (int)off; a.ldLg = 36; off += 64LL * 36 * 4;
+  a.lddZ = r16(maxN) + padA;
+  a.offdZ0 = (int)off; off += 64LL * a.lddZ * esz;
+  a.offdZ1 = (int)off; off += 64LL * a.lddZ * esz;
+  a.offY = (int)off; off += 64LL * 32 * 4;
+  a.offSrow = (int)off; off += 64 * 4;
+  if (off > 160 * 1024) return false;
+  a.lds_bytes = (int)off;
+  check(hipMalloc(&d_fly_, sizeof(FusedLayer) * L), "hipMalloc(fused layers)");
+  check(hipMemcpy(d_fly_, fl.data(), sizeof(FusedLayer) * L, hipMemcpyHostToDevice), "hipMemcpy(fused layers)");
+  const LayerCfg& l0 = c_.layers[0];
+  a.L = L;
+  a.nsplit = std::max(1, c_.fused_split);
+  a.ly = d_fly_;
+  a.R = c_.R; a.B = c_.B; a.Bp = c_.Bp;
+  a.D0 = reinterpret_cast<const void*>(l0.D); a.sD0 = (long long)c_.B * l0.Np;
+  a.Z0 = reinterpret_cast<const float*>(l0.Z); a.sZ0 = (long long)c_.B * l0.N;
+  a.Y = reinterpret_cast<const float*>(c_.Y); a.sY = c_.sY; a.ldy = c_.ldy;
+  a.perm = reinterpret_cast<const int*>(c_.perm); a.sPerm = c_.sPerm;
+  a.ntrain = reinterpret_cast<const int*>(c_.ntrain);
+  a.dZ0T = reinterpret_cast<void*>(l0.dZT); a.sdZ0T = (long long)l0.N * c_.Bp;
+  a.P = reinterpret_cast<float*>(c_.P); a.sP = c_.sP;
+  a.S = reinterpret_cast<float*>(c_.S); a.sS = c_.sS;
+  a.op = c_.op;
+  a.Wsh = reinterpret_cast<void*>(c_.Wsh); a.sWsh = c_.sWsh; a.wsh_par = c_.wsh_par;
+  a.WTsh = reinterpret_cast<void*>(c_.WTsh); a.sWTsh = c_.sWTsh; a.wtsh_par = c_.wtsh_par;
+  a.loss = c_.loss; a.nmet = c_.nmet;
+  for (int i = 0; i < 4; ++i) a.met[i] = c_.met[i];
+  a.acc = reinterpret_cast<double*>(c_.acc); a.acc_stride = c_.acc_stride;
+  a.ctr = reinterpret_cast<long long*>(c_.ctr);
+  a.seed = c_.seed;
+  // grouped launches around the tail: layer-0 forward (+ X^T), layer-0 update
+  ffwd_.assign(1, fwd_[0]);
+  ffwd_[0].ga.p[0].DT = nullptr;  // D_0^T is not needed: the tail reads D_0 into LDS
+  fbwd_.assign(1, bwd_.back());
+  return true;
+}
+
+void Executor::run_tail(hipStream_t s, int step_off) const {
+  FusedArgs a = fa_;
+  a.step_off = step_off;
+  check(ea_fused_tail(&a, c_.bf16, s), "fused_tail");
+}
+
+void Executor::run_step(hipStream_t s, int step_off) const {
+  if (fused_) {
+    run(ffwd_, s, step_off);
+    run_tail(s, step_off);
+    run(fbwd_, s, step_off);
+  } else {
+    run(fwd_, s, step_off);
+    run(bwd_, s, step_off);
+  }
+}
 
 void Executor::destroy_graphs() {
   for (auto& g : graphs_) {
@@ -333,18 +432,33 @@ void Executor::advance(int nsteps, hipStream_t s) const {
 }
 
 void Executor::train_launch(int idx, hipStream_t s) {
+  // one launch of the active step plan, step_off 0, no counter advance
+  if (fused_) {
+    if (idx == (int)ffwd_.size()) { run_tail(s, 0); return; }
+    const Launch& L = idx < (int)ffwd_.size() ? ffwd_[idx] : fbwd_[idx - ffwd_.size() - 1];
+    check(ea_gemm_grouped(&L.ga, c_.bf16, L.cfg, s), "train_launch");
+    return;
+  }
   const int nf = (int)fwd_.size();
   const Launch& L = idx < nf ? fwd_[idx] : bwd_[idx - nf];
-  check(ea_gemm_grouped(&L.ga, c_.bf16, L.cfg, s), "train_launch");  // step_off 0, no advance
+  check(ea_gemm_grouped(&L.ga, c_.bf16, L.cfg, s), "train_launch");
 }
 
 void Executor::set_stamps(uintptr_t buf) {
-  for (auto& L : fwd_) L.ga.stamps = reinterpret_cast<long long*>(buf);
-  for (auto& L : bwd_) L.ga.stamps = reinterpret_cast<long long*>(buf);
+  long long* p = reinterpret_cast<long long*>(buf);
+  for (auto* v : {&fwd_, &bwd_, &ffwd_, &fbwd_})
+    for (auto& L : *v) L.ga.stamps = p;
+  fa_.stamps = p;
 }
 
 std::vector<int> Executor::launch_blocks() const {
   std::vector<int> v;
+  if (fused_) {
+    for (auto& L : ffwd_) v.push_back(L.ga.total_blocks);
+    v.push_back(c_.R * fa_.nsplit);
+    for (auto& L : fbwd_) v.push_back(L.ga.total_blocks);
+    return v;
+  }
   for (auto& L : fwd_) v.push_back(L.ga.total_blocks);
   for (auto& L : bwd_) v.push_back(L.ga.total_blocks);
   return v;
@@ -352,14 +466,19 @@ std::vector<int> Executor::launch_blocks() const {
 
 std::vector<int> Executor::launch_cfgs() const {
   std::vector<int> v;
+  if (fused_) {
+    for (auto& L : ffwd_) v.push_back(L.cfg);
+    v.push_back(-1);  // fused tail
+    for (auto& L : fbwd_) v.push_back(L.cfg);
+    return v;
+  }
   for (auto& L : fwd_) v.push_back(L.cfg);
   for (auto& L : bwd_) v.push_back(L.cfg);
   return v;
 }
 
 void Executor::train_step(hipStream_t s) {
-  run(fwd_, s, 0);
-  run(bwd_, s, 0);
+  run_step(s, 0);
   advance(1, s);
 }
 
@@ -438,10 +557,7 @@ int Executor::capture(int nsteps, int mode, hipStream_t s) {
   try {
     if (mode == 0) {
       // one chunk: steps at offsets 0..nsteps-1 from the counter base, then one advance
-      for (int i = 0; i < nsteps; ++i) {
-        run(fwd_, s, i);
-        run(bwd_, s, i);
-      }
+      for (int i = 0; i < nsteps; ++i) run_step(s, i);
       advance(nsteps, s);
     } else {
       for (int i = 0; i < nsteps; ++i) {

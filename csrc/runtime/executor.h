@@ -54,6 +54,8 @@ struct ExecCfg {
   uintptr_t acc = 0; int acc_stride = 6;
   uintptr_t ctr = 0;
   int force_cfg = -1;  // -1 auto, 0 LAT, 1 THR
+  int fused = -1;      // fused small-MLP tail: -1 auto (when eligible), 0 off, 1 required
+  int fused_split = 16; // workgroups per replica in the fused tail
 };
 
 struct EvalSource {
@@ -84,7 +86,9 @@ class Executor {
   void destroy_graphs();
 
   // GEMM launches per step (a captured chunk adds one 1-block counter advance)
-  int launches_per_step() const { return (int)fwd_.size() + (int)bwd_.size(); }
+  int launches_per_step() const { return fused_ ? (int)ffwd_.size() + 1 + (int)fbwd_.size() : (int)fwd_.size() + (int)bwd_.size(); }
+  bool fused() const { return fused_; }
+  int fused_lds_bytes() const { return fused_ ? fa_.lds_bytes : 0; }
   std::vector<int> launch_cfgs() const;
   // diagnostics: bind a [blocks_max][16] int64 buffer for in-kernel stamps (0 = off)
   void set_stamps(uintptr_t buf);
@@ -98,6 +102,14 @@ class Executor {
   };
   ExecCfg c_;
   std::vector<Launch> fwd_, bwd_;
+  // fused plan: [FWD_0 + X^T gather] [fused tail, one block per replica] [DW_0 update]
+  bool fused_ = false;
+  std::vector<Launch> ffwd_, fbwd_;
+  FusedArgs fa_{};
+  FusedLayer* d_fly_ = nullptr;
+  bool build_fused();
+  void run_tail(hipStream_t s, int step_off) const;
+  void run_step(hipStream_t s, int step_off) const;
   std::vector<std::pair<hipGraph_t, hipGraphExec_t>> graphs_;
 
   Prob base_prob() const;

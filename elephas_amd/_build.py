@@ -22,6 +22,7 @@ ARCH = os.environ.get("ELEPHAS_AMD_ARCH", "gfx950")
 SOURCES = [
     "kernels/gemm.hip",
     "kernels/flat.hip",
+    "kernels/fused.hip",
     "runtime/executor.cpp",
     "runtime/param_server.cpp",
     "runtime/host_loader.cpp",

@@ -41,9 +41,13 @@ class NativeTrainer(TrainerBase):
     GRAPH_CHUNK = 16
 
     def __init__(self, model, plan, R: int = 1, batch_size: int = 32, device=None, seed: Optional[int] = None,
-                 policy: Optional[str] = None, eval_batch: int = 2048):
+                 policy: Optional[str] = None, eval_batch: int = 2048, fused: Optional[int] = None):
         super().__init__(model, plan, R, batch_size)
         self.C = native.require()
+        # fused small-MLP tail kernel (csrc/kernels/fused.hip): None -> $ELEPHAS_AMD_FUSED
+        # (default 0: the grouped per-layer launches measure faster on MI355X, see
+        # profiles/README.md), -1 when eligible, 1 required
+        self.fused_mode = int(os.environ.get("ELEPHAS_AMD_FUSED", "0")) if fused is None else int(fused)
         if not plan.native_ok:
             raise ValueError(f"model is not supported by the native engine: {plan.reason}")
         self.dev = torch.device(device) if device is not None else config.get_device()
@@ -141,6 +145,8 @@ class NativeTrainer(TrainerBase):
         return dict(
             R=self.R, B=ws["B"], Bp=ws["Bp"], bf16=int(self.bf16), seed=self.seed,
             force_cfg=int(os.environ.get("ELEPHAS_AMD_GEMM_CFG", "-1")),
+            fused=self.fused_mode if ws is self.ws else 0,
+            fused_split=int(os.environ.get("ELEPHAS_AMD_FUSED_SPLIT", "16")),
             layers=layers,
             X=self.X.data_ptr(), sX=self.nmax * self.Kp0, ldx=self.Kp0,
             Y=self.Y.data_ptr(), sY=self.nmax * self.ldy, ldy=self.ldy,
@@ -440,3 +446,8 @@ class NativeTrainer(TrainerBase):
 
     def launch_count(self) -> int:
         return self.exe.launches_per_step()
+
+    @property
+    def fused(self) -> bool:
+        """True when training steps run the fused small-MLP tail kernel (csrc/kernels/fused.hip)."""
+        return bool(self.exe.fused())

@@ -182,3 +182,68 @@ def test_graph_replay_equals_eager():
         ws.append(t.get_weights_flat())
     assert np.array_equal(ws[0], ws[1])
     assert not np.array_equal(ws[0][0], ws[0][1])  # replicas draw different dropout masks
+
+
+def _fit_weights(model, policy, B, xs, ys, fused, epochs=1, val=0.0, R=None, seed=7):
+    from elephas_amd import config
+    from elephas_amd.ops.plan import build_plan
+    from elephas_amd.ops.native_engine import NativeTrainer
+    config.set_policy(policy)
+    R = R or len(xs)
+    t = NativeTrainer(model, build_plan(model), R, B, torch.device("cuda"), seed=seed, fused=fused)
+    t.set_data(xs, ys, val, shuffle=True)
+    np.random.seed(3)
+    torch.manual_seed(5)   # epoch shuffles draw from the global CUDA generator
+    h = t.fit(epochs)
+    return t, t.get_weights_flat(), h
+
+
+@pytest.mark.parametrize("case", ["mnist_bf16_dropout", "tanh_f32_adam", "mse_f32", "sparse_bf16_rmsprop"])
+def test_fused_tail_matches_grouped_path(case):
+    """The fused small-MLP tail (one block per replica) must reproduce the grouped
+    per-layer launches: same masks, same update rules, fp32 accumulation."""
+    from elephas_amd.models.optimizers import SGD, Adam, RMSprop
+    rng = np.random.default_rng(11)
+    if case == "mnist_bf16_dropout":
+        model = _mlp(784, [128, 128], 10, dropout=0.2)
+        model.compile(SGD(learning_rate=0.1), "categorical_crossentropy", ["acc"])
+        policy, B, d, k, tol = "mixed_bfloat16", 64, 784, 10, 2e-2
+        sizes = [300, 130, 40]            # third replica runs out of batches early
+    elif case == "tanh_f32_adam":
+        model = _mlp(30, [64, 48], 5, act="tanh", dropout=0.1)
+        model.compile(Adam(learning_rate=0.01), "categorical_crossentropy", ["acc", "mse"])
+        policy, B, d, k, tol = "float32", 32, 30, 5, 1e-4
+        sizes = [200, 200]
+    elif case == "mse_f32":
+        model = _mlp(20, [32], 1, out_act="linear")
+        model.compile(SGD(learning_rate=0.05, momentum=0.9), "mse", ["mae"])
+        policy, B, d, k, tol = "float32", 16, 20, 1, 1e-4
+        sizes = [160]
+    else:
+        model = _mlp(50, [96, 64], 7, dropout=0.3)
+        model.compile(RMSprop(learning_rate=0.005), "sparse_categorical_crossentropy", ["acc"])
+        policy, B, d, k, tol = "mixed_bfloat16", 48, 50, 7, 3e-2
+        sizes = [250, 180]
+    xs, ys = [], []
+    for n in sizes:
+        x = rng.random((n, d), dtype=np.float32)
+        if k == 1:
+            y = rng.normal(size=(n, 1)).astype(np.float32)
+        elif case.startswith("sparse"):
+            y = rng.integers(0, k, (n, 1)).astype(np.float32)
+        else:
+            y = np.eye(k, dtype=np.float32)[rng.integers(0, k, n)]
+        xs.append(x)
+        ys.append(y)
+    tf, wf, hf = _fit_weights(model, policy, B, xs, ys, fused=1, epochs=2, val=0.1)
+    tg, wg, hg = _fit_weights(model, policy, B, xs, ys, fused=0, epochs=2, val=0.1)
+    assert tf.fused and not tg.fused
+    assert tf.launch_count() == 3
+    scale = np.abs(wg).max()
+    assert np.abs(wf - wg).max() <= tol * scale, (np.abs(wf - wg).max(), scale)
+    for a, b in zip(hf, hg):
+        if a is None:
+            assert b is None
+            continue
+        for key in a:
+            assert np.allclose(a[key], b[key], rtol=5 * tol, atol=5 * tol), (key, a[key], b[key])

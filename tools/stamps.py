@@ -19,8 +19,21 @@ blocks = t.exe.launch_blocks()
 buf = torch.zeros(max(blocks) * 16, dtype=torch.int64, device="cuda")
 t.exe.set_stamps(buf.data_ptr())
 names = ["start", "setup", "mainloop", "reduce", "end", "e5", "e6", "e7", "e8"]
+cfgs = t.exe.launch_cfgs()
 for rep in range(2):
     for i, nb in enumerate(blocks):
+        if cfgs[i] == -1:  # fused tail: 32 stamps per block
+            buf.zero_()
+            torch.cuda.synchronize()
+            t.exe.train_launch(i, t.s)
+            t.stream.synchronize()
+            st = buf[:nb * 32].view(nb, 32).cpu().numpy().astype(np.int64)
+            if rep == 1:
+                t0 = st[:, 0].min()
+                rel = np.where(st > 0, (st - t0) * 10.0, np.nan)
+                med = np.nanmedian(rel, axis=0)
+                print(f"launch {i} fused tail blocks {nb}: " + " ".join(f"{k}:{v:.0f}" for k, v in enumerate(med) if v == v), flush=True)
+            continue
         buf.zero_()
         torch.cuda.synchronize()
         t.exe.train_launch(i, t.s)
