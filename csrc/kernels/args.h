@@ -121,6 +121,7 @@ struct FlatArgs {
   Seg seg[MAX_SEG];
   void* Wsh; long long sWsh, wsh_par;
   void* WTsh; long long sWTsh, wtsh_par;
+  float* Bsh; long long sBsh, bsh_par;  // fp32 bias images per parity (fused tail only), flat index
   long long* ctr;
   const int* ntrain; int B;
   int both_parities;  // refresh: write both shadow parities
@@ -167,6 +168,9 @@ struct FusedArgs {
   OptParams op;
   void* Wsh; long long sWsh, wsh_par;
   void* WTsh; long long sWTsh, wtsh_par;
+  // fp32 bias images per parity, indexed like P: the forward of layer l reads the
+  // current parity while other workgroups of the replica write the next one
+  float* Bsh; long long sBsh, bsh_par;
   int loss, nmet, met[4];
   double* acc; int acc_stride;
   long long* ctr; int step_off;

@@ -33,7 +33,11 @@ template <typename T>
 __device__ __forceinline__ void write_shadow(const FlatArgs& a, int r, long long i, float w, long long par) {
   const SegV g = find_seg(a, i);
   const long long rel = i - g.p_off;
-  if (rel < 0 || rel >= (long long)g.K * g.N) return;  // bias: no shadow
+  if (rel < 0) return;
+  if (rel >= (long long)g.K * g.N) {  // bias: fp32 image only (read by the fused tail)
+    if (a.Bsh) a.Bsh[(long long)r * a.sBsh + par * a.bsh_par + i] = w;
+    return;
+  }
   const long long k = rel / g.N, nn = rel % g.N;
   if (a.Wsh)
     reinterpret_cast<T*>(a.Wsh)[(long long)r * a.sWsh + par * a.wsh_par + g.wsh_off + k * g.ldwsh + nn] = from_f<T>(w);

@@ -304,6 +304,12 @@ __device__ __forceinline__ void dw_pass(const FusedArgs& a, const FusedLayer& ly
           if (np > 1) S[splane + pi + q] = s1[j * 4 + q];
         }
     }
+    if (k == ly.K) {  // bias row: next-parity fp32 bias image
+      float* bn = a.Bsh + (long long)blockIdx.x / a.nsplit * a.sBsh + ((iter + 1) & 1) * a.bsh_par + pi;
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (n0 + q < ly.N) bn[q] = nw[q];
+    }
     if (k < ly.K) {  // weight images (no image for the bias row)
       T* wrow = Wn + ((int)ly.wsh_off + k * ly.Np + n0);  // 4 consecutive n (Np % 8 == 0)
       if constexpr (sizeof(T) == 2) {
@@ -458,7 +464,9 @@ __global__ __launch_bounds__(256) void fused_tail_kernel(FusedArgs a) {
     const bool last = l == L - 1;
     float* Zs = reinterpret_cast<float*>(smem + (last ? a.offLg : ly.offG));
     const int ldz = last ? a.ldLg : ly.ldG;
-    const float* bias = P + ly.p_off + (long long)ly.K * ly.N;
+    // bias from this step's parity image: P's bias row may already hold the
+    // update written by another workgroup of this replica
+    const float* bias = a.Bsh + (long long)r * a.sBsh + rpar * a.bsh_par + ly.p_off + (long long)ly.K * ly.N;
     const int ntt = (ly.N + 15) >> 4;
 #pragma unroll
     for (int s = 0; s < 4; ++s) {

@@ -184,7 +184,8 @@ __device__ __forceinline__ void run_prob(const GroupArgs& ga, const Prob& p, con
     const int tm = t / p.tiles_n, tn = t % p.tiles_n;
     const int m0 = tm * BM, n0 = tn * BN;
     const long long step = ga.ctr[0] + ga.step_off;
-    const long long iter = iter_at(ga.ctr, p.ntrain, p.B, r, ga.ctr[0], ga.step_off);
+    // plain / inference problems carry no per-replica batch counts (ntrain == nullptr)
+    const long long iter = p.ntrain ? iter_at(ga.ctr, p.ntrain, p.B, r, ga.ctr[0], ga.step_off) : 0;
     const int valid = (p.kind == PK_PLAIN) ? p.M : batch_valid(p, r, step);
     const bool skip_update = (p.kind == PK_DW_UPDATE) && valid == 0;
     stamp(ga, 1);

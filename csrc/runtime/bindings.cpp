@@ -111,6 +111,9 @@ static ExecCfg parse_cfg(const py::dict& d) {
   c.WTsh = get<uintptr_t>(d, "WTsh", 0);
   c.sWTsh = get<long long>(d, "sWTsh", 0);
   c.wtsh_par = get<long long>(d, "wtsh_par", 0);
+  c.Bsh = get<uintptr_t>(d, "Bsh", 0);
+  c.sBsh = get<long long>(d, "sBsh", 0);
+  c.bsh_par = get<long long>(d, "bsh_par", 0);
   c.op = parse_opt(d["opt"].cast<py::dict>());
   c.loss = get<int>(d, "loss", 0);
   auto mets = get<std::vector<int>>(d, "metrics", {});
@@ -174,6 +177,12 @@ PYBIND11_MODULE(_C, m) {
   // single PLAIN GEMM (C fp32 = A . BT^T) for kernel tests / generic matmul
   m.def("gemm_nt", [](uintptr_t A, uintptr_t BT, uintptr_t C, int M, int N, int K, long long lda, long long ldb,
                       long long ldc, int bf16, int cfg, uintptr_t s) {
+    // the kernel issues unconditional 16-byte fragment loads along K: rows must be
+    // 16-byte aligned and K padded to whole chunks, or it reads out of bounds
+    const int epl = bf16 ? 8 : 4;
+    if (M <= 0 || N <= 0 || K <= 0 || (K % epl) || (lda % epl) || (ldb % epl) || lda < K || ldb < K || ldc < N ||
+        (A % 16) || (BT % 16) || (C % 4) || (cfg != 0 && cfg != 1))
+      throw std::invalid_argument("gemm_nt: K, lda, ldb must be multiples of 16 bytes, pointers 16-byte aligned");
     ea_gemm_init();
     GroupArgs ga;
     std::memset(&ga, 0, sizeof(ga));

@@ -46,6 +46,7 @@ Executor::~Executor() {
 bool Executor::build_fused() {
   const int L = (int)c_.layers.size();
   if (L < 2 || L > FUSED_MAX_L || c_.B > 64 || c_.Bp > 64) return false;
+  if (!c_.Bsh) return false;  // needs the per-parity fp32 bias images
   if (c_.layers[0].N > 256) return false;
   for (int l = 1; l < L; ++l)
     if (c_.layers[l].K > 256 || c_.layers[l].N > 256) return false;
@@ -103,6 +104,7 @@ bool Executor::build_fused() {
   a.op = c_.op;
   a.Wsh = reinterpret_cast<void*>(c_.Wsh); a.sWsh = c_.sWsh; a.wsh_par = c_.wsh_par;
   a.WTsh = reinterpret_cast<void*>(c_.WTsh); a.sWTsh = c_.sWTsh; a.wtsh_par = c_.wtsh_par;
+  a.Bsh = reinterpret_cast<float*>(c_.Bsh); a.sBsh = c_.sBsh; a.bsh_par = c_.bsh_par;
   a.loss = c_.loss; a.nmet = c_.nmet;
   for (int i = 0; i < 4; ++i) a.met[i] = c_.met[i];
   a.acc = reinterpret_cast<double*>(c_.acc); a.acc_stride = c_.acc_stride;
@@ -523,6 +525,9 @@ FlatArgs Executor::flat_args() const {
   a.WTsh = reinterpret_cast<void*>(c_.WTsh);
   a.sWTsh = c_.sWTsh;
   a.wtsh_par = c_.wtsh_par;
+  a.Bsh = reinterpret_cast<float*>(c_.Bsh);
+  a.sBsh = c_.sBsh;
+  a.bsh_par = c_.bsh_par;
   a.ctr = reinterpret_cast<long long*>(c_.ctr);
   a.ntrain = reinterpret_cast<const int*>(c_.ntrain);
   a.B = c_.B;

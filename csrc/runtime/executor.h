@@ -49,6 +49,7 @@ struct ExecCfg {
   uintptr_t S = 0; long long sS = 0;
   uintptr_t Wsh = 0; long long sWsh = 0, wsh_par = 0;
   uintptr_t WTsh = 0; long long sWTsh = 0, wtsh_par = 0;
+  uintptr_t Bsh = 0; long long sBsh = 0, bsh_par = 0;  // fp32 bias images (fused tail)
   OptParams op{};
   int loss = 0, nmet = 0, met[4] = {0, 0, 0, 0};
   uintptr_t acc = 0; int acc_stride = 6;

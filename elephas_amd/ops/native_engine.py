@@ -93,6 +93,10 @@ class NativeTrainer(TrainerBase):
             self.G = torch.zeros(R, self.n, dtype=torch.float32, device=dev)
             self.Wsh = torch.zeros(R, 2, max(wsh, 1), dtype=self.T, device=dev)
             self.WTsh = torch.zeros(R, 2, max(wtsh, 1), dtype=self.T, device=dev)
+            # fp32 bias images per parity for the fused tail (indexed like P); only
+            # small MLPs are eligible, so the [R, 2, n] mirror stays small
+            self.Bsh = torch.zeros(R, 2, self.n, dtype=torch.float32, device=dev) \
+                if self.fused_mode != 0 and self.n <= (4 << 20) else None
             self.ctr = torch.zeros(2 + R, dtype=torch.int64, device=dev)
             self.acc = torch.zeros(R, 6, dtype=torch.float64, device=dev)
             self.acc_val = torch.zeros(R, 6, dtype=torch.float64, device=dev)
@@ -158,6 +162,7 @@ class NativeTrainer(TrainerBase):
             S=self.S.data_ptr(), sS=self.S.shape[1] * self.n,
             Wsh=self.Wsh.data_ptr(), sWsh=2 * self.Wsh.shape[2], wsh_par=self.Wsh.shape[2],
             WTsh=self.WTsh.data_ptr(), sWTsh=2 * self.WTsh.shape[2], wtsh_par=self.WTsh.shape[2],
+            Bsh=self.Bsh.data_ptr() if self.Bsh is not None else 0, sBsh=2 * self.n, bsh_par=self.n,
             opt=opt, loss=self.loss.native, metrics=[m.native for m in self.metrics],
             acc=self.acc.data_ptr(), acc_stride=6, ctr=self.ctr.data_ptr())
 

@@ -247,3 +247,46 @@ def test_fused_tail_matches_grouped_path(case):
             continue
         for key in a:
             assert np.allclose(a[key], b[key], rtol=5 * tol, atol=5 * tol), (key, a[key], b[key])
+
+
+@pytest.mark.parametrize("cfg", [0, 1])
+@pytest.mark.parametrize("bf16", [1, 0])
+@pytest.mark.parametrize("M,N,K", [(64, 128, 784), (64, 10, 128), (785, 128, 64), (300, 200, 136), (512, 512, 512)])
+def test_plain_gemm_matches_torch_fp32(M, N, K, bf16, cfg):
+    """Library entry of the MFMA GEMM (LAT / THR tiles) vs. a torch fp32 matmul."""
+    from elephas_amd.ops import native
+    C = native.require()
+    torch.manual_seed(0)
+    dt = torch.bfloat16 if bf16 else torch.float32
+    A = torch.randn(M, K, device="cuda").to(dt)
+    BT = torch.randn(N, K, device="cuda").to(dt)
+    out = torch.zeros(M, N, device="cuda")
+    C.gemm_nt(A.data_ptr(), BT.data_ptr(), out.data_ptr(), M, N, K, K, K, N, bf16, cfg,
+              torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    ref = A.float() @ BT.float().t()
+    err = (out - ref).abs().max().item() / ref.abs().max().item()
+    assert err < (1e-4 if not bf16 else 1e-3), err
+
+
+def test_plain_gemm_rejects_misaligned_shapes():
+    from elephas_amd.ops import native
+    C = native.require()
+    A = torch.zeros(4, 10, device="cuda")
+    with pytest.raises(Exception):
+        C.gemm_nt(A.data_ptr(), A.data_ptr(), A.data_ptr(), 4, 4, 10, 10, 10, 4, 0, 0, 0)
+
+
+@pytest.mark.parametrize("fused", [0, 1])
+def test_training_is_bit_deterministic(fused):
+    """Same seeds -> bit-identical weights (no races between the update epilogue
+    and the GEMMs that read the weight shadows, no order-dependent reductions)."""
+    from elephas_amd.models.optimizers import SGD
+    rng = np.random.default_rng(11)
+    model = _mlp(784, [128, 128], 10, dropout=0.2)
+    model.compile(SGD(learning_rate=0.1), "categorical_crossentropy", ["acc"])
+    xs = [rng.random((n, 784), dtype=np.float32) for n in (300, 130, 40)]
+    ys = [np.eye(10, dtype=np.float32)[rng.integers(0, 10, len(x))] for x in xs]
+    _, w1, _ = _fit_weights(model, "mixed_bfloat16", 64, xs, ys, fused=fused, epochs=2, val=0.1)
+    _, w2, _ = _fit_weights(model, "mixed_bfloat16", 64, xs, ys, fused=fused, epochs=2, val=0.1)
+    assert np.array_equal(w1, w2), np.abs(w1 - w2).max()

@@ -32,5 +32,10 @@ for cfg in (0, 1):
     for _ in range(10): C.gemm_nt(A.data_ptr(), BT.data_ptr(), Cm.data_ptr(), M, N, K, K, K, N, 1, cfg, s)
     torch.cuda.synchronize(); dt = (time.time() - t) / 10
     print(f"4096^3 bf16 cfg={cfg}: {dt*1e3:.3f} ms  {2*M*N*K/dt/1e12:.1f} TFLOP/s", flush=True)
+for _ in range(3): torch.matmul(A, BT.t())
+torch.cuda.synchronize(); t = time.time()
+for _ in range(10): torch.matmul(A, BT.t())
+torch.cuda.synchronize(); dt = (time.time() - t) / 10
+print(f"4096^3 bf16 torch.matmul (hipBLASLt): {dt*1e3:.3f} ms  {2*M*N*K/dt/1e12:.1f} TFLOP/s", flush=True)
 print("OK" if ok else "FAIL")
 sys.exit(0 if ok else 1)
