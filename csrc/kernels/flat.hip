@@ -195,3 +195,21 @@ extern "C" hipError_t ea_sub(const float* a, const float* b, float* out, long lo
   hipLaunchKernelGGL(sub_kernel, dim3(grid_for(n)), dim3(256), 0, s, a, b, out, n);
   return hipGetLastError();
 }
+
+// Diagnostics: fill every CU's LDS with a pattern (e.g. NaN) so a kernel that
+// reads LDS it never wrote shows it deterministically instead of inheriting
+// whatever the previous workgroup on that CU left there.
+__global__ __launch_bounds__(256) void poison_lds_kernel(unsigned pattern, int bytes) {
+  extern __shared__ __attribute__((aligned(16))) unsigned lds_words[];
+  for (int i = threadIdx.x; i < bytes / 4; i += 256) lds_words[i] = pattern;
+  __syncthreads();
+  if (threadIdx.x == 0 && lds_words[(blockIdx.x * 97) % (bytes / 4)] != pattern) lds_words[0] = 0u;  // keep the stores live
+}
+
+extern "C" hipError_t ea_poison_lds(unsigned pattern, hipStream_t s) {
+  const int bytes = 160 * 1024;
+  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&poison_lds_kernel),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+  hipLaunchKernelGGL(poison_lds_kernel, dim3(4096), dim3(256), bytes, s, pattern, bytes);
+  return hipGetLastError();
+}

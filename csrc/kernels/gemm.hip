@@ -165,6 +165,79 @@ __device__ __forceinline__ void stamp_clk(const GroupArgs& ga, int k) {
   if (ga.stamps && threadIdx.x == 0) ga.stamps[(long long)blockIdx.x * 16 + k] = (long long)__builtin_amdgcn_s_memtime();
 }
 
+// ------------------------------------------------------- LDS-staged main loop
+// THR tile (128x128, 2x2 waves of 64x64, bf16): both operand tiles [128][64] are
+// staged global -> LDS with 16-byte global_load_lds (no VGPR round trip), double
+// buffered so the copy of k-tile t+1 overlaps the MFMAs of tile t, and shared by
+// the block's 4 waves (the register-direct loop loads every operand twice).
+// LDS image per operand: row-major [128][64] bf16 (128-byte rows) whose 16-byte
+// chunk c of row r lives in slot c ^ (r & 7): glds writes lane-linear, so the
+// swizzle is applied to the per-lane SOURCE address and undone on the ds_read
+// (the 16 lanes of a fragment read then spread over 8 slots: <= 2-way conflicts).
+constexpr int THR_BK = 64;
+constexpr int THR_STAGE_BYTES = 2 * 128 * THR_BK * 2;  // A + B tiles of one k-step
+
+__device__ __forceinline__ void glds16(const void* g, char* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
+                                   (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
+}
+
+// arow_ld/bcol_ld: per lane, the 4 source rows it stages (already clamped to valid memory);
+// amask/aones_m/bmask: validity of the 4+4 fragment rows it READS (as in the register loop)
+__device__ __forceinline__ void thr_lds_mainloop(const __bf16* const (&arow_ld)[4], const __bf16* const (&bcol_ld)[4],
+                                                 int K, unsigned amask, unsigned aones_m, unsigned bmask, int wm, int wn,
+                                                 f32x4 (&acc)[4][4], char* sbase) {
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int g = lane >> 4, i16 = lane & 15;
+  const int c8 = ((lane & 7) ^ ((lane >> 3) & 7)) * 8;  // element offset of this lane's staged chunk
+  const int nk = (K + THR_BK - 1) / THR_BK;
+  auto stage = [&](int kt, int buf) {
+    const int kk = kt * THR_BK + c8;
+    const int koff = kk < K ? kk : 0;  // past K: any in-bounds chunk (masked on read)
+    char* dA = sbase + buf * THR_STAGE_BYTES + wave * 1024;
+    char* dB = dA + THR_STAGE_BYTES / 2;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) glds16(arow_ld[t] + koff, dA + t * 4096);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) glds16(bcol_ld[t] + koff, dB + t * 4096);
+  };
+  const uint4 zero = make_uint4(0u, 0u, 0u, 0u);
+  const uint4 one = ones_frag<__bf16>();
+  auto sel = [](bool c, const uint4& a, const uint4& b) {
+    return make_uint4(c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z, c ? a.w : b.w);
+  };
+  stage(0, 0);
+  for (int kt = 0; kt < nk; ++kt) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's copies of tile kt landed
+    __syncthreads();                                   // ... and every other wave's; buffer kt+1 is free
+    if (kt + 1 < nk) stage(kt + 1, (kt + 1) & 1);
+    const char* bA = sbase + (kt & 1) * THR_STAGE_BYTES;
+    const char* bB = bA + THR_STAGE_BYTES / 2;
+#pragma unroll
+    for (int u = 0; u < THR_BK / 32; ++u) {
+      const bool kin = kt * THR_BK + u * 32 + g * 8 < K;
+      const int slot = ((u * 4 + g) ^ (i16 & 7)) * 16;
+      uint4 a[4], b[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const uint4 v = *reinterpret_cast<const uint4*>(bA + (wm * 64 + i * 16 + i16) * 128 + slot);
+        a[i] = sel(kin && ((amask >> i) & 1u), v, sel(kin && ((aones_m >> i) & 1u), one, zero));
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint4 v = *reinterpret_cast<const uint4*>(bB + (wn * 64 + j * 16 + i16) * 128 + slot);
+        b[j] = sel(kin && ((bmask >> j) & 1u), v, zero);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) mma16<__bf16>(acc[i][j], a[i], b[j]);
+    }
+  }
+  __syncthreads();  // the epilogue reuses the staging LDS
+}
+
 // --------------------------------------------------------------- the kernel
 template <typename T, int WM, int WN, int WAVES_M, int WAVES_N, int KSPLIT>
 __device__ __forceinline__ void run_prob(const GroupArgs& ga, const Prob& p, const int lb, float* smem) {
@@ -184,8 +257,8 @@ __device__ __forceinline__ void run_prob(const GroupArgs& ga, const Prob& p, con
     const int tm = t / p.tiles_n, tn = t % p.tiles_n;
     const int m0 = tm * BM, n0 = tn * BN;
     const long long step = ga.ctr[0] + ga.step_off;
-    // plain / inference problems carry no per-replica batch counts (ntrain == nullptr)
-    const long long iter = p.ntrain ? iter_at(ga.ctr, p.ntrain, p.B, r, ga.ctr[0], ga.step_off) : 0;
+    // (every launcher passes a valid ntrain: the plain-GEMM entry points it at zeros)
+    const long long iter = iter_at(ga.ctr, p.ntrain, p.B, r, ga.ctr[0], ga.step_off);
     const int valid = (p.kind == PK_PLAIN) ? p.M : batch_valid(p, r, step);
     const bool skip_update = (p.kind == PK_DW_UPDATE) && valid == 0;
     stamp(ga, 1);
@@ -241,6 +314,29 @@ __device__ __forceinline__ void run_prob(const GroupArgs& ga, const Prob& p, con
           bmask |= 1u << j;
         }
       }
+      if constexpr (sizeof(T) == 2 && KSPLIT == 1 && BM == 128 && BN == 128 && WM == 4 && WN == 4) {
+        // staged rows of this lane: r = 32 t + 8 wave + lane / 8 of the A and B^T tiles
+        const __bf16* arow_ld[4];
+        const __bf16* bcol_ld[4];
+        const __bf16* Ab = reinterpret_cast<const __bf16*>(A);
+        const __bf16* Bb = reinterpret_cast<const __bf16*>(BTp);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const int rr = t * 32 + (threadIdx.x >> 3);
+          const int m = m0 + rr, n = n0 + rr;
+          arow_ld[t] = Ab;
+          if (m < p.M && m != p.ones_row) {
+            if (p.a_gather) {
+              if (m < valid) arow_ld[t] = Ab + batch_row(p, r, step, m) * p.lda;
+            } else {
+              arow_ld[t] = Ab + (long long)m * p.lda;
+            }
+          }
+          bcol_ld[t] = n < p.N ? Bb + (long long)n * p.ldb : Bb;
+        }
+        thr_lds_mainloop(arow_ld, bcol_ld, p.K, amask, aones_m, bmask, wm, wn,
+                         reinterpret_cast<f32x4(&)[4][4]>(acc), reinterpret_cast<char*>(smem));
+      } else {
       const uint4 zero = make_uint4(0u, 0u, 0u, 0u);
       const uint4 one = ones_frag<T>();
       auto sel = [](bool c, const uint4& a, const uint4& b) {
@@ -289,6 +385,7 @@ __device__ __forceinline__ void run_prob(const GroupArgs& ga, const Prob& p, con
           }
         }
       }
+      }  // register-direct loop
     }
 
     stamp(ga, 2);

@@ -24,6 +24,7 @@ extern "C" hipError_t ea_replica_average(float* P, long long sP, int R, long lon
                                          hipStream_t s);
 extern "C" hipError_t ea_axpby(const float* x, float* y, long long n, float alpha, float beta, hipStream_t s);
 extern "C" hipError_t ea_ps_sub(float* p, const float* d, long long n, float scale, int atomic, hipStream_t s);
+extern "C" hipError_t ea_poison_lds(unsigned pattern, hipStream_t s);
 extern "C" hipError_t ea_sub(const float* a, const float* b, float* out, long long n, hipStream_t s);
 
 static void chk(hipError_t e, const char* w) {
@@ -204,6 +205,7 @@ PYBIND11_MODULE(_C, m) {
       chk(hipMemset(dctr, 0, 64 * sizeof(long long)), "hipMemset");
     }
     ga.ctr = dctr;
+    p.ntrain = reinterpret_cast<const int*>(dctr);  // zero batch counts: the kernel reads ntrain[0]
     chk(ea_gemm_grouped(&ga, bf16, cfg, S(s)), "gemm_nt");
   });
   m.def("tile_shape", [](int cfg) { return py::make_tuple(ea_gemm_tile_m(cfg), ea_gemm_tile_n(cfg)); });
@@ -219,6 +221,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("ps_sub", [](uintptr_t p, uintptr_t d, long long n, float scale, int atomic, uintptr_t s) {
     chk(ea_ps_sub(reinterpret_cast<float*>(p), reinterpret_cast<const float*>(d), n, scale, atomic, S(s)), "ps_sub");
   });
+  m.def("poison_lds", [](unsigned pattern, uintptr_t s) { chk(ea_poison_lds(pattern, S(s)), "poison_lds"); });
   m.def("sub", [](uintptr_t a, uintptr_t b, uintptr_t out, long long n, uintptr_t s) {
     chk(ea_sub(reinterpret_cast<const float*>(a), reinterpret_cast<const float*>(b), reinterpret_cast<float*>(out), n,
                S(s)),

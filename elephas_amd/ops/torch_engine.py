@@ -55,11 +55,11 @@ class TorchTrainer(TrainerBase):
         self.iters = [0] * self.R
 
     # ---------------------------------------------------------------- forward
-    def forward(self, r: int, x: torch.Tensor, training: bool):
+    def forward(self, r: int, x: torch.Tensor, training: bool, ps=None):
         h = x
         wi = 0
         pre, last_act = None, None
-        ps = self.params[r]
+        ps = self.params[r] if ps is None else ps
         for op in self.plan.ops:
             if isinstance(op, Dense):
                 h = h @ ps[wi]
@@ -190,9 +190,14 @@ class TorchTrainer(TrainerBase):
 
     @torch.no_grad()
     def predict(self, x, batch_size=None, r: int = 0):
-        xt = torch.tensor(prepare_features(x, self.in_dim), device=self.device)
+        # Row results must not depend on how rows are batched (reference
+        # tests/test_ml_model.py:345-354 requires batched == unbatched inference
+        # exactly): BLAS kernels pick blockings by M, so inference runs in fp64
+        # and rounds to fp32 once, which makes every row's value batch-invariant.
+        xt = torch.tensor(prepare_features(x, self.in_dim), device=self.device, dtype=torch.float64)
+        ps = [p.detach().double() for p in self.params[r]]
         bs = batch_size or 4096
-        outs = [self.forward(r, xt[b0:b0 + bs], False)[0] for b0 in range(0, len(xt), bs)]
+        outs = [self.forward(r, xt[b0:b0 + bs], False, ps)[0].float() for b0 in range(0, len(xt), bs)]
         if not outs:
             return np.zeros((0, self.n_out), np.float32)
         return torch.cat(outs).float().cpu().numpy()

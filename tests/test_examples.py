@@ -1,0 +1,31 @@
+"""The ported reference examples (examples/*.py, reference examples/) run end to
+end on the CPU engine with trimmed synthetic data."""
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+EX = os.path.join(ROOT, "examples")
+
+
+@pytest.mark.parametrize("script,expect", [
+    ("mnist_mlp_spark_synchronous.py", "Test accuracy"),
+    ("mnist_mlp_spark_asynchronous.py", "Test accuracy"),
+    ("mllib_mlp.py", "Test accuracy"),
+    ("ml_mlp_regression.py", ""),
+    ("ml_pipeline_otto.py", "precision"),
+])
+def test_example_runs(tmp_path, script, expect):
+    env = dict(os.environ, PYTHONPATH=ROOT, EXAMPLE_ROWS="800", EXAMPLE_EPOCHS="1", OTTO_ROWS="600",
+               CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    if script == "ml_pipeline_otto.py":   # writes its synthetic CSV next to a copy of the script
+        import shutil
+        shutil.copy(os.path.join(EX, script), tmp_path / script)
+        cwd, path = str(tmp_path), str(tmp_path / script)
+    else:
+        cwd, path = EX, os.path.join(EX, script)
+    r = subprocess.run([sys.executable, path], cwd=cwd, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    assert expect in r.stdout

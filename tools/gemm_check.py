@@ -22,20 +22,24 @@ for (M, N, K) in [(64, 128, 784), (64, 10, 128), (785, 128, 64), (300, 200, 136)
             print(f"M={M} N={N} K={K} bf16={bf16} cfg={cfg} relerr={err:.2e}", flush=True)
             if err > 1e-2:
                 ok = False
-# timing of the big one
-M = N = K = 4096
-A = torch.randn(M, K, device=dev).to(torch.bfloat16); BT = torch.randn(N, K, device=dev).to(torch.bfloat16)
-Cm = torch.zeros(M, N, device=dev); s = torch.cuda.current_stream().cuda_stream
-for cfg in (0, 1):
-    for _ in range(3): C.gemm_nt(A.data_ptr(), BT.data_ptr(), Cm.data_ptr(), M, N, K, K, K, N, 1, cfg, s)
-    torch.cuda.synchronize(); t = time.time()
-    for _ in range(10): C.gemm_nt(A.data_ptr(), BT.data_ptr(), Cm.data_ptr(), M, N, K, K, K, N, 1, cfg, s)
-    torch.cuda.synchronize(); dt = (time.time() - t) / 10
-    print(f"4096^3 bf16 cfg={cfg}: {dt*1e3:.3f} ms  {2*M*N*K/dt/1e12:.1f} TFLOP/s", flush=True)
-for _ in range(3): torch.matmul(A, BT.t())
-torch.cuda.synchronize(); t = time.time()
-for _ in range(10): torch.matmul(A, BT.t())
-torch.cuda.synchronize(); dt = (time.time() - t) / 10
-print(f"4096^3 bf16 torch.matmul (hipBLASLt): {dt*1e3:.3f} ms  {2*M*N*K/dt/1e12:.1f} TFLOP/s", flush=True)
+# timing of the wide-MLP shapes: FWD/DX (M=batch 1024) and DW (K=batch)
+s = torch.cuda.current_stream().cuda_stream
+for (M, N, K) in [(4096, 4096, 4096), (1024, 4096, 4096), (4096, 4096, 1024), (1024, 1000, 4096)]:
+    A = (torch.rand(M, K, device=dev) * 2 - 1).to(torch.bfloat16)
+    BT = (torch.rand(N, K, device=dev) * 2 - 1).to(torch.bfloat16)
+    Cm = torch.zeros(M, N, device=dev)
+    res = []
+    for cfg in (0, 1, "torch"):
+        def f():
+            if cfg == "torch":
+                torch.matmul(A, BT.t())
+            else:
+                C.gemm_nt(A.data_ptr(), BT.data_ptr(), Cm.data_ptr(), M, N, K, K, K, N, 1, cfg, s)
+        for _ in range(3): f()
+        torch.cuda.synchronize(); t = time.time()
+        for _ in range(20): f()
+        torch.cuda.synchronize(); dt = (time.time() - t) / 20
+        res.append(f"{cfg}: {dt*1e6:.0f} us {2*M*N*K/dt/1e12:.0f} TF")
+    print(f"M={M} N={N} K={K} bf16 random:", " | ".join(res), flush=True)
 print("OK" if ok else "FAIL")
 sys.exit(0 if ok else 1)
