@@ -176,64 +176,112 @@ __device__ __forceinline__ void stamp_clk(const GroupArgs& ga, int k) {
 // (the 16 lanes of a fragment read then spread over 8 slots: <= 2-way conflicts).
 constexpr int THR_BK = 64;
 constexpr int THR_STAGE_BYTES = 2 * 128 * THR_BK * 2;  // A + B tiles of one k-step
+constexpr int THR_NS = 2;                              // ring depth (2 keeps 2 blocks/CU: 837 vs 603 TF at 4096^3 for 4)
+constexpr int THR_GLDS = 8;                            // glds per wave per k-tile (4 A + 4 B)
+
+// Masking happens on the SOURCE of each staged chunk: a row past M (or past the
+// valid batch rows), a B^T row past N and any chunk past K copy 16 zero bytes,
+// and the bias "ones row" copies 16 bytes of bf16 1.0 -- so the LDS image is
+// exactly the operand tile and the fragment reads need no per-element selects.
+__device__ __attribute__((aligned(16))) const unsigned short g_thr_zero[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+__device__ __attribute__((aligned(16))) const unsigned short g_thr_ones[8] = {0x3F80, 0x3F80, 0x3F80, 0x3F80,
+                                                                             0x3F80, 0x3F80, 0x3F80, 0x3F80};
+
+__device__ __forceinline__ void ds_read16(uint4& v, unsigned lds_addr) {
+  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(lds_addr) : "memory");
+}
 
 __device__ __forceinline__ void glds16(const void* g, char* lds_wave_base) {
   __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
                                    (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
 }
 
-// arow_ld/bcol_ld: per lane, the 4 source rows it stages (already clamped to valid memory);
-// amask/aones_m/bmask: validity of the 4+4 fragment rows it READS (as in the register loop)
+// arow_ld/bcol_ld: per lane, the 4 source rows it stages (nullptr = zero row);
+// aones: bit t set when staged A row t is the bias ones row.
 __device__ __forceinline__ void thr_lds_mainloop(const __bf16* const (&arow_ld)[4], const __bf16* const (&bcol_ld)[4],
-                                                 int K, unsigned amask, unsigned aones_m, unsigned bmask, int wm, int wn,
-                                                 f32x4 (&acc)[4][4], char* sbase) {
+                                                 unsigned aones, int K, int wm, int wn, f32x4 (&acc)[4][4],
+                                                 char* sbase) {
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int g = lane >> 4, i16 = lane & 15;
+  const int i16 = lane & 15, g = lane >> 4;
   const int c8 = ((lane & 7) ^ ((lane >> 3) & 7)) * 8;  // element offset of this lane's staged chunk
   const int nk = (K + THR_BK - 1) / THR_BK;
+  const unsigned lds_base = (unsigned)(size_t)((__attribute__((address_space(3))) char*)sbase);
+  // 64-bit source addresses selected arithmetically (v_cndmask, no branches: a
+  // divergent branch would split each glds into several exec-masked copies and
+  // break the per-tile glds count the counted waits rely on)
+  typedef unsigned long long u64;
+  const u64 zp = (u64)(const void*)g_thr_zero, op = (u64)(const void*)g_thr_ones;
+  u64 abase[4], bbase[4];
+  unsigned amov = 0, bmov = 0;  // bit t: staged row t advances with k (a real operand row)
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const bool ar = arow_ld[t] != nullptr, br = bcol_ld[t] != nullptr;
+    abase[t] = ((aones >> t) & 1u) ? op : (ar ? (u64)arow_ld[t] : zp);
+    bbase[t] = br ? (u64)bcol_ld[t] : zp;
+    amov |= (ar && !((aones >> t) & 1u)) ? 1u << t : 0u;
+    bmov |= br ? 1u << t : 0u;
+  }
   auto stage = [&](int kt, int buf) {
     const int kk = kt * THR_BK + c8;
-    const int koff = kk < K ? kk : 0;  // past K: any in-bounds chunk (masked on read)
+    const bool kin = kk < K;
+    const u64 koff = (u64)kk * 2u;
     char* dA = sbase + buf * THR_STAGE_BYTES + wave * 1024;
     char* dB = dA + THR_STAGE_BYTES / 2;
 #pragma unroll
-    for (int t = 0; t < 4; ++t) glds16(arow_ld[t] + koff, dA + t * 4096);
+    for (int t = 0; t < 4; ++t) {
+      const u64 a = abase[t] + (((amov >> t) & 1u) ? koff : 0u);
+      glds16((const void*)(kin ? a : zp), dA + t * 4096);
+    }
 #pragma unroll
-    for (int t = 0; t < 4; ++t) glds16(bcol_ld[t] + koff, dB + t * 4096);
+    for (int t = 0; t < 4; ++t) {
+      const u64 b = bbase[t] + (((bmov >> t) & 1u) ? koff : 0u);
+      glds16((const void*)(kin ? b : zp), dB + t * 4096);
+    }
   };
-  const uint4 zero = make_uint4(0u, 0u, 0u, 0u);
-  const uint4 one = ones_frag<__bf16>();
-  auto sel = [](bool c, const uint4& a, const uint4& b) {
-    return make_uint4(c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z, c ? a.w : b.w);
-  };
-  stage(0, 0);
+#pragma unroll
+  for (int s = 0; s < THR_NS - 1; ++s)
+    if (s < nk) stage(s, s);
   for (int kt = 0; kt < nk; ++kt) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's copies of tile kt landed
-    __syncthreads();                                   // ... and every other wave's; buffer kt+1 is free
-    if (kt + 1 < nk) stage(kt + 1, (kt + 1) & 1);
-    const char* bA = sbase + (kt & 1) * THR_STAGE_BYTES;
-    const char* bB = bA + THR_STAGE_BYTES / 2;
+    // counted wait: the copies of the tiles issued after kt may stay in flight
+    const int ahead = (kt + THR_NS - 2 < nk - 1 ? kt + THR_NS - 2 : nk - 1) - kt;
+    static_assert(THR_GLDS == 8 && THR_NS <= 4, "vmcnt immediates below assume <= 4 stages x 8 glds");
+    if (ahead >= 2) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    else if (ahead == 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of the slot refilled below
+    __builtin_amdgcn_s_barrier();                        // tile kt landed for every wave; slot kt-1 is free
+    asm volatile("" ::: "memory");
+    if (kt + THR_NS - 1 < nk) stage(kt + THR_NS - 1, (kt + THR_NS - 1) % THR_NS);
+    // Fragment reads are inline-asm ds_read_b128: for compiler-visible LDS loads
+    // hipcc cannot tell the slot being read from the slot the glds above is
+    // filling and waits vmcnt(0) before the first read (draining the prefetch,
+    // so every k-step paid a full HBM round trip). The waits for these reads are
+    // explicit lgkmcnt + sched_barrier (the MFMAs must not be hoisted above them).
+    const unsigned bA = lds_base + (unsigned)((kt % THR_NS) * THR_STAGE_BYTES);
+    const unsigned bB = bA + THR_STAGE_BYTES / 2;
+    uint4 fa[2][4], fb[2][4];
 #pragma unroll
     for (int u = 0; u < THR_BK / 32; ++u) {
-      const bool kin = kt * THR_BK + u * 32 + g * 8 < K;
-      const int slot = ((u * 4 + g) ^ (i16 & 7)) * 16;
-      uint4 a[4], b[4];
+      const unsigned slot = (unsigned)(((u * 4 + g) ^ (i16 & 7)) * 16);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const uint4 v = *reinterpret_cast<const uint4*>(bA + (wm * 64 + i * 16 + i16) * 128 + slot);
-        a[i] = sel(kin && ((amask >> i) & 1u), v, sel(kin && ((aones_m >> i) & 1u), one, zero));
-      }
+      for (int i = 0; i < 4; ++i) ds_read16(fa[u][i], bA + (unsigned)((wm * 64 + i * 16 + i16) * 128) + slot);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const uint4 v = *reinterpret_cast<const uint4*>(bB + (wn * 64 + j * 16 + i16) * 128 + slot);
-        b[j] = sel(kin && ((bmask >> j) & 1u), v, zero);
-      }
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) mma16<__bf16>(acc[i][j], a[i], b[j]);
+      for (int j = 0; j < 4; ++j) ds_read16(fb[u][j], bB + (unsigned)((wn * 64 + j * 16 + i16) * 128) + slot);
+      if (u == 0) continue;  // substep 1's reads are issued before substep 0's MFMAs
     }
+    asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");  // substep 0 landed (substep 1's 8 reads may be in flight)
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) mma16<__bf16>(acc[i][j], fa[0][i], fb[0][j]);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) mma16<__bf16>(acc[i][j], fa[1][i], fb[1][j]);
   }
   __syncthreads();  // the epilogue reuses the staging LDS
 }
@@ -318,24 +366,27 @@ __device__ __forceinline__ void run_prob(const GroupArgs& ga, const Prob& p, con
         // staged rows of this lane: r = 32 t + 8 wave + lane / 8 of the A and B^T tiles
         const __bf16* arow_ld[4];
         const __bf16* bcol_ld[4];
+        unsigned aones = 0;
         const __bf16* Ab = reinterpret_cast<const __bf16*>(A);
         const __bf16* Bb = reinterpret_cast<const __bf16*>(BTp);
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
           const int rr = t * 32 + (threadIdx.x >> 3);
           const int m = m0 + rr, n = n0 + rr;
-          arow_ld[t] = Ab;
-          if (m < p.M && m != p.ones_row) {
+          arow_ld[t] = nullptr;
+          if (m == p.ones_row) {
+            aones |= 1u << t;
+          } else if (m < p.M) {
             if (p.a_gather) {
               if (m < valid) arow_ld[t] = Ab + batch_row(p, r, step, m) * p.lda;
             } else {
               arow_ld[t] = Ab + (long long)m * p.lda;
             }
           }
-          bcol_ld[t] = n < p.N ? Bb + (long long)n * p.ldb : Bb;
+          bcol_ld[t] = n < p.N ? Bb + (long long)n * p.ldb : nullptr;
         }
-        thr_lds_mainloop(arow_ld, bcol_ld, p.K, amask, aones_m, bmask, wm, wn,
-                         reinterpret_cast<f32x4(&)[4][4]>(acc), reinterpret_cast<char*>(smem));
+        thr_lds_mainloop(arow_ld, bcol_ld, aones, p.K, wm, wn, reinterpret_cast<f32x4(&)[4][4]>(acc),
+                         reinterpret_cast<char*>(smem));
       } else {
       const uint4 zero = make_uint4(0u, 0u, 0u, 0u);
       const uint4 one = ones_frag<T>();
@@ -679,6 +730,8 @@ static size_t lds_bytes(bool loss = true) {
   constexpr int BN = WAVES_N * WN * 16;
   const size_t tile = (size_t)BM * (BN + 4);
   size_t floats = (size_t)KSPLIT * tile;
+  if (sizeof(T) == 2 && KSPLIT == 1 && BM == 128 && BN == 128)  // glds staging ring (thr_lds_mainloop)
+    floats = std::max(floats, (size_t)THR_NS * THR_STAGE_BYTES / sizeof(float));
   if (loss) floats = std::max(floats, tile + BM + (size_t)BM * BN);  // + row map + staged targets
   floats = std::max(floats, (size_t)64 * 65);                       // gather-transpose
   return floats * sizeof(float);

@@ -2,7 +2,9 @@
 import importlib.util, sys, os, time
 import torch
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-spec = importlib.util.spec_from_file_location('_C', os.path.join(ROOT, 'elephas_amd', '_C.cpython-310-x86_64-linux-gnu.so'))
+SO = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, 'elephas_amd', '_C.cpython-310-x86_64-linux-gnu.so')
+print("module:", SO, flush=True)
+spec = importlib.util.spec_from_file_location('_C', SO)
 C = importlib.util.module_from_spec(spec); spec.loader.exec_module(C)
 dev = 'cuda'
 torch.manual_seed(0)
