@@ -91,6 +91,101 @@ __global__ __launch_bounds__(256) void refresh_shadows_kernel(FlatArgs a) {
   }
 }
 
+// ---- tiled shadow writers: one 64x64 tile of one layer's kernel [K][N] per
+// block. P / G / S rows are read coalesced, the row-major W image is written
+// coalesced, and W^T goes through an LDS transpose so its stores are coalesced
+// too (the element-wise writer above scatters W^T with a stride of Kp elements:
+// 0.82 ms for the 37.7 M-parameter wide MLP). UPDATE additionally applies the
+// optimizer (per-step all-reduce path); bias rows ride with the k-tile 0 blocks.
+struct TileV {
+  long long p_off, wsh_off, ldwsh, wtsh_off, ldwtsh;
+  int K, N, has_bias, tk, tn;
+};
+
+__device__ __forceinline__ TileV find_tile(const FlatArgs& a, int t, int& lt) {
+  TileV v{};
+  int base = 0;
+  lt = t;
+#pragma unroll
+  for (int q = 0; q < MAX_SEG; ++q) {
+    if (q < a.nseg) {
+      const int tk = (a.seg[q].K + 63) / 64, tn = (a.seg[q].N + 63) / 64;
+      if (t >= base) {
+        v = TileV{a.seg[q].p_off, a.seg[q].wsh_off, a.seg[q].ldwsh, a.seg[q].wtsh_off, a.seg[q].ldwtsh,
+                  a.seg[q].K, a.seg[q].N, a.seg[q].has_bias, tk, tn};
+        lt = t - base;
+      }
+      base += tk * tn;
+    }
+  }
+  return v;
+}
+
+template <typename T, bool UPDATE>
+__global__ __launch_bounds__(256) void shadow_tiles_kernel(FlatArgs a, int tiles_per_replica) {
+  __shared__ float tile[64][65];
+  const int r = blockIdx.x / tiles_per_replica;
+  int lt;
+  const TileV g = find_tile(a, blockIdx.x - r * tiles_per_replica, lt);
+  const int k0 = (lt / g.tn) * 64, n0 = (lt % g.tn) * 64;
+  long long iter = a.ctr[2 + r];
+  if (UPDATE && (long long)a.ntrain[r] - a.ctr[0] * a.B <= 0) return;  // replica has no batch this step
+  const int p0 = UPDATE ? (int)((iter + 1) & 1) : (a.both_parities ? 0 : (int)(iter & 1));
+  const int p1 = UPDATE ? p0 : (a.both_parities ? 1 : p0);
+  float* P = a.P + (long long)r * a.sP;
+  float* S = a.S ? a.S + (long long)r * a.sS : nullptr;
+  const int tid = threadIdx.x, nn = tid & 63;
+  T* W = a.Wsh ? reinterpret_cast<T*>(a.Wsh) + (long long)r * a.sWsh + g.wsh_off : nullptr;
+  T* WT = a.WTsh ? reinterpret_cast<T*>(a.WTsh) + (long long)r * a.sWTsh + g.wtsh_off : nullptr;
+#pragma unroll 4
+  for (int i = 0; i < 16; ++i) {
+    const int kk = (tid >> 6) + 4 * i, k = k0 + kk, n = n0 + nn;
+    float w = 0.f;
+    if (k < g.K && n < g.N) {
+      const long long pi = g.p_off + (long long)k * g.N + n;
+      w = P[pi];
+      if (UPDATE) {
+        w = opt_update(a.op, w, a.G[(long long)r * a.sG + pi] * a.op.grad_scale, S, pi, iter);
+        P[pi] = w;
+      }
+      if (W) {
+        W[p0 * a.wsh_par + (long long)k * g.ldwsh + n] = from_f<T>(w);
+        if (p1 != p0) W[p1 * a.wsh_par + (long long)k * g.ldwsh + n] = from_f<T>(w);
+      }
+    }
+    tile[kk][nn] = w;
+  }
+  if (k0 == 0 && g.has_bias && tid < 64 && n0 + tid < g.N) {
+    const long long pi = g.p_off + (long long)g.K * g.N + n0 + tid;
+    float w = P[pi];
+    if (UPDATE) {
+      w = opt_update(a.op, w, a.G[(long long)r * a.sG + pi] * a.op.grad_scale, S, pi, iter);
+      P[pi] = w;
+    }
+    if (a.Bsh) {
+      a.Bsh[(long long)r * a.sBsh + p0 * a.bsh_par + pi] = w;
+      if (p1 != p0) a.Bsh[(long long)r * a.sBsh + p1 * a.bsh_par + pi] = w;
+    }
+  }
+  if (!WT) return;
+  __syncthreads();
+#pragma unroll 4
+  for (int i = 0; i < 16; ++i) {
+    const int nl = (tid >> 6) + 4 * i, kl = tid & 63, k = k0 + kl, n = n0 + nl;
+    if (k < g.K && n < g.N) {
+      const T v = from_f<T>(tile[kl][nl]);
+      WT[p0 * a.wtsh_par + (long long)n * g.ldwtsh + k] = v;
+      if (p1 != p0) WT[p1 * a.wtsh_par + (long long)n * g.ldwtsh + k] = v;
+    }
+  }
+}
+
+static int shadow_tiles(const FlatArgs& a) {
+  int t = 0;
+  for (int q = 0; q < a.nseg; ++q) t += ((a.seg[q].K + 63) / 64) * ((a.seg[q].N + 63) / 64);
+  return t;
+}
+
 // mean over R replicas of P[r][i]; result written to every replica (and to out if given)
 __global__ __launch_bounds__(256) void replica_average_kernel(float* P, long long sP, int R, long long n,
                                                               float* out, int write_back) {
@@ -156,9 +251,11 @@ static inline int grid_for(long long n) {
 using namespace ea;
 
 extern "C" hipError_t ea_apply_update(FlatArgs* a, int bf16, hipStream_t s) {
-  a->total_blocks = grid_for((long long)a->R * a->n);
-  if (bf16) hipLaunchKernelGGL(apply_update_kernel<__bf16>, dim3(a->total_blocks), dim3(256), 0, s, *a);
-  else hipLaunchKernelGGL(apply_update_kernel<float>, dim3(a->total_blocks), dim3(256), 0, s, *a);
+  const int tiles = shadow_tiles(*a);
+  a->total_blocks = a->R * tiles;
+  if (a->total_blocks <= 0) return hipSuccess;
+  if (bf16) hipLaunchKernelGGL((shadow_tiles_kernel<__bf16, true>), dim3(a->total_blocks), dim3(256), 0, s, *a, tiles);
+  else hipLaunchKernelGGL((shadow_tiles_kernel<float, true>), dim3(a->total_blocks), dim3(256), 0, s, *a, tiles);
   return hipGetLastError();
 }
 
@@ -168,9 +265,11 @@ extern "C" hipError_t ea_advance(long long* ctr, const int* ntrain, int R, int B
 }
 
 extern "C" hipError_t ea_refresh_shadows(FlatArgs* a, int bf16, hipStream_t s) {
-  a->total_blocks = grid_for((long long)a->R * a->n);
-  if (bf16) hipLaunchKernelGGL(refresh_shadows_kernel<__bf16>, dim3(a->total_blocks), dim3(256), 0, s, *a);
-  else hipLaunchKernelGGL(refresh_shadows_kernel<float>, dim3(a->total_blocks), dim3(256), 0, s, *a);
+  const int tiles = shadow_tiles(*a);
+  a->total_blocks = a->R * tiles;
+  if (a->total_blocks <= 0) return hipSuccess;
+  if (bf16) hipLaunchKernelGGL((shadow_tiles_kernel<__bf16, false>), dim3(a->total_blocks), dim3(256), 0, s, *a, tiles);
+  else hipLaunchKernelGGL((shadow_tiles_kernel<float, false>), dim3(a->total_blocks), dim3(256), 0, s, *a, tiles);
   return hipGetLastError();
 }
 

@@ -334,3 +334,49 @@ def test_native_inference_is_batch_invariant():
     assert np.array_equal(full, chunks)
     assert np.array_equal(full, odd)
     config.set_policy("float32")
+
+
+@pytest.mark.parametrize("policy", ["float32", "mixed_bfloat16"])
+@pytest.mark.parametrize("opt", ["sgd_mom", "adam"])
+def test_allreduce_apply_path_equals_fused_update(policy, opt):
+    """Per-step gradient path ([fwd+bwd -> G] -> all-reduce -> tiled apply kernel
+    that also rebuilds the W / W^T images) == the fused DW_UPDATE epilogue."""
+    from elephas_amd import config
+    from elephas_amd.models import optimizers as O
+    from elephas_amd.ops.plan import build_plan
+    from elephas_amd.ops.native_engine import NativeTrainer
+    config.set_policy(policy)
+    model = _mlp(130, [200, 72], 9, dropout=0.25)
+    model.compile(O.SGD(0.05, momentum=0.9) if opt == "sgd_mom" else O.Adam(0.002), "categorical_crossentropy")
+    x, y = _data(400, 130, 9, seed=4)
+    ws = []
+    for path in ("fused", "allreduce"):
+        t = NativeTrainer(model, build_plan(model), 2, 32, torch.device("cuda"), seed=3)
+        t.set_data([x, x[::-1].copy()], [y, y[::-1].copy()], 0.0, shuffle=False)
+        t.begin_epoch()
+        if path == "fused":
+            t.run_steps(12, use_graph=True)
+        else:
+            t.run_steps_allreduce(12, lambda g: None, use_graph=True)
+        ws.append(t.get_weights_flat())
+    w0 = np.concatenate([w.reshape(-1) for w in model.get_weights()])
+    err = np.abs(ws[0] - ws[1]).max() / np.abs(ws[0] - w0).max()
+    assert err < (1e-4 if policy == "float32" else 2e-2), err
+    config.set_policy("float32")
+
+
+def test_refresh_shadows_round_trip():
+    """set_weights -> tiled refresh -> forward uses exactly the new weights."""
+    from elephas_amd import config
+    config.set_policy("float32")
+    model = _mlp(70, [130], 3, out_act="linear")
+    model.compile("sgd", "mse")
+    x, _ = _data(50, 70, 3)
+    p0 = model.predict(x)
+    rng = np.random.default_rng(0)
+    model.set_weights([rng.normal(size=w.shape).astype(np.float32) for w in model.get_weights()])
+    p1 = model.predict(x)
+    W = model.get_weights()
+    ref = np.maximum(x @ W[0] + W[1], 0) @ W[2] + W[3]
+    assert not np.allclose(p0, p1)
+    assert np.allclose(p1, ref, rtol=1e-4, atol=1e-4)
