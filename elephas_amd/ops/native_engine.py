@@ -217,6 +217,21 @@ class NativeTrainer(TrainerBase):
     def iterations(self) -> np.ndarray:
         return self._host(self.ctr[2:])
 
+    def get_state_flat(self):
+        return self._host(self.S), self.iterations()
+
+    def set_state_flat(self, state, iterations):
+        st = torch.from_numpy(np.array(np.broadcast_to(np.asarray(state, np.float32), tuple(self.S.shape)),
+                                       dtype=np.float32))
+        it = torch.from_numpy(np.array(np.broadcast_to(np.asarray(iterations, np.int64), (self.R,)),
+                                       dtype=np.int64))
+        self._enter()
+        with torch.cuda.stream(self.stream):
+            self.S.copy_(st.to(self.dev))
+            self.ctr[2:].copy_(it.to(self.dev))
+            self.exe.refresh_shadows(True, self.s)
+        self._exit()
+
     # ------------------------------------------------------------------- data
     def _upload_rows(self, dst: torch.Tensor, x: np.ndarray):
         """Stream host rows into a device tensor through the native pinned loader."""

@@ -41,14 +41,42 @@ class TorchTrainer(TrainerBase):
         flat = np.asarray(flat, np.float32)
         if flat.ndim == 1:
             flat = np.broadcast_to(flat, (self.R, flat.size))
-        self.params = []
+        # like keras set_weights: the optimizer state (moments, iteration) is kept
+        fresh = not getattr(self, "params", None)
+        if fresh:
+            self.params = []
         for r in range(self.R):
             ws = unflatten_weights(flat[r], self.like)
-            self.params.append([torch.tensor(w, device=self.device) for w in ws])
-        self.state = [opt.init_state(p) for opt, p in zip(self.opts, self.params)]
+            if fresh:
+                self.params.append([torch.tensor(w, device=self.device) for w in ws])
+            else:
+                for p, w in zip(self.params[r], ws):
+                    p.copy_(torch.from_numpy(np.ascontiguousarray(w)).to(p.device))
+        if fresh:
+            self.state = [opt.init_state(p) for opt, p in zip(self.opts, self.params)]
 
     def get_weights_flat(self):
         return np.stack([np.concatenate([p.detach().cpu().numpy().reshape(-1) for p in ps]) for ps in self.params])
+
+    def get_state_flat(self):
+        k = self.opts[0].n_state() if self.opts else 0
+        out = np.zeros((self.R, max(k, 1), sum(p.numel() for p in self.params[0])), np.float32)
+        for r in range(self.R):
+            for j in range(k):
+                out[r, j] = np.concatenate([s[j].detach().cpu().numpy().reshape(-1) for s in self.state[r]])
+        return out, np.asarray(self.iters, np.int64)
+
+    def set_state_flat(self, state, iterations):
+        state = np.asarray(state, np.float32)
+        k = self.opts[0].n_state() if self.opts else 0
+        for r in range(self.R):
+            for j in range(k):
+                off = 0
+                for s in self.state[r]:
+                    n = s[j].numel()
+                    s[j].copy_(torch.from_numpy(state[r, j, off:off + n].reshape(s[j].shape)).to(s[j].device))
+                    off += n
+        self.iters = [int(i) for i in np.broadcast_to(np.asarray(iterations), (self.R,))]
 
     def reset_optimizer_state(self):
         self.state = [opt.init_state(p) for opt, p in zip(self.opts, self.params)]
@@ -129,7 +157,67 @@ class TorchTrainer(TrainerBase):
         self.iters[r] += 1
         return per.detach(), [m.detach() for m in mvals]
 
-    def fit(self, epochs, verbose=0):
+    def _grads(self, r, xb, yb):
+        ps = self.params[r]
+        for p in ps:
+            p.requires_grad_(True)
+        pred, logits = self.forward(r, xb, True)
+        per, mvals = self._loss_and_metrics(yb, pred, logits)
+        grads = torch.autograd.grad(per.mean(), ps, allow_unused=True)
+        for p in ps:
+            p.requires_grad_(False)
+        grads = [g if g is not None else torch.zeros_like(p) for g, p in zip(grads, ps)]
+        return torch.cat([g.reshape(-1) for g in grads]), per.detach(), [m.detach() for m in mvals]
+
+    def fit_allreduce(self, epochs, allreduce, verbose=0):
+        """Per-step synchronous DP: every replica computes its batch gradient, the
+        [R, n] gradient block goes through ``allreduce`` (which leaves the
+        averaged gradient in every row), then every replica applies it."""
+        hist = [dict() if self.active[r] else None for r in range(self.R)]
+        shapes = [p.shape for p in self.params[0]]
+        sizes = [p.numel() for p in self.params[0]]
+        for epoch in range(int(epochs)):
+            idx = [torch.randperm(self.split[r], generator=self.gen) if self.shuffle else torch.arange(self.split[r])
+                   for r in range(self.R)]
+            steps = max([int(math.ceil(self.split[r] / self.B)) for r in range(self.R) if self.active[r]] or [0])
+            sums = [np.zeros(2 + len(self.metrics)) for _ in range(self.R)]
+            for s in range(steps):
+                G = torch.zeros(self.R, sum(sizes), device=self.device)
+                has = []
+                for r in range(self.R):
+                    bi = idx[r][s * self.B:(s + 1) * self.B]
+                    if not self.active[r] or len(bi) == 0:
+                        has.append(False)
+                        continue
+                    bi = bi.to(self.device)
+                    G[r], per, mvals = self._grads(r, self.xs[r][bi], self.ys[r][bi])
+                    has.append(True)
+                    sums[r][0] += float(per.sum())
+                    sums[r][1] += per.numel()
+                    for i, v in enumerate(mvals):
+                        sums[r][2 + i] += float(v.sum())
+                allreduce(G)
+                for r in range(self.R):
+                    if has[r]:
+                        grads = [g.reshape(sh) for g, sh in zip(torch.split(G[r], sizes), shapes)]
+                        self.opts[r].apply_torch(self.params[r], grads, self.state[r], self.iters[r])
+                        self.iters[r] += 1
+            for r in range(self.R):
+                if not self.active[r]:
+                    continue
+                n = self.split[r]
+                h = self._history_from_sums(sums[r]) if n > 0 else {}
+                if len(self.xs[r]) - n > 0:
+                    h.update(self._history_from_sums(self._eval_tensors(r, self.xs[r][n:], self.ys[r][n:]), "val_"))
+                for k, v in h.items():
+                    hist[r].setdefault(k, []).append(v)
+                if verbose:
+                    self.print_epoch(epoch, epochs, h, r)
+        return hist
+
+    def fit(self, epochs, verbose=0, allreduce=None):
+        if allreduce is not None:
+            return self.fit_allreduce(epochs, allreduce, verbose)
         hist = [dict() if self.active[r] else None for r in range(self.R)]
         for epoch in range(int(epochs)):
             for r in range(self.R):

@@ -78,6 +78,13 @@ class TrainerBase:
         """[R, n_params] fp32"""
         raise NotImplementedError
 
+    def get_state_flat(self):
+        """Optimizer state for checkpoints: ([R, planes, n_params] fp32, iterations [R])."""
+        raise NotImplementedError
+
+    def set_state_flat(self, state: np.ndarray, iterations) -> None:
+        raise NotImplementedError
+
     # ------------------------------------------------------------------- data
     def set_data(self, xs: Sequence[np.ndarray], ys: Sequence[np.ndarray], validation_split: float = 0.0,
                  active: Optional[Sequence[bool]] = None, shuffle: bool = True) -> None:

@@ -40,6 +40,8 @@ from .models import optimizers as O
 from .models import load_model
 from .ops.plan import flatten_weights, unflatten_weights
 from .parallel import dist
+from .profiling import MetricsLogger, PhaseTimer, device_sync, trace_range
+from .utils import checkpoint as ckpt
 from .parameter.factory import ClientServerFactory
 from .utils.functional_utils import divide_by, subtract_params
 from .utils.rdd_utils import lp_to_simple_rdd, to_simple_rdd
@@ -93,6 +95,15 @@ class SparkModel:
         self.port = port
         self.kwargs = kwargs
         self.serialized_model = model_to_dict(model)
+        # synchronous-mode averaging granularity (an extension):
+        #   'fit'   -- the reference: train all epochs locally, average once per fit
+        #   'epoch' -- average the workers' weights after every epoch
+        #   'batch' -- per-step gradient all-reduce (standard synchronous DP)
+        self.sync_granularity = kwargs.get("sync_granularity", "fit")
+        if self.sync_granularity not in ("fit", "epoch", "batch"):
+            raise ValueError("sync_granularity must be 'fit', 'epoch' or 'batch'")
+        self.metrics: Dict[str, Any] = {}
+        self.metrics_logger = MetricsLogger(kwargs.get("metrics_path"), rank=dist.rank())
         self.parameter_server = None
         self.client = None
         if self.mode != "synchronous":
@@ -207,6 +218,10 @@ class SparkModel:
 
         :param epochs: number of epochs; :param batch_size: per-worker batch size;
         :param verbose: 0/1/2; :param validation_split: tail fraction held out per worker
+        :param checkpoint_dir: (extension, synchronous mode) write a resumable
+            checkpoint there after every averaging point (each epoch for
+            sync_granularity 'epoch'/'batch', the end of fit for 'fit')
+        :param resume: continue from the checkpoint in checkpoint_dir if present
         """
         print(">>> Fit model")
         if self.num_workers:
@@ -232,44 +247,144 @@ class SparkModel:
         self._master_network.compile(optimizer=O.get(self.master_optimizer), loss=self.master_loss,
                                      metrics=self.master_metrics, custom_objects=self.custom_objects)
         train_config = dict(kwargs)
+        checkpoint_dir = train_config.pop("checkpoint_dir", None)
+        resume = bool(train_config.pop("resume", False))
         train_config.setdefault("epochs", 1)
         train_config.setdefault("batch_size", 32)
-        model_json = self._master_network.to_json()
-        init = self._broadcast_init()
-        parts = rdd.partitions()
-        lo, hi = dist.block_range(len(parts))
-        local = parts[lo:hi]
-        if self.mode in ["asynchronous", "hogwild"]:
-            new_parameters = self._fit_async(model_json, init, local, train_config)
-        elif self.mode == "synchronous":
-            new_parameters = self._fit_sync(model_json, init, local, len(parts), train_config)
-        else:
-            raise ValueError("Unsupported mode {}".format(self.mode))
-        self._master_network.set_weights(new_parameters)
+        timer = PhaseTimer(sync=device_sync())
+        self._timer = timer
+        t0 = __import__("time").perf_counter()
+        with trace_range("elephas.fit"):
+            model_json = self._master_network.to_json()
+            with timer.phase("broadcast"):
+                init = self._broadcast_init()
+            parts = rdd.partitions()
+            lo, hi = dist.block_range(len(parts))
+            local = parts[lo:hi]
+            if self.mode in ["asynchronous", "hogwild"]:
+                new_parameters = self._fit_async(model_json, init, local, train_config)
+            elif self.mode == "synchronous":
+                new_parameters = self._fit_sync(model_json, init, local, len(parts), train_config,
+                                                checkpoint_dir, resume)
+            else:
+                raise ValueError("Unsupported mode {}".format(self.mode))
+            self._master_network.set_weights(new_parameters)
+        wall = __import__("time").perf_counter() - t0
+        rows = sum(len(p) for p in parts)
+        epochs = int(train_config.get("epochs", 1))
+        vs = float(train_config.get("validation_split", 0.0) or 0.0)
+        samples = int(rows * (1.0 - vs)) * epochs
+        self.metrics = dict(mode=self.mode, granularity=self.sync_granularity if self.mode == "synchronous" else None,
+                            workers=len(parts), world_size=dist.world_size(), epochs=epochs, samples=samples,
+                            seconds=round(wall, 6), samples_per_sec=round(samples / wall, 2) if wall > 0 else None,
+                            phases=timer.as_dict())
+        self.metrics_logger.log("fit", **self.metrics)
 
-    def _fit_sync(self, model_json, init, local, n_parts, train_config):
+    # ------------------------------------------------------ sync averaging
+    def _sum_replicas(self, trainer, n):
+        """Sum over this rank's replicas of their weights, as a tensor on the
+        collective's device (stays in HBM on the native engine)."""
         import torch
-        worker = SparkWorker(model_json, init, train_config, self.master_optimizer, self.master_loss,
-                             self.master_metrics, self.custom_objects)
-        trainer, hist, active = worker.train_partitions(local)
-        # sum of the local workers' final weights, all-reduced over the job
-        if local and hasattr(trainer, "P"):           # native: stays on the device
+        if hasattr(trainer, "P"):                      # native: stays on the device
             trainer.stream.synchronize()
             total = trainer.P.sum(0, dtype=torch.float32)
-            if dist.backend() != "nccl":
-                total = total.cpu()
+            return total if dist.backend() == "nccl" else total.cpu()
+        w = trainer.get_weights_flat()
+        total = torch.from_numpy(w.sum(0).astype(np.float32) if len(w) else np.zeros(n, np.float32))
+        return total.cuda() if dist.backend() == "nccl" else total
+
+    def _average_into(self, trainer, n_params, n_parts, active_local):
+        """theta <- mean over all N workers of theta_i (reference spark_model.py:221-227:
+        theta0 - sum(delta_i)/N), written back into every local replica."""
+        with self._timer.phase("allreduce"):
+            total = self._sum_replicas(trainer, n_params) if active_local else self._zeros(n_params)
+            dist.all_reduce_sum_(total)
+            mean = total / float(max(n_parts, 1))
+        if active_local:
+            if hasattr(trainer, "P"):
+                import torch
+                with torch.cuda.stream(trainer.stream):
+                    trainer.P.copy_(mean.to(trainer.P.device).expand_as(trainer.P))
+                    trainer.sync_shadows()
+            else:
+                trainer.set_weights_flat(mean.cpu().numpy())
+        return mean
+
+    def _zeros(self, n):
+        import torch
+        z = torch.zeros(n, dtype=torch.float32)
+        return z.cuda() if dist.backend() == "nccl" else z
+
+    def _grad_allreduce(self, n_parts):
+        """Per-step gradient averaging over all workers of the job for [R, n] G blocks."""
+        def allreduce(G):
+            tot = G.sum(0)
+            dist.all_reduce_sum_(tot)
+            G.copy_((tot / float(max(n_parts, 1))).expand_as(G))
+        return allreduce
+
+    def _fit_sync(self, model_json, init, local, n_parts, train_config, checkpoint_dir=None, resume=False):
+        worker = SparkWorker(model_json, init, train_config, self.master_optimizer, self.master_loss,
+                             self.master_metrics, self.custom_objects)
+        n_params = len(flatten_weights(init))
+        gran = self.sync_granularity
+        epochs = int(train_config.get("epochs", 1))
+        verbose = int(train_config.get("verbose", 0))
+        with self._timer.phase("setup"):
+            trainer, active = worker.prepare_partitions(local)
+        start = 0
+        if checkpoint_dir and resume and ckpt.exists(checkpoint_dir):
+            with self._timer.phase("checkpoint"):
+                start, weights, state = ckpt.load(checkpoint_dir, dist.rank(), len(local))
+                if local:
+                    trainer.set_weights_flat(weights)
+                    if state is not None:
+                        trainer.set_state_flat(*state)
+            print(f">>> Resuming from epoch {start} of {epochs} ({checkpoint_dir})")
+        hist = [dict() if a else None for a in active]
+        if gran == "fit":
+            # the reference: every worker trains all epochs on its own, one average at the end
+            if start < epochs and local and any(active):
+                with self._timer.phase("train"):
+                    h = trainer.fit(epochs - start, verbose=verbose)
+                hist = [hh if a else None for hh, a in zip(h, active)]
+            mean = self._average_into(trainer, n_params, n_parts, bool(local))
+            if checkpoint_dir:
+                self._save_checkpoint(checkpoint_dir, epochs, epochs, mean, trainer, local)
         else:
-            w = trainer.get_weights_flat() if local else np.zeros((0, len(flatten_weights(init))), np.float32)
-            total = torch.from_numpy(w.sum(0).astype(np.float32) if len(w) else
-                                     np.zeros(len(flatten_weights(init)), np.float32))
-            if dist.backend() == "nccl":
-                total = total.cuda()
-        dist.all_reduce_sum_(total)
-        new = (total / float(max(n_parts, 1))).cpu().numpy()
-        for h in dist.all_gather_object(hist):
-            self._training_histories.extend(h)
+            mean = None
+            allreduce = self._grad_allreduce(n_parts) if gran == "batch" else None
+            for e in range(start, epochs):
+                if local and any(active):
+                    with self._timer.phase("train"):
+                        h = trainer.fit(1, verbose=verbose, allreduce=allreduce) if allreduce is not None \
+                            else trainer.fit(1, verbose=verbose)
+                    for r, (hh, a) in enumerate(zip(h, active)):
+                        if a and hh:
+                            for k, v in hh.items():
+                                hist[r].setdefault(k, []).extend(v)
+                elif gran == "batch":
+                    raise RuntimeError("per-step all-reduce needs at least one partition on every rank")
+                mean = self._average_into(trainer, n_params, n_parts, bool(local))
+                if checkpoint_dir:
+                    self._save_checkpoint(checkpoint_dir, e + 1, epochs, mean, trainer, local)
+            if mean is None:
+                mean = self._average_into(trainer, n_params, n_parts, bool(local))
+        with self._timer.phase("gather_histories"):
+            for h in dist.all_gather_object(hist if local else []):
+                self._training_histories.extend(h)
         print(">>> Synchronous training complete.")
-        return unflatten_weights(new, init)
+        return unflatten_weights(mean.cpu().numpy(), init)
+
+    def _save_checkpoint(self, directory, epoch, epochs, mean, trainer, local):
+        with self._timer.phase("checkpoint"), trace_range("elephas.checkpoint"):
+            state = trainer.get_state_flat() if local else None
+            weights = mean.cpu().numpy()
+            if dist.rank() == 0:
+                self._master_network.set_weights(unflatten_weights(weights, self._master_network.get_weights()))
+            ckpt.save(directory, epoch, epochs, self._master_network, weights, state, dist.rank(),
+                      dict(class_name=self.__class__.__name__, config=self.get_config()))
+            dist.barrier()
 
     def _fit_async(self, model_json, init, local, train_config):
         import torch

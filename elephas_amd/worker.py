@@ -81,6 +81,25 @@ class SparkWorker:
         after = self.model.get_weights()
         yield [subtract_params(before, after), history]
 
+    def prepare_partitions(self, partitions: Sequence[list], engine: Optional[str] = None,
+                           seed: Optional[int] = None):
+        """Build the shared executor with one replica per partition and load the
+        shards (no training). Returns (trainer, active)."""
+        from .ops.engine import make_trainer
+        self.model = _build_model(self.json, self.custom_objects, self.master_optimizer, self.master_loss,
+                                  self.master_metrics, _value(self.parameters))
+        bs, epochs, verbose, vs, shuffle = self._cfg()
+        xs, ys = [], []
+        for p in partitions:
+            x, y = partition_to_numpy(p)
+            xs.append(x)
+            ys.append(y)
+        active = [len(x) > bs for x in xs]   # reference worker.py:41 (`if n > batch_size: fit`)
+        trainer = make_trainer(self.model, max(1, len(partitions)), bs, engine=engine, seed=seed)
+        if partitions:
+            trainer.set_data(xs, ys, vs, active=active, shuffle=shuffle)
+        return trainer, active
+
     def train_partitions(self, partitions: Sequence[list], engine: Optional[str] = None, seed: Optional[int] = None):
         """Batched: train every partition as one replica of a shared executor.
 

@@ -36,7 +36,7 @@ def _model():
     return m
 
 
-def _worker(rank, world, port, mode, ps_mode, out_dir):
+def _worker(rank, world, port, mode, ps_mode, out_dir, gran="fit"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank), SPARK_LOCAL_IP="127.0.0.1", CUDA_VISIBLE_DEVICES="",
                       HIP_VISIBLE_DEVICES="")
@@ -50,7 +50,7 @@ def _worker(rank, world, port, mode, ps_mode, out_dir):
     x, y = _data()
     sc = SparkContext(master="local[4]")
     m = _model()
-    sm = SparkModel(m, mode=mode, parameter_server_mode=ps_mode, port=port + 1)
+    sm = SparkModel(m, mode=mode, parameter_server_mode=ps_mode, port=port + 1, sync_granularity=gran)
     sm.fit(to_simple_rdd(sc, x, y), epochs=2, batch_size=16, verbose=0, shuffle=False)
     preds = np.stack(sm.predict(x[:50]))
     ev = sm.evaluate(x, y)
@@ -60,15 +60,16 @@ def _worker(rank, world, port, mode, ps_mode, out_dir):
     dist.destroy_process_group()
 
 
-def _run(mode, ps_mode, tmp_path, world=2):
+def _run(mode, ps_mode, tmp_path, world=2, gran="fit"):
     port = _free_port()
-    mp.start_processes(_worker, args=(world, port, mode, ps_mode, str(tmp_path)), nprocs=world, join=True,
+    mp.start_processes(_worker, args=(world, port, mode, ps_mode, str(tmp_path), gran), nprocs=world, join=True,
                        start_method="spawn")
     return [np.load(tmp_path / f"r{r}.npz") for r in range(world)]
 
 
-def test_sync_two_ranks_equals_single_process(tmp_path):
-    outs = _run("synchronous", "http", tmp_path)
+@pytest.mark.parametrize("gran", ["fit", "batch"])
+def test_sync_two_ranks_equals_single_process(tmp_path, gran):
+    outs = _run("synchronous", "http", tmp_path, gran=gran)
     a, b = outs
     for k in a.files:
         assert np.array_equal(a[k], b[k]), k
@@ -80,7 +81,7 @@ def test_sync_two_ranks_equals_single_process(tmp_path):
     from elephas_amd.spark_model import SparkModel
     from elephas_amd.utils.rdd_utils import to_simple_rdd
     x, y = _data()
-    sm = SparkModel(_model(), mode="synchronous")
+    sm = SparkModel(_model(), mode="synchronous", sync_granularity=gran)
     sm.fit(to_simple_rdd(SparkContext(master="local[4]"), x, y), epochs=2, batch_size=16, verbose=0,
            shuffle=False)
     for i, w in enumerate(sm.master_network.get_weights()):

@@ -380,3 +380,29 @@ def test_refresh_shadows_round_trip():
     ref = np.maximum(x @ W[0] + W[1], 0) @ W[2] + W[3]
     assert not np.allclose(p0, p1)
     assert np.allclose(p1, ref, rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("gran", ["fit", "epoch", "batch"])
+def test_spark_model_granularities_native_vs_torch(gran, tmp_path):
+    """SparkModel sync modes on the native executor (device replica sums, G
+    all-reduce callback, checkpoint state) agree with the torch engine."""
+    from elephas_amd import config
+    from elephas_amd.data import SparkContext
+    from elephas_amd.models.optimizers import Adam
+    from elephas_amd.spark_model import SparkModel
+    from elephas_amd.models import initializers
+    config.set_policy("float32")
+    x, y = _data(600, 40, 5, seed=2)
+    ws = []
+    for engine in ("native", "torch"):
+        config.set_engine(engine)
+        initializers.set_seed(3)
+        m = _mlp(40, [64, 32], 5)
+        m.compile(Adam(0.005), "categorical_crossentropy", ["acc"])
+        sm = SparkModel(m, mode="synchronous", sync_granularity=gran)
+        rdd = SparkContext.getOrCreate().parallelize(list(zip(x, y)), 3)
+        sm.fit(rdd, epochs=3, batch_size=32, verbose=0, shuffle=False,
+               checkpoint_dir=str(tmp_path / engine))
+        ws.append(np.concatenate([w.reshape(-1) for w in sm.master_network.get_weights()]))
+    config.set_engine("auto")
+    assert np.abs(ws[0] - ws[1]).max() < 2e-4, np.abs(ws[0] - ws[1]).max()
