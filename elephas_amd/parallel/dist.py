@@ -25,10 +25,15 @@ def is_initialized() -> bool:
     return dist.is_available() and dist.is_initialized()
 
 
-def init_from_env(backend: str = None, timeout_s: int = 600) -> bool:
-    """Join a torchrun-style job if the environment describes one."""
+def init_from_env(backend: str = None, timeout_s: int = None) -> bool:
+    """Join a torchrun-style job if the environment describes one. Collectives
+    time out after ``timeout_s`` (``$ELEPHAS_AMD_COLLECTIVE_TIMEOUT``, default 600 s)
+    and RCCL errors abort asynchronously (see parallel/fault.py)."""
+    from . import fault
     if is_initialized():
         return True
+    timeout_s = fault.collective_timeout_s() if timeout_s is None else timeout_s
+    fault.enable_async_error_handling()
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     if ws <= 1:
         return False

@@ -1,0 +1,58 @@
+"""Failure detection and fault injection.
+
+The reference has none of its own (Spark task retry re-runs a failed
+partition, which is not idempotent for async pushes). Here a failure is fatal and
+visible instead of silent:
+
+* collectives run with a timeout (``$ELEPHAS_AMD_COLLECTIVE_TIMEOUT`` seconds,
+  default 600) and RCCL's asynchronous error handling, so a rank that dies or
+  hangs makes its peers raise instead of blocking forever;
+* worker threads (async / hogwild) re-raise their first exception in the driver;
+* ``$ELEPHAS_AMD_FAULT_INJECT`` (``rank=R,phase=P[,after=N]``) raises
+  ``InjectedFault`` on rank R the (N+1)-th time phase P is reached -- the hook the
+  failure tests use. Phases: ``train``, ``allreduce``, ``push``, ``pull``.
+"""
+from __future__ import annotations
+
+import os
+from typing import Dict
+
+_counts: Dict[str, int] = {}
+
+
+class InjectedFault(RuntimeError):
+    pass
+
+
+def collective_timeout_s(default: int = 600) -> int:
+    return int(os.environ.get("ELEPHAS_AMD_COLLECTIVE_TIMEOUT", str(default)))
+
+
+def enable_async_error_handling() -> None:
+    """Make a hung / failed RCCL collective abort the process (torch watchdog)."""
+    os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
+
+
+def _spec():
+    raw = os.environ.get("ELEPHAS_AMD_FAULT_INJECT", "")
+    if not raw:
+        return None
+    kv = dict(item.split("=", 1) for item in raw.split(",") if "=" in item)
+    return int(kv.get("rank", 0)), kv.get("phase", "train"), int(kv.get("after", 0))
+
+
+def maybe_inject(phase: str, rank: int) -> None:
+    spec = _spec()
+    if spec is None:
+        return
+    r, p, after = spec
+    if r != rank or p != phase:
+        return
+    n = _counts.get(phase, 0)
+    _counts[phase] = n + 1
+    if n >= after:
+        raise InjectedFault(f"injected fault: rank {rank}, phase {phase}, occurrence {n}")
+
+
+def reset() -> None:
+    _counts.clear()

@@ -39,7 +39,7 @@ from .mllib.adapter import from_matrix, from_vector, to_matrix, to_vector
 from .models import optimizers as O
 from .models import load_model
 from .ops.plan import flatten_weights, unflatten_weights
-from .parallel import dist
+from .parallel import dist, fault
 from .profiling import MetricsLogger, PhaseTimer, device_sync, trace_range
 from .utils import checkpoint as ckpt
 from .parameter.factory import ClientServerFactory
@@ -296,6 +296,7 @@ class SparkModel:
     def _average_into(self, trainer, n_params, n_parts, active_local):
         """theta <- mean over all N workers of theta_i (reference spark_model.py:221-227:
         theta0 - sum(delta_i)/N), written back into every local replica."""
+        fault.maybe_inject("allreduce", dist.rank())
         with self._timer.phase("allreduce"):
             total = self._sum_replicas(trainer, n_params) if active_local else self._zeros(n_params)
             dist.all_reduce_sum_(total)
@@ -345,6 +346,7 @@ class SparkModel:
         if gran == "fit":
             # the reference: every worker trains all epochs on its own, one average at the end
             if start < epochs and local and any(active):
+                fault.maybe_inject("train", dist.rank())
                 with self._timer.phase("train"):
                     h = trainer.fit(epochs - start, verbose=verbose)
                 hist = [hh if a else None for hh, a in zip(h, active)]
@@ -356,6 +358,7 @@ class SparkModel:
             allreduce = self._grad_allreduce(n_parts) if gran == "batch" else None
             for e in range(start, epochs):
                 if local and any(active):
+                    fault.maybe_inject("train", dist.rank())
                     with self._timer.phase("train"):
                         h = trainer.fit(1, verbose=verbose, allreduce=allreduce) if allreduce is not None \
                             else trainer.fit(1, verbose=verbose)

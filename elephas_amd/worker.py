@@ -187,6 +187,8 @@ class AsynchronousSparkWorker:
 
     # --- parameter-server exchange
     def _pull(self, trainer, native):
+        from .parallel import dist, fault
+        fault.maybe_inject("pull", dist.rank())
         if native:
             import torch
             with torch.cuda.stream(trainer.stream):
@@ -199,6 +201,8 @@ class AsynchronousSparkWorker:
             trainer.set_weights_flat(self._before)
 
     def _push(self, trainer, native):
+        from .parallel import dist, fault
+        fault.maybe_inject("push", dist.rank())
         if native:
             import torch
             with torch.cuda.stream(trainer.stream):
