@@ -162,6 +162,10 @@ struct FusedArgs {
   const int* ntrain;
   // out: dZ_0^T [N0][Bp] (B^T operand of the layer-0 weight update)
   void* dZ0T; long long sdZ0T;
+  // deferred layer-1 update (nsplit == 1 mode): the tail writes dZ_1^T [N1][Bp]
+  // and skips layer 1's weight update, which runs with layer 0's in the next
+  // grouped launch; nullptr = the tail updates every layer >= 1 itself
+  void* dZ1T; long long sdZ1T;
   // parameters
   float* P; long long sP;
   float* S; long long sS;

@@ -304,7 +304,7 @@ __device__ __forceinline__ void dw_pass(const FusedArgs& a, const FusedLayer& ly
           if (np > 1) S[splane + pi + q] = s1[j * 4 + q];
         }
     }
-    if (k == ly.K) {  // bias row: next-parity fp32 bias image
+    if (k == ly.K && a.Bsh) {  // bias row: next-parity fp32 bias image
       float* bn = a.Bsh + (long long)blockIdx.x / a.nsplit * a.sBsh + ((iter + 1) & 1) * a.bsh_par + pi;
 #pragma unroll
       for (int q = 0; q < 4; ++q)
@@ -466,7 +466,10 @@ __global__ __launch_bounds__(256) void fused_tail_kernel(FusedArgs a) {
     const int ldz = last ? a.ldLg : ly.ldG;
     // bias from this step's parity image: P's bias row may already hold the
     // update written by another workgroup of this replica
-    const float* bias = a.Bsh + (long long)r * a.sBsh + rpar * a.bsh_par + ly.p_off + (long long)ly.K * ly.N;
+    // (without split workgroups -- nsplit == 1 -- nothing else writes this replica's P
+    //  during the launch and the fp32 master is read directly)
+    const float* bias = a.Bsh ? a.Bsh + (long long)r * a.sBsh + rpar * a.bsh_par + ly.p_off + (long long)ly.K * ly.N
+                              : P + ly.p_off + (long long)ly.K * ly.N;
     const int ntt = (ly.N + 15) >> 4;
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
@@ -581,7 +584,8 @@ __global__ __launch_bounds__(256) void fused_tail_kernel(FusedArgs a) {
     dt.S = a.nsplit;
     dt.w = w;
     float wv[DWG * 4], sa[DWG * 4], sb[DWG * 4];
-    dw_prefetch(ly, dt, 0, P, S, splane, np, lane, wv, sa, sb);
+    const bool deferred = l == 1 && a.dZ1T;  // layer-1 update runs in the next grouped launch
+    if (!deferred) dw_prefetch(ly, dt, 0, P, S, splane, np, lane, wv, sa, sb);
     // DX: dD_{l-1} = dZ_l . W_l^T  (current-parity W images, untouched by the update)
     f32x4 acc[4][4];
     const bool first = l == 1;
@@ -635,8 +639,16 @@ __global__ __launch_bounds__(256) void fused_tail_kernel(FusedArgs a) {
       }
     }
     fstamp(a, 14 + 3 * (L - 1 - l));
+    if (deferred) {
+      // deferred layer-1 update: publish dZ_1^T [N1][Bp] for the grouped DW_UPDATE launch
+      T* out = reinterpret_cast<T*>(a.dZ1T) + (long long)r * a.sdZ1T;
+      for (int e = tid; e < ly.N * a.Bp; e += 256) {
+        const int n = e / a.Bp, m = e - n * a.Bp;
+        out[(long long)n * a.Bp + m] = dZ[m * a.lddZ + n];
+      }
+    }
     // weight update of layer l from LDS (D_{l-1} with its ones column, dZ_l)
-    for (int j0 = 0; dt.valid(j0); j0 += DWG) {
+    for (int j0 = 0; !deferred && dt.valid(j0); j0 += DWG) {
       if (j0 > 0) dw_prefetch(ly, dt, j0, P, S, splane, np, lane, wv, sa, sb);
       dw_pass<T>(a, ly, dt, j0, Dp, pv.ldA, dZ, a.lddZ, P, S, splane, np, Wnext, WTnext, iter, lane, wv, sa, sb);
     }

@@ -33,7 +33,7 @@ Executor::Executor(const ExecCfg& cfg) : c_(cfg) {
   ea_fused_init();
   build();
   fused_ = c_.fused != 0 && build_fused();
-  if (c_.fused == 1 && !fused_) throw std::invalid_argument("fused MLP tail requested but the model is not eligible");
+  if ((c_.fused == 1 || c_.fused == 2) && !fused_) throw std::invalid_argument("fused MLP tail requested but the model is not eligible");
 }
 
 Executor::~Executor() {
@@ -46,7 +46,11 @@ Executor::~Executor() {
 bool Executor::build_fused() {
   const int L = (int)c_.layers.size();
   if (L < 2 || L > FUSED_MAX_L || c_.B > 64 || c_.Bp > 64) return false;
-  if (!c_.Bsh) return false;  // needs the per-parity fp32 bias images
+  // mode 1 (split workgroups update weights in the tail) needs the per-parity fp32
+  // bias images; mode 2 (one workgroup per replica, layer-1 update deferred to the
+  // grouped launch of layer 0) reads the fp32 master directly
+  const bool deferred = c_.fused == 2;
+  if (!deferred && !c_.Bsh) return false;
   if (c_.layers[0].N > 256) return false;
   for (int l = 1; l < L; ++l)
     if (c_.layers[l].K > 256 || c_.layers[l].N > 256) return false;
@@ -90,7 +94,7 @@ bool Executor::build_fused() {
   check(hipMemcpy(d_fly_, fl.data(), sizeof(FusedLayer) * L, hipMemcpyHostToDevice), "hipMemcpy(fused layers)");
   const LayerCfg& l0 = c_.layers[0];
   a.L = L;
-  a.nsplit = std::max(1, c_.fused_split);
+  a.nsplit = deferred ? 1 : std::max(1, c_.fused_split);
   a.ly = d_fly_;
   a.R = c_.R; a.B = c_.B; a.Bp = c_.Bp;
   a.D0 = reinterpret_cast<const void*>(l0.D); a.sD0 = (long long)c_.B * l0.Np;
@@ -104,7 +108,11 @@ bool Executor::build_fused() {
   a.op = c_.op;
   a.Wsh = reinterpret_cast<void*>(c_.Wsh); a.sWsh = c_.sWsh; a.wsh_par = c_.wsh_par;
   a.WTsh = reinterpret_cast<void*>(c_.WTsh); a.sWTsh = c_.sWTsh; a.wtsh_par = c_.wtsh_par;
-  a.Bsh = reinterpret_cast<float*>(c_.Bsh); a.sBsh = c_.sBsh; a.bsh_par = c_.bsh_par;
+  a.Bsh = deferred ? nullptr : reinterpret_cast<float*>(c_.Bsh); a.sBsh = c_.sBsh; a.bsh_par = c_.bsh_par;
+  if (deferred) {
+    a.dZ1T = reinterpret_cast<void*>(c_.layers[1].dZT);
+    a.sdZ1T = (long long)c_.layers[1].N * c_.Bp;
+  }
   a.loss = c_.loss; a.nmet = c_.nmet;
   for (int i = 0; i < 4; ++i) a.met[i] = c_.met[i];
   a.acc = reinterpret_cast<double*>(c_.acc); a.acc_stride = c_.acc_stride;
@@ -112,8 +120,18 @@ bool Executor::build_fused() {
   a.seed = c_.seed;
   // grouped launches around the tail: layer-0 forward (+ X^T), layer-0 update
   ffwd_.assign(1, fwd_[0]);
-  ffwd_[0].ga.p[0].DT = nullptr;  // D_0^T is not needed: the tail reads D_0 into LDS
   fbwd_.assign(1, bwd_.back());
+  if (deferred) {
+    // layer 0 and layer 1 updates in one grouped launch: DW_1 reads D_0^T (kept in
+    // the forward launch) and the dZ_1^T the tail wrote
+    const Launch& b1 = bwd_[bwd_.size() - 2];  // {DW_1, DX_1}
+    Launch& u = fbwd_[0];
+    u.ga.p[1] = b1.ga.p[0];
+    u.ga.nprob = 2;
+    finalize(u);
+  } else {
+    ffwd_[0].ga.p[0].DT = nullptr;  // D_0^T is not needed: the tail reads D_0 into LDS
+  }
   return true;
 }
 

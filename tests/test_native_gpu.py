@@ -206,6 +206,10 @@ def _fit_weights(model, policy, B, xs, ys, fused, epochs=1, val=0.0, R=None, see
 def test_fused_tail_matches_grouped_path(case):
     """The fused small-MLP tail (one block per replica) must reproduce the grouped
     per-layer launches: same masks, same update rules, fp32 accumulation."""
+    _fused_case(case, 1)
+
+
+def _fused_case(case, fmode):
     from elephas_amd.models.optimizers import SGD, Adam, RMSprop
     rng = np.random.default_rng(11)
     if case == "mnist_bf16_dropout":
@@ -239,7 +243,7 @@ def test_fused_tail_matches_grouped_path(case):
             y = np.eye(k, dtype=np.float32)[rng.integers(0, k, n)]
         xs.append(x)
         ys.append(y)
-    tf, wf, hf = _fit_weights(model, policy, B, xs, ys, fused=1, epochs=2, val=0.1)
+    tf, wf, hf = _fit_weights(model, policy, B, xs, ys, fused=fmode, epochs=2, val=0.1)
     tg, wg, hg = _fit_weights(model, policy, B, xs, ys, fused=0, epochs=2, val=0.1)
     assert tf.fused and not tg.fused
     assert tf.launch_count() == 3
@@ -281,7 +285,7 @@ def test_plain_gemm_rejects_misaligned_shapes():
         C.gemm_nt(A.data_ptr(), A.data_ptr(), A.data_ptr(), 4, 4, 10, 10, 10, 4, 0, 0, 0)
 
 
-@pytest.mark.parametrize("fused", [0, 1])
+@pytest.mark.parametrize("fused", [0, 1, 2])
 def test_training_is_bit_deterministic(fused):
     """Same seeds -> bit-identical weights (no races between the update epilogue
     and the GEMMs that read the weight shadows, no order-dependent reductions)."""
@@ -406,3 +410,11 @@ def test_spark_model_granularities_native_vs_torch(gran, tmp_path):
         ws.append(np.concatenate([w.reshape(-1) for w in sm.master_network.get_weights()]))
     config.set_engine("auto")
     assert np.abs(ws[0] - ws[1]).max() < 2e-4, np.abs(ws[0] - ws[1]).max()
+
+
+@pytest.mark.parametrize("case", ["mnist_bf16_dropout", "tanh_f32_adam", "mse_f32", "sparse_bf16_rmsprop"])
+def test_deferred_tail_matches_grouped_path(case):
+    """Fused mode 2: one workgroup per replica runs layers 1..L-1 forward, loss and
+    input gradients in LDS; layer 1's update is deferred into layer 0's grouped
+    launch (3 launches per step, no cross-workgroup writes inside the tail)."""
+    _fused_case(case, 2)
