@@ -12,7 +12,7 @@
 // and lets concurrent updates race (reference server.py:109-131 guards).
 #pragma once
 #include <hip/hip_runtime.h>
-#include <pthread.h>
+#include "rwlock.h"
 
 #include <atomic>
 #include <memory>
@@ -20,19 +20,6 @@
 #include <string>
 
 namespace ea {
-
-class RWLockBase {
- public:
-  virtual ~RWLockBase() = default;
-  virtual void lock_shared() = 0;
-  virtual void unlock_shared() = 0;
-  virtual void lock() = 0;
-  virtual void unlock() = 0;
-};
-
-std::unique_ptr<RWLockBase> make_lock(const std::string& shm_name);  // "" -> in-process
-void shm_rwlock_create(const std::string& name);
-void shm_rwlock_destroy(const std::string& name);
 
 class DeviceParameterServer {
  public:

@@ -24,6 +24,7 @@ SOURCES = [
     "kernels/flat.hip",
     "kernels/fused.hip",
     "runtime/executor.cpp",
+    "runtime/rwlock.cpp",
     "runtime/param_server.cpp",
     "runtime/host_loader.cpp",
     "runtime/bindings.cpp",
