@@ -175,7 +175,6 @@ __device__ __forceinline__ void stamp_clk(const GroupArgs& ga, int k) {
 // swizzle is applied to the per-lane SOURCE address and undone on the ds_read
 // (the 16 lanes of a fragment read then spread over 8 slots: <= 2-way conflicts).
 constexpr int THR_BK = 64;
-constexpr int THR_STAGE_BYTES = 2 * 128 * THR_BK * 2;  // A + B tiles of one k-step
 constexpr int THR_NS = 2;                              // ring depth (2 keeps 2 blocks/CU: 837 vs 603 TF at 4096^3 for 4)
 constexpr int THR_GLDS = 8;                            // glds per wave per k-tile (4 A + 4 B)
 
@@ -196,11 +195,21 @@ __device__ __forceinline__ void glds16(const void* g, char* lds_wave_base) {
                                    (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
 }
 
-// arow_ld/bcol_ld: per lane, the 4 source rows it stages (nullptr = zero row);
+// Stage / fragment geometry for a 128 x BN tile (BN = 128 or 64), 2 x 2 waves of
+// 64 x (BN/2): every lane stages AR = 4 rows of the A tile and BR = BN/32 rows of
+// the B^T tile per k-tile (one 16-byte chunk each).
+template <int BN> struct ThrGeom {
+  static constexpr int AR = 4, BR = BN / 32, WNF = BN / 32;  // WNF: 16-col fragments per wave
+  static constexpr int A_BYTES = 128 * THR_BK * 2, B_BYTES = BN * THR_BK * 2, STAGE = A_BYTES + B_BYTES;
+};
+
+// arow_ld/bcol_ld: per lane, the rows it stages (nullptr = zero row);
 // aones: bit t set when staged A row t is the bias ones row.
-__device__ __forceinline__ void thr_lds_mainloop(const __bf16* const (&arow_ld)[4], const __bf16* const (&bcol_ld)[4],
-                                                 unsigned aones, int K, int wm, int wn, f32x4 (&acc)[4][4],
-                                                 char* sbase) {
+template <int BN>
+__device__ __forceinline__ void thr_lds_mainloop(const __bf16* const (&arow_ld)[4],
+                                                 const __bf16* const (&bcol_ld)[ThrGeom<BN>::BR], unsigned aones, int K,
+                                                 int wm, int wn, f32x4 (&acc)[4][ThrGeom<BN>::WNF], char* sbase) {
+  using G = ThrGeom<BN>;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int i16 = lane & 15, g = lane >> 4;
@@ -212,29 +221,33 @@ __device__ __forceinline__ void thr_lds_mainloop(const __bf16* const (&arow_ld)[
   // break the per-tile glds count the counted waits rely on)
   typedef unsigned long long u64;
   const u64 zp = (u64)(const void*)g_thr_zero, op = (u64)(const void*)g_thr_ones;
-  u64 abase[4], bbase[4];
+  u64 abase[G::AR], bbase[G::BR];
   unsigned amov = 0, bmov = 0;  // bit t: staged row t advances with k (a real operand row)
 #pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    const bool ar = arow_ld[t] != nullptr, br = bcol_ld[t] != nullptr;
+  for (int t = 0; t < G::AR; ++t) {
+    const bool ar = arow_ld[t] != nullptr;
     abase[t] = ((aones >> t) & 1u) ? op : (ar ? (u64)arow_ld[t] : zp);
-    bbase[t] = br ? (u64)bcol_ld[t] : zp;
     amov |= (ar && !((aones >> t) & 1u)) ? 1u << t : 0u;
+  }
+#pragma unroll
+  for (int t = 0; t < G::BR; ++t) {
+    const bool br = bcol_ld[t] != nullptr;
+    bbase[t] = br ? (u64)bcol_ld[t] : zp;
     bmov |= br ? 1u << t : 0u;
   }
   auto stage = [&](int kt, int buf) {
     const int kk = kt * THR_BK + c8;
     const bool kin = kk < K;
     const u64 koff = (u64)kk * 2u;
-    char* dA = sbase + buf * THR_STAGE_BYTES + wave * 1024;
-    char* dB = dA + THR_STAGE_BYTES / 2;
+    char* dA = sbase + buf * G::STAGE + wave * 1024;
+    char* dB = sbase + buf * G::STAGE + G::A_BYTES + wave * 1024;
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
+    for (int t = 0; t < G::AR; ++t) {
       const u64 a = abase[t] + (((amov >> t) & 1u) ? koff : 0u);
       glds16((const void*)(kin ? a : zp), dA + t * 4096);
     }
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
+    for (int t = 0; t < G::BR; ++t) {
       const u64 b = bbase[t] + (((bmov >> t) & 1u) ? koff : 0u);
       glds16((const void*)(kin ? b : zp), dB + t * 4096);
     }
@@ -245,7 +258,7 @@ __device__ __forceinline__ void thr_lds_mainloop(const __bf16* const (&arow_ld)[
   for (int kt = 0; kt < nk; ++kt) {
     // counted wait: the copies of the tiles issued after kt may stay in flight
     const int ahead = (kt + THR_NS - 2 < nk - 1 ? kt + THR_NS - 2 : nk - 1) - kt;
-    static_assert(THR_GLDS == 8 && THR_NS <= 4, "vmcnt immediates below assume <= 4 stages x 8 glds");
+    static_assert(THR_NS <= 2 || (THR_GLDS == 8 && BN == 128), "counted vmcnt immediates assume 8 glds per tile");
     if (ahead >= 2) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
     else if (ahead == 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -258,30 +271,31 @@ __device__ __forceinline__ void thr_lds_mainloop(const __bf16* const (&arow_ld)[
     // filling and waits vmcnt(0) before the first read (draining the prefetch,
     // so every k-step paid a full HBM round trip). The waits for these reads are
     // explicit lgkmcnt + sched_barrier (the MFMAs must not be hoisted above them).
-    const unsigned bA = lds_base + (unsigned)((kt % THR_NS) * THR_STAGE_BYTES);
-    const unsigned bB = bA + THR_STAGE_BYTES / 2;
-    uint4 fa[2][4], fb[2][4];
+    const unsigned bA = lds_base + (unsigned)((kt % THR_NS) * G::STAGE);
+    const unsigned bB = bA + G::A_BYTES;
+    uint4 fa[2][4], fb[2][G::WNF];
 #pragma unroll
     for (int u = 0; u < THR_BK / 32; ++u) {
       const unsigned slot = (unsigned)(((u * 4 + g) ^ (i16 & 7)) * 16);
 #pragma unroll
       for (int i = 0; i < 4; ++i) ds_read16(fa[u][i], bA + (unsigned)((wm * 64 + i * 16 + i16) * 128) + slot);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) ds_read16(fb[u][j], bB + (unsigned)((wn * 64 + j * 16 + i16) * 128) + slot);
-      if (u == 0) continue;  // substep 1's reads are issued before substep 0's MFMAs
+      for (int j = 0; j < G::WNF; ++j)
+        ds_read16(fb[u][j], bB + (unsigned)((wn * (BN / 2) + j * 16 + i16) * 128) + slot);
     }
-    asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");  // substep 0 landed (substep 1's 8 reads may be in flight)
+    if constexpr (G::WNF == 4) asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");  // substep 0 landed
+    else asm volatile("s_waitcnt lgkmcnt(6)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) mma16<__bf16>(acc[i][j], fa[0][i], fb[0][j]);
+      for (int j = 0; j < G::WNF; ++j) mma16<__bf16>(acc[i][j], fa[0][i], fb[0][j]);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) mma16<__bf16>(acc[i][j], fa[1][i], fb[1][j]);
+      for (int j = 0; j < G::WNF; ++j) mma16<__bf16>(acc[i][j], fa[1][i], fb[1][j]);
   }
   __syncthreads();  // the epilogue reuses the staging LDS
 }
@@ -362,17 +376,19 @@ __device__ __forceinline__ void run_prob(const GroupArgs& ga, const Prob& p, con
           bmask |= 1u << j;
         }
       }
-      if constexpr (sizeof(T) == 2 && KSPLIT == 1 && BM == 128 && BN == 128 && WM == 4 && WN == 4) {
+      if constexpr (sizeof(T) == 2 && KSPLIT == 1 && BM == 128 && (BN == 128 || BN == 64) && WM == 4 &&
+                    WN == BN / 32) {
         // staged rows of this lane: r = 32 t + 8 wave + lane / 8 of the A and B^T tiles
+        constexpr int BR = ThrGeom<BN>::BR;
         const __bf16* arow_ld[4];
-        const __bf16* bcol_ld[4];
+        const __bf16* bcol_ld[BR];
         unsigned aones = 0;
         const __bf16* Ab = reinterpret_cast<const __bf16*>(A);
         const __bf16* Bb = reinterpret_cast<const __bf16*>(BTp);
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
           const int rr = t * 32 + (threadIdx.x >> 3);
-          const int m = m0 + rr, n = n0 + rr;
+          const int m = m0 + rr;
           arow_ld[t] = nullptr;
           if (m == p.ones_row) {
             aones |= 1u << t;
@@ -383,10 +399,14 @@ __device__ __forceinline__ void run_prob(const GroupArgs& ga, const Prob& p, con
               arow_ld[t] = Ab + (long long)m * p.lda;
             }
           }
+        }
+#pragma unroll
+        for (int t = 0; t < BR; ++t) {
+          const int n = n0 + t * 32 + (threadIdx.x >> 3);
           bcol_ld[t] = n < p.N ? Bb + (long long)n * p.ldb : nullptr;
         }
-        thr_lds_mainloop(arow_ld, bcol_ld, aones, p.K, wm, wn, reinterpret_cast<f32x4(&)[4][4]>(acc),
-                         reinterpret_cast<char*>(smem));
+        thr_lds_mainloop<BN>(arow_ld, bcol_ld, aones, p.K, wm, wn,
+                             reinterpret_cast<f32x4(&)[4][ThrGeom<BN>::WNF]>(acc), reinterpret_cast<char*>(smem));
       } else {
       const uint4 zero = make_uint4(0u, 0u, 0u, 0u);
       const uint4 one = ones_frag<T>();
@@ -730,8 +750,8 @@ static size_t lds_bytes(bool loss = true) {
   constexpr int BN = WAVES_N * WN * 16;
   const size_t tile = (size_t)BM * (BN + 4);
   size_t floats = (size_t)KSPLIT * tile;
-  if (sizeof(T) == 2 && KSPLIT == 1 && BM == 128 && BN == 128)  // glds staging ring (thr_lds_mainloop)
-    floats = std::max(floats, (size_t)THR_NS * THR_STAGE_BYTES / sizeof(float));
+  if (sizeof(T) == 2 && KSPLIT == 1 && BM == 128 && (BN == 128 || BN == 64))  // glds staging ring
+    floats = std::max(floats, (size_t)THR_NS * (size_t)(128 + BN) * THR_BK * 2 / sizeof(float));
   if (loss) floats = std::max(floats, tile + BM + (size_t)BM * BN);  // + row map + staged targets
   floats = std::max(floats, (size_t)64 * 65);                       // gather-transpose
   return floats * sizeof(float);
@@ -757,14 +777,17 @@ static hipError_t launch_cfg(const GroupArgs& ga, hipStream_t s) {
 
 }  // namespace ea
 
-// cfg: 0 = LAT (64x32, split-K 4), 1 = THR (128x128)
+// cfg: 0 = LAT (64x32, split-K 4), 1 = THR (128x128), 2 = THR-N64 (128x64: twice the
+// workgroups for grids that would otherwise leave CUs with a single workgroup)
 extern "C" hipError_t ea_gemm_grouped(const ea::GroupArgs* ga, int bf16, int cfg, hipStream_t s) {
   using namespace ea;
   if (bf16) {
     if (cfg == 0) return launch_cfg<__bf16, 4, 2, 1, 1, 4>(*ga, s);
+    if (cfg == 2) return launch_cfg<__bf16, 4, 2, 2, 2, 1>(*ga, s);
     return launch_cfg<__bf16, 4, 4, 2, 2, 1>(*ga, s);
   } else {
     if (cfg == 0) return launch_cfg<float, 4, 2, 1, 1, 4>(*ga, s);
+    if (cfg == 2) return launch_cfg<float, 4, 2, 2, 2, 1>(*ga, s);
     return launch_cfg<float, 4, 4, 2, 2, 1>(*ga, s);
   }
 }
@@ -775,11 +798,13 @@ extern "C" void ea_gemm_init() {
   if (done) return;
   set_attr<__bf16, 4, 2, 1, 1, 4>();
   set_attr<__bf16, 4, 4, 2, 2, 1>();
+  set_attr<__bf16, 4, 2, 2, 2, 1>();
   set_attr<float, 4, 2, 1, 1, 4>();
   set_attr<float, 4, 4, 2, 2, 1>();
+  set_attr<float, 4, 2, 2, 2, 1>();
   done = true;
 }
 
 extern "C" int ea_gemm_tile_m(int cfg) { return cfg == 0 ? 64 : 128; }
-extern "C" int ea_gemm_tile_n(int cfg) { return cfg == 0 ? 32 : 128; }
+extern "C" int ea_gemm_tile_n(int cfg) { return cfg == 0 ? 32 : (cfg == 2 ? 64 : 128); }
 extern "C" int ea_gather_tile() { return 64; }

@@ -257,7 +257,7 @@ def _fused_case(case, fmode):
             assert np.allclose(a[key], b[key], rtol=5 * tol, atol=5 * tol), (key, a[key], b[key])
 
 
-@pytest.mark.parametrize("cfg", [0, 1])
+@pytest.mark.parametrize("cfg", [0, 1, 2])
 @pytest.mark.parametrize("bf16", [1, 0])
 @pytest.mark.parametrize("M,N,K", [(64, 128, 784), (64, 10, 128), (785, 128, 64), (300, 200, 136), (512, 512, 512)])
 def test_plain_gemm_matches_torch_fp32(M, N, K, bf16, cfg):
@@ -300,13 +300,14 @@ def test_training_is_bit_deterministic(fused):
     assert np.array_equal(w1, w2), np.abs(w1 - w2).max()
 
 
+@pytest.mark.parametrize("cfg", ["1", "2"])
 @pytest.mark.parametrize("policy,tol", [("mixed_bfloat16", 5e-2), ("float32", 1e-3)])
-def test_throughput_tiles_match_reference(monkeypatch, policy, tol):
+def test_throughput_tiles_match_reference(monkeypatch, policy, tol, cfg):
     """Force the 128x128 THR tiles (LDS-staged glds main loop for bf16) on every
     layer: gathered layer-0 rows, the ones row of the bias gradient, K / N / M
     tails (K=100, N=70, B=48 of 64) and the fused SGD update must all match."""
     from elephas_amd.models.optimizers import SGD
-    monkeypatch.setenv("ELEPHAS_AMD_GEMM_CFG", "1")
+    monkeypatch.setenv("ELEPHAS_AMD_GEMM_CFG", cfg)
     model = _mlp(200, [136, 72], 70, dropout=0.0)
     model.compile(SGD(0.05), "categorical_crossentropy", ["acc"])
     x, y = _data(48, 200, 70)

@@ -31,7 +31,7 @@ for (M, N, K) in [(4096, 4096, 4096), (1024, 4096, 4096), (4096, 4096, 1024), (1
     BT = (torch.rand(N, K, device=dev) * 2 - 1).to(torch.bfloat16)
     Cm = torch.zeros(M, N, device=dev)
     res = []
-    for cfg in (0, 1, "torch"):
+    for cfg in (0, 1, 2, "torch"):
         def f():
             if cfg == "torch":
                 torch.matmul(A, BT.t())
