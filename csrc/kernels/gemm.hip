@@ -175,8 +175,6 @@ __device__ __forceinline__ void stamp_clk(const GroupArgs& ga, int k) {
 // swizzle is applied to the per-lane SOURCE address and undone on the ds_read
 // (the 16 lanes of a fragment read then spread over 8 slots: <= 2-way conflicts).
 constexpr int THR_BK = 64;
-constexpr int THR_NS = 2;                              // ring depth (2 keeps 2 blocks/CU: 837 vs 603 TF at 4096^3 for 4)
-constexpr int THR_GLDS = 8;                            // glds per wave per k-tile (4 A + 4 B)
 
 // Masking happens on the SOURCE of each staged chunk: a row past M (or past the
 // valid batch rows), a B^T row past N and any chunk past K copy 16 zero bytes,
@@ -201,6 +199,11 @@ __device__ __forceinline__ void glds16(const void* g, char* lds_wave_base) {
 template <int BN> struct ThrGeom {
   static constexpr int AR = 4, BR = BN / 32, WNF = BN / 32;  // WNF: 16-col fragments per wave
   static constexpr int A_BYTES = 128 * THR_BK * 2, B_BYTES = BN * THR_BK * 2, STAGE = A_BYTES + B_BYTES;
+  static constexpr int GLDS = AR + BR;  // glds per wave per k-tile
+  // ring depth 2: a 4-deep ring (1 workgroup per CU) measured 603 vs 837 TF at
+  // 4096^3, and a 3-deep ring for 128x64 600 vs 613 TF at 1024x4096x4096 -- the
+  // k-step waits are not the global-load latency (profiles/pmc_gemm_thr.txt)
+  static constexpr int NS = 2;
 };
 
 // arow_ld/bcol_ld: per lane, the rows it stages (nullptr = zero row);
@@ -253,25 +256,31 @@ __device__ __forceinline__ void thr_lds_mainloop(const __bf16* const (&arow_ld)[
     }
   };
 #pragma unroll
-  for (int s = 0; s < THR_NS - 1; ++s)
+  for (int s = 0; s < G::NS - 1; ++s)
     if (s < nk) stage(s, s);
   for (int kt = 0; kt < nk; ++kt) {
     // counted wait: the copies of the tiles issued after kt may stay in flight
-    const int ahead = (kt + THR_NS - 2 < nk - 1 ? kt + THR_NS - 2 : nk - 1) - kt;
-    static_assert(THR_NS <= 2 || (THR_GLDS == 8 && BN == 128), "counted vmcnt immediates assume 8 glds per tile");
-    if (ahead >= 2) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-    else if (ahead == 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int ahead = (kt + G::NS - 2 < nk - 1 ? kt + G::NS - 2 : nk - 1) - kt;
+    static_assert(G::NS <= 3 && (G::GLDS == 8 || G::GLDS == 6), "vmcnt immediates below");
+    if (ahead >= 2) {
+      if constexpr (G::GLDS == 8) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    } else if (ahead == 1) {
+      if constexpr (G::GLDS == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of the slot refilled below
     __builtin_amdgcn_s_barrier();                        // tile kt landed for every wave; slot kt-1 is free
     asm volatile("" ::: "memory");
-    if (kt + THR_NS - 1 < nk) stage(kt + THR_NS - 1, (kt + THR_NS - 1) % THR_NS);
+    if (kt + G::NS - 1 < nk) stage(kt + G::NS - 1, (kt + G::NS - 1) % G::NS);
     // Fragment reads are inline-asm ds_read_b128: for compiler-visible LDS loads
     // hipcc cannot tell the slot being read from the slot the glds above is
     // filling and waits vmcnt(0) before the first read (draining the prefetch,
     // so every k-step paid a full HBM round trip). The waits for these reads are
     // explicit lgkmcnt + sched_barrier (the MFMAs must not be hoisted above them).
-    const unsigned bA = lds_base + (unsigned)((kt % THR_NS) * G::STAGE);
+    const unsigned bA = lds_base + (unsigned)((kt % G::NS) * G::STAGE);
     const unsigned bB = bA + G::A_BYTES;
     uint4 fa[2][4], fb[2][G::WNF];
 #pragma unroll
@@ -751,7 +760,7 @@ static size_t lds_bytes(bool loss = true) {
   const size_t tile = (size_t)BM * (BN + 4);
   size_t floats = (size_t)KSPLIT * tile;
   if (sizeof(T) == 2 && KSPLIT == 1 && BM == 128 && (BN == 128 || BN == 64))  // glds staging ring
-    floats = std::max(floats, (size_t)THR_NS * (size_t)(128 + BN) * THR_BK * 2 / sizeof(float));
+    floats = std::max(floats, (size_t)ThrGeom<BN>::NS * ThrGeom<BN>::STAGE / sizeof(float));
   if (loss) floats = std::max(floats, tile + BM + (size_t)BM * BN);  // + row map + staged targets
   floats = std::max(floats, (size_t)64 * 65);                       // gather-transpose
   return floats * sizeof(float);
