@@ -82,55 +82,167 @@ __device__ __forceinline__ void gather_transpose_block(const GroupArgs& ga, cons
 
 // ----------------------------------------------------------- wide loss rows
 // Final layers wider than one GEMM tile (e.g. 1000 classes): the FWD GEMM writes
-// the logits Z, then one wave per row runs the same row_loss math as the fused
-// epilogue with wave-wide reductions.
+// the logits Z, then each wave runs the same row_loss math as the fused epilogue
+// with wave-wide reductions over LOSS_RPB / 4 rows. dZ^T (the B^T operand of the
+// last layer's weight update) is staged in LDS as [N][LOSS_RPB] and written with
+// one 16-byte store per class column instead of one scattered 2-byte store per
+// element (66 us -> see profiles/kernels_wide_b1024.txt for 1024 x 1000 bf16).
+constexpr int LOSS_RPB = 8;                       // rows per workgroup
+constexpr int LOSS_LDS_MAX_N = 64 * 65 * 4 / (LOSS_RPB * 2);  // fits the smallest launch's LDS (LAT)
+
+// Wide softmax + CCE row (one wave, NV values per lane in registers): the same
+// math as loss_tile_cce / row_loss's logits path (loss = -sum y (z - lse),
+// dL/dz = softmax(z) * sum(y) - y, accuracy = argmax z == argmax y, first index
+// on ties), with every global load of the row issued up front.
+__device__ __forceinline__ bool softmax_cce_wide(const Prob& p) {
+  if (p.act != ACT_SOFTMAX || !(p.loss == LOSS_CCE || p.loss == LOSS_SPARSE_CCE)) return false;
+  bool ok = true;
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    if (q < p.nmet)
+      ok = ok && (p.met[q] == MET_ACC_CAT || p.met[q] == MET_ACC_SPARSE || p.met[q] == LOSS_CCE ||
+                  p.met[q] == LOSS_SPARSE_CCE);
+  return ok;
+}
+
+template <int NV, typename DZ>
+__device__ __forceinline__ void row_softmax_cce_reg(const Prob& p, int lane, const float* zrow, const float* yrow,
+                                                    bool train, DZ dz, RowOut& ro) {
+  const int N = p.N;
+  const bool sparse = p.loss == LOSS_SPARSE_CCE;
+  const int ycls = sparse ? (int)yrow[0] : -1;
+  float z[NV], y[NV];
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int j = lane + 64 * i;
+    z[i] = j < N ? zrow[j] : -INFINITY;
+    y[i] = sparse ? (j == ycls ? 1.f : 0.f) : (j < N ? yrow[j] : 0.f);
+  }
+  float zmax = -INFINITY, bz = -INFINITY, by = -INFINITY;
+  int iz = 0x7fffffff, iy = 0x7fffffff;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int j = lane + 64 * i;
+    zmax = fmaxf(zmax, z[i]);
+    if (j < N && z[i] > bz) { bz = z[i]; iz = j; }
+    if (j < N && y[i] > by) { by = y[i]; iy = j; }
+  }
+  zmax = row_max<64>(zmax);
+  row_argmax<64>(bz, iz);
+  row_argmax<64>(by, iy);
+  float se = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i)
+    if (lane + 64 * i < N) se += __expf(z[i] - zmax);
+  se = row_sum<64>(se);
+  const float lse = zmax + logf(se);
+  float l = 0.f, ysum = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i)
+    if (lane + 64 * i < N) {
+      l += -y[i] * (z[i] - lse);
+      ysum += y[i];
+    }
+  l = row_sum<64>(l);
+  ysum = row_sum<64>(ysum);
+  ro.loss = l;
+  if (sparse) iy = ycls;
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    if (q < p.nmet) ro.metric[q] = (p.met[q] == MET_ACC_CAT || p.met[q] == MET_ACC_SPARSE) ? (iz == iy ? 1.f : 0.f) : l;
+  if (train) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int j = lane + 64 * i;
+      if (j < N) dz(0, j, __expf(z[i] - lse) * ysum - y[i]);
+    }
+  }
+}
+
 template <typename T>
-__device__ __forceinline__ void loss_rows_block(const GroupArgs& ga, const Prob& p, int lb) {
+__device__ __forceinline__ void loss_rows_block(const GroupArgs& ga, const Prob& p, int lb, float* smem) {
   const int r = lb / p.tiles_m;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int row = (lb % p.tiles_m) * 4 + wave;
-  if (row >= p.M) return;
+  const int row0 = (lb % p.tiles_m) * LOSS_RPB;
   const long long step = ga.ctr[0] + ga.step_off;
   const int valid = batch_valid(p, r, step);
   const bool train = !p.eval_mode && p.D;
+  // LDS-staged transposed store (bf16 only: 8 rows x 2 B = one 16-byte store)
+  const bool stage_t = train && p.DT && sizeof(T) == 2 && p.N <= LOSS_LDS_MAX_N;
+  unsigned short* sdt = reinterpret_cast<unsigned short*>(smem);
   const float inv_valid = valid > 0 ? 1.f / (float)valid : 0.f;
-  if (row >= valid) {
-    if (train) {
-      for (int j = lane; j < p.N; j += 64) {
-        st<T>(p.D, (long long)r * p.sD + (long long)row * p.ldd + j, 0.f);
-        if (p.DT) st<T>(p.DT, (long long)r * p.sDT + (long long)j * p.lddt + row, 0.f);
+  float wsum[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int rr = 0; rr < LOSS_RPB / 4; ++rr) {
+    const int lr = wave * (LOSS_RPB / 4) + rr, row = row0 + lr;
+    auto put_t = [&](int j, float v) {
+      if (stage_t) sdt[j * LOSS_RPB + lr] = __builtin_bit_cast(unsigned short, from_f<__bf16>(v));
+      else if (p.DT) st<T>(p.DT, (long long)r * p.sDT + (long long)j * p.lddt + row, v);
+    };
+    if (row >= p.M || row >= valid) {
+      if (train && row < p.M) {
+        for (int j = lane; j < p.N; j += 64) {
+          st<T>(p.D, (long long)r * p.sD + (long long)row * p.ldd + j, 0.f);
+          put_t(j, 0.f);
+        }
+      } else if (stage_t) {
+        for (int j = lane; j < p.N; j += 64) sdt[j * LOSS_RPB + lr] = 0;
       }
+      continue;
     }
-    return;
-  }
-  const float* zrow = p.Z + (long long)r * p.sZ + (long long)row * p.ldz;
-  float* prow = p.pred ? p.pred + (long long)r * p.sPred + (p.chunk * p.B + row) * p.ldp : nullptr;
-  if (!p.Y) {  // predict only
-    if (prow) row_predict<64, 0>(lane, p.N, p.act, [&](int, int j) { return zrow[j]; }, [&](int, int j, float v) { prow[j] = v; });
-    return;
-  }
-  const long long drow = batch_row(p, r, step, row);
-  const float* yrow = p.Y + (long long)r * p.sY + drow * p.ldy;
-  RowOut ro;
-  ro.loss = 0.f;
+    const float* zrow = p.Z + (long long)r * p.sZ + (long long)row * p.ldz;
+    float* prow = p.pred ? p.pred + (long long)r * p.sPred + (p.chunk * p.B + row) * p.ldp : nullptr;
+    if (!p.Y) {  // predict only
+      if (prow) row_predict<64, 0>(lane, p.N, p.act, [&](int, int j) { return zrow[j]; }, [&](int, int j, float v) { prow[j] = v; });
+      continue;
+    }
+    const long long drow = batch_row(p, r, step, row);
+    const float* yrow = p.Y + (long long)r * p.sY + drow * p.ldy;
+    RowOut ro;
+    ro.loss = 0.f;
 #pragma unroll
-  for (int q = 0; q < 4; ++q) ro.metric[q] = 0.f;
-  row_loss<64, 0>(lane, p.N, p.act, p.loss, p.met, p.nmet,
-               [&](int, int j) { return zrow[j]; },
-               [&](int, int j) { return yrow[j]; }, yrow[0],
-               train,
-               [&](int, int j, float v) {
-                 st<T>(p.D, (long long)r * p.sD + (long long)row * p.ldd + j, v * inv_valid);
-                 if (p.DT) st<T>(p.DT, (long long)r * p.sDT + (long long)j * p.lddt + row, v * inv_valid);
-               },
-               prow != nullptr, [&](int, int j, float v) { prow[j] = v; }, ro);
-  if (p.acc && lane == 0) {
-    double* a = p.acc + (long long)r * p.acc_stride;
-    atomicAdd(a + 0, (double)ro.loss);
-    atomicAdd(a + 1, 1.0);
+    for (int q = 0; q < 4; ++q) ro.metric[q] = 0.f;
+    auto dz = [&](int, int j, float v) {
+      st<T>(p.D, (long long)r * p.sD + (long long)row * p.ldd + j, v * inv_valid);
+      put_t(j, v * inv_valid);
+    };
+    auto pw = [&](int, int j, float v) { prow[j] = v; };
+    if (p.N <= 16 * 64 && softmax_cce_wide(p)) {
+      // softmax + (sparse) categorical cross-entropy: the row lives in registers
+      // (16 values per lane, all loads in flight at once); the generic loop below
+      // re-reads global memory once per pass and per 64-column chunk, one
+      // dependent round trip each (66 us for 1024 x 1000)
+      row_softmax_cce_reg<16>(p, lane, zrow, yrow, train, dz, ro);
+    } else {
+      row_loss<64, 0>(lane, p.N, p.act, p.loss, p.met, p.nmet, [&](int, int j) { return zrow[j]; },
+                      [&](int, int j) { return yrow[j]; }, yrow[0], train, dz, prow != nullptr, pw, ro);
+    }
+    // per-wave partial sums; one set of atomics per workgroup below (same-address
+    // fp64 atomics serialise: one per row was ~60 ns x rows x counters)
+    wsum[0] += ro.loss;
+    wsum[1] += 1.f;
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
-      if (q < p.nmet) atomicAdd(a + 2 + q, (double)ro.metric[q]);
+    for (int q = 0; q < 4; ++q) wsum[2 + q] += ro.metric[q];
+  }
+  if (p.acc) {
+    float* red = smem + (stage_t ? (LOSS_RPB * p.N * 2 + 15) / 16 * 4 : 0);  // past the dZ^T stage
+    __syncthreads();
+    if (lane == 0)
+#pragma unroll
+      for (int q = 0; q < 6; ++q) red[wave * 6 + q] = wsum[q];
+    __syncthreads();
+    if (threadIdx.x < 2 + p.nmet) {
+      const float v = red[threadIdx.x] + red[6 + threadIdx.x] + red[12 + threadIdx.x] + red[18 + threadIdx.x];
+      if (v != 0.f) atomicAdd(p.acc + (long long)r * p.acc_stride + threadIdx.x, (double)v);
+    }
+  }
+  if (stage_t) {
+    __syncthreads();
+    // rows row0 .. row0+7 of dZ^T column j: 16 contiguous bytes (row0 % 8 == 0, lddt % 8 == 0)
+    unsigned short* out = reinterpret_cast<unsigned short*>(p.DT) + (long long)r * p.sDT + row0;
+    for (int j = threadIdx.x; j < p.N; j += 256)
+      if (row0 + LOSS_RPB <= p.lddt)
+        *reinterpret_cast<uint4*>(out + (long long)j * p.lddt) = *reinterpret_cast<const uint4*>(sdt + j * LOSS_RPB);
   }
 }
 
@@ -319,8 +431,6 @@ __device__ __forceinline__ void run_prob(const GroupArgs& ga, const Prob& p, con
   constexpr int EPL = KT<T>::EPL, KC = KT<T>::KC;
   if (p.kind == PK_GATHER_T) {
     gather_transpose_block<T>(ga, p, lb, smem);
-  } else if (p.kind == PK_LOSS_ROWS) {
-    loss_rows_block<T>(ga, p, lb);
   } else {
     const int per_r = p.tiles_m * p.tiles_n;
     const int r = lb / per_r;
@@ -752,6 +862,16 @@ __global__ __launch_bounds__(256) void gemm_grouped(GroupArgs ga) {
   stamp_clk(ga, 11);
 }
 
+// Wide-output loss rows run in a kernel of their own: inside gemm_grouped their
+// register-resident row (16 z + 16 y values per lane) raised every GEMM tile's
+// VGPR allocation (104 -> 132 on the 128x128 config, plus scratch) and slowed
+// the weight-update launches of the same model by up to 50 %.
+template <typename T>
+__global__ __launch_bounds__(256) void loss_rows_kernel(GroupArgs ga) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  loss_rows_block<T>(ga, ga.p[0], blockIdx.x - ga.p[0].block_begin, smem);
+}
+
 // ------------------------------------------------------------- host side
 template <typename T, int WM, int WN, int WAVES_M, int WAVES_N, int KSPLIT>
 static size_t lds_bytes(bool loss = true) {
@@ -776,6 +896,12 @@ static void set_attr() {
 template <typename T, int WM, int WN, int WAVES_M, int WAVES_N, int KSPLIT>
 static hipError_t launch_cfg(const GroupArgs& ga, hipStream_t s) {
   if (ga.total_blocks <= 0) return hipSuccess;
+  if (ga.nprob == 1 && ga.p[0].kind == PK_LOSS_ROWS) {
+    // dZ^T stage (bf16, LOSS_RPB rows) + the 4-wave x 6 partial-sum reduction
+    const size_t lds = (size_t)(LOSS_RPB * LOSS_LDS_MAX_N * 2 + 15) / 16 * 16 + 32 * sizeof(float);
+    hipLaunchKernelGGL(loss_rows_kernel<T>, dim3(ga.total_blocks), dim3(256), lds, s, ga);
+    return hipGetLastError();
+  }
   bool loss = false;
   for (int i = 0; i < ga.nprob; ++i) loss |= ga.p[i].kind == PK_FWD_LOSS;
   const size_t lds = lds_bytes<T, WM, WN, WAVES_M, WAVES_N, KSPLIT>(loss);

@@ -103,17 +103,28 @@ def test_evaluate_predict_match_reference(loss, act, metrics, out):
     assert np.allclose(pn, pr, rtol=1e-4, atol=1e-5)
 
 
-def test_wide_output_loss_rows_path():
-    # 200 classes > GEMM tile width: wave-per-row loss kernel
+@pytest.mark.parametrize("policy", ["float32", "mixed_bfloat16"])
+@pytest.mark.parametrize("B", [64, 60])
+def test_wide_output_loss_rows_path(policy, B):
+    # 200 classes > GEMM tile width: wave-per-row loss kernel (bf16: dZ^T staged in LDS;
+    # B = 60 leaves a partial 8-row group and invalid rows in the last batch)
     model = _mlp(64, [96], 200)
     model.compile("sgd", "categorical_crossentropy", ["acc"])
-    x, y = _data(128, 64, 200)
-    nat, ref = _engines(model, 64, "float32")
+    x, y = _data(250, 64, 200)
+    nat, ref = _engines(model, B, policy)
     for t in (nat, ref):
         t.set_data([x], [y], 0.0, shuffle=False)
-        t.fit(1)
-    assert np.allclose(nat.get_weights_flat(), ref.get_weights_flat(), atol=1e-5)
-    assert np.allclose(nat.evaluate(x, y), ref.evaluate(x, y), rtol=1e-4)
+        t.fit(2)
+    wn, wr = nat.get_weights_flat(), ref.get_weights_flat()
+    if policy == "float32":
+        assert np.allclose(wn, wr, atol=1e-5)
+        assert np.allclose(nat.evaluate(x, y), ref.evaluate(x, y), rtol=1e-4)
+    else:
+        w0 = np.concatenate([w.reshape(-1) for w in model.get_weights()])
+        assert np.abs(wn - wr).mean() / np.abs(wr - w0).mean() < 0.05
+        assert np.allclose(nat.evaluate(x, y), ref.evaluate(x, y), rtol=2e-2, atol=2e-2)
+    from elephas_amd import config
+    config.set_policy("float32")
 
 
 def test_partial_batches_and_validation():
