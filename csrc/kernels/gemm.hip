@@ -247,6 +247,19 @@ __device__ __forceinline__ void loss_rows_block(const GroupArgs& ga, const Prob&
 }
 
 
+__device__ __forceinline__ void ld8f(const float* p, float (&v)[8]) {
+  const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+__device__ __forceinline__ void st8f(float* p, const float (&v)[8]) {
+  *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+  *reinterpret_cast<float4*>(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
+}
+__device__ __forceinline__ void zero8(float (&v)[8]) {
+#pragma unroll
+  for (int q = 0; q < 8; ++q) v[q] = 0.f;
+}
+
 // 8 contiguous outputs -> one 16-byte (bf16) or two 16-byte (fp32) stores.
 // Callers guarantee 16-byte alignment (row strides and column chunks are multiples of 8).
 template <typename T>
@@ -625,11 +638,27 @@ __device__ __forceinline__ void run_prob(const GroupArgs& ga, const Prob& p, con
       *reinterpret_cast<float4*>(C + row * LDC + c0) = make_float4(v[0], v[1], v[2], v[3]);
       *reinterpret_cast<float4*>(C + row * LDC + c0 + 4) = make_float4(v[4], v[5], v[6], v[7]);
     };
-    // transposed store of the tile (D^T, dZ^T, W^T): consecutive threads -> consecutive rows
+    // transposed store of the tile (D^T, dZ^T, W^T): each thread moves 8 consecutive
+    // rows of one column (8 LDS reads -> one 16-byte bf16 store, or two for fp32);
+    // the BM/8 threads of a column are consecutive, so a column's rows are one
+    // contiguous run in memory. Every destination here has ld % 8 == 0 and an
+    // 8-element-aligned base (Bp / Kp padding), checked on the host.
     auto store_transposed = [&](void* base, long long off, long long ld, int nrows) {
-      for (int e = threadIdx.x; e < BM * BN; e += 256) {
-        const int col = e / BM, row = e % BM, gm = m0 + row, gn = n0 + col;
-        if (gm < nrows && gn < p.N) st<T>(base, off + (long long)gn * ld + gm, C[row * LDC + col]);
+      constexpr int RC = BM / 8;  // 8-row chunks per column
+      for (int e = threadIdx.x; e < RC * BN; e += 256) {
+        const int rc = e % RC, col = e / RC, row = rc * 8, gm = m0 + row, gn = n0 + col;
+        if (gn >= p.N || gm >= nrows) continue;
+        float v[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] = C[(row + q) * LDC + col];
+        const long long idx = off + (long long)gn * ld + gm;
+        if (gm + 8 <= nrows) {
+          st8<T>(base, idx, v);
+        } else {
+#pragma unroll
+          for (int q = 0; q < 8; ++q)
+            if (gm + q < nrows) st<T>(base, idx + q, v[q]);
+        }
       }
     };
 
@@ -802,12 +831,20 @@ __device__ __forceinline__ void run_prob(const GroupArgs& ga, const Prob& p, con
             continue;
           }
           float w[8], s0[8], s1[8];
+          // whole 16-byte-aligned chunks (the common case) move as float4 pairs
+          const bool vec = gn0 + 8 <= p.N && (pidx & 3) == 0 && (p.op.s_plane & 3) == 0;
+          if (vec) {
+            ld8f(P + pidx, w);
+            if (np > 0) ld8f(S + pidx, s0); else zero8(s0);
+            if (np > 1) ld8f(S + p.op.s_plane + pidx, s1); else zero8(s1);
+          } else {
 #pragma unroll
-          for (int q = 0; q < 8; ++q) {  // loads first
-            const bool in = gn0 + q < p.N;
-            w[q] = in ? P[pidx + q] : 0.f;
-            s0[q] = (in && np > 0) ? S[pidx + q] : 0.f;
-            s1[q] = (in && np > 1) ? S[p.op.s_plane + pidx + q] : 0.f;
+            for (int q = 0; q < 8; ++q) {  // loads first
+              const bool in = gn0 + q < p.N;
+              w[q] = in ? P[pidx + q] : 0.f;
+              s0[q] = (in && np > 0) ? S[pidx + q] : 0.f;
+              s1[q] = (in && np > 1) ? S[p.op.s_plane + pidx + q] : 0.f;
+            }
           }
           {
             float gq[8];
@@ -816,14 +853,20 @@ __device__ __forceinline__ void run_prob(const GroupArgs& ga, const Prob& p, con
             opt_update_v<8>(p.op, w, gq, s0, s1, iter);  // lanes past N are discarded below
           }
           if (ps == 0) stamp(ga, 5);
+          if (vec) {
+            st8f(P + pidx, w);
+            if (np > 0) st8f(S + pidx, s0);
+            if (np > 1) st8f(S + p.op.s_plane + pidx, s1);
+          } else {
 #pragma unroll
-          for (int q = 0; q < 8; ++q) {
-            if (gn0 + q < p.N) {
-              P[pidx + q] = w[q];
-              if (np > 0) S[pidx + q] = s0[q];
-              if (np > 1) S[p.op.s_plane + pidx + q] = s1[q];
-            } else {
-              w[q] = 0.f;
+            for (int q = 0; q < 8; ++q) {
+              if (gn0 + q < p.N) {
+                P[pidx + q] = w[q];
+                if (np > 0) S[pidx + q] = s0[q];
+                if (np > 1) S[p.op.s_plane + pidx + q] = s1[q];
+              } else {
+                w[q] = 0.f;
+              }
             }
           }
           if (p.Wsh && gm < krows)

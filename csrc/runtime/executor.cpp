@@ -195,6 +195,11 @@ void Executor::finalize(Launch& L) const {
   int begin = 0;
   for (int i = 0; i < L.ga.nprob; ++i) {
     Prob& p = L.ga.p[i];
+    // the epilogues' transposed stores move 8 consecutive elements at a time
+    if (p.DT && (p.lddt % 8 || p.sDT % 8))
+      throw std::invalid_argument("transposed output needs 8-element aligned rows");
+    if (p.WTsh && (p.ldwtsh % 8 || p.sWTsh % 8 || p.wtsh_par % 8))
+      throw std::invalid_argument("W^T image needs 8-element aligned rows");
     if (p.kind == PK_GATHER_T) {
       p.tiles_m = cdiv(p.B, 64);
       p.tiles_n = cdiv(p.K, 64);
