@@ -65,6 +65,7 @@ static ExecCfg parse_cfg(const py::dict& d) {
   c.bf16 = get<int>(d, "bf16", 1);
   c.seed = get<unsigned long long>(d, "seed", 0);
   c.force_cfg = get<int>(d, "force_cfg", -1);
+  c.thr_min_k = get<int>(d, "thr_min_k", 64);
   c.fused = get<int>(d, "fused", -1);
   c.fused_split = get<int>(d, "fused_split", 16);
   for (auto item : d["layers"].cast<py::list>()) {

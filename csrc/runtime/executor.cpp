@@ -162,7 +162,7 @@ void Executor::destroy_graphs() {
 
 int Executor::pick_cfg(long long M, long long N, long long K) const {
   if (c_.force_cfg >= 0) return c_.force_cfg;
-  if (M >= 256 && N >= 256 && K >= 256) {
+  if (M >= 256 && N >= 256 && K >= c_.thr_min_k) {
     // 128x128 tiles while they give every CU at least two workgroups (256 CUs),
     // else 128x64 tiles (twice the workgroups; measured on MI355X, profiles/)
     const long long tiles = (long long)c_.R * cdiv((int)M, 128) * cdiv((int)N, 128);

@@ -54,7 +54,8 @@ struct ExecCfg {
   int loss = 0, nmet = 0, met[4] = {0, 0, 0, 0};
   uintptr_t acc = 0; int acc_stride = 6;
   uintptr_t ctr = 0;
-  int force_cfg = -1;  // -1 auto, 0 LAT, 1 THR
+  int force_cfg = -1;  // -1 auto, 0 LAT, 1 THR, 2 THR-N64
+  int thr_min_k = 64;  // smallest reduction depth for the 128-row THR tiles (Otto DW, K = batch 128: 135 -> 127 us/step)
   int fused = -1;      // fused small-MLP tail: -1 auto (when eligible), 0 off, 1 required
   int fused_split = 16; // workgroups per replica in the fused tail
 };

@@ -149,6 +149,7 @@ class NativeTrainer(TrainerBase):
         return dict(
             R=self.R, B=ws["B"], Bp=ws["Bp"], bf16=int(self.bf16), seed=self.seed,
             force_cfg=int(os.environ.get("ELEPHAS_AMD_GEMM_CFG", "-1")),
+            thr_min_k=int(os.environ.get("ELEPHAS_AMD_THR_MIN_K", "64")),
             fused=self.fused_mode if ws is self.ws else 0,
             fused_split=int(os.environ.get("ELEPHAS_AMD_FUSED_SPLIT", "16")),
             layers=layers,
