@@ -53,6 +53,8 @@ struct Prob {
   const void* A; long long lda, sA;
   const void* BT; long long ldb, sB;
   int a_gather;            // 1: A rows come from the batch window (train: perm, eval: contiguous)
+  int a_rowstep;           // with a_gather: the epoch's rows are pre-permuted, batch row m = step * B + m
+  int a_colstep;           // A advances by step * B elements per step (pre-permuted X^T of layer 0)
   int ones_row;            // >= 0: index of a virtual all-ones A row (bias gradient)
   int bt_shadow;           // 1: BT is a parity-double-buffered shadow (offset by par * bt_par)
   long long bt_par;

@@ -470,7 +470,7 @@ __device__ __forceinline__ void run_prob(const GroupArgs& ga, const Prob& p, con
       for (int j = 0; j < WN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
     if (!skip_update) {
-      const T* A = reinterpret_cast<const T*>(p.A) + (long long)r * p.sA;
+      const T* A = reinterpret_cast<const T*>(p.A) + (long long)r * p.sA + (p.a_colstep ? step * p.B : 0);
       const T* BTp = reinterpret_cast<const T*>(p.BT) + (long long)r * p.sB +
                      (p.bt_shadow ? (iter & 1) * p.bt_par : 0);
       // Every fragment load is an unconditional, in-bounds 16-byte global load
@@ -488,7 +488,7 @@ __device__ __forceinline__ void run_prob(const GroupArgs& ga, const Prob& p, con
         } else if (m < p.M) {
           if (p.a_gather) {
             if (m < valid) {
-              arow[i] = A + batch_row(p, r, step, m) * p.lda;
+              arow[i] = A + (p.a_rowstep ? step * p.B + m : batch_row(p, r, step, m)) * p.lda;
               amask |= 1u << i;
             }
           } else {
@@ -526,7 +526,7 @@ __device__ __forceinline__ void run_prob(const GroupArgs& ga, const Prob& p, con
             aones |= 1u << t;
           } else if (m < p.M) {
             if (p.a_gather) {
-              if (m < valid) arow_ld[t] = Ab + batch_row(p, r, step, m) * p.lda;
+              if (m < valid) arow_ld[t] = Ab + (p.a_rowstep ? step * p.B + m : batch_row(p, r, step, m)) * p.lda;
             } else {
               arow_ld[t] = Ab + (long long)m * p.lda;
             }

@@ -25,6 +25,8 @@ extern "C" hipError_t ea_replica_average(float* P, long long sP, int R, long lon
 extern "C" hipError_t ea_axpby(const float* x, float* y, long long n, float alpha, float beta, hipStream_t s);
 extern "C" hipError_t ea_ps_sub(float* p, const float* d, long long n, float scale, int atomic, hipStream_t s);
 extern "C" hipError_t ea_poison_lds(unsigned pattern, hipStream_t s);
+extern "C" hipError_t ea_permute_rows(const void* X, const int* perm, void* Xp, void* XpT, int R, int nmax, int ldx,
+                                      long long ldxpt, hipStream_t s);
 extern "C" hipError_t ea_sub(const float* a, const float* b, float* out, long long n, hipStream_t s);
 
 static void chk(hipError_t e, const char* w) {
@@ -66,6 +68,7 @@ static ExecCfg parse_cfg(const py::dict& d) {
   c.seed = get<unsigned long long>(d, "seed", 0);
   c.force_cfg = get<int>(d, "force_cfg", -1);
   c.thr_min_k = get<int>(d, "thr_min_k", 64);
+  c.thr_min_n = get<int>(d, "thr_min_n", 256);
   c.fused = get<int>(d, "fused", -1);
   c.fused_split = get<int>(d, "fused_split", 16);
   for (auto item : d["layers"].cast<py::list>()) {
@@ -100,6 +103,9 @@ static ExecCfg parse_cfg(const py::dict& d) {
   c.vstart = get<uintptr_t>(d, "vstart", 0);
   c.vcount = get<uintptr_t>(d, "vcount", 0);
   c.XT = get<uintptr_t>(d, "XT", 0);
+  c.Xp = get<uintptr_t>(d, "Xp", 0);
+  c.XpT = get<uintptr_t>(d, "XpT", 0);
+  c.ldxpt = get<long long>(d, "ldxpt", 0);
   c.P = get<uintptr_t>(d, "P", 0);
   c.sP = get<long long>(d, "sP", 0);
   c.nparams = get<long long>(d, "nparams", 0);
@@ -221,6 +227,12 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("ps_sub", [](uintptr_t p, uintptr_t d, long long n, float scale, int atomic, uintptr_t s) {
     chk(ea_ps_sub(reinterpret_cast<float*>(p), reinterpret_cast<const float*>(d), n, scale, atomic, S(s)), "ps_sub");
+  });
+  m.def("permute_rows", [](uintptr_t X, uintptr_t perm, uintptr_t Xp, uintptr_t XpT, int R, int nmax, int ldx,
+                           long long ldxpt, uintptr_t s) {
+    chk(ea_permute_rows(reinterpret_cast<const void*>(X), reinterpret_cast<const int*>(perm),
+                        reinterpret_cast<void*>(Xp), reinterpret_cast<void*>(XpT), R, nmax, ldx, ldxpt, S(s)),
+        "permute_rows");
   });
   m.def("poison_lds", [](unsigned pattern, uintptr_t s) { chk(ea_poison_lds(pattern, S(s)), "poison_lds"); });
   m.def("sub", [](uintptr_t a, uintptr_t b, uintptr_t out, long long n, uintptr_t s) {

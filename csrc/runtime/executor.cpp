@@ -162,7 +162,7 @@ void Executor::destroy_graphs() {
 
 int Executor::pick_cfg(long long M, long long N, long long K) const {
   if (c_.force_cfg >= 0) return c_.force_cfg;
-  if (M >= 256 && N >= 256 && K >= c_.thr_min_k) {
+  if (M >= 256 && N >= c_.thr_min_n && K >= c_.thr_min_k) {
     // 128x128 tiles while they give every CU at least two workgroups (256 CUs),
     // else 128x64 tiles (twice the workgroups; measured on MI355X, profiles/)
     const long long tiles = (long long)c_.R * cdiv((int)M, 128) * cdiv((int)N, 128);
@@ -240,6 +240,10 @@ std::vector<Executor::Launch> Executor::build_forward(bool eval, long long chunk
       p.lda = eval ? src->ldx : c_.ldx;
       p.sA = eval ? src->sX : c_.sX;
       p.a_gather = 1;
+      if (!eval && c_.Xp) {  // the epoch's batch rows are contiguous in the permuted copy
+        p.A = reinterpret_cast<const void*>(c_.Xp);
+        p.a_rowstep = 1;
+      }
     } else {
       const LayerCfg& pv = c_.layers[l - 1];
       p.A = reinterpret_cast<const void*>(pv.D);
@@ -335,7 +339,7 @@ std::vector<Executor::Launch> Executor::build_forward(bool eval, long long chunk
         La.ga.nprob = 1;
       }
     }
-    if (l == 0 && !eval && L > 0) {
+    if (l == 0 && !eval && L > 0 && !c_.XpT) {
       // X^T of the batch for the layer-0 weight gradient, in the same launch
       Prob t = base_prob();
       t.kind = PK_GATHER_T;
@@ -374,7 +378,13 @@ void Executor::build() {
     const LayerCfg& ly = c_.layers[l];
     Prob w = base_prob();
     w.kind = PK_DW_UPDATE;
-    if (l == 0) {
+    if (l == 0 && c_.XpT) {
+      // X^T of this step's batch = columns [step*B, step*B + Bp) of the epoch's
+      // permuted X^T: no per-step gather-transpose launch problem
+      w.A = reinterpret_cast<const void*>(c_.XpT);
+      w.sA = (long long)ly.Kp * c_.ldxpt;
+      w.a_colstep = 1;
+    } else if (l == 0) {
       w.A = reinterpret_cast<const void*>(c_.XT);
       w.sA = (long long)ly.Kp * c_.Bp;
     } else {
@@ -382,7 +392,7 @@ void Executor::build() {
       w.A = reinterpret_cast<const void*>(pv.DT);
       w.sA = (long long)pv.N * c_.Bp;
     }
-    w.lda = c_.Bp;
+    w.lda = (l == 0 && c_.XpT) ? c_.ldxpt : c_.Bp;
     w.M = ly.K + (ly.has_bias ? 1 : 0);
     w.ones_row = ly.has_bias ? ly.K : -1;
     w.N = ly.N;

@@ -43,6 +43,9 @@ struct ExecCfg {
   uintptr_t perm = 0; long long sPerm = 0;
   uintptr_t ntrain = 0, vstart = 0, vcount = 0;
   uintptr_t XT = 0;
+  // optional per-epoch pre-permuted copies of the training shard (B % 8 == 0):
+  // Xp [R][nmax][ldx] row-major, XpT [R][ldx][ldxpt] transposed
+  uintptr_t Xp = 0, XpT = 0; long long ldxpt = 0;
   // parameters
   uintptr_t P = 0; long long sP = 0, nparams = 0;
   uintptr_t G = 0; long long sG = 0;
@@ -55,6 +58,7 @@ struct ExecCfg {
   uintptr_t acc = 0; int acc_stride = 6;
   uintptr_t ctr = 0;
   int force_cfg = -1;  // -1 auto, 0 LAT, 1 THR, 2 THR-N64
+  int thr_min_n = 256;
   int thr_min_k = 64;  // smallest reduction depth for the 128-row THR tiles (Otto DW, K = batch 128: 135 -> 127 us/step)
   int fused = -1;      // fused small-MLP tail: -1 auto (when eligible), 0 off, 1 required
   int fused_split = 16; // workgroups per replica in the fused tail

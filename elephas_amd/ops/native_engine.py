@@ -110,6 +110,15 @@ class NativeTrainer(TrainerBase):
             self.ntrain = torch.zeros(R, dtype=torch.int32, device=dev)
             self.vstart = torch.zeros(R, dtype=torch.int32, device=dev)
             self.vcount = torch.zeros(R, dtype=torch.int32, device=dev)
+        # optional per-epoch pre-permuted copies of the shards (ELEPHAS_AMD_XP=1): layer 0
+        # reads contiguous batch rows and its weight update a column window of X^T, so
+        # the step has no perm-indirect gather and no gather-transpose workgroups
+        # (-3.3 us of kernel time per MNIST step), but the one-pass permute kernel per
+        # epoch costs about as much at ~105 steps per epoch: measured 67.0 vs 65.7
+        # us/step on MNIST, equal on Otto (profiles/README.md) -- off by default
+        self.xp_layout = (self.B % 8 == 0 and self.fused_mode == 0 and self.bf16 and
+                          os.environ.get("ELEPHAS_AMD_XP", "0") == "1")
+        self.Xp = self.XpT = None
         self.ntrain_h = [0] * R
         self.vcount_h = [0] * R
         self.active = [True] * R
@@ -150,6 +159,7 @@ class NativeTrainer(TrainerBase):
             R=self.R, B=ws["B"], Bp=ws["Bp"], bf16=int(self.bf16), seed=self.seed,
             force_cfg=int(os.environ.get("ELEPHAS_AMD_GEMM_CFG", "-1")),
             thr_min_k=int(os.environ.get("ELEPHAS_AMD_THR_MIN_K", "64")),
+            thr_min_n=int(os.environ.get("ELEPHAS_AMD_THR_MIN_N", "256")),
             fused=self.fused_mode if ws is self.ws else 0,
             fused_split=int(os.environ.get("ELEPHAS_AMD_FUSED_SPLIT", "16")),
             layers=layers,
@@ -158,6 +168,9 @@ class NativeTrainer(TrainerBase):
             perm=self.perm.data_ptr(), sPerm=self.nmax,
             ntrain=self.ntrain.data_ptr(), vstart=self.vstart.data_ptr(), vcount=self.vcount.data_ptr(),
             XT=ws["XT"].data_ptr(),
+            Xp=self.Xp.data_ptr() if (self.Xp is not None and ws is self.ws) else 0,
+            XpT=self.XpT.data_ptr() if (self.XpT is not None and ws is self.ws) else 0,
+            ldxpt=getattr(self, "ldxpt", 0),
             P=self.P.data_ptr(), sP=self.n, nparams=self.n,
             G=self.G.data_ptr(), sG=self.n,
             S=self.S.data_ptr(), sS=self.S.shape[1] * self.n,
@@ -257,9 +270,13 @@ class NativeTrainer(TrainerBase):
         nmax = max(1, max(len(x) for x in xs))
         self._enter()
         with torch.cuda.stream(self.stream):
-            if nmax != self.nmax:
+            if nmax != self.nmax or (self.xp_layout and self.Xp is None):
                 self.nmax = nmax
                 self.X = torch.zeros(self.R, nmax, self.Kp0, dtype=self.T, device=self.dev)
+                if self.xp_layout:
+                    self.Xp = torch.zeros(self.R, nmax, self.Kp0, dtype=self.T, device=self.dev)
+                    self.ldxpt = pad8(nmax) + pad8(self.B)   # zero tail: last partial batch
+                    self.XpT = torch.zeros(self.R, self.Kp0, self.ldxpt, dtype=self.T, device=self.dev)
                 self.Y = torch.zeros(self.R, nmax, self.ldy, dtype=torch.float32, device=self.dev)
                 self.perm = torch.zeros(self.R, nmax, dtype=torch.int32, device=self.dev)
                 rebuild = True
@@ -301,6 +318,9 @@ class NativeTrainer(TrainerBase):
                 self.perm.copy_(torch.argsort(keys, dim=1).to(torch.int32))
             else:
                 self.perm.copy_(torch.arange(nmax, device=self.dev, dtype=torch.int32).expand(R, nmax))
+            if self.Xp is not None:   # one pass: Xp rows in epoch order + their transpose
+                self.C.permute_rows(self.X.data_ptr(), self.perm.data_ptr(), self.Xp.data_ptr(), self.XpT.data_ptr(),
+                                    R, nmax, self.Kp0, self.ldxpt, self.s)
 
     # ------------------------------------------------------------------ train
     def steps_per_epoch(self) -> int:

@@ -430,3 +430,21 @@ def test_deferred_tail_matches_grouped_path(case):
     input gradients in LDS; layer 1's update is deferred into layer 0's grouped
     launch (3 launches per step, no cross-workgroup writes inside the tail)."""
     _fused_case(case, 2)
+
+
+def test_permuted_epoch_layout_matches_gather_path(monkeypatch):
+    """ELEPHAS_AMD_XP=1 (per-epoch permuted X / X^T copies) trains bit-identically to
+    the per-step perm-gather path (same rows, same order, same math)."""
+    from elephas_amd.models.optimizers import SGD
+    rng = np.random.default_rng(5)
+    model = _mlp(784, [128, 128], 10, dropout=0.2)
+    model.compile(SGD(learning_rate=0.1), "categorical_crossentropy", ["acc"])
+    xs = [rng.random((n, 784), dtype=np.float32) for n in (300, 131, 64)]
+    ys = [np.eye(10, dtype=np.float32)[rng.integers(0, 10, len(x))] for x in xs]
+    ws = []
+    for xp in ("0", "1"):
+        monkeypatch.setenv("ELEPHAS_AMD_XP", xp)
+        t, w, _ = _fit_weights(model, "mixed_bfloat16", 64, xs, ys, fused=0, epochs=2, val=0.1)
+        assert (t.Xp is not None) == (xp == "1")
+        ws.append(w)
+    assert np.array_equal(ws[0], ws[1]), np.abs(ws[0] - ws[1]).max()
