@@ -29,3 +29,19 @@ def test_example_runs(tmp_path, script, expect):
     r = subprocess.run([sys.executable, path], cwd=cwd, env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     assert expect in r.stdout
+
+
+def test_notebook_cells_run(tmp_path, monkeypatch):
+    """examples/Spark_ML_Pipeline.ipynb (reference notebook port): execute its code
+    cells in order with a smaller synthetic CSV and 2 epochs."""
+    import json
+    nb = json.load(open(os.path.join(EX, "Spark_ML_Pipeline.ipynb")))
+    monkeypatch.chdir(tmp_path)
+    g = {}
+    for c in nb["cells"]:
+        if c["cell_type"] != "code":
+            continue
+        src = "".join(c["source"]).replace("os.path.abspath('..')", repr(ROOT))
+        src = src.replace("61878", "600").replace("set_epochs(20)", "set_epochs(1)")
+        exec(compile(src, "cell", "exec"), g)
+    assert 0.0 <= g["metrics"].precision() <= 1.0
