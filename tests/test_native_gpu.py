@@ -448,3 +448,32 @@ def test_permuted_epoch_layout_matches_gather_path(monkeypatch):
         assert (t.Xp is not None) == (xp == "1")
         ws.append(w)
     assert np.array_equal(ws[0], ws[1]), np.abs(ws[0] - ws[1]).max()
+
+
+@pytest.mark.parametrize("mode,freq", [("synchronous", "epoch"), ("asynchronous", "epoch"), ("asynchronous", "batch"),
+                                       ("hogwild", "epoch"), ("hogwild", "batch")])
+def test_spark_model_end_to_end_on_gpu(mode, freq):
+    """Reference tests/integration/test_end_to_end.py on the MI355X path: native
+    executor workers, device parameter server (HBM, locked / lock-free), and the
+    reference's consistency checks (distributed predict == master predict,
+    distributed evaluate within 0.01 of the master network's)."""
+    from elephas_amd import config
+    from elephas_amd.data import SparkContext
+    from elephas_amd.models.optimizers import SGD
+    from elephas_amd.spark_model import SparkModel
+    from elephas_amd.utils.rdd_utils import to_simple_rdd
+    config.set_policy("mixed_bfloat16")
+    x, y = _data(1000, 784, 10, seed=8)
+    x = (x - x.min()) / (x.max() - x.min())
+    model = _mlp(784, [128, 128], 10, dropout=0.2)
+    model.compile(SGD(learning_rate=0.1), "categorical_crossentropy", ["acc"])
+    sm = SparkModel(model, mode=mode, frequency=freq, parameter_server_mode="device", num_workers=2)
+    sm.fit(to_simple_rdd(SparkContext.getOrCreate(), x, y), epochs=2, batch_size=64, verbose=0,
+           validation_split=0.1)
+    preds = np.stack(sm.predict(x[:300]))
+    assert np.array_equal(np.argmax(preds, 1), np.argmax(sm.master_network.predict(x[:300]), 1))
+    ev = sm.evaluate(x, y)
+    ref = sm.master_network.evaluate(x, y)
+    assert np.allclose(ev, ref, atol=0.01), (ev, ref)
+    assert np.isfinite(ev).all()
+    config.set_policy("float32")
