@@ -76,6 +76,8 @@ def main():
     ap.add_argument("--granularity", default="fit", choices=["fit", "batch"])
     ap.add_argument("--validation-split", type=float, default=0.1)
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--overlap", action="store_true",
+                    help="batch granularity: per-layer gradient buckets all-reduced beside the backward")
     ap.add_argument("--dropout", type=float, default=None, help="override the model's dropout (diagnostics)")
     ap.add_argument("--out", default=None, help="also append the JSON line to this file")
     args = ap.parse_args()
@@ -132,7 +134,7 @@ def main():
     def allreduce_grads(G):
         dist.all_reduce_sum_(G)
 
-    if batch_mode and gpu and world > 1:
+    if batch_mode and gpu and (world > 1 or args.overlap):
         t.set_grad_scale(1.0 / world)   # mean of the ranks' gradients after the sum all-reduce
 
     state = {"step_in_epoch": steps_per_epoch, "rows": 0}
@@ -147,7 +149,9 @@ def main():
                 state["step_in_epoch"] = 0
             n = min(k, steps_per_epoch - state["step_in_epoch"])
             if gpu:
-                if batch_mode and world > 1:
+                if batch_mode and args.overlap:
+                    t.run_steps_allreduce_overlap(n, dist.all_reduce_sum_)
+                elif batch_mode and world > 1:
                     t.run_steps_allreduce(n, allreduce_grads, use_graph=not args.no_graph)
                 else:
                     t.run_steps(n, use_graph=not args.no_graph)

@@ -180,7 +180,10 @@ PYBIND11_MODULE(_C, m) {
       .def("fused", &Executor::fused)
       .def("fused_lds_bytes", &Executor::fused_lds_bytes)
       .def("set_stamps", &Executor::set_stamps)
-      .def("train_launch", [](Executor& e, int idx, uintptr_t s) { e.train_launch(idx, S(s)); });
+      .def("train_launch", [](Executor& e, int idx, uintptr_t s) { e.train_launch(idx, S(s)); })
+      .def("grad_launches", &Executor::grad_launches)
+      .def("grad_launch_layer", &Executor::grad_launch_layer)
+      .def("grad_launch", [](Executor& e, int idx, uintptr_t s) { e.grad_launch(idx, S(s)); });
 
   // single PLAIN GEMM (C fp32 = A . BT^T) for kernel tests / generic matmul
   m.def("gemm_nt", [](uintptr_t A, uintptr_t BT, uintptr_t C, int M, int N, int K, long long lda, long long ldb,

@@ -485,6 +485,22 @@ void Executor::train_launch(int idx, hipStream_t s) {
   check(ea_gemm_grouped(&L.ga, c_.bf16, L.cfg, s), "train_launch");
 }
 
+int Executor::grad_launch_layer(int idx) const {
+  const int nf = (int)fwd_.size();
+  if (idx < nf) return -1;
+  return (int)c_.layers.size() - 1 - (idx - nf);
+}
+
+void Executor::grad_launch(int idx, hipStream_t s) {
+  const int nf = (int)fwd_.size();
+  if (idx < 0 || idx >= grad_launches()) throw std::out_of_range("grad_launch index");
+  Launch L = idx < nf ? fwd_[idx] : bwd_[idx - nf];
+  for (int i = 0; i < L.ga.nprob; ++i)
+    if (L.ga.p[i].kind == PK_DW_UPDATE) L.ga.p[i].kind = PK_DW_GRAD;
+  L.ga.step_off = 0;
+  check(ea_gemm_grouped(&L.ga, c_.bf16, L.cfg, s), "grad_launch");
+}
+
 void Executor::set_stamps(uintptr_t buf) {
   long long* p = reinterpret_cast<long long*>(buf);
   for (auto* v : {&fwd_, &bwd_, &ffwd_, &fbwd_})

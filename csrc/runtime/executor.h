@@ -99,6 +99,12 @@ class Executor {
   // diagnostics: bind a [blocks_max][16] int64 buffer for in-kernel stamps (0 = off)
   void set_stamps(uintptr_t buf);
   void train_launch(int idx, hipStream_t s);
+  // gradient path one launch at a time (bucketed all-reduce overlapped with the
+  // backward): launches [0, nf) are the forward, then one per layer from the last
+  // layer down; grad_launch_layer(i) = the layer whose dW / db launch i completes (-1: none)
+  int grad_launches() const { return (int)fwd_.size() + (int)bwd_.size(); }
+  int grad_launch_layer(int idx) const;
+  void grad_launch(int idx, hipStream_t s);
   std::vector<int> launch_blocks() const;
 
  private:

@@ -361,6 +361,40 @@ class NativeTrainer(TrainerBase):
             else:
                 self.exe.apply(self.s)
 
+    def run_steps_allreduce_overlap(self, nsteps: int, allreduce_bucket, comm_stream=None):
+        """Per-step gradient path with the all-reduce bucketed per layer and overlapped
+        with the rest of the backward: as soon as the launch that completes layer l's
+        dW / db has run, ``allreduce_bucket(G[:, lo:hi])`` is issued on ``comm_stream``
+        (RCCL runs it beside the next backward launch); the optimizer apply waits for
+        every bucket. Eager launches (the buckets' host calls sit between them)."""
+        comm = comm_stream or getattr(self, "_comm_stream", None)
+        if comm is None:
+            comm = self._comm_stream = torch.cuda.Stream(device=self.dev)
+        nl = self.exe.grad_launches()
+        spans = []
+        for s in self.plan.layers:
+            lo = int(s.p_off)
+            spans.append((lo, lo + s.in_dim * s.units + (s.units if s.use_bias else 0)))
+        for _ in range(nsteps):
+            done = []
+            for i in range(nl):
+                self.exe.grad_launch(i, self.s)
+                layer = self.exe.grad_launch_layer(i)
+                if layer < 0:
+                    continue
+                ev = torch.cuda.Event()
+                ev.record(self.stream)
+                with torch.cuda.stream(comm):
+                    comm.wait_event(ev)
+                    lo, hi = spans[layer]
+                    allreduce_bucket(self.G[:, lo:hi])
+                    d = torch.cuda.Event()
+                    d.record(comm)
+                    done.append(d)
+            for d in done:
+                self.stream.wait_event(d)
+            self.exe.apply(self.s)
+
     def begin_epoch(self, gen=None):
         with torch.cuda.stream(self.stream):
             self.exe.reset_epoch(self.s)
