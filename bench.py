@@ -80,6 +80,9 @@ def main():
                     help="batch granularity: per-layer gradient buckets all-reduced beside the backward")
     ap.add_argument("--dropout", type=float, default=None, help="override the model's dropout (diagnostics)")
     ap.add_argument("--out", default=None, help="also append the JSON line to this file")
+    ap.add_argument("--mode", default="synchronous", choices=["synchronous", "asynchronous", "hogwild"],
+                    help="asynchronous / hogwild: every worker pulls from and pushes to the HBM "
+                         "parameter server around each step (frequency='batch', BASELINE config #3)")
     args = ap.parse_args()
 
     import torch
@@ -101,6 +104,8 @@ def main():
         d, dr, c, r, lr = MODELS[args.model]
         MODELS[args.model] = (d, args.dropout, c, r, lr)
     model = build_model(args.model)
+    if args.mode != "synchronous":
+        return bench_async(args, model, dist, rank, world, dev)
     plan = build_plan(model)
     dims, drop, classes, rows, _ = MODELS[args.model]
     W = args.workers_per_gpu
@@ -237,6 +242,108 @@ def main():
                 f.write(s + "\n")
     if dist.is_initialized():
         dist.barrier()
+        import torch.distributed as tdist
+        tdist.destroy_process_group()
+
+
+def bench_async(args, model, dist, rank, world, dev):
+    """Async / hogwild DP through the device parameter server (reference worker.py:114-127,
+    frequency='batch'): W worker threads per GPU, each step = pull theta from the PS (HBM on
+    rank 0; other ranks over xGMI IPC) -> one optimizer step -> push theta_pulled - theta.
+    'asynchronous' serialises pulls/pushes with the writer-priority RW lock, 'hogwild' not."""
+    import threading
+    import torch
+    from elephas_amd.ops.native_engine import NativeTrainer
+    from elephas_amd.ops.plan import build_plan
+    from elephas_amd.parameter.client import DeviceClient
+    from elephas_amd.parameter.server import DeviceServer
+    from elephas_amd.utils.serialization import model_to_dict
+    dims, drop, classes, rows, _ = MODELS[args.model]
+    W, B = args.workers_per_gpu, args.batch
+    ps = None
+    if rank == 0:
+        ps = DeviceServer(model_to_dict(model), 0, args.mode)
+        client = DeviceClient(server=ps)
+        handle = ps.handle() if world > 1 else None
+    else:
+        handle, client = None, None
+    handle = dist.broadcast_object(handle, 0)
+    if rank != 0:
+        client = DeviceClient(handle=handle)
+    plan = build_plan(model)
+    rng = np.random.default_rng(1000 + rank)
+    centers = rng.normal(0, 1, size=(classes, dims[0])).astype(np.float32)
+    trainers = []
+    for w in range(W):
+        y = rng.integers(0, classes, rows)
+        x = centers[y] + rng.normal(0, 2.0, size=(rows, dims[0])).astype(np.float32)
+        x = ((x - x.min()) / (x.max() - x.min())).astype(np.float32)
+        t = NativeTrainer(model, plan, 1, B, dev, seed=4321 + 97 * rank + w)
+        t.set_data([x], [np.eye(classes, dtype=np.float32)[y]], args.validation_split, shuffle=True)
+        t.begin_epoch()
+        trainers.append(t)
+    spe = int(math.ceil(trainers[0].ntrain_h[0] / B))
+    errors = []
+
+    def worker(t, k):
+        try:
+            done = 0
+            while done < k:
+                if t._pos >= spe:
+                    t.begin_epoch()
+                    t._pos = 0
+                with torch.cuda.stream(t.stream):
+                    client.pull_into(t.P.data_ptr(), t.s)
+                    t.sync_shadows()
+                    before = t.P.clone()
+                t.run_steps(1, use_graph=True)
+                with torch.cuda.stream(t.stream):
+                    delta = before - t.P
+                    client.push_from(delta.data_ptr(), t.s)
+                t._pos += 1
+                done += 1
+            t.stream.synchronize()
+        except BaseException as e:  # noqa: BLE001 - surfaced below
+            errors.append(e)
+
+    def run(k):
+        ths = [threading.Thread(target=worker, args=(t, k)) for t in trainers]
+        for th in ths:
+            th.start()
+        for th in ths:
+            th.join()
+        if errors:
+            raise errors[0]
+
+    for t in trainers:
+        t._pos = 0
+    run(args.warmup)
+    torch.cuda.synchronize()
+    dist.barrier()
+    t0 = time.perf_counter()
+    run(args.steps)
+    torch.cuda.synchronize()
+    dist.barrier()
+    dt = time.perf_counter() - t0
+    dt_max = max(dist.all_gather_object(dt))
+    if rank == 0:
+        value = W * B * args.steps * world / dt_max
+        line = {
+            "metric": f"samples/sec (whole node) {args.model.upper()}-MLP {args.mode} DP (device parameter server)",
+            "value": round(value, 1), "unit": "samples/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(dt_max / args.steps * 1e3, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None,
+            "dtype": "bf16" if args.policy == "mixed_bfloat16" else "fp32",
+            "data": "synthetic, random-init weights",
+            "config": {"model": args.model, "global_batch": B * W * world, "seq_len": None,
+                       "parallelism": f"{args.mode}-dp{world}", "workers_per_gpu": W, "batch_per_worker": B,
+                       "frequency": "batch", "ps": "device (HBM, rank 0; xGMI IPC for other ranks)"},
+        }
+        print(json.dumps(line), flush=True)
+    dist.barrier()
+    if ps is not None:
+        ps.close()
+    if dist.is_initialized():
         import torch.distributed as tdist
         tdist.destroy_process_group()
 
