@@ -80,6 +80,9 @@ def main():
                     help="batch granularity: per-layer gradient buckets all-reduced beside the backward")
     ap.add_argument("--dropout", type=float, default=None, help="override the model's dropout (diagnostics)")
     ap.add_argument("--out", default=None, help="also append the JSON line to this file")
+    ap.add_argument("--async-threads", action="store_true",
+                    help="async/hogwild: one Python thread + executor per worker instead of the lockstep "
+                         "replica executor (worker.BatchedAsynchronousWorker)")
     ap.add_argument("--mode", default="synchronous", choices=["synchronous", "asynchronous", "hogwild"],
                     help="asynchronous / hogwild: every worker pulls from and pushes to the HBM "
                          "parameter server around each step (frequency='batch', BASELINE config #3)")
@@ -284,6 +287,40 @@ def bench_async(args, model, dist, rank, world, dev):
         trainers.append(t)
     spe = int(math.ceil(trainers[0].ntrain_h[0] / B))
     errors = []
+    if not args.async_threads:
+        # lockstep replicas (the SparkModel GPU path, worker.BatchedAsynchronousWorker):
+        # one pull into all W replicas, one grouped step, one push of the summed deltas
+        xs = [t.X for t in trainers]
+        del trainers
+        t = NativeTrainer(model, plan, W, B, dev, seed=4321 + 97 * rank)
+        rngd = np.random.default_rng(1000 + rank)
+        centers = rngd.normal(0, 1, size=(classes, dims[0])).astype(np.float32)
+        dx, dy = [], []
+        for w in range(W):
+            y = rngd.integers(0, classes, rows)
+            x = centers[y] + rngd.normal(0, 2.0, size=(rows, dims[0])).astype(np.float32)
+            dx.append(((x - x.min()) / (x.max() - x.min())).astype(np.float32))
+            dy.append(np.eye(classes, dtype=np.float32)[y])
+        t.set_data(dx, dy, args.validation_split, shuffle=True)
+        t.begin_epoch()
+        state = {"pos": 0}
+
+        def run_lockstep(k):
+            for _ in range(k):
+                if state["pos"] >= spe:
+                    t.begin_epoch()
+                    state["pos"] = 0
+                with torch.cuda.stream(t.stream):
+                    client.pull_into(t.P[0].data_ptr(), t.s)
+                    t.P[1:].copy_(t.P[0].expand(W - 1, -1))
+                    t.sync_shadows()
+                    before = t.P[0].clone()
+                t.run_steps(1, use_graph=True)
+                with torch.cuda.stream(t.stream):
+                    delta = before * float(W) - t.P.sum(0)
+                    client.push_from(delta.data_ptr(), t.s)
+                state["pos"] += 1
+            t.stream.synchronize()
 
     def worker(t, k):
         try:
@@ -315,8 +352,11 @@ def bench_async(args, model, dist, rank, world, dev):
         if errors:
             raise errors[0]
 
-    for t in trainers:
-        t._pos = 0
+    if args.async_threads:
+        for t in trainers:
+            t._pos = 0
+    else:
+        run = run_lockstep
     run(args.warmup)
     torch.cuda.synchronize()
     dist.barrier()
@@ -337,7 +377,8 @@ def bench_async(args, model, dist, rank, world, dev):
             "data": "synthetic, random-init weights",
             "config": {"model": args.model, "global_batch": B * W * world, "seq_len": None,
                        "parallelism": f"{args.mode}-dp{world}", "workers_per_gpu": W, "batch_per_worker": B,
-                       "frequency": "batch", "ps": "device (HBM, rank 0; xGMI IPC for other ranks)"},
+                       "frequency": "batch", "ps": "device (HBM, rank 0; xGMI IPC for other ranks)",
+                       "workers": "python threads" if args.async_threads else "lockstep replicas of one executor"},
         }
         print(json.dumps(line), flush=True)
     dist.barrier()

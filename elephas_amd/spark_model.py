@@ -46,7 +46,7 @@ from .parameter.factory import ClientServerFactory
 from .utils.functional_utils import divide_by, subtract_params
 from .utils.rdd_utils import lp_to_simple_rdd, to_simple_rdd
 from .utils.serialization import model_to_dict
-from .worker import AsynchronousSparkWorker, SparkWorker
+from .worker import AsynchronousSparkWorker, BatchedAsynchronousWorker, SparkWorker
 
 
 def _resolve_ps_mode(mode: Optional[str]) -> str:
@@ -389,6 +389,15 @@ class SparkModel:
                       dict(class_name=self.__class__.__name__, config=self.get_config()))
             dist.barrier()
 
+    def _native_ok(self) -> bool:
+        import torch
+        from .ops.engine import native_supported
+        from . import config
+        if not torch.cuda.is_available() or config.get_engine() == "torch":
+            return False
+        ok, _ = native_supported(self._master_network)
+        return ok
+
     def _fit_async(self, model_json, init, local, train_config):
         import torch
         ps = self.parameter_server
@@ -421,6 +430,16 @@ class SparkModel:
                 errors.append(e)
 
         print(">>> Distribute load")
+        if self._ps_type == "device" and self._native_ok() and local:
+            # MI355X path: the rank's partitions as replicas of one native executor
+            # exchanging with the HBM parameter server in lockstep (worker.py)
+            try:
+                BatchedAsynchronousWorker(model_json, init, client, train_config, self.frequency,
+                                          self.master_optimizer, self.master_loss, self.master_metrics,
+                                          self.custom_objects).train_partitions(local)
+            except BaseException as e:  # noqa: BLE001 - fail fast, after the server is stopped below
+                errors.append(e)
+            local = []
         threads = [threading.Thread(target=run, args=(p,)) for p in local]
         for t in threads:
             t.start()

@@ -212,3 +212,86 @@ class AsynchronousSparkWorker:
             after = trainer.get_weights_flat()[0]
             delta = self._before - after
             self.client.update_parameters(unflatten_weights(delta, self.model.get_weights()))
+
+
+class BatchedAsynchronousWorker:
+    """GPU path of the asynchronous / hogwild workers for all of a rank's partitions.
+
+    The reference runs one AsynchronousSparkWorker per partition in its own process
+    (worker.py:52-131). On an MI355X the rank's partitions are replicas of ONE native
+    executor that advance in lockstep: per epoch (frequency='epoch') or per batch
+    (frequency='batch') every replica pulls the same theta from the parameter server,
+    trains, and the replicas' deltas are pushed as one sum -- one admissible
+    interleaving of the reference's independent workers (all pull, all push), with one
+    pull and one push per exchange instead of one per worker, and the pushes of a
+    rank applied atomically under the server's write lock in 'asynchronous' mode.
+    Replicas without a batch in a step (shorter partitions) push a zero delta, as do
+    partitions with n <= batch_size (reference worker.py:116).
+    """
+
+    def __init__(self, json, parameters, client, train_config, frequency, master_optimizer, master_loss,
+                 master_metrics, custom_objects):
+        self.json, self.parameters, self.client = json, parameters, client
+        self.train_config = dict(train_config)
+        self.frequency = frequency
+        self.master_optimizer, self.master_loss, self.master_metrics = master_optimizer, master_loss, master_metrics
+        self.custom_objects = custom_objects or {}
+        self.model = None
+
+    def train_partitions(self, partitions):
+        import torch
+        from .ops.engine import make_trainer
+        if self.frequency not in ("epoch", "batch"):
+            raise ValueError("frequency parameter can be `epoch` or `batch, got {}".format(self.frequency))
+        parts = [p for p in partitions if len(p)]
+        if not parts:
+            return None
+        self.model = _build_model(self.json, self.custom_objects, self.master_optimizer, self.master_loss,
+                                  self.master_metrics, _value(self.parameters))
+        tc = self.train_config
+        epochs, bs = int(tc.get("epochs", 1)), int(tc.get("batch_size", 32))
+        verbose, vs = int(tc.get("verbose", 0)), float(tc.get("validation_split", 0.0))
+        xs, ys = zip(*[partition_to_numpy(p) for p in parts])
+        R = len(parts)
+        t = make_trainer(self.model, R, bs, engine="native")
+        if self.frequency == "epoch":
+            active = [len(x) > bs for x in xs]   # inactive replicas push a zero delta
+            t.set_data(list(xs), list(ys), vs, active=active, shuffle=True)
+            for _ in range(epochs):
+                before = self._pull(t)
+                if any(active):
+                    t.fit(1, verbose=verbose)
+                self._push(t, before)
+        else:
+            active = [len(x) > bs for x in xs]
+            if not any(active):
+                return t
+            t.set_data(list(xs), list(ys), 0.0, active=active, shuffle=False)
+            nb = t.steps_per_epoch()
+            for _ in range(epochs):
+                t.begin_epoch()
+                for _ in range(nb):
+                    before = self._pull(t)
+                    t.run_steps(1, use_graph=True)
+                    self._push(t, before)
+        t.stream.synchronize()
+        return t
+
+    def _pull(self, t):
+        import torch
+        from .parallel import dist, fault
+        fault.maybe_inject("pull", dist.rank())
+        with torch.cuda.stream(t.stream):
+            self.client.pull_into(t.P[0].data_ptr(), t.s)
+            if t.R > 1:
+                t.P[1:].copy_(t.P[0].expand(t.R - 1, -1))
+            t.sync_shadows()
+            return t.P[0].clone()
+
+    def _push(self, t, before):
+        import torch
+        from .parallel import dist, fault
+        fault.maybe_inject("push", dist.rank())
+        with torch.cuda.stream(t.stream):
+            delta = before * float(t.R) - t.P.sum(0)     # sum_r (theta_pulled - theta_r)
+            self.client.push_from(delta.data_ptr(), t.s)
