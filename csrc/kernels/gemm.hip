@@ -956,16 +956,20 @@ static hipError_t launch_cfg(const GroupArgs& ga, hipStream_t s) {
 }  // namespace ea
 
 // cfg: 0 = LAT (64x32, split-K 4), 1 = THR (128x128), 2 = THR-N64 (128x64: twice the
-// workgroups for grids that would otherwise leave CUs with a single workgroup)
+// workgroups for grids that would otherwise leave CUs with a single workgroup),
+// 3 = LAT-64 (64x64, 2 N-waves x split-K 2: shallow reductions such as K = batch 64,
+// where split-K 4 leaves two waves without a 32-deep chunk)
 extern "C" hipError_t ea_gemm_grouped(const ea::GroupArgs* ga, int bf16, int cfg, hipStream_t s) {
   using namespace ea;
   if (bf16) {
     if (cfg == 0) return launch_cfg<__bf16, 4, 2, 1, 1, 4>(*ga, s);
     if (cfg == 2) return launch_cfg<__bf16, 4, 2, 2, 2, 1>(*ga, s);
+    if (cfg == 3) return launch_cfg<__bf16, 4, 2, 1, 2, 2>(*ga, s);
     return launch_cfg<__bf16, 4, 4, 2, 2, 1>(*ga, s);
   } else {
     if (cfg == 0) return launch_cfg<float, 4, 2, 1, 1, 4>(*ga, s);
     if (cfg == 2) return launch_cfg<float, 4, 2, 2, 2, 1>(*ga, s);
+    if (cfg == 3) return launch_cfg<float, 4, 2, 1, 2, 2>(*ga, s);
     return launch_cfg<float, 4, 4, 2, 2, 1>(*ga, s);
   }
 }
@@ -977,12 +981,14 @@ extern "C" void ea_gemm_init() {
   set_attr<__bf16, 4, 2, 1, 1, 4>();
   set_attr<__bf16, 4, 4, 2, 2, 1>();
   set_attr<__bf16, 4, 2, 2, 2, 1>();
+  set_attr<__bf16, 4, 2, 1, 2, 2>();
   set_attr<float, 4, 2, 1, 1, 4>();
+  set_attr<float, 4, 2, 1, 2, 2>();
   set_attr<float, 4, 4, 2, 2, 1>();
   set_attr<float, 4, 2, 2, 2, 1>();
   done = true;
 }
 
-extern "C" int ea_gemm_tile_m(int cfg) { return cfg == 0 ? 64 : 128; }
-extern "C" int ea_gemm_tile_n(int cfg) { return cfg == 0 ? 32 : (cfg == 2 ? 64 : 128); }
+extern "C" int ea_gemm_tile_m(int cfg) { return (cfg == 0 || cfg == 3) ? 64 : 128; }
+extern "C" int ea_gemm_tile_n(int cfg) { return cfg == 0 ? 32 : ((cfg == 2 || cfg == 3) ? 64 : 128); }
 extern "C" int ea_gather_tile() { return 64; }

@@ -69,6 +69,7 @@ static ExecCfg parse_cfg(const py::dict& d) {
   c.force_cfg = get<int>(d, "force_cfg", -1);
   c.thr_min_k = get<int>(d, "thr_min_k", 64);
   c.thr_min_n = get<int>(d, "thr_min_n", 256);
+  c.lat64_max_k = get<int>(d, "lat64_max_k", 0);
   c.fused = get<int>(d, "fused", -1);
   c.fused_split = get<int>(d, "fused_split", 16);
   for (auto item : d["layers"].cast<py::list>()) {
@@ -192,7 +193,7 @@ PYBIND11_MODULE(_C, m) {
     // 16-byte aligned and K padded to whole chunks, or it reads out of bounds
     const int epl = bf16 ? 8 : 4;
     if (M <= 0 || N <= 0 || K <= 0 || (K % epl) || (lda % epl) || (ldb % epl) || lda < K || ldb < K || ldc < N ||
-        (A % 16) || (BT % 16) || (C % 4) || cfg < 0 || cfg > 2)
+        (A % 16) || (BT % 16) || (C % 4) || cfg < 0 || cfg > 3)
       throw std::invalid_argument("gemm_nt: K, lda, ldb must be multiples of 16 bytes, pointers 16-byte aligned");
     ea_gemm_init();
     GroupArgs ga;

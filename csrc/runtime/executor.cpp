@@ -162,6 +162,7 @@ void Executor::destroy_graphs() {
 
 int Executor::pick_cfg(long long M, long long N, long long K) const {
   if (c_.force_cfg >= 0) return c_.force_cfg;
+  if (K <= c_.lat64_max_k && N >= 64 && M >= 128 && !(M >= 256 && N >= c_.thr_min_n && K >= c_.thr_min_k)) return 3;
   if (M >= 256 && N >= c_.thr_min_n && K >= c_.thr_min_k) {
     // 128x128 tiles while they give every CU at least two workgroups (256 CUs),
     // else 128x64 tiles (twice the workgroups; measured on MI355X, profiles/)

@@ -59,6 +59,7 @@ struct ExecCfg {
   uintptr_t ctr = 0;
   int force_cfg = -1;  // -1 auto, 0 LAT, 1 THR, 2 THR-N64
   int thr_min_n = 256;
+  int lat64_max_k = 0;  // reductions this shallow use the 64x64 split-K-2 tile (0 = off)
   int thr_min_k = 64;  // smallest reduction depth for the 128-row THR tiles (Otto DW, K = batch 128: 135 -> 127 us/step)
   int fused = -1;      // fused small-MLP tail: -1 auto (when eligible), 0 off, 1 required
   int fused_split = 16; // workgroups per replica in the fused tail

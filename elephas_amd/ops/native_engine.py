@@ -160,6 +160,7 @@ class NativeTrainer(TrainerBase):
             force_cfg=int(os.environ.get("ELEPHAS_AMD_GEMM_CFG", "-1")),
             thr_min_k=int(os.environ.get("ELEPHAS_AMD_THR_MIN_K", "64")),
             thr_min_n=int(os.environ.get("ELEPHAS_AMD_THR_MIN_N", "256")),
+            lat64_max_k=int(os.environ.get("ELEPHAS_AMD_LAT64_MAX_K", "0")),
             fused=self.fused_mode if ws is self.ws else 0,
             fused_split=int(os.environ.get("ELEPHAS_AMD_FUSED_SPLIT", "16")),
             layers=layers,

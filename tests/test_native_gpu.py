@@ -268,7 +268,7 @@ def _fused_case(case, fmode):
             assert np.allclose(a[key], b[key], rtol=5 * tol, atol=5 * tol), (key, a[key], b[key])
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 2])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3])
 @pytest.mark.parametrize("bf16", [1, 0])
 @pytest.mark.parametrize("M,N,K", [(64, 128, 784), (64, 10, 128), (785, 128, 64), (300, 200, 136), (512, 512, 512)])
 def test_plain_gemm_matches_torch_fp32(M, N, K, bf16, cfg):
