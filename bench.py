@@ -210,8 +210,12 @@ def main():
     if rank == 0:
         value = samples / dt_max
         launches = t.launch_count() if gpu else None
+        names = {"mnist": "MNIST-MLP 784-128-128-10", "otto": "Otto-MLP 93-512-512-512-9",
+                 "wide": "Wide-MLP 4096-4096-4096-1000"}
+        metric = ("samples/sec (whole node) MNIST-MLP 784-128-128-10 sync DP at 1/2/4/8 MI355X"
+                  if args.model == "mnist" else f"samples/sec (whole node) {names[args.model]} sync DP")
         line = {
-            "metric": "samples/sec (whole node) MNIST-MLP 784-128-128-10 sync DP at 1/2/4/8 MI355X",
+            "metric": metric,
             "value": round(value, 1),
             "unit": "samples/s",
             "n_gpus": world,
