@@ -21,6 +21,11 @@ ARCH = os.environ.get("ELEPHAS_AMD_ARCH", "gfx950")
 
 SOURCES = [
     "kernels/gemm.hip",
+    "kernels/gemm_cfg0_bf16.hip",
+    "kernels/gemm_cfg1_bf16.hip",
+    "kernels/gemm_cfg2_bf16.hip",
+    "kernels/gemm_cfg3_bf16.hip",
+    "kernels/gemm_f32.hip",
     "kernels/flat.hip",
     "kernels/fused.hip",
     "runtime/executor.cpp",
