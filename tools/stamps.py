@@ -6,12 +6,16 @@ from elephas_amd import config
 from elephas_amd.ops.plan import build_plan
 from elephas_amd.ops.native_engine import NativeTrainer
 config.set_policy("mixed_bfloat16")
-m = bench.build_model("mnist")
+# usage: stamps.py [replicas] [model] [batch]
+MODEL = sys.argv[2] if len(sys.argv) > 2 else "mnist"
+BATCH = int(sys.argv[3]) if len(sys.argv) > 3 else 64
+m = bench.build_model(MODEL)
 R = int(sys.argv[1]) if len(sys.argv) > 1 else 8
-t = NativeTrainer(m, build_plan(m), R, 64, torch.device("cuda"))
+t = NativeTrainer(m, build_plan(m), R, BATCH, torch.device("cuda"))
 rng = np.random.default_rng(0)
-xs = [rng.random((7500, 784), dtype=np.float32) for _ in range(R)]
-ys = [np.eye(10, dtype=np.float32)[rng.integers(0, 10, 7500)] for _ in range(R)]
+din, dout = bench.MODELS[MODEL][0][0], bench.MODELS[MODEL][2]
+xs = [rng.random((7500, din), dtype=np.float32) for _ in range(R)]
+ys = [np.eye(dout, dtype=np.float32)[rng.integers(0, dout, 7500)] for _ in range(R)]
 t.set_data(xs, ys, 0.1)
 t.begin_epoch()
 t.run_steps(30)
