@@ -86,6 +86,10 @@ def main():
     ap.add_argument("--mode", default="synchronous", choices=["synchronous", "asynchronous", "hogwild"],
                     help="asynchronous / hogwild: every worker pulls from and pushes to the HBM "
                          "parameter server around each step (frequency='batch', BASELINE config #3)")
+    ap.add_argument("--task", default="train", choices=["train", "predict", "evaluate"],
+                    help="predict / evaluate: distributed inference of the master network "
+                         "(SparkModel.predict / evaluate path, BASELINE config #5)")
+    ap.add_argument("--infer-rows", type=int, default=None, help="rows per GPU for --task predict/evaluate")
     args = ap.parse_args()
 
     import torch
@@ -107,6 +111,8 @@ def main():
         d, dr, c, r, lr = MODELS[args.model]
         MODELS[args.model] = (d, args.dropout, c, r, lr)
     model = build_model(args.model)
+    if args.task != "train":
+        return bench_infer(args, model, dist, rank, world, dev)
     if args.mode != "synchronous":
         return bench_async(args, model, dist, rank, world, dev)
     plan = build_plan(model)
@@ -247,6 +253,70 @@ def main():
         if args.out:
             with open(args.out, "a") as f:
                 f.write(s + "\n")
+    if dist.is_initialized():
+        dist.barrier()
+        import torch.distributed as tdist
+        tdist.destroy_process_group()
+
+
+def bench_infer(args, model, dist, rank, world, dev):
+    """Distributed predict / evaluate of the master network, the SparkModel path
+    (spark_model.py _predict / _evaluate): every rank runs its block of the rows through
+    the native eval executor; predict gathers the rows with one tensor all-gather
+    (RCCL), evaluate all-reduces the loss / metric sums. A "step" = one call over all
+    rows; weak scaling (--infer-rows per GPU). Host -> device upload and the
+    device -> host result copies are inside the timed region."""
+    import torch
+    dims, _, classes, _, _ = MODELS[args.model]
+    per = args.infer_rows or (16384 if args.model == "wide" else 65536)
+    n = per * world
+    lo, hi = dist.block_range(n)
+    rng = np.random.default_rng(77 + rank)
+    x = rng.random((hi - lo, dims[0]), dtype=np.float32)
+    y = np.eye(classes, dtype=np.float32)[rng.integers(0, classes, hi - lo)]
+    bs = 2048
+
+    def call():
+        if args.task == "predict":
+            out = dist.all_gather_rows(model.predict(x, batch_size=bs), n)
+            assert out.shape == (n, classes)
+        else:
+            t = model._trainer(bs)
+            s = torch.tensor(np.asarray(t.evaluate_sums(x, y), np.float64))
+            dist.all_reduce_sum_(s)
+
+    def sync():
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+        dist.barrier()
+
+    for _ in range(max(args.warmup, 1)):
+        call()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        call()
+    sync()
+    dt = time.perf_counter() - t0
+    dt_max = max(dist.all_gather_object(dt))
+    if rank == 0:
+        names = {"mnist": "MNIST-MLP 784-128-128-10", "otto": "Otto-MLP 93-512-512-512-9",
+                 "wide": "Wide-MLP 4096-4096-4096-1000"}
+        line = {
+            "metric": f"samples/sec (whole node) {names[args.model]} distributed {args.task}",
+            "value": round(n * args.steps / dt_max, 1), "unit": "samples/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt_max / args.steps * 1e3, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "bf16" if args.policy == "mixed_bfloat16" else "fp32",
+            "data": "synthetic (uniform features, random labels), random-init weights",
+            "config": {"model": names[args.model], "global_batch": n, "seq_len": None,
+                       "parallelism": f"dp{world}", "rows_per_gpu": per, "eval_batch": bs,
+                       "engine": "native HIP eval executor" if torch.cuda.is_available() else "torch CPU"},
+        }
+        print(json.dumps(line), flush=True)
+        if args.out:
+            with open(args.out, "a") as f:
+                f.write(json.dumps(line) + "\n")
     if dist.is_initialized():
         dist.barrier()
         import torch.distributed as tdist

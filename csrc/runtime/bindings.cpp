@@ -284,7 +284,7 @@ PYBIND11_MODULE(_C, m) {
 
   // ---- host loader (pinned, double-buffered H2D)
   py::class_<HostLoader>(m, "HostLoader")
-      .def(py::init<long long, int>(), py::arg("chunk_bytes"), py::arg("nbuf") = 2)
+      .def(py::init<long long, int, int>(), py::arg("chunk_bytes"), py::arg("nbuf") = 2, py::arg("threads") = 0)
       .def("upload", [](HostLoader& L, uintptr_t host, uintptr_t dev, long long nbytes, uintptr_t s) {
         py::gil_scoped_release rel;
         L.upload(reinterpret_cast<const void*>(host), reinterpret_cast<void*>(dev), nbytes, S(s));
@@ -295,5 +295,6 @@ PYBIND11_MODULE(_C, m) {
         L.upload_rows(reinterpret_cast<const char*>(host), host_ld, reinterpret_cast<char*>(dev), dev_ld, nrows,
                       row_bytes, S(s));
       })
-      .def_property_readonly("bytes_uploaded", &HostLoader::bytes_uploaded);
+      .def_property_readonly("bytes_uploaded", &HostLoader::bytes_uploaded)
+      .def_property_readonly("threads", &HostLoader::threads);
 }

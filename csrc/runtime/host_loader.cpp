@@ -1,7 +1,9 @@
 #include "host_loader.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
+#include <thread>
 #include <stdexcept>
 #include <string>
 
@@ -11,8 +13,13 @@ static void chk(hipError_t e, const char* w) {
   if (e != hipSuccess) throw std::runtime_error(std::string("HIP error in ") + w + ": " + hipGetErrorString(e));
 }
 
-HostLoader::HostLoader(long long chunk_bytes, int nbuf) : chunk_(chunk_bytes) {
+HostLoader::HostLoader(long long chunk_bytes, int nbuf, int threads) : chunk_(chunk_bytes) {
   if (chunk_bytes <= 0 || nbuf < 1) throw std::invalid_argument("HostLoader: bad sizes");
+  if (threads <= 0) {
+    const char* e = getenv("ELEPHAS_AMD_LOADER_THREADS");
+    threads = e ? atoi(e) : (int)std::min(8u, std::max(1u, std::thread::hardware_concurrency()));
+  }
+  threads_ = std::max(1, threads);
   for (int i = 0; i < nbuf; ++i) {
     void* p = nullptr;
     chk(hipHostMalloc(&p, (size_t)chunk_bytes, hipHostMallocDefault), "hipHostMalloc");
@@ -51,11 +58,34 @@ void HostLoader::upload(const void* host, void* dev, long long nbytes, hipStream
   for (long long off = 0; off < nbytes; off += chunk_) {
     const long long n = std::min(chunk_, nbytes - off);
     char* buf = acquire(s);
-    std::memcpy(buf, h + off, (size_t)n);
+    const long long pg = 4096, full = n / pg * pg;  // split contiguous bytes into 4 KB rows
+    pack(buf, h + off, pg, pg, full / pg);
+    if (n > full) std::memcpy(buf + full, h + off + full, (size_t)(n - full));
     chk(hipMemcpyAsync(d + off, buf, (size_t)n, hipMemcpyHostToDevice, s), "loader H2D");
     release(s);
     bytes_ += n;
   }
+}
+
+void HostLoader::pack(char* buf, const char* host, long long host_ld, long long row_bytes, long long nr) const {
+  auto part = [&](long long r0, long long r1) {
+    if (host_ld == row_bytes) {
+      std::memcpy(buf + r0 * row_bytes, host + r0 * host_ld, (size_t)((r1 - r0) * row_bytes));
+    } else {
+      for (long long r = r0; r < r1; ++r) std::memcpy(buf + r * row_bytes, host + r * host_ld, (size_t)row_bytes);
+    }
+  };
+  // below ~1 MB a thread costs more than it saves
+  const int nt = (int)std::min<long long>(threads_, std::max<long long>(1, nr * row_bytes >> 20));
+  if (nt <= 1) {
+    part(0, nr);
+    return;
+  }
+  std::vector<std::thread> ts;
+  ts.reserve(nt - 1);
+  for (int i = 1; i < nt; ++i) ts.emplace_back(part, nr * i / nt, nr * (i + 1) / nt);
+  part(0, nr / nt);
+  for (auto& t : ts) t.join();
 }
 
 void HostLoader::upload_rows(const char* host, long long host_ld, char* dev, long long dev_ld, long long nrows,
@@ -65,7 +95,7 @@ void HostLoader::upload_rows(const char* host, long long host_ld, char* dev, lon
   for (long long r0 = 0; r0 < nrows; r0 += rows_per_chunk) {
     const long long nr = std::min(rows_per_chunk, nrows - r0);
     char* buf = acquire(s);
-    for (long long r = 0; r < nr; ++r) std::memcpy(buf + r * row_bytes, host + (r0 + r) * host_ld, (size_t)row_bytes);
+    pack(buf, host + r0 * host_ld, host_ld, row_bytes, nr);
     chk(hipMemcpy2DAsync(dev + r0 * dev_ld, (size_t)dev_ld, buf, (size_t)row_bytes, (size_t)row_bytes, (size_t)nr,
                          hipMemcpyHostToDevice, s),
         "loader H2D 2D");

@@ -3,7 +3,9 @@
 // Replaces Spark's parallelize/repartition data shipping (reference
 // utils/rdd_utils.py:10-20, spark_model.py:182-183): a rank's partition
 // (contiguous rows of the host dataset) is streamed into HBM through `nbuf`
-// pinned chunks; the CPU packs chunk i+1 while the DMA engine moves chunk i.
+// pinned chunks; the CPU packs chunk i+1 (several threads: one thread's memcpy
+// into pinned memory runs at ~5 GB/s, below the DMA rate) while the DMA engine
+// moves chunk i.
 // Sized for 288 GB HBM: whole shards stay resident on the device afterwards.
 #pragma once
 #include <hip/hip_runtime.h>
@@ -14,7 +16,8 @@ namespace ea {
 
 class HostLoader {
  public:
-  HostLoader(long long chunk_bytes, int nbuf = 2);
+  // threads: CPU threads packing each chunk (0 = $ELEPHAS_AMD_LOADER_THREADS or min(8, cores))
+  HostLoader(long long chunk_bytes, int nbuf = 2, int threads = 0);
   ~HostLoader();
   // contiguous copy
   void upload(const void* host, void* dev, long long nbytes, hipStream_t s);
@@ -22,9 +25,13 @@ class HostLoader {
   void upload_rows(const char* host, long long host_ld, char* dev, long long dev_ld, long long nrows,
                    long long row_bytes, hipStream_t s);
   long long bytes_uploaded() const { return bytes_; }
+  int threads() const { return threads_; }
 
  private:
   long long chunk_;
+  int threads_ = 1;
+  // rows [0, nr) of `host` (stride host_ld) -> dense rows in `buf`, split over threads_
+  void pack(char* buf, const char* host, long long host_ld, long long row_bytes, long long nr) const;
   std::vector<char*> bufs_;
   std::vector<hipEvent_t> evs_;
   std::vector<bool> busy_;

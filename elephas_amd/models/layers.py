@@ -48,7 +48,22 @@ class KerasTensor:
         return f"<KerasTensor shape={self.shape} from {self.layer.name}>"
 
 
+# Bumped whenever any layer attribute is (re)bound to an ndarray (build, set_weights,
+# load): a model's device trainer re-uploads its weights only when this moved since
+# its last sync (in-place edits of a weight array are not seen; use set_weights).
+_WEIGHT_EPOCH = [0]
+
+
+def weight_epoch() -> int:
+    return _WEIGHT_EPOCH[0]
+
+
 class Layer:
+    def __setattr__(self, name, value):
+        if isinstance(value, np.ndarray):
+            _WEIGHT_EPOCH[0] += 1
+        object.__setattr__(self, name, value)
+
     def __init__(self, name: Optional[str] = None, trainable: bool = True, dtype: str = "float32",
                  input_shape=None, batch_input_shape=None, input_dim=None, **kwargs):
         self.name = name or unique_name(_snake(type(self).__name__))

@@ -189,18 +189,24 @@ class Model:
     def _trainer(self, batch_size: int):
         from ..ops.engine import make_trainer
         key = int(batch_size)
+        from .layers import weight_epoch
         t = self._trainers.get(key)
         if t is None:
             t = make_trainer(self, 1, key)
             self._trainers = {key: t}  # one live trainer: it owns the optimizer state
-        else:
+        elif getattr(t, "_weight_epoch", None) != weight_epoch():
+            # the host weights changed since the trainer last saw them (a repeated
+            # predict / evaluate on unchanged weights skips this upload: 150 MB on Wide)
             from ..ops.plan import flatten_weights
             t.set_weights_flat(flatten_weights(self.get_weights()))
+        t._weight_epoch = weight_epoch()
         return t
 
     def _pull(self, t):
         from ..ops.plan import unflatten_weights
+        from .layers import weight_epoch
         self.set_weights(unflatten_weights(t.get_weights_flat()[0], self.get_weights()))
+        t._weight_epoch = weight_epoch()  # host and device copies agree again
 
     def fit(self, x=None, y=None, batch_size=None, epochs=1, verbose=1, callbacks=None, validation_split=0.0,
             validation_data=None, shuffle=True, initial_epoch=0, **kwargs) -> History:

@@ -100,6 +100,27 @@ def all_gather_object(obj: Any) -> List[Any]:
     return out
 
 
+def all_gather_rows(local, n: int):
+    """Concatenate, in rank order, every rank's ``block_range(n)`` rows (numpy arrays of
+    one trailing shape) with ONE tensor all-gather on the backend's device (RCCL over
+    xGMI on GPUs) instead of pickling arrays through ``all_gather_object``."""
+    import numpy as np
+    local = np.asarray(local, np.float32)
+    if not is_initialized() or world_size() == 1:
+        return local
+    w = world_size()
+    sizes = [hi - lo for lo, hi in (block_range(n, r, w) for r in range(w))]
+    mx = max(max(sizes), 1)
+    dev = _comm_device()
+    buf = torch.zeros((mx,) + local.shape[1:], dtype=torch.float32, device=dev)
+    if len(local):
+        buf[:len(local)].copy_(torch.from_numpy(np.ascontiguousarray(local)))
+    out = torch.empty((w * mx,) + local.shape[1:], dtype=torch.float32, device=dev)
+    dist.all_gather_into_tensor(out, buf)
+    host = out.cpu().numpy()
+    return np.concatenate([host[r * mx:r * mx + sizes[r]] for r in range(w)])
+
+
 def broadcast_object(obj: Any, src: int = 0) -> Any:
     if not is_initialized() or world_size() == 1:
         return obj

@@ -188,8 +188,7 @@ class SparkModel:
         lo, hi = dist.block_range(len(x))
         local = self._master_network.predict(x[lo:hi]) if hi > lo else \
             np.zeros((0,) + tuple(self._master_network.output_shape[1:]), np.float32)
-        parts = dist.all_gather_object(local)
-        out = np.concatenate([p for p in parts if len(p)] or [local])
+        out = dist.all_gather_rows(local, len(x))
         return list(out)
 
     def _evaluate(self, x, y, **kwargs):

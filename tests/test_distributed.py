@@ -99,3 +99,26 @@ def test_async_two_ranks_shared_parameter_server(tmp_path, mode, ps):
             assert np.array_equal(a[k], b[k]), k
     x, y = _data()
     assert np.isfinite(a["ev"]).all()
+
+
+def _gather_rows_worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    import torch.distributed as tdist
+    tdist.init_process_group("gloo", rank=rank, world_size=world)
+    from elephas_amd.parallel import dist
+    n = 11  # uneven blocks: 3 / 4 / 4 rows
+    lo, hi = dist.block_range(n)
+    local = np.arange(lo, hi, dtype=np.float32)[:, None] * np.ones((1, 5), np.float32)
+    out = dist.all_gather_rows(local, n)
+    np.save(os.path.join(out_dir, f"g{rank}.npy"), out)
+    tdist.barrier()
+    tdist.destroy_process_group()
+
+
+def test_all_gather_rows_uneven_blocks(tmp_path):
+    """Distributed predict's row gather (one tensor all-gather, padded blocks)."""
+    port = _free_port()
+    mp.start_processes(_gather_rows_worker, args=(3, port, str(tmp_path)), nprocs=3, join=True, start_method="spawn")
+    want = np.arange(11, dtype=np.float32)[:, None] * np.ones((1, 5), np.float32)
+    for r in range(3):
+        np.testing.assert_array_equal(np.load(tmp_path / f"g{r}.npy"), want)

@@ -503,3 +503,27 @@ def test_overlapped_bucket_allreduce_equals_graph_path():
     assert np.array_equal(ws[0], ws[1])
     assert sorted(set(calls)) == sorted({785 * 128, 129 * 128, 129 * 10}) and len(calls) == 24
     config.set_policy("float32")
+
+
+@pytest.mark.parametrize("threads", [1, 4])
+def test_host_loader_uploads(threads):
+    """Pinned double-buffered loader: contiguous and row-strided uploads (multi-threaded
+    packing of each chunk) reproduce the host data exactly, across chunk boundaries."""
+    from elephas_amd.ops import native
+    C = native.require()
+    L = C.HostLoader(1 << 20, 2, threads)
+    assert L.threads == threads
+    s = torch.cuda.Stream()
+    rng = np.random.default_rng(5)
+    a = rng.random(3_000_001, dtype=np.float32)          # ~12 MB: 12 chunks + a ragged tail
+    d = torch.empty(a.size, dtype=torch.float32, device="cuda")
+    L.upload(a.ctypes.data, d.data_ptr(), a.nbytes, s.cuda_stream)
+    s.synchronize()
+    np.testing.assert_array_equal(d.cpu().numpy(), a)
+    x = rng.random((5000, 781), dtype=np.float32)          # rows padded to 784 on the device
+    dx = torch.zeros(5000, 784, dtype=torch.float32, device="cuda")
+    L.upload_rows(x.ctypes.data, 781 * 4, dx.data_ptr(), 784 * 4, 5000, 781 * 4, s.cuda_stream)
+    s.synchronize()
+    got = dx.cpu().numpy()
+    np.testing.assert_array_equal(got[:, :781], x)
+    assert not got[:, 781:].any()
