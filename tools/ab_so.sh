@@ -3,7 +3,7 @@
 # Two rounds of MNIST (8 x 64), Otto (8 x 128) and Wide (1 x 1024); gpurun_out/ab.log.
 SO=elephas_amd/_C.cpython-310-x86_64-linux-gnu.so
 mkdir -p gpurun_out
-for round in 1 2; do for v in old new; do cp tmp_so/$v.so $SO; for m in mnist otto wide; do
+for round in 1 2; do for v in old new; do cp tmp_so/$v.so $SO; for m in ${AB_MODELS:-mnist otto wide}; do
   extra="--steps 1500 --warmup 150"
   [ $m = otto ] && extra="--batch 128 --steps 1500 --warmup 150"
   [ $m = wide ] && extra="--workers-per-gpu 1 --batch 1024 --steps 100 --warmup 10"
