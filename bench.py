@@ -378,21 +378,19 @@ def bench_async(args, model, dist, rank, world, dev):
         t.set_data(dx, dy, args.validation_split, shuffle=True)
         t.begin_epoch()
         state = {"pos": 0}
+        before = torch.empty(t.P.shape[1], dtype=torch.float32, device=t.P.device)
 
         def run_lockstep(k):
             for _ in range(k):
                 if state["pos"] >= spe:
                     t.begin_epoch()
                     state["pos"] = 0
-                with torch.cuda.stream(t.stream):
-                    client.pull_into(t.P[0].data_ptr(), t.s)
-                    t.P[1:].copy_(t.P[0].expand(W - 1, -1))
+                with torch.cuda.stream(t.stream):   # one kernel: theta -> all W replicas + before
+                    client.pull_replicas(t.P.data_ptr(), t.P.stride(0), W, before.data_ptr(), t.s)
                     t.sync_shadows()
-                    before = t.P[0].clone()
                 t.run_steps(1, use_graph=True)
-                with torch.cuda.stream(t.stream):
-                    delta = before * float(W) - t.P.sum(0)
-                    client.push_from(delta.data_ptr(), t.s)
+                with torch.cuda.stream(t.stream):   # one kernel: theta += sum_w P[w] - W * before
+                    client.push_replicas(t.P.data_ptr(), t.P.stride(0), W, before.data_ptr(), t.s)
                 state["pos"] += 1
             t.stream.synchronize()
 

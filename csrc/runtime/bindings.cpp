@@ -257,6 +257,14 @@ PYBIND11_MODULE(_C, m) {
         py::gil_scoped_release rel;
         ps.push(reinterpret_cast<const float*>(delta), S(s));
       })
+      .def("pull_replicas", [](DeviceParameterServer& ps, uintptr_t P, long long sP, int R, uintptr_t before, uintptr_t s) {
+        py::gil_scoped_release rel;
+        ps.pull_replicas(reinterpret_cast<float*>(P), sP, R, reinterpret_cast<float*>(before), S(s));
+      })
+      .def("push_replicas", [](DeviceParameterServer& ps, uintptr_t P, long long sP, int R, uintptr_t before, uintptr_t s) {
+        py::gil_scoped_release rel;
+        ps.push_replicas(reinterpret_cast<const float*>(P), sP, R, reinterpret_cast<const float*>(before), S(s));
+      })
       .def("set", [](DeviceParameterServer& ps, uintptr_t src, uintptr_t s) {
         py::gil_scoped_release rel;
         ps.set(reinterpret_cast<const float*>(src), S(s));
@@ -278,6 +286,14 @@ PYBIND11_MODULE(_C, m) {
       .def("push", [](RemoteParameterServer& ps, uintptr_t delta, uintptr_t s) {
         py::gil_scoped_release rel;
         ps.push(reinterpret_cast<const float*>(delta), S(s));
+      })
+      .def("pull_replicas", [](RemoteParameterServer& ps, uintptr_t P, long long sP, int R, uintptr_t before, uintptr_t s) {
+        py::gil_scoped_release rel;
+        ps.pull_replicas(reinterpret_cast<float*>(P), sP, R, reinterpret_cast<float*>(before), S(s));
+      })
+      .def("push_replicas", [](RemoteParameterServer& ps, uintptr_t P, long long sP, int R, uintptr_t before, uintptr_t s) {
+        py::gil_scoped_release rel;
+        ps.push_replicas(reinterpret_cast<const float*>(P), sP, R, reinterpret_cast<const float*>(before), S(s));
       });
   m.def("shm_rwlock_create", &shm_rwlock_create);
   m.def("shm_rwlock_destroy", &shm_rwlock_destroy);

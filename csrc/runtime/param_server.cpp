@@ -9,6 +9,10 @@
 #include <stdexcept>
 
 extern "C" hipError_t ea_ps_sub(float* p, const float* d, long long n, float scale, int atomic, hipStream_t s);
+extern "C" hipError_t ea_ps_pull_replicas(const float* src, float* P, long long sP, int R, float* before, long long n,
+                                          hipStream_t s);
+extern "C" hipError_t ea_ps_push_replicas(float* p, const float* P, long long sP, int R, const float* before,
+                                          long long n, int atomic, hipStream_t s);
 
 namespace ea {
 
@@ -46,6 +50,32 @@ void DeviceParameterServer::push(const float* delta, hipStream_t s) {
   try {
     chk(ea_ps_sub(p_, delta, n_, 1.f, 0, s), "ps.push");
     if (locked_) chk(hipStreamSynchronize(s), "ps.push sync");
+  } catch (...) {
+    if (locked_) lock_->unlock();
+    throw;
+  }
+  if (locked_) lock_->unlock();
+  pushes_++;
+}
+
+void DeviceParameterServer::pull_replicas(float* P, long long sP, int R, float* before, hipStream_t s) {
+  if (locked_) lock_->lock_shared();
+  try {
+    chk(ea_ps_pull_replicas(p_, P, sP, R, before, n_, s), "ps.pull_replicas");
+    if (locked_) chk(hipStreamSynchronize(s), "ps.pull_replicas sync");
+  } catch (...) {
+    if (locked_) lock_->unlock_shared();
+    throw;
+  }
+  if (locked_) lock_->unlock_shared();
+  pulls_++;
+}
+
+void DeviceParameterServer::push_replicas(const float* P, long long sP, int R, const float* before, hipStream_t s) {
+  if (locked_) lock_->lock();
+  try {
+    chk(ea_ps_push_replicas(p_, P, sP, R, before, n_, 0, s), "ps.push_replicas");
+    if (locked_) chk(hipStreamSynchronize(s), "ps.push_replicas sync");
   } catch (...) {
     if (locked_) lock_->unlock();
     throw;
@@ -105,6 +135,30 @@ void RemoteParameterServer::push(const float* delta, hipStream_t s) {
   try {
     chk(ea_ps_sub(p_, delta, n_, 1.f, 0, s), "remote.push");
     chk(hipStreamSynchronize(s), "remote.push sync");
+  } catch (...) {
+    if (locked_) lock_->unlock();
+    throw;
+  }
+  if (locked_) lock_->unlock();
+}
+
+void RemoteParameterServer::pull_replicas(float* P, long long sP, int R, float* before, hipStream_t s) {
+  if (locked_) lock_->lock_shared();
+  try {
+    chk(ea_ps_pull_replicas(p_, P, sP, R, before, n_, s), "remote.pull_replicas");
+    chk(hipStreamSynchronize(s), "remote.pull_replicas sync");
+  } catch (...) {
+    if (locked_) lock_->unlock_shared();
+    throw;
+  }
+  if (locked_) lock_->unlock_shared();
+}
+
+void RemoteParameterServer::push_replicas(const float* P, long long sP, int R, const float* before, hipStream_t s) {
+  if (locked_) lock_->lock();
+  try {
+    chk(ea_ps_push_replicas(p_, P, sP, R, before, n_, 0, s), "remote.push_replicas");
+    chk(hipStreamSynchronize(s), "remote.push_replicas sync");
   } catch (...) {
     if (locked_) lock_->unlock();
     throw;

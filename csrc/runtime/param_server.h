@@ -27,6 +27,10 @@ class DeviceParameterServer {
   ~DeviceParameterServer();
   void pull(float* dst, hipStream_t s);
   void push(const float* delta, hipStream_t s);
+  // R lockstep replicas (rows of P, stride sP): pull into all of them + `before`;
+  // push theta += sum_r P[r] - R * before
+  void pull_replicas(float* P, long long sP, int R, float* before, hipStream_t s);
+  void push_replicas(const float* P, long long sP, int R, const float* before, hipStream_t s);
   void set(const float* src, hipStream_t s);
   std::string ipc_handle() const;
   float* data() const { return p_; }
@@ -49,6 +53,8 @@ class RemoteParameterServer {
   ~RemoteParameterServer();
   void pull(float* dst, hipStream_t s);
   void push(const float* delta, hipStream_t s);
+  void pull_replicas(float* P, long long sP, int R, float* before, hipStream_t s);
+  void push_replicas(const float* P, long long sP, int R, const float* before, hipStream_t s);
 
  private:
   long long n_;

@@ -114,6 +114,15 @@ class DeviceClient(BaseParameterClient):
     def push_from(self, delta_ptr: int, stream: int) -> None:
         self._ps().push(delta_ptr, stream)
 
+    # R lockstep replicas (rows of a [R, n] fp32 buffer, row stride sP elements)
+    def pull_replicas(self, P_ptr: int, sP: int, R: int, before_ptr: int, stream: int) -> None:
+        """P[r] = theta for every replica and before = theta (one kernel)."""
+        self._ps().pull_replicas(P_ptr, sP, R, before_ptr, stream)
+
+    def push_replicas(self, P_ptr: int, sP: int, R: int, before_ptr: int, stream: int) -> None:
+        """theta -= sum_r (before - P[r]) (one kernel)."""
+        self._ps().push_replicas(P_ptr, sP, R, before_ptr, stream)
+
     # list-of-arrays API (reference compatibility)
     def get_parameters(self):
         if self.server is not None:

@@ -282,6 +282,13 @@ class BatchedAsynchronousWorker:
         from .parallel import dist, fault
         fault.maybe_inject("pull", dist.rank())
         with torch.cuda.stream(t.stream):
+            if hasattr(self.client, "pull_replicas"):
+                before = getattr(self, "_before", None)
+                if before is None or before.numel() != t.P.shape[1] or before.device != t.P.device:
+                    before = self._before = torch.empty(t.P.shape[1], dtype=torch.float32, device=t.P.device)
+                self.client.pull_replicas(t.P.data_ptr(), t.P.stride(0), t.R, before.data_ptr(), t.s)
+                t.sync_shadows()
+                return before
             self.client.pull_into(t.P[0].data_ptr(), t.s)
             if t.R > 1:
                 t.P[1:].copy_(t.P[0].expand(t.R - 1, -1))
@@ -293,5 +300,8 @@ class BatchedAsynchronousWorker:
         from .parallel import dist, fault
         fault.maybe_inject("push", dist.rank())
         with torch.cuda.stream(t.stream):
+            if hasattr(self.client, "push_replicas"):
+                self.client.push_replicas(t.P.data_ptr(), t.P.stride(0), t.R, before.data_ptr(), t.s)
+                return
             delta = before * float(t.R) - t.P.sum(0)     # sum_r (theta_pulled - theta_r)
             self.client.push_from(delta.data_ptr(), t.s)

@@ -527,3 +527,32 @@ def test_host_loader_uploads(threads):
     got = dx.cpu().numpy()
     np.testing.assert_array_equal(got[:, :781], x)
     assert not got[:, 781:].any()
+
+
+@pytest.mark.parametrize("locked", [0, 1])
+def test_ps_replica_pull_push(locked):
+    """Fused lockstep-replica exchange with the HBM parameter server:
+    pull_replicas writes theta into every replica row and `before`; push_replicas
+    applies theta += sum_r P[r] - R * before (fp32 reference)."""
+    from elephas_amd.ops import native
+    C = native.require()
+    n, R = 118_282, 8
+    ps = C.DeviceParameterServer(n, locked, 0, "")
+    rng = np.random.default_rng(9)
+    theta = torch.from_numpy(rng.normal(size=n).astype(np.float32)).cuda()
+    s = torch.cuda.Stream()
+    ps.set(theta.data_ptr(), s.cuda_stream)
+    P = torch.zeros(R, n + 6, dtype=torch.float32, device="cuda")[:, :n]   # padded row stride
+    before = torch.empty(n, dtype=torch.float32, device="cuda")
+    ps.pull_replicas(P.data_ptr(), P.stride(0), R, before.data_ptr(), s.cuda_stream)
+    s.synchronize()
+    assert torch.equal(before, theta)
+    assert torch.equal(P, theta.expand(R, n))
+    P.add_(torch.from_numpy(rng.normal(size=(R, n)).astype(np.float32)).cuda() * 1e-2)
+    want = (theta.double() + P.double().sum(0) - R * before.double()).float()
+    ps.push_replicas(P.data_ptr(), P.stride(0), R, before.data_ptr(), s.cuda_stream)
+    s.synchronize()
+    got = torch.empty(n, dtype=torch.float32, device="cuda")
+    ps.pull(got.data_ptr(), s.cuda_stream)
+    s.synchronize()
+    torch.testing.assert_close(got, want, rtol=0, atol=1e-5)
