@@ -385,9 +385,8 @@ def bench_async(args, model, dist, rank, world, dev):
                 if state["pos"] >= spe:
                     t.begin_epoch()
                     state["pos"] = 0
-                with torch.cuda.stream(t.stream):   # one kernel: theta -> all W replicas + before
-                    client.pull_replicas(t.P.data_ptr(), t.P.stride(0), W, before.data_ptr(), t.s)
-                    t.sync_shadows()
+                with torch.cuda.stream(t.stream):   # one kernel: theta -> all W replicas' P + images, before
+                    client.pull_refresh(t, before.data_ptr())
                 t.run_steps(1, use_graph=True)
                 with torch.cuda.stream(t.stream):   # one kernel: theta += sum_w P[w] - W * before
                     client.push_replicas(t.P.data_ptr(), t.P.stride(0), W, before.data_ptr(), t.s)

@@ -127,6 +127,9 @@ struct FlatArgs {
   long long* ctr;
   const int* ntrain; int B;
   int both_parities;  // refresh: write both shadow parities
+  // refresh from an external vector (parameter-server pull): every replica's P and
+  // shadows are rebuilt from src; replica 0 also copies src into src_copy
+  const float* src; float* src_copy;
   int total_blocks;
 };
 

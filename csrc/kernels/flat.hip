@@ -143,7 +143,13 @@ __global__ __launch_bounds__(256) void shadow_tiles_kernel(FlatArgs a, int tiles
     float w = 0.f;
     if (k < g.K && n < g.N) {
       const long long pi = g.p_off + (long long)k * g.N + n;
-      w = P[pi];
+      if (!UPDATE && a.src) {
+        w = a.src[pi];
+        P[pi] = w;
+        if (r == 0 && a.src_copy) a.src_copy[pi] = w;
+      } else {
+        w = P[pi];
+      }
       if (UPDATE) {
         w = opt_update(a.op, w, a.G[(long long)r * a.sG + pi] * a.op.grad_scale, S, pi, iter);
         P[pi] = w;
@@ -157,7 +163,14 @@ __global__ __launch_bounds__(256) void shadow_tiles_kernel(FlatArgs a, int tiles
   }
   if (k0 == 0 && g.has_bias && tid < 64 && n0 + tid < g.N) {
     const long long pi = g.p_off + (long long)g.K * g.N + n0 + tid;
-    float w = P[pi];
+    float w;
+    if (!UPDATE && a.src) {
+      w = a.src[pi];
+      P[pi] = w;
+      if (r == 0 && a.src_copy) a.src_copy[pi] = w;
+    } else {
+      w = P[pi];
+    }
     if (UPDATE) {
       w = opt_update(a.op, w, a.G[(long long)r * a.sG + pi] * a.op.grad_scale, S, pi, iter);
       P[pi] = w;

@@ -295,6 +295,18 @@ PYBIND11_MODULE(_C, m) {
         py::gil_scoped_release rel;
         ps.push_replicas(reinterpret_cast<const float*>(P), sP, R, reinterpret_cast<const float*>(before), S(s));
       });
+  // parameter-server pull fused with the executor's shadow refresh: one kernel reads
+  // theta and writes every replica's P, both W / W^T parities and `before`
+  m.def("ps_pull_refresh", [](DeviceParameterServer& ps, Executor& exe, uintptr_t before, uintptr_t s) {
+    if (exe.covered_params() != ps.size()) throw std::invalid_argument("ps_pull_refresh: parameter count mismatch");
+    py::gil_scoped_release rel;
+    ps.pull_with(S(s), [&](float* theta) { exe.refresh_from(theta, reinterpret_cast<float*>(before), S(s)); });
+  });
+  m.def("ps_pull_refresh", [](RemoteParameterServer& ps, Executor& exe, uintptr_t before, uintptr_t s) {
+    if (exe.covered_params() != ps.size()) throw std::invalid_argument("ps_pull_refresh: parameter count mismatch");
+    py::gil_scoped_release rel;
+    ps.pull_with(S(s), [&](float* theta) { exe.refresh_from(theta, reinterpret_cast<float*>(before), S(s)); });
+  });
   m.def("shm_rwlock_create", &shm_rwlock_create);
   m.def("shm_rwlock_destroy", &shm_rwlock_destroy);
 

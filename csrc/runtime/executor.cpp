@@ -602,6 +602,21 @@ void Executor::refresh_shadows(bool both, hipStream_t s) {
   check(ea_refresh_shadows(&a, c_.bf16, s), "refresh_shadows");
 }
 
+void Executor::refresh_from(const float* src, float* copy, hipStream_t s) {
+  FlatArgs a = flat_args();
+  a.both_parities = 1;
+  a.src = src;
+  a.src_copy = copy;
+  check(ea_refresh_shadows(&a, c_.bf16, s), "refresh_from");
+}
+
+long long Executor::covered_params() const {
+  FlatArgs a = flat_args();
+  long long t = 0;
+  for (int q = 0; q < a.nseg; ++q) t += (long long)a.seg[q].K * a.seg[q].N + (a.seg[q].has_bias ? a.seg[q].N : 0);
+  return t;
+}
+
 void Executor::reset_epoch(hipStream_t s) {
   check(hipMemsetAsync(reinterpret_cast<void*>(c_.ctr), 0, 2 * sizeof(long long), s), "reset_epoch");
 }

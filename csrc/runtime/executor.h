@@ -84,6 +84,10 @@ class Executor {
   void apply(hipStream_t s);               // gradient path: optimizer apply + advance
   void eval_chunk(long long chunk, const EvalSource& src, hipStream_t s);
   void refresh_shadows(bool both, hipStream_t s);
+  // P[r] and both shadow parities of every replica rebuilt from src (a parameter-server
+  // pull fused with the refresh); replica 0 also writes src into copy (may be null)
+  void refresh_from(const float* src, float* copy, hipStream_t s);
+  long long covered_params() const;  // parameters the shadow segments cover
   void reset_epoch(hipStream_t s);
 
   // hipGraph capture / replay of `nsteps` training steps (mode 0: train_step,

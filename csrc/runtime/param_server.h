@@ -17,9 +17,28 @@
 #include <atomic>
 #include <memory>
 #include <shared_mutex>
+#include <stdexcept>
 #include <string>
 
 namespace ea {
+
+// Run `enqueue(theta)` (device work reading the server's vector on stream s) under
+// the read lock; with `sync` the stream is drained before the lock is released.
+template <class Lock, class F>
+inline void locked_read(Lock* lock, bool locked, bool sync, float* theta, hipStream_t s, F&& enqueue) {
+  if (locked) lock->lock_shared();
+  try {
+    enqueue(theta);
+    if (sync) {
+      const hipError_t e = hipStreamSynchronize(s);
+      if (e != hipSuccess) throw std::runtime_error(std::string("HIP error in ps read sync: ") + hipGetErrorString(e));
+    }
+  } catch (...) {
+    if (locked) lock->unlock_shared();
+    throw;
+  }
+  if (locked) lock->unlock_shared();
+}
 
 class DeviceParameterServer {
  public:
@@ -32,6 +51,11 @@ class DeviceParameterServer {
   void pull_replicas(float* P, long long sP, int R, float* before, hipStream_t s);
   void push_replicas(const float* P, long long sP, int R, const float* before, hipStream_t s);
   void set(const float* src, hipStream_t s);
+  // pull fused into a caller's kernel (e.g. Executor::refresh_from)
+  template <class F> void pull_with(hipStream_t s, F&& enqueue) {
+    locked_read(lock_.get(), locked_ != 0, locked_ != 0, p_, s, enqueue);
+    pulls_++;
+  }
   std::string ipc_handle() const;
   float* data() const { return p_; }
   long long size() const { return n_; }
@@ -55,6 +79,10 @@ class RemoteParameterServer {
   void push(const float* delta, hipStream_t s);
   void pull_replicas(float* P, long long sP, int R, float* before, hipStream_t s);
   void push_replicas(const float* P, long long sP, int R, const float* before, hipStream_t s);
+  template <class F> void pull_with(hipStream_t s, F&& enqueue) {
+    locked_read(lock_.get(), locked_ != 0, true, p_, s, enqueue);
+  }
+  long long size() const { return n_; }
 
  private:
   long long n_;

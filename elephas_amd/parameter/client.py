@@ -119,6 +119,12 @@ class DeviceClient(BaseParameterClient):
         """P[r] = theta for every replica and before = theta (one kernel)."""
         self._ps().pull_replicas(P_ptr, sP, R, before_ptr, stream)
 
+    def pull_refresh(self, trainer, before_ptr: int) -> None:
+        """Pull fused with the trainer's weight-image refresh: ONE kernel reads theta and
+        writes every replica's fp32 master, both bf16 W / W^T parities and `before`."""
+        from ..ops import native
+        native.require().ps_pull_refresh(self._ps(), trainer.exe, before_ptr, trainer.s)
+
     def push_replicas(self, P_ptr: int, sP: int, R: int, before_ptr: int, stream: int) -> None:
         """theta -= sum_r (before - P[r]) (one kernel)."""
         self._ps().push_replicas(P_ptr, sP, R, before_ptr, stream)

@@ -282,12 +282,11 @@ class BatchedAsynchronousWorker:
         from .parallel import dist, fault
         fault.maybe_inject("pull", dist.rank())
         with torch.cuda.stream(t.stream):
-            if hasattr(self.client, "pull_replicas"):
+            if hasattr(self.client, "pull_refresh"):
                 before = getattr(self, "_before", None)
                 if before is None or before.numel() != t.P.shape[1] or before.device != t.P.device:
                     before = self._before = torch.empty(t.P.shape[1], dtype=torch.float32, device=t.P.device)
-                self.client.pull_replicas(t.P.data_ptr(), t.P.stride(0), t.R, before.data_ptr(), t.s)
-                t.sync_shadows()
+                self.client.pull_refresh(t, before.data_ptr())
                 return before
             self.client.pull_into(t.P[0].data_ptr(), t.s)
             if t.R > 1:

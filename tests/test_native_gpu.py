@@ -556,3 +556,44 @@ def test_ps_replica_pull_push(locked):
     ps.pull(got.data_ptr(), s.cuda_stream)
     s.synchronize()
     torch.testing.assert_close(got, want, rtol=0, atol=1e-5)
+
+
+def test_ps_pull_refresh_matches_two_step_pull():
+    """The fused pull (theta -> every replica's master + both weight-image parities +
+    `before`, one kernel) leaves the executor in the same state as pull + refresh:
+    the next training steps give bit-identical weights."""
+    from elephas_amd.ops import native
+    from elephas_amd.ops.plan import build_plan
+    from elephas_amd.ops.native_engine import NativeTrainer
+    from elephas_amd.models import optimizers as O
+    from elephas_amd import config
+    C = native.require()
+    config.set_policy("mixed_bfloat16")
+    model = _mlp(784, [128, 128], 10, dropout=0.2)
+    model.compile(O.SGD(0.1), "categorical_crossentropy", ["acc"])
+    R = 4
+    x, y = _data(512, 784, 10)
+    ts = [NativeTrainer(model, build_plan(model), R, 64, torch.device("cuda"), seed=77) for _ in range(2)]
+    n = ts[0].P.shape[1]
+    ps = C.DeviceParameterServer(n, 1, 0, "")
+    theta = torch.from_numpy(np.random.default_rng(3).normal(size=n).astype(np.float32) * 0.05).cuda()
+    s = torch.cuda.Stream()
+    ps.set(theta.data_ptr(), s.cuda_stream)
+    befores = []
+    for i, t in enumerate(ts):
+        t.set_data([x] * R, [y] * R, 0.0, shuffle=False)
+        t.begin_epoch()
+        before = torch.empty(n, dtype=torch.float32, device="cuda")
+        with torch.cuda.stream(t.stream):
+            if i == 0:
+                C.ps_pull_refresh(ps, t.exe, before.data_ptr(), t.s)
+            else:
+                ps.pull_replicas(t.P.data_ptr(), t.P.stride(0), R, before.data_ptr(), t.s)
+                t.sync_shadows()
+        t.stream.synchronize()
+        befores.append(before)
+        t.run_steps(2, use_graph=False)
+    assert torch.equal(befores[0], theta) and torch.equal(befores[1], theta)
+    w0, w1 = ts[0].get_weights_flat(), ts[1].get_weights_flat()
+    assert np.abs(w0 - theta.cpu().numpy()).max() > 0
+    np.testing.assert_array_equal(w0, w1)
