@@ -19,7 +19,14 @@ Semantics (``--granularity``):
 A "step" = one optimizer step on one batch of 64 rows by every worker; epoch
 rollover (reshuffle) happens inside the timed region as it does in fit().
 
-Usage: python bench.py --gpus N --steps K --warmup W   (N>1 via torch.distributed.run)
+Precision: fp32 by default (the reference trains with Keras's default float32); bf16
+MFMA operands with fp32 master weights under --policy mixed_bfloat16.
+Scaling (``--scaling``): weak (default) = 8 workers on every GPU; strong = the reference
+job (8 partitions in total) split over the GPUs.
+
+Usage: python bench.py --gpus N --steps K --warmup W
+  (N>1: launched by torch.distributed.run, or -- without WORLD_SIZE in the environment --
+  bench.py starts the N ranks itself as a child torchrun job before touching the GPU)
 Prints ONE JSON line on rank 0.
 """
 from __future__ import annotations
@@ -64,15 +71,36 @@ def build_model(name):
     return m
 
 
+def _spawn_ranks(argv, n):
+    """--gpus N without a launcher: start N ranks (one process per GPU) as a child
+    torchrun job and exit with its status. Runs before anything touches the GPU."""
+    import socket
+    import subprocess
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+    return subprocess.call(cmd, env=env)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=500)
     ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--model", default="mnist", choices=sorted(MODELS))
+    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
+                    help="weak: --workers-per-gpu workers on every GPU (each GPU is one local[8] node); "
+                         "strong: the reference job itself -- 8 partitions in total (examples/"
+                         "mnist_mlp_spark_synchronous.py local[8]), 8/N workers per GPU")
     ap.add_argument("--workers-per-gpu", type=int, default=8)
     ap.add_argument("--batch", type=int, default=64)
-    ap.add_argument("--policy", default="mixed_bfloat16", choices=["mixed_bfloat16", "float32"])
+    ap.add_argument("--policy", default="float32", choices=["mixed_bfloat16", "float32"],
+                    help="float32 = the reference's Keras precision (default); mixed_bfloat16 = bf16 MFMA "
+                         "operands with fp32 master weights")
     ap.add_argument("--granularity", default="fit", choices=["fit", "batch"])
     ap.add_argument("--validation-split", type=float, default=0.1)
     ap.add_argument("--no-graph", action="store_true")
@@ -92,6 +120,9 @@ def main():
     ap.add_argument("--infer-rows", type=int, default=None, help="rows per GPU for --task predict/evaluate")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(_spawn_ranks(sys.argv[1:], args.gpus))
+
     import torch
     from elephas_amd import config
     from elephas_amd.parallel import dist
@@ -99,8 +130,8 @@ def main():
 
     dist.init_from_env()
     rank, world = dist.rank(), dist.world_size()
-    if world != args.gpus and rank == 0:
-        print(f"warning: --gpus {args.gpus} but world size {world}", file=sys.stderr)
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the job has {world} rank(s)")
     gpu = torch.cuda.is_available()
     dev = torch.device("cuda", torch.cuda.current_device()) if gpu else torch.device("cpu")
     config.set_device(dev)
@@ -117,7 +148,12 @@ def main():
         return bench_async(args, model, dist, rank, world, dev)
     plan = build_plan(model)
     dims, drop, classes, rows, _ = MODELS[args.model]
-    W = args.workers_per_gpu
+    if args.scaling == "strong":
+        if 8 % world:
+            raise SystemExit("bench.py --scaling strong: the 8 reference partitions must split evenly over the GPUs")
+        W = 8 // world
+    else:
+        W = args.workers_per_gpu
     B = args.batch
     batch_mode = args.granularity == "batch"
     R = 1 if batch_mode else W
@@ -151,16 +187,21 @@ def main():
     if batch_mode and gpu and (world > 1 or args.overlap):
         t.set_grad_scale(1.0 / world)   # mean of the ranks' gradients after the sum all-reduce
 
-    state = {"step_in_epoch": steps_per_epoch, "rows": 0}
+    state = {"step_in_epoch": steps_per_epoch, "epochs": 0, "val_passes": 0}
 
     def run(k):
-        """k optimizer steps with epoch rollover; returns rows processed per worker."""
+        """k optimizer steps with epoch rollover (the epoch-end validation pass of the
+        reference's Keras fit runs at every epoch boundary); returns rows per worker."""
         done_rows = 0
         while k > 0:
             if state["step_in_epoch"] >= steps_per_epoch:
+                if state["epochs"] > 0 and args.validation_split > 0 and gpu:
+                    t._val_sums()
+                    state["val_passes"] += 1
                 if gpu:
                     t.begin_epoch()
                 state["step_in_epoch"] = 0
+                state["epochs"] += 1
             n = min(k, steps_per_epoch - state["step_in_epoch"])
             if gpu:
                 if batch_mode and args.overlap:
@@ -179,15 +220,12 @@ def main():
         return done_rows
 
     def average():
-        """Reference sync mode: theta <- mean_i theta_i over all workers of the job."""
+        """Reference sync mode: theta <- mean_i theta_i over all workers of the job
+        (device replica mean -> RCCL all-reduce -> write-back into every replica)."""
         if batch_mode:
             return
         if gpu:
-            with torch.cuda.stream(t.stream):
-                tot = t.P.sum(0)
-                dist.all_reduce_sum_(tot)
-                t.P.copy_((tot / float(R * world)).expand_as(t.P))
-                t.sync_shadows()
+            t.average_replicas(dist.all_reduce_sum_, world)
         else:
             w = t.get_weights_flat().sum(0)
             tt = torch.from_numpy(w)
@@ -229,23 +267,27 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(dt_max / args.steps * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": "bf16" if args.policy == "mixed_bfloat16" else "fp32",
             "data": "synthetic MNIST-shaped (784 features, 10 classes), random-init weights",
             "config": {
-                "model": {"mnist": "MNIST-MLP 784-128-128-10", "otto": "Otto-MLP 93-512-512-512-9",
-                          "wide": "Wide-MLP 4096-4096-4096-1000"}[args.model],
+                "model": names[args.model],
                 "global_batch": B * W * world,
                 "seq_len": None,
                 "parallelism": f"dp{world}",
+                "ranks": world,
+                "backend": dist.backend(),
                 "workers_per_gpu": W,
+                "workers_total": W * world,
                 "batch_per_worker": B,
+                "rows_per_worker": rows,
                 "sync": "reference (one-shot averaging per fit)" if not batch_mode else "per-step gradient all-reduce",
                 "optimizer": "SGD(lr=%g)" % MODELS[args.model][4],
                 "engine": "native HIP executor + hipGraph" if gpu else "torch CPU reference",
                 "launches_per_step": launches,
                 "policy": args.policy,
+                "validation_passes_timed": state["val_passes"],
             },
         }
         s = json.dumps(line)

@@ -322,8 +322,12 @@ __global__ __launch_bounds__(256) void ps_push_replicas_kernel(float* p, const f
                                                                const float* __restrict__ before, long long n,
                                                                int atomic) {
   for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
-    float d = -(float)R * before[i];
-    for (int r = 0; r < R; ++r) d += P[(long long)r * sP + i];
+    // sum of per-replica differences: each P[r] - before is (nearly) exact because
+    // the two are close (Sterbenz); -R*before + sum P[r] would round every add at
+    // ulp(R*|w|) and lose the small deltas
+    const float b = before[i];
+    float d = 0.f;
+    for (int r = 0; r < R; ++r) d += P[(long long)r * sP + i] - b;
     if (atomic) atomicAdd(p + i, d);
     else p[i] += d;
   }

@@ -165,6 +165,9 @@ PYBIND11_MODULE(_C, m) {
       })
       .def("refresh_shadows", [](Executor& e, bool both, uintptr_t s) { e.refresh_shadows(both, S(s)); })
       .def("reset_epoch", [](Executor& e, uintptr_t s) { e.reset_epoch(S(s)); })
+      .def("refresh_from", [](Executor& e, uintptr_t src, uintptr_t copy, uintptr_t s) {
+        e.refresh_from(reinterpret_cast<const float*>(src), reinterpret_cast<float*>(copy), S(s));
+      })
       .def("capture", [](Executor& e, int n, int mode, uintptr_t s) { return e.capture(n, mode, S(s)); })
       .def("replay", [](Executor& e, int id, uintptr_t s) {
         py::gil_scoped_release rel;
@@ -324,5 +327,6 @@ PYBIND11_MODULE(_C, m) {
                       row_bytes, S(s));
       })
       .def_property_readonly("bytes_uploaded", &HostLoader::bytes_uploaded)
-      .def_property_readonly("threads", &HostLoader::threads);
+      .def_property_readonly("threads", &HostLoader::threads)
+      .def_property_readonly("last_pack_threads", &HostLoader::last_pack_threads);
 }

@@ -75,8 +75,10 @@ void HostLoader::pack(char* buf, const char* host, long long host_ld, long long 
       for (long long r = r0; r < r1; ++r) std::memcpy(buf + r * row_bytes, host + r * host_ld, (size_t)row_bytes);
     }
   };
-  // below ~1 MB a thread costs more than it saves
-  const int nt = (int)std::min<long long>(threads_, std::max<long long>(1, nr * row_bytes >> 20));
+  // one thread per 256 KB of the chunk (a 1 MB chunk uses up to 4): below that a
+  // thread costs more to start than its share of the copy
+  const int nt = (int)std::min<long long>(threads_, std::max<long long>(1, (nr * row_bytes) >> 18));
+  last_nt_ = nt;
   if (nt <= 1) {
     part(0, nr);
     return;

@@ -26,10 +26,13 @@ class HostLoader {
                    long long row_bytes, hipStream_t s);
   long long bytes_uploaded() const { return bytes_; }
   int threads() const { return threads_; }
+  // threads the most recent chunk was packed with (diagnostics / tests)
+  int last_pack_threads() const { return last_nt_; }
 
  private:
   long long chunk_;
   int threads_ = 1;
+  mutable int last_nt_ = 0;
   // rows [0, nr) of `host` (stride host_ld) -> dense rows in `buf`, split over threads_
   void pack(char* buf, const char* host, long long host_ld, long long row_bytes, long long nr) const;
   std::vector<char*> bufs_;

@@ -223,6 +223,21 @@ class NativeTrainer(TrainerBase):
     def get_weights_flat(self):
         return self._host(self.P)
 
+    def average_replicas(self, allreduce=None, world: int = 1):
+        """Reference synchronous averaging (spark_model.py:221-227) on the device: the mean
+        of the R replicas (one kernel, fp64 accumulation), optionally summed over ranks by
+        ``allreduce`` and divided by ``world``, then written back into every replica's
+        master and both weight-image parities (one kernel)."""
+        with torch.cuda.stream(self.stream):
+            avg = getattr(self, "_avg_buf", None)
+            if avg is None or avg.numel() != self.n:
+                avg = self._avg_buf = torch.empty(self.n, dtype=torch.float32, device=self.dev)
+            self.C.replica_average(self.P.data_ptr(), self.P.stride(0), self.R, self.n, avg.data_ptr(), 0, self.s)
+            if allreduce is not None and world > 1:
+                allreduce(avg)
+                avg.mul_(1.0 / world)
+            self.exe.refresh_from(avg.data_ptr(), 0, self.s)
+
     def reset_optimizer_state(self):
         with torch.cuda.stream(self.stream):
             self.S.fill_(float(self.opt_hp.get("state_init", 0.0)))

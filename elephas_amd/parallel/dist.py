@@ -137,6 +137,17 @@ def barrier() -> None:
             dist.barrier()
 
 
+def any_failed(failed: bool) -> bool:
+    """Collective failure vote (replaces a barrier at the end of a phase): every rank
+    contributes whether it failed; all ranks learn whether ANY did, so the healthy
+    ones raise too instead of waiting in the next collective until it times out."""
+    if not is_initialized() or world_size() == 1:
+        return bool(failed)
+    t = torch.tensor([1.0 if failed else 0.0], dtype=torch.float32, device=_comm_device())
+    dist.all_reduce(t)
+    return bool(t.item() > 0)
+
+
 def block_range(n: int, r: int = None, w: int = None):
     """Contiguous block [lo, hi) of n items owned by rank r of w."""
     r = rank() if r is None else r

@@ -429,36 +429,41 @@ class SparkModel:
                 errors.append(e)
 
         print(">>> Distribute load")
-        if self._ps_type == "device" and self._native_ok() and local:
-            # MI355X path: the rank's partitions as replicas of one native executor
-            # exchanging with the HBM parameter server in lockstep (worker.py)
-            try:
-                BatchedAsynchronousWorker(model_json, init, client, train_config, self.frequency,
-                                          self.master_optimizer, self.master_loss, self.master_metrics,
-                                          self.custom_objects).train_partitions(local)
-            except BaseException as e:  # noqa: BLE001 - fail fast, after the server is stopped below
-                errors.append(e)
-            local = []
-        threads = [threading.Thread(target=run, args=(p,)) for p in local]
-        for t in threads:
-            t.start()
-        for t in threads:
-            t.join()
-        if errors:
-            raise errors[0]
-        dist.barrier()
-        print(">>> Async training complete.")
-        if dist.rank() == 0:
-            new_parameters = ps.get_weights()
-            flat = flatten_weights(new_parameters)
-        else:
-            flat = np.zeros(len(flatten_weights(init)), np.float32)
-        t = torch.from_numpy(flat.copy())
-        if dist.backend() == "nccl":
-            t = t.cuda()
-        dist.broadcast_(t, 0)
-        if dist.rank() == 0:
-            self.stop_server()
+        try:
+            if self._ps_type == "device" and self._native_ok() and local:
+                # MI355X path: the rank's partitions as replicas of one native executor
+                # exchanging with the HBM parameter server in lockstep (worker.py)
+                try:
+                    BatchedAsynchronousWorker(model_json, init, client, train_config, self.frequency,
+                                              self.master_optimizer, self.master_loss, self.master_metrics,
+                                              self.custom_objects).train_partitions(local)
+                except BaseException as e:  # noqa: BLE001 - voted on below, then raised
+                    errors.append(e)
+                local = []
+            threads = [threading.Thread(target=run, args=(p,)) for p in local]
+            for t in threads:
+                t.start()
+            for t in threads:
+                t.join()
+            # failure vote instead of a barrier: a healthy rank learns that a peer failed
+            # and raises now rather than blocking in the next collective until it times out
+            if dist.any_failed(bool(errors)):
+                if errors:
+                    raise errors[0]
+                raise RuntimeError("asynchronous training failed on another rank")
+            print(">>> Async training complete.")
+            if dist.rank() == 0:
+                new_parameters = ps.get_weights()
+                flat = flatten_weights(new_parameters)
+            else:
+                flat = np.zeros(len(flatten_weights(init)), np.float32)
+            t = torch.from_numpy(flat.copy())
+            if dist.backend() == "nccl":
+                t = t.cuda()
+            dist.broadcast_(t, 0)
+        finally:
+            if dist.rank() == 0:
+                self.stop_server()   # always, also when a worker failed
         return unflatten_weights(t.cpu().numpy(), init)
 
 

@@ -302,5 +302,7 @@ class BatchedAsynchronousWorker:
             if hasattr(self.client, "push_replicas"):
                 self.client.push_replicas(t.P.data_ptr(), t.P.stride(0), t.R, before.data_ptr(), t.s)
                 return
-            delta = before * float(t.R) - t.P.sum(0)     # sum_r (theta_pulled - theta_r)
+            # sum_r (theta_pulled - theta_r), each difference formed before summing (exact
+            # for close values; R*before - sum P rounds at ulp(R*|w|) and loses the deltas)
+            delta = (before.unsqueeze(0) - t.P).sum(0)
             self.client.push_from(delta.data_ptr(), t.s)

@@ -5,6 +5,7 @@ CPU torch engine with synthetic MNIST/Boston-shaped data.
 Asserted like the reference: consistency, not accuracy -- predict(numpy) ==
 predict(RDD) == master_network.predict (argmax), distributed evaluate ==
 local evaluate within abs 0.01."""
+import os
 from itertools import count
 from math import isclose
 
@@ -16,7 +17,7 @@ from elephas_amd.models.optimizers import SGD, RMSprop
 from elephas_amd.spark_model import SparkMLlibModel, SparkModel, load_spark_model
 from elephas_amd.utils.rdd_utils import to_labeled_point, to_simple_rdd
 
-_port = count(5200)
+_port = count(5200 + 97 * int(os.environ.get("PYTEST_XDIST_WORKER", "gw0")[2:] or 0))
 
 MATRIX = [("synchronous", None, None), ("synchronous", None, 2),
           ("asynchronous", "http", None), ("asynchronous", "http", 2),

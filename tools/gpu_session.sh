@@ -16,16 +16,16 @@ step() {  # name timeout cmd...
 }
 MODE=${1:-all}
 if [ "$MODE" = all ] || [ "$MODE" = tests ]; then
-  step gpu_tests 600 python -m pytest tests -q -m gpu -x; rc=$?
+  step gpu_tests 900 python -u -m pytest tests -v -m gpu -x --timeout 120 --timeout-method thread; rc=$?
   [ $rc -gt 1 ] && exit $rc
   step smoke 180 python -c "import __graft_entry__ as g; g.smoke()" || exit $?
 fi
 if [ "$MODE" = all ] || [ "$MODE" = bench ]; then
+  step bench_driver 300 python bench.py --gpus 1 --steps 20 --warmup 5 || exit $?
   step bench_default 300 python bench.py --steps 2000 --warmup 200 || exit $?
   step bench_w1 300 python bench.py --steps 2000 --warmup 200 --workers-per-gpu 1 || exit $?
   step bench_batch 300 python bench.py --steps 1000 --warmup 100 --granularity batch || exit $?
-  step bench_f32 300 python bench.py --steps 1000 --warmup 100 --policy float32 || exit $?
-  step bench_nograph 300 python bench.py --steps 500 --warmup 50 --no-graph || exit $?
+  step bench_bf16 300 python bench.py --steps 1000 --warmup 100 --policy mixed_bfloat16 || exit $?
 fi
 if [ "$MODE" = all ] || [ "$MODE" = prof ]; then
   ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
