@@ -40,7 +40,8 @@ enum ProbKind : int {
   PK_DW_UPDATE = 4,  // dW -> fused optimizer update of master params + bf16/f32 shadows
   PK_DW_GRAD = 5,    // dW -> flat gradient buffer (all-reduce path)
   PK_GATHER_T = 6,   // X^T batch (gathered through perm) for DW of layer 1
-  PK_LOSS_ROWS = 7   // wide final layer: one wave per row over fp32 logits Z
+  PK_LOSS_ROWS = 7,  // wide final layer: one wave per row over fp32 logits Z
+  PK_PARTIAL = 8     // split-K slab: fp32 C over K chunk kc -> D + r*sD + kc*sPart (row-chain plan)
 };
 
 struct Prob {
@@ -48,13 +49,14 @@ struct Prob {
   int M, N, K;             // K: padded reduction length (multiple of 8)
   int R;                   // replicas
   int tiles_m, tiles_n;
+  int tiles_k;             // split-K chunks over workgroups (PK_PARTIAL; 1 otherwise)
+  int kchunk;              // reduction elements per chunk (multiple of 8)
+  long long sPart;         // element stride between the chunks' output slabs
   int block_begin;
   // operands
   const void* A; long long lda, sA;
   const void* BT; long long ldb, sB;
   int a_gather;            // 1: A rows come from the batch window (train: perm, eval: contiguous)
-  int a_rowstep;           // with a_gather: the epoch's rows are pre-permuted, batch row m = step * B + m
-  int a_colstep;           // A advances by step * B elements per step (pre-permuted X^T of layer 0)
   int ones_row;            // >= 0: index of a virtual all-ones A row (bias gradient)
   int bt_shadow;           // 1: BT is a parity-double-buffered shadow (offset by par * bt_par)
   long long bt_par;
@@ -102,6 +104,54 @@ struct GroupArgs {
   long long* stamps;        // diagnostics: [block][16] s_memrealtime stamps (null = off)
 };
 
+// A grouped launch whose problems live in a device table (csrc/runtime/executor.cpp
+// row-chain plan): up to TABLE_MAX problems of one kind set, problem i owns blocks
+// [begin[i], begin[i+1]). Problem fields are read through the pointer with scalar
+// loads (the index is wave-uniform); GroupArgs keeps two problems in kernarg.
+constexpr int TABLE_MAX = 4;
+struct TableArgs {
+  const Prob* probs;
+  int nprob;
+  int begin[TABLE_MAX];
+  int total_blocks;
+  long long* ctr;
+  unsigned long long seed;
+  int step_off;
+  long long* stamps;
+};
+
+// --------------------------------------------------------- row-chain MLP step
+// Layers 1..L-1 of a small MLP (every width <= RC_MAXW) for RC_ROWS batch rows
+// per workgroup: forward, loss, and input gradients (see rowchain.hip).
+constexpr int RC_MAXL = 4;
+constexpr int RC_ROWS = 16;
+constexpr int RC_MAXW = 256;
+constexpr int RC_MAXSPLIT = 8;   // layer-0 split-K slabs
+struct RcLayer {
+  int K, N, Kp, Np, act, has_bias;
+  float rate;
+  long long p_off, wsh_off, wtsh_off;
+  void* DT;    // D_l^T [N][Bp] (compute dtype), the next layer's DW operand (l < L-1)
+  void* dZT;   // dZ_l^T [N][Bp], this layer's DW operand
+};
+struct RcArgs {
+  int L, R, B, Bp;
+  int nsplitk;                  // layer-0 split-K partial slabs
+  const float* Zp; long long sZp, sZpk;   // [R][nsplitk][B][N0] fp32
+  RcLayer ly[RC_MAXL];          // indexed with compile-time layer numbers only
+  const float* Y; long long sY, ldy;
+  const int* perm; long long sPerm;
+  const int* ntrain;
+  const float* P; long long sP;            // fp32 master (biases)
+  const void* Wsh; long long sWsh, wsh_par;
+  const void* WTsh; long long sWTsh, wtsh_par;
+  int loss, nmet, met[4];
+  double* acc; int acc_stride;
+  long long* ctr; int step_off;
+  unsigned long long seed;
+  long long* stamps;
+};
+
 constexpr int MAX_SEG = 16;
 
 struct Seg {
@@ -123,7 +173,6 @@ struct FlatArgs {
   Seg seg[MAX_SEG];
   void* Wsh; long long sWsh, wsh_par;
   void* WTsh; long long sWTsh, wtsh_par;
-  float* Bsh; long long sBsh, bsh_par;  // fp32 bias images per parity (fused tail only), flat index
   long long* ctr;
   const int* ntrain; int B;
   int both_parities;  // refresh: write both shadow parities
@@ -131,66 +180,6 @@ struct FlatArgs {
   // shadows are rebuilt from src; replica 0 also copies src into src_copy
   const float* src; float* src_copy;
   int total_blocks;
-};
-
-// ------------------------------------------------------------ fused MLP tail
-// One workgroup per replica runs, for layers 1..L-1 of a small MLP, the
-// forward pass, the loss, and the backward pass with every weight update, with
-// all activations resident in LDS (see fused.hip). Layer 0's forward (wide K)
-// and weight update (many tiles) stay on the grouped GEMM kernel.
-constexpr int FUSED_MAX_L = 8;
-
-struct FusedLayer {
-  int K, N, Kp, Np;        // dims; Kp/Np padded to 8
-  int act, has_bias;
-  float rate;
-  int ldA;                 // LDS row stride (elements) of this layer's output D_l / dZ_l tiles
-  int offD;                // LDS byte offset of D_l (compute dtype, [64][ldA]) (l < L-1)
-  int offG;                // LDS byte offset of G_l (fp32 [64][ldG]): z, then act'(z)*dropout (l < L-1)
-  int ldG;
-  int pvec;                // P/S rows of this layer allow float4 access (N % 4 == 0, p_off % 4 == 0)
-  long long p_off;         // flat parameter offset (kernel K*N, then bias N)
-  long long wsh_off, wtsh_off;
-};
-
-struct FusedArgs {
-  int L;
-  int nsplit;              // workgroups per replica (each owns 1/nsplit of the update tiles)
-  const FusedLayer* ly;    // device array [L] (uniform loads)
-  int R, B, Bp;
-  // layer-0 outputs of the grouped forward launch
-  const void* D0; long long sD0;   // [B][Np0] compute dtype
-  const float* Z0; long long sZ0;  // [B][N0]  fp32
-  // targets
-  const float* Y; long long sY, ldy;
-  const int* perm; long long sPerm;
-  const int* ntrain;
-  // out: dZ_0^T [N0][Bp] (B^T operand of the layer-0 weight update)
-  void* dZ0T; long long sdZ0T;
-  // deferred layer-1 update (nsplit == 1 mode): the tail writes dZ_1^T [N1][Bp]
-  // and skips layer 1's weight update, which runs with layer 0's in the next
-  // grouped launch; nullptr = the tail updates every layer >= 1 itself
-  void* dZ1T; long long sdZ1T;
-  // parameters
-  float* P; long long sP;
-  float* S; long long sS;
-  OptParams op;
-  void* Wsh; long long sWsh, wsh_par;
-  void* WTsh; long long sWTsh, wtsh_par;
-  // fp32 bias images per parity, indexed like P: the forward of layer l reads the
-  // current parity while other workgroups of the replica write the next one
-  float* Bsh; long long sBsh, bsh_par;
-  int loss, nmet, met[4];
-  double* acc; int acc_stride;
-  long long* ctr; int step_off;
-  unsigned long long seed;
-  // LDS layout
-  int offLg, ldLg;         // logits / dZ_{L-1} fp32 [64][ldLg]
-  int offdZ0, offdZ1;      // dZ ping-pong (compute dtype [64][lddZ])
-  int lddZ;
-  int offY, offSrow;       // targets fp32 [64][32], row flags int[64]
-  int lds_bytes;
-  long long* stamps;
 };
 
 }  // namespace ea

@@ -34,10 +34,7 @@ __device__ __forceinline__ void write_shadow(const FlatArgs& a, int r, long long
   const SegV g = find_seg(a, i);
   const long long rel = i - g.p_off;
   if (rel < 0) return;
-  if (rel >= (long long)g.K * g.N) {  // bias: fp32 image only (read by the fused tail)
-    if (a.Bsh) a.Bsh[(long long)r * a.sBsh + par * a.bsh_par + i] = w;
-    return;
-  }
+  if (rel >= (long long)g.K * g.N) return;  // bias: no image (read from the fp32 master)
   const long long k = rel / g.N, nn = rel % g.N;
   if (a.Wsh)
     reinterpret_cast<T*>(a.Wsh)[(long long)r * a.sWsh + par * a.wsh_par + g.wsh_off + k * g.ldwsh + nn] = from_f<T>(w);
@@ -174,10 +171,6 @@ __global__ __launch_bounds__(256) void shadow_tiles_kernel(FlatArgs a, int tiles
     if (UPDATE) {
       w = opt_update(a.op, w, a.G[(long long)r * a.sG + pi] * a.op.grad_scale, S, pi, iter);
       P[pi] = w;
-    }
-    if (a.Bsh) {
-      a.Bsh[(long long)r * a.sBsh + p0 * a.bsh_par + pi] = w;
-      if (p1 != p0) a.Bsh[(long long)r * a.sBsh + p1 * a.bsh_par + pi] = w;
     }
   }
   if (!WT) return;
@@ -368,62 +361,3 @@ extern "C" hipError_t ea_poison_lds(unsigned pattern, hipStream_t s) {
   return hipGetLastError();
 }
 
-// Per-epoch shard permutation (native_engine.NativeTrainer._new_perm): one pass
-// over the replica's rows in epoch order writes the row-major permuted copy Xp
-// [nmax][ldx] and its transpose XpT [ldx][ldxpt] (layer 0's weight update reads a
-// column window of it per step). 64 x 64 tiles through LDS so both the gathered
-// row reads and the transposed writes are coalesced (16-byte chunks).
-__global__ __launch_bounds__(256) void permute_rows_kernel(const unsigned short* __restrict__ X,
-                                                           const int* __restrict__ perm, unsigned short* __restrict__ Xp,
-                                                           unsigned short* __restrict__ XpT, int nmax, int ldx,
-                                                           long long ldxpt, int tiles_m, int tiles_k) {
-  __shared__ unsigned short tile[64][64 + 8];
-  const int per_r = tiles_m * tiles_k;
-  const int r = blockIdx.x / per_r, t = blockIdx.x % per_r;
-  const int m0 = (t / tiles_k) * 64, k0 = (t % tiles_k) * 64;
-  const long long xoff = (long long)r * nmax * ldx;
-  const int tid = threadIdx.x;
-  // 64 rows x 8 chunks of 8 bf16: 512 chunks, 2 per thread
-#pragma unroll
-  for (int c = 0; c < 2; ++c) {
-    const int e = tid + 256 * c, row = e >> 3, ch = (e & 7) * 8, m = m0 + row, k = k0 + ch;
-    uint4 v = make_uint4(0u, 0u, 0u, 0u);
-    if (m < nmax && k < ldx) {
-      const int src = perm[(long long)r * nmax + m];
-      v = *reinterpret_cast<const uint4*>(X + xoff + (long long)src * ldx + k);
-      *reinterpret_cast<uint4*>(Xp + xoff + (long long)m * ldx + k) = v;
-    }
-    const unsigned short* pv = reinterpret_cast<const unsigned short*>(&v);
-#pragma unroll
-    for (int q = 0; q < 8; ++q) tile[row][ch + q] = pv[q];
-  }
-  __syncthreads();
-  // transposed: 64 k-rows x 8 chunks of 8 m
-  const long long toff = (long long)r * ldx * ldxpt;
-#pragma unroll
-  for (int c = 0; c < 2; ++c) {
-    const int e = tid + 256 * c, kr = e >> 3, ch = (e & 7) * 8, k = k0 + kr, m = m0 + ch;
-    if (k < ldx && m < nmax) {
-      unsigned short w[8];
-#pragma unroll
-      for (int q = 0; q < 8; ++q) w[q] = tile[ch + q][kr];
-      if (m + 8 <= nmax) {
-        *reinterpret_cast<uint4*>(XpT + toff + (long long)k * ldxpt + m) = *reinterpret_cast<const uint4*>(w);
-      } else {
-#pragma unroll
-        for (int q = 0; q < 8; ++q)
-          if (m + q < nmax) XpT[toff + (long long)k * ldxpt + m + q] = w[q];
-      }
-    }
-  }
-}
-
-extern "C" hipError_t ea_permute_rows(const void* X, const int* perm, void* Xp, void* XpT, int R, int nmax, int ldx,
-                                      long long ldxpt, hipStream_t s) {
-  if ((ldx % 8) || (ldxpt % 8)) return hipErrorInvalidValue;
-  const int tiles_m = (nmax + 63) / 64, tiles_k = (ldx + 63) / 64;
-  hipLaunchKernelGGL(permute_rows_kernel, dim3(R * tiles_m * tiles_k), dim3(256), 0, s,
-                     reinterpret_cast<const unsigned short*>(X), perm, reinterpret_cast<unsigned short*>(Xp),
-                     reinterpret_cast<unsigned short*>(XpT), nmax, ldx, ldxpt, tiles_m, tiles_k);
-  return hipGetLastError();
-}

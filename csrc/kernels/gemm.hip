@@ -7,19 +7,17 @@ extern "C" {
 hipError_t ea_gemm_launch_lat_bf16(const ea::GroupArgs* ga, hipStream_t s);
 hipError_t ea_gemm_launch_thr_bf16(const ea::GroupArgs* ga, hipStream_t s);
 hipError_t ea_gemm_launch_thr64_bf16(const ea::GroupArgs* ga, hipStream_t s);
-hipError_t ea_gemm_launch_lat64_bf16(const ea::GroupArgs* ga, hipStream_t s);
 hipError_t ea_gemm_launch_f32(const ea::GroupArgs* ga, int cfg, hipStream_t s);
+hipError_t ea_gemm_table_lat_bf16(const ea::TableArgs* ta, int dw, hipStream_t s);
+hipError_t ea_gemm_table_f32(const ea::TableArgs* ta, int dw, hipStream_t s);
 void ea_gemm_init_lat_bf16();
 void ea_gemm_init_thr_bf16();
 void ea_gemm_init_thr64_bf16();
-void ea_gemm_init_lat64_bf16();
 void ea_gemm_init_f32();
 }
 
 // cfg: 0 = LAT (64x32, split-K 4), 1 = THR (128x128), 2 = THR-N64 (128x64: twice the
-// workgroups for grids that would otherwise leave CUs with a single workgroup),
-// 3 = LAT-64 (64x64, 2 N-waves x split-K 2: shallow reductions such as K = batch 64,
-// where split-K 4 leaves two waves without a 32-deep chunk)
+// workgroups for grids that would otherwise leave CUs with a single workgroup)
 extern "C" hipError_t ea_gemm_grouped(const ea::GroupArgs* ga, int bf16, int cfg, hipStream_t s) {
   using namespace ea;
   if (ga->total_blocks <= 0) return hipSuccess;
@@ -35,8 +33,13 @@ extern "C" hipError_t ea_gemm_grouped(const ea::GroupArgs* ga, int bf16, int cfg
   if (!bf16) return ea_gemm_launch_f32(ga, cfg, s);
   if (cfg == 0) return ea_gemm_launch_lat_bf16(ga, s);
   if (cfg == 2) return ea_gemm_launch_thr64_bf16(ga, s);
-  if (cfg == 3) return ea_gemm_launch_lat64_bf16(ga, s);
   return ea_gemm_launch_thr_bf16(ga, s);
+}
+
+// row-chain plan table launches: dw = 0 -> {layer-0 split-K partial, X^T gather}
+// on the 64x32 LAT tile; dw = 1 -> {DW of every layer} on a 64x64 tile
+extern "C" hipError_t ea_gemm_table(const ea::TableArgs* ta, int bf16, int dw, hipStream_t s) {
+  return bf16 ? ea_gemm_table_lat_bf16(ta, dw, s) : ea_gemm_table_f32(ta, dw, s);
 }
 
 extern "C" void ea_gemm_init() {
@@ -45,11 +48,12 @@ extern "C" void ea_gemm_init() {
   ea_gemm_init_lat_bf16();
   ea_gemm_init_thr_bf16();
   ea_gemm_init_thr64_bf16();
-  ea_gemm_init_lat64_bf16();
   ea_gemm_init_f32();
   done = true;
 }
 
+// cfg 3: the 64x64 tile of the row-chain weight-gradient table launch (not a
+// grouped-launch config)
 extern "C" int ea_gemm_tile_m(int cfg) { return (cfg == 0 || cfg == 3) ? 64 : 128; }
 extern "C" int ea_gemm_tile_n(int cfg) { return cfg == 0 ? 32 : ((cfg == 2 || cfg == 3) ? 64 : 128); }
 extern "C" int ea_gather_tile() { return 64; }

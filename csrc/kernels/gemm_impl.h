@@ -56,8 +56,8 @@ template <typename T> __device__ __forceinline__ void st(void* base, long long i
 }
 
 // ------------------------------------------------------- gather-transpose
-template <typename T>
-__device__ __forceinline__ void gather_transpose_block(const GroupArgs& ga, const Prob& p, int lb, float* sm) {
+template <typename T, typename GA>
+__device__ __forceinline__ void gather_transpose_block(const GA& ga, const Prob& p, int lb, float* sm) {
   // one block = 64 batch rows x 64 features; output XT[k][m] (ld = lddt)
   // tiles_m: batch blocks, tiles_n: feature blocks
   const int per_r = p.tiles_m * p.tiles_n;
@@ -70,15 +70,25 @@ __device__ __forceinline__ void gather_transpose_block(const GroupArgs& ga, cons
   const T* A = reinterpret_cast<const T*>(p.A) + (long long)r * p.sA;
   T* XT = reinterpret_cast<T*>(p.DT) + (long long)r * p.sDT;
   const int tid = threadIdx.x;
-  for (int e = tid; e < 64 * 64; e += 256) {
-    const int m = e / 64, k = e % 64;
-    float v = 0.f;
-    if (b0 + m < valid && k0 + k < p.K) {
-      const long long row = batch_row(p, r, step, b0 + m);
-      v = to_f<T>(A[row * p.lda + k0 + k]);
-    }
-    sm[m * 65 + k] = v;
+  // thread: column k = tid % 64 of rows tid / 64 + 4 i; every perm load, then every
+  // row load, is issued before the first use (one memory round trip each instead of
+  // one per row)
+  const int k = tid & 63, mb = tid >> 6;
+  int rows[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int m = mb + 4 * i;
+    rows[i] = (b0 + m < valid) ? (int)batch_row(p, r, step, b0 + m) : -1;
   }
+  float v[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const bool in = rows[i] >= 0 && k0 + k < p.K;
+    const T x = A[(in ? (long long)rows[i] * p.lda + k0 + k : 0)];
+    v[i] = in ? to_f<T>(x) : 0.f;
+  }
+#pragma unroll
+  for (int i = 0; i < 16; ++i) sm[(mb + 4 * i) * 65 + k] = v[i];
   __syncthreads();
   for (int e = tid; e < 64 * 64; e += 256) {
     const int k = e / 64, m = e % 64;
@@ -288,11 +298,11 @@ __device__ __forceinline__ void st8(void* base, long long idx, const float (&v)[
 // Fused loss over the tile's rows: groups of W lanes own one row each
 // (W = 16/32/64 by output width), reductions are W-lane shuffles.
 // diagnostics: wall-clock stamps (100 MHz s_memrealtime) of block-relative phases
-__device__ __forceinline__ void stamp(const GroupArgs& ga, int k) {
+template <typename GA> __device__ __forceinline__ void stamp(const GA& ga, int k) {
   if (ga.stamps && threadIdx.x == 0) ga.stamps[(long long)blockIdx.x * 16 + k] = (long long)__builtin_amdgcn_s_memrealtime();
 }
 // shader-clock counter (slots 10..15) to estimate the SCLK the kernel runs at
-__device__ __forceinline__ void stamp_clk(const GroupArgs& ga, int k) {
+template <typename GA> __device__ __forceinline__ void stamp_clk(const GA& ga, int k) {
   if (ga.stamps && threadIdx.x == 0) ga.stamps[(long long)blockIdx.x * 16 + k] = (long long)__builtin_amdgcn_s_memtime();
 }
 
@@ -450,9 +460,14 @@ constexpr unsigned KM_NONE = 0u;
 constexpr unsigned KM_FWD = KB(PK_FWD), KM_GATHER = KB(PK_GATHER_T);
 constexpr unsigned KM_LOSS = KB(PK_FWD_LOSS);
 constexpr unsigned KM_DW = KB(PK_DW_UPDATE) | KB(PK_DW_GRAD), KM_DX = KB(PK_DX);
+constexpr unsigned KM_PARTIAL = KB(PK_PARTIAL);
 
-template <typename T, int WM, int WN, int WAVES_M, int WAVES_N, int KSPLIT, unsigned KM = KM_ALL>
-__device__ __forceinline__ void run_prob(const GroupArgs& ga, const Prob& p, const int lb, float* smem) {
+// PF_: k-steps of fragments in flight per wave in the register-direct loop (0 = by
+// tile size); the weight-gradient table launch (K = batch: one or two k-steps per
+// wave) uses a shallow ring so three workgroups fit on a CU
+template <typename T, int WM, int WN, int WAVES_M, int WAVES_N, int KSPLIT, unsigned KM = KM_ALL, int PF_ = 0,
+          typename GA>
+__device__ __forceinline__ void run_prob(const GA& ga, const Prob& p, const int lb, float* smem) {
   static_assert(WAVES_M * WAVES_N * KSPLIT == 4, "4 waves per block");
   constexpr int BM = WAVES_M * WM * 16;
   constexpr int BN = WAVES_N * WN * 16;
@@ -461,10 +476,19 @@ __device__ __forceinline__ void run_prob(const GroupArgs& ga, const Prob& p, con
   if ((KM & KB(PK_GATHER_T)) && p.kind == PK_GATHER_T) {
     gather_transpose_block<T>(ga, p, lb, smem);
   } else {
-    const int per_r = p.tiles_m * p.tiles_n;
+    // split-K over workgroups (PK_PARTIAL): chunk kc covers reduction elements
+    // [kc * kchunk, kc * kchunk + Keff) and writes its own fp32 slab
+    const bool partial = (KM & KB(PK_PARTIAL)) && p.kind == PK_PARTIAL;
+    const int tk = partial ? p.tiles_k : 1;
+    const int per_mn = p.tiles_m * p.tiles_n;
+    const int per_r = per_mn * tk;
     const int r = lb / per_r;
-    const int t = lb % per_r;
+    const int tkm = lb % per_r;
+    const int kch = partial ? tkm / per_mn : 0;
+    const int t = partial ? tkm - kch * per_mn : tkm;
     const int tm = t / p.tiles_n, tn = t % p.tiles_n;
+    const int koff = partial ? kch * p.kchunk : 0;
+    const int Keff = partial ? min(p.kchunk, p.K - koff) : p.K;
     const int m0 = tm * BM, n0 = tn * BN;
     const long long step = ga.ctr[0] + ga.step_off;
     // (every launcher passes a valid ntrain: the plain-GEMM entry points it at zeros)
@@ -472,6 +496,39 @@ __device__ __forceinline__ void run_prob(const GroupArgs& ga, const Prob& p, con
     const int valid = (p.kind == PK_PLAIN) ? p.M : batch_valid(p, r, step);
     const bool skip_update = (p.kind == PK_DW_UPDATE) && valid == 0;
     stamp(ga, 1);
+
+    // Epilogue thread mapping (used below): each thread owns 8 contiguous columns of
+    // one row per pass.
+    constexpr int CPR = BN / 8;          // 8-column chunks per row
+    constexpr int RPP = 256 / CPR;       // rows per pass
+    constexpr int PASSES = BM / RPP;
+    const int t_row = threadIdx.x / CPR, t_c0 = (threadIdx.x % CPR) * 8;
+    // Weight-update launches of one pass per thread (the LAT tile of the row-chain
+    // DW table launch): the fp32 master / optimizer-state operands of the update do
+    // not depend on the GEMM, so their loads are issued before the main loop and
+    // their memory round trip overlaps it instead of following it.
+    constexpr bool DW_PF = (KM & ~KM_DW) == 0u && PASSES <= 2;
+    constexpr int PFP = DW_PF ? PASSES : 1;
+    float pf_w[PFP][8], pf_s0[PFP][8], pf_s1[PFP][8];
+    bool pf_vec[PFP];
+#pragma unroll
+    for (int ps = 0; ps < PFP; ++ps) {
+      pf_vec[ps] = false;
+      if constexpr (DW_PF) {
+        const int gm = m0 + ps * RPP + t_row, gn0 = n0 + t_c0;
+        pf_vec[ps] = p.kind == PK_DW_UPDATE && !skip_update && gm < p.M && gn0 + 8 <= p.N &&
+                     ((p.p_off + (long long)gm * p.N + gn0) & 3) == 0 && (p.op.s_plane & 3) == 0;
+        if (pf_vec[ps]) {
+          const long long pidx = p.p_off + (long long)gm * p.N + gn0;
+          const float* Pp = p.P + (long long)r * p.sP;
+          const float* Sp = p.S ? p.S + (long long)r * p.sS : nullptr;
+          const int np = Sp ? opt_planes(p.op) : 0;
+          ld8f(Pp + pidx, pf_w[ps]);
+          if (np > 0) ld8f(Sp + pidx, pf_s0[ps]); else zero8(pf_s0[ps]);
+          if (np > 1) ld8f(Sp + p.op.s_plane + pidx, pf_s1[ps]); else zero8(pf_s1[ps]);
+        }
+      }
+    }
 
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int wk = wave % KSPLIT;
@@ -486,9 +543,9 @@ __device__ __forceinline__ void run_prob(const GroupArgs& ga, const Prob& p, con
       for (int j = 0; j < WN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
     if (!skip_update) {
-      const T* A = reinterpret_cast<const T*>(p.A) + (long long)r * p.sA + (p.a_colstep ? step * p.B : 0);
+      const T* A = reinterpret_cast<const T*>(p.A) + (long long)r * p.sA + koff;
       const T* BTp = reinterpret_cast<const T*>(p.BT) + (long long)r * p.sB +
-                     (p.bt_shadow ? (iter & 1) * p.bt_par : 0);
+                     (p.bt_shadow ? (iter & 1) * p.bt_par : 0) + koff;
       // Every fragment load is an unconditional, in-bounds 16-byte global load
       // (invalid rows read row 0, k past the end reads k=0) followed by a value
       // select, so hipcc emits global_load_dwordx4 and never a pointer select
@@ -504,7 +561,7 @@ __device__ __forceinline__ void run_prob(const GroupArgs& ga, const Prob& p, con
         } else if (m < p.M) {
           if (p.a_gather) {
             if (m < valid) {
-              arow[i] = A + (p.a_rowstep ? step * p.B + m : batch_row(p, r, step, m)) * p.lda;
+              arow[i] = A + batch_row(p, r, step, m) * p.lda;
               amask |= 1u << i;
             }
           } else {
@@ -542,7 +599,7 @@ __device__ __forceinline__ void run_prob(const GroupArgs& ga, const Prob& p, con
             aones |= 1u << t;
           } else if (m < p.M) {
             if (p.a_gather) {
-              if (m < valid) arow_ld[t] = Ab + (p.a_rowstep ? step * p.B + m : batch_row(p, r, step, m)) * p.lda;
+              if (m < valid) arow_ld[t] = Ab + batch_row(p, r, step, m) * p.lda;
             } else {
               arow_ld[t] = Ab + (long long)m * p.lda;
             }
@@ -553,7 +610,7 @@ __device__ __forceinline__ void run_prob(const GroupArgs& ga, const Prob& p, con
           const int n = n0 + t * 32 + (threadIdx.x >> 3);
           bcol_ld[t] = n < p.N ? Bb + (long long)n * p.ldb : nullptr;
         }
-        thr_lds_mainloop<BN>(arow_ld, bcol_ld, aones, p.K, wm, wn,
+        thr_lds_mainloop<BN>(arow_ld, bcol_ld, aones, Keff, wm, wn,
                              reinterpret_cast<f32x4(&)[4][ThrGeom<BN>::WNF]>(acc), reinterpret_cast<char*>(smem));
       } else {
       const uint4 zero = make_uint4(0u, 0u, 0u, 0u);
@@ -563,7 +620,7 @@ __device__ __forceinline__ void run_prob(const GroupArgs& ga, const Prob& p, con
       };
       auto load_frags = [&](int kc, uint4 (&a)[WM], uint4 (&b)[WN]) {
         const int kk = kc + g * EPL;
-        const bool kin = kk < p.K;
+        const bool kin = kk < Keff;
         const int kq = kin ? kk : 0;
 #pragma unroll
         for (int i = 0; i < WM; ++i) {
@@ -579,9 +636,9 @@ __device__ __forceinline__ void run_prob(const GroupArgs& ga, const Prob& p, con
       // PF-deep register ring: PF k-steps of fragments in flight per wave, so a
       // K = 784 layer waits on ~2 load round trips instead of one per step.
       constexpr int KSTEP = KSPLIT * KC;
-      constexpr int PF = (WM * WN >= 16) ? 3 : 4;
+      constexpr int PF = PF_ > 0 ? PF_ : ((WM * WN >= 16) ? 3 : 4);
       const int kbeg = wk * KC;
-      const int nsteps = kbeg < p.K ? (p.K - kbeg + KSTEP - 1) / KSTEP : 0;
+      const int nsteps = kbeg < Keff ? (Keff - kbeg + KSTEP - 1) / KSTEP : 0;
       uint4 ra[PF][WM], rb[PF][WN];
 #pragma unroll
       for (int u = 0; u < PF; ++u)
@@ -641,10 +698,6 @@ __device__ __forceinline__ void run_prob(const GroupArgs& ga, const Prob& p, con
     // per pass and issues all of its global loads before any store, so the
     // loads of a pass overlap instead of serialising behind possibly-aliasing
     // stores.
-    constexpr int CPR = BN / 8;          // 8-column chunks per row
-    constexpr int RPP = 256 / CPR;       // rows per pass
-    constexpr int PASSES = BM / RPP;
-    const int t_row = threadIdx.x / CPR, t_c0 = (threadIdx.x % CPR) * 8;
     auto lds8 = [&](int row, int c0, float (&v)[8]) {
       const float4 a = *reinterpret_cast<const float4*>(C + row * LDC + c0);
       const float4 b = *reinterpret_cast<const float4*>(C + row * LDC + c0 + 4);
@@ -679,6 +732,26 @@ __device__ __forceinline__ void run_prob(const GroupArgs& ga, const Prob& p, con
     };
 
     switch (p.kind) {
+      case PK_PARTIAL: {
+        if constexpr (!(KM & KB(PK_PARTIAL))) break;
+        // raw fp32 slab of this K chunk; rows past the valid batch are zero (masked A)
+        float* out = reinterpret_cast<float*>(p.D) + (long long)r * p.sD + (long long)kch * p.sPart;
+#pragma unroll
+        for (int ps = 0; ps < PASSES; ++ps) {
+          const int row = ps * RPP + t_row, gm = m0 + row, gn0 = n0 + t_c0;
+          if (gm >= p.M || gn0 >= p.N) continue;
+          float v[8];
+          lds8(row, t_c0, v);
+          if (gn0 + 8 <= p.N && (p.ldd & 3) == 0) {
+            st8f(out + (long long)gm * p.ldd + gn0, v);
+          } else {
+#pragma unroll
+            for (int q = 0; q < 8; ++q)
+              if (gn0 + q < p.N) out[(long long)gm * p.ldd + gn0 + q] = v[q];
+          }
+        }
+        break;
+      }
       case PK_PLAIN: {
         if constexpr (!(KM & KB(PK_PLAIN))) break;
         float* out = reinterpret_cast<float*>(p.D) + (long long)r * p.sD;
@@ -853,7 +926,14 @@ __device__ __forceinline__ void run_prob(const GroupArgs& ga, const Prob& p, con
           float w[8], s0[8], s1[8];
           // whole 16-byte-aligned chunks (the common case) move as float4 pairs
           const bool vec = gn0 + 8 <= p.N && (pidx & 3) == 0 && (p.op.s_plane & 3) == 0;
-          if (vec) {
+          if (DW_PF && pf_vec[DW_PF ? ps : 0]) {
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+              w[q] = pf_w[DW_PF ? ps : 0][q];
+              s0[q] = pf_s0[DW_PF ? ps : 0][q];
+              s1[q] = pf_s1[DW_PF ? ps : 0][q];
+            }
+          } else if (vec) {
             ld8f(P + pidx, w);
             if (np > 0) ld8f(S + pidx, s0); else zero8(s0);
             if (np > 1) ld8f(S + p.op.s_plane + pidx, s1); else zero8(s1);
@@ -939,6 +1019,25 @@ __global__ __launch_bounds__(256) void loss_rows_kernel(GroupArgs ga) {
   loss_rows_block<T>(ga, ga.p[0], blockIdx.x - ga.p[0].block_begin, smem);
 }
 
+// Grouped launch over a device table of problems (row-chain plan, up to
+// TABLE_MAX problems of the kinds in KM): block -> problem by the kernarg
+// begin[] table; the problem's fields are read through a wave-uniform pointer.
+template <typename T, int WM, int WN, int WAVES_M, int WAVES_N, int KSPLIT, unsigned KM>
+__global__ __launch_bounds__(256) void gemm_table(TableArgs ta) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  stamp(ta, 0);
+  stamp_clk(ta, 10);
+  const int bid = blockIdx.x;
+  int i = 0;
+#pragma unroll
+  for (int j = 1; j < TABLE_MAX; ++j) i += (j < ta.nprob && bid >= ta.begin[j]) ? 1 : 0;
+  i = __builtin_amdgcn_readfirstlane(i);
+  const Prob* __restrict__ p = ta.probs + i;
+  run_prob<T, WM, WN, WAVES_M, WAVES_N, KSPLIT, KM, (KM == KM_DW) ? 2 : 0>(ta, *p, bid - ta.begin[i], smem);
+  stamp(ta, 4);
+  stamp_clk(ta, 11);
+}
+
 // ------------------------------------------------------------- host side
 template <typename T, int WM, int WN, int WAVES_M, int WAVES_N, int KSPLIT>
 static size_t lds_bytes(bool loss = true) {
@@ -1002,6 +1101,35 @@ static hipError_t launch_cfg(const GroupArgs& ga, hipStream_t s) {
   hipLaunchKernelGGL((gemm_grouped<T, WM, WN, WAVES_M, WAVES_N, KSPLIT>), dim3(ga.total_blocks), dim3(256), lds, s,
                      ga);
   return hipGetLastError();
+}
+
+// table launches of the row-chain plan: {layer-0 split-K partial, X^T gather} and
+// {DW of every layer}
+// The layer-0 table launch uses the 64x32 LAT tile (split-K 4 inside the block);
+// the weight-gradient launch a 64x64 tile with 2 N-waves x split-K 2: half the
+// workgroups, so every DW problem of a small MLP is resident at once (the 64x32
+// tile's 536 MNIST workgroups exceed the 2 per CU its registers allow and the last
+// ones ran as a second round, +7 us)
+template <typename T>
+static hipError_t launch_table(const TableArgs& ta, int dw, hipStream_t s) {
+  if (ta.total_blocks <= 0) return hipSuccess;
+  if (dw) {
+    const size_t lds = lds_bytes<T, 4, 2, 1, 2, 2>(false);
+    hipLaunchKernelGGL((gemm_table<T, 4, 2, 1, 2, 2, KM_DW>), dim3(ta.total_blocks), dim3(256), lds, s, ta);
+  } else {
+    const size_t lds = lds_bytes<T, 4, 2, 1, 1, 4>(false);
+    hipLaunchKernelGGL((gemm_table<T, 4, 2, 1, 1, 4, KM_PARTIAL | KM_GATHER>), dim3(ta.total_blocks), dim3(256), lds,
+                       s, ta);
+  }
+  return hipGetLastError();
+}
+
+template <typename T>
+static void set_attr_table() {
+  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_table<T, 4, 2, 1, 2, 2, KM_DW>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes<T, 4, 2, 1, 2, 2>(false));
+  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_table<T, 4, 2, 1, 1, 4, KM_PARTIAL | KM_GATHER>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes<T, 4, 2, 1, 1, 4>(false));
 }
 
 template <typename T, int WM, int WN, int WAVES_M, int WAVES_N, int KSPLIT>

@@ -25,8 +25,6 @@ extern "C" hipError_t ea_replica_average(float* P, long long sP, int R, long lon
 extern "C" hipError_t ea_axpby(const float* x, float* y, long long n, float alpha, float beta, hipStream_t s);
 extern "C" hipError_t ea_ps_sub(float* p, const float* d, long long n, float scale, int atomic, hipStream_t s);
 extern "C" hipError_t ea_poison_lds(unsigned pattern, hipStream_t s);
-extern "C" hipError_t ea_permute_rows(const void* X, const int* perm, void* Xp, void* XpT, int R, int nmax, int ldx,
-                                      long long ldxpt, hipStream_t s);
 extern "C" hipError_t ea_sub(const float* a, const float* b, float* out, long long n, hipStream_t s);
 
 static void chk(hipError_t e, const char* w) {
@@ -69,9 +67,8 @@ static ExecCfg parse_cfg(const py::dict& d) {
   c.force_cfg = get<int>(d, "force_cfg", -1);
   c.thr_min_k = get<int>(d, "thr_min_k", 64);
   c.thr_min_n = get<int>(d, "thr_min_n", 256);
-  c.lat64_max_k = get<int>(d, "lat64_max_k", 0);
-  c.fused = get<int>(d, "fused", -1);
-  c.fused_split = get<int>(d, "fused_split", 16);
+  c.rowchain = get<int>(d, "rowchain", -1);
+  c.rc_split = get<int>(d, "rc_split", 0);
   for (auto item : d["layers"].cast<py::list>()) {
     py::dict l = item.cast<py::dict>();
     LayerCfg lc;
@@ -104,9 +101,6 @@ static ExecCfg parse_cfg(const py::dict& d) {
   c.vstart = get<uintptr_t>(d, "vstart", 0);
   c.vcount = get<uintptr_t>(d, "vcount", 0);
   c.XT = get<uintptr_t>(d, "XT", 0);
-  c.Xp = get<uintptr_t>(d, "Xp", 0);
-  c.XpT = get<uintptr_t>(d, "XpT", 0);
-  c.ldxpt = get<long long>(d, "ldxpt", 0);
   c.P = get<uintptr_t>(d, "P", 0);
   c.sP = get<long long>(d, "sP", 0);
   c.nparams = get<long long>(d, "nparams", 0);
@@ -120,9 +114,6 @@ static ExecCfg parse_cfg(const py::dict& d) {
   c.WTsh = get<uintptr_t>(d, "WTsh", 0);
   c.sWTsh = get<long long>(d, "sWTsh", 0);
   c.wtsh_par = get<long long>(d, "wtsh_par", 0);
-  c.Bsh = get<uintptr_t>(d, "Bsh", 0);
-  c.sBsh = get<long long>(d, "sBsh", 0);
-  c.bsh_par = get<long long>(d, "bsh_par", 0);
   c.op = parse_opt(d["opt"].cast<py::dict>());
   c.loss = get<int>(d, "loss", 0);
   auto mets = get<std::vector<int>>(d, "metrics", {});
@@ -181,8 +172,9 @@ PYBIND11_MODULE(_C, m) {
       .def("launches_per_step", &Executor::launches_per_step)
       .def("launch_cfgs", &Executor::launch_cfgs)
       .def("launch_blocks", &Executor::launch_blocks)
-      .def("fused", &Executor::fused)
-      .def("fused_lds_bytes", &Executor::fused_lds_bytes)
+      .def("table_begins", &Executor::table_begins)
+      .def("rowchain", &Executor::rowchain)
+      .def("rowchain_split", &Executor::rowchain_split)
       .def("set_stamps", &Executor::set_stamps)
       .def("train_launch", [](Executor& e, int idx, uintptr_t s) { e.train_launch(idx, S(s)); })
       .def("grad_launches", &Executor::grad_launches)
@@ -196,7 +188,7 @@ PYBIND11_MODULE(_C, m) {
     // 16-byte aligned and K padded to whole chunks, or it reads out of bounds
     const int epl = bf16 ? 8 : 4;
     if (M <= 0 || N <= 0 || K <= 0 || (K % epl) || (lda % epl) || (ldb % epl) || lda < K || ldb < K || ldc < N ||
-        (A % 16) || (BT % 16) || (C % 4) || cfg < 0 || cfg > 3)
+        (A % 16) || (BT % 16) || (C % 4) || cfg < 0 || cfg > 2)
       throw std::invalid_argument("gemm_nt: K, lda, ldb must be multiples of 16 bytes, pointers 16-byte aligned");
     ea_gemm_init();
     GroupArgs ga;
@@ -234,12 +226,6 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("ps_sub", [](uintptr_t p, uintptr_t d, long long n, float scale, int atomic, uintptr_t s) {
     chk(ea_ps_sub(reinterpret_cast<float*>(p), reinterpret_cast<const float*>(d), n, scale, atomic, S(s)), "ps_sub");
-  });
-  m.def("permute_rows", [](uintptr_t X, uintptr_t perm, uintptr_t Xp, uintptr_t XpT, int R, int nmax, int ldx,
-                           long long ldxpt, uintptr_t s) {
-    chk(ea_permute_rows(reinterpret_cast<const void*>(X), reinterpret_cast<const int*>(perm),
-                        reinterpret_cast<void*>(Xp), reinterpret_cast<void*>(XpT), R, nmax, ldx, ldxpt, S(s)),
-        "permute_rows");
   });
   m.def("poison_lds", [](unsigned pattern, uintptr_t s) { chk(ea_poison_lds(pattern, S(s)), "poison_lds"); });
   m.def("sub", [](uintptr_t a, uintptr_t b, uintptr_t out, long long n, uintptr_t s) {

@@ -9,8 +9,8 @@ extern "C" hipError_t ea_gemm_grouped(const ea::GroupArgs* ga, int bf16, int cfg
 extern "C" int ea_gemm_tile_m(int cfg);
 extern "C" int ea_gemm_tile_n(int cfg);
 extern "C" void ea_gemm_init();
-extern "C" void ea_fused_init();
-extern "C" hipError_t ea_fused_tail(const ea::FusedArgs* a, int bf16, hipStream_t s);
+extern "C" hipError_t ea_gemm_table(const ea::TableArgs* ta, int bf16, int dw, hipStream_t s);
+extern "C" hipError_t ea_rowchain(const ea::RcArgs* a, int bf16, int nbw, hipStream_t s);
 extern "C" hipError_t ea_apply_update(ea::FlatArgs* a, int bf16, hipStream_t s);
 extern "C" hipError_t ea_refresh_shadows(ea::FlatArgs* a, int bf16, hipStream_t s);
 extern "C" hipError_t ea_advance(long long* ctr, const int* ntrain, int R, int B, int n, hipStream_t s);
@@ -30,122 +30,142 @@ Executor::Executor(const ExecCfg& cfg) : c_(cfg) {
     if (l.Kp % 8 || l.Np % 8 || l.Kp < l.K || l.Np < l.N) throw std::invalid_argument("layer dims must be padded to 8");
   }
   ea_gemm_init();
-  ea_fused_init();
   build();
-  fused_ = c_.fused != 0 && build_fused();
-  if ((c_.fused == 1 || c_.fused == 2) && !fused_) throw std::invalid_argument("fused MLP tail requested but the model is not eligible");
+  rc_.on = c_.rowchain != 0 && build_rowchain();
+  if (c_.rowchain == 1 && !rc_) throw std::invalid_argument("row-chain plan requested but the model is not eligible");
 }
 
 Executor::~Executor() {
   destroy_graphs();
-  if (d_fly_) (void)hipFree(d_fly_);
+  if (d_probs_) (void)hipFree(d_probs_);
+  if (d_zp_) (void)hipFree(d_zp_);
 }
 
-// Eligibility + LDS layout of the fused tail (fused.hip): batch <= 64, every
-// layer width <= 256, a final layer of <= 32 units, everything in 160 KB of LDS.
-bool Executor::build_fused() {
+// Row-chain plan (rowchain.hip): 2 <= L <= RC_MAXL Dense layers, every layer but
+// the last at most RC_MAXW wide, a last layer of at most 32 units (its loss runs
+// on whole rows inside one workgroup).
+bool Executor::build_rowchain() {
   const int L = (int)c_.layers.size();
-  if (L < 2 || L > FUSED_MAX_L || c_.B > 64 || c_.Bp > 64) return false;
-  // mode 1 (split workgroups update weights in the tail) needs the per-parity fp32
-  // bias images; mode 2 (one workgroup per replica, layer-1 update deferred to the
-  // grouped launch of layer 0) reads the fp32 master directly
-  const bool deferred = c_.fused == 2;
-  if (!deferred && !c_.Bsh) return false;
-  if (c_.layers[0].N > 256) return false;
-  for (int l = 1; l < L; ++l)
-    if (c_.layers[l].K > 256 || c_.layers[l].N > 256) return false;
-  if (c_.layers[L - 1].N > 32) return false;
+  if (L < 2 || L > RC_MAXL || L > TABLE_MAX) return false;
+  int wmax = 0;
+  for (int l = 0; l < L - 1; ++l) wmax = std::max(wmax, c_.layers[l].N);
+  if (wmax > RC_MAXW || c_.layers[L - 1].N > 32 || c_.ldy > 32) return false;
   if (fwd_.empty() || fwd_[0].ga.nprob != 2 || fwd_[0].ga.p[0].kind != PK_FWD || fwd_[0].ga.p[1].kind != PK_GATHER_T)
     return false;
-  const int esz = c_.bf16 ? 2 : 4, padA = c_.bf16 ? 8 : 4;
-  auto r16 = [](int x) { return (x + 15) / 16 * 16; };
-  std::vector<FusedLayer> fl(L);
-  long long off = 0;
-  int maxN = 0;
+  if ((int)bwd_.size() != L) return false;
+  const LayerCfg& l0 = c_.layers[0];
+  // split-K slabs of layer 0: chunks of >= ~112 reduction elements (K = 784 -> 7)
+  int ns = c_.rc_split > 0 ? c_.rc_split : cdiv(l0.Kp, 112);
+  ns = std::max(1, std::min(ns, RC_MAXSPLIT));
+  const int kchunk = cdiv(cdiv(l0.Kp, ns), 8) * 8;
+  ns = cdiv(l0.Kp, kchunk);
+  rc_.nsplitk = ns;
+  rc_.nbw = wmax <= 128 ? 2 : 4;
+  const long long slab = (long long)c_.B * l0.N;
+  check(hipMalloc(&d_zp_, sizeof(float) * (size_t)c_.R * ns * slab), "hipMalloc(row-chain slabs)");
+  check(hipMemset(d_zp_, 0, sizeof(float) * (size_t)c_.R * ns * slab), "hipMemset(row-chain slabs)");
+
+  // tile geometry of the table launches: 64x32 (layer 0), 64x64 (weight gradients)
+  auto blocks = [&](const Prob& p) {
+    if (p.kind == PK_GATHER_T) return p.R * cdiv(p.B, 64) * cdiv(p.K, 64);
+    return p.R * p.tiles_m * p.tiles_n * std::max(1, p.tiles_k);
+  };
+  auto table = [&](TableArgs& ta, Prob* host, int n, Prob* dev, int cfg) {
+    const int bm = ea_gemm_tile_m(cfg), bn = ea_gemm_tile_n(cfg);
+    std::memset(&ta, 0, sizeof(ta));
+    int begin = 0;
+    for (int i = 0; i < n; ++i) {
+      Prob& p = host[i];
+      if (p.kind == PK_GATHER_T) {
+        p.tiles_m = cdiv(p.B, 64);
+        p.tiles_n = cdiv(p.K, 64);
+      } else {
+        p.tiles_m = cdiv(p.M, bm);
+        p.tiles_n = cdiv(p.N, bn);
+      }
+      if (p.kind != PK_PARTIAL) p.tiles_k = 1;
+      p.block_begin = 0;
+      ta.begin[i] = begin;
+      begin += blocks(p);
+    }
+    ta.probs = dev;
+    ta.nprob = n;
+    ta.total_blocks = begin;
+    ta.ctr = reinterpret_cast<long long*>(c_.ctr);
+    ta.seed = c_.seed;
+    check(hipMemcpy(dev, host, sizeof(Prob) * n, hipMemcpyHostToDevice), "hipMemcpy(problem table)");
+  };
+  check(hipMalloc(&d_probs_, sizeof(Prob) * 3 * TABLE_MAX), "hipMalloc(problem tables)");
+
+  // A: layer-0 product as split-K slabs + the X^T gather (from the grouped FWD_0 launch)
+  Prob pa[2] = {fwd_[0].ga.p[0], fwd_[0].ga.p[1]};
+  Prob& z = pa[0];
+  z.kind = PK_PARTIAL;
+  z.tiles_k = ns;
+  z.kchunk = kchunk;
+  z.D = d_zp_;
+  z.ldd = l0.N;
+  z.sD = ns * slab;
+  z.sPart = slab;
+  z.Z = nullptr;
+  z.DT = nullptr;
+  table(rc_.ta_fwd, pa, 2, d_probs_, 0);
+
+  // C: DW of every layer (the grouped plan's DW problems), update and gradient forms
+  Prob pu[TABLE_MAX], pg[TABLE_MAX];
+  for (int l = 0; l < L; ++l) {
+    pu[l] = bwd_[L - 1 - l].ga.p[0];  // bwd_ runs from the last layer down
+    if (pu[l].kind != PK_DW_UPDATE) return false;
+    pg[l] = pu[l];
+    pg[l].kind = PK_DW_GRAD;
+  }
+  table(rc_.ta_dw, pu, L, d_probs_ + TABLE_MAX, 3);
+  table(rc_.ta_grad, pg, L, d_probs_ + 2 * TABLE_MAX, 3);
+
+  // B: the row chain
+  RcArgs& a = rc_.rc;
+  std::memset(&a, 0, sizeof(a));
+  a.L = L; a.R = c_.R; a.B = c_.B; a.Bp = c_.Bp;
+  a.nsplitk = ns;
+  a.Zp = d_zp_; a.sZp = ns * slab; a.sZpk = slab;
   for (int l = 0; l < L; ++l) {
     const LayerCfg& ly = c_.layers[l];
-    FusedLayer& f = fl[l];
-    std::memset(&f, 0, sizeof(f));
-    f.K = ly.K; f.N = ly.N; f.Kp = ly.Kp; f.Np = ly.Np;
-    f.act = ly.act; f.has_bias = ly.has_bias; f.rate = ly.rate;
-    f.p_off = ly.p_off; f.wsh_off = ly.wsh_off; f.wtsh_off = ly.wtsh_off;
-    f.pvec = (ly.N % 4 == 0 && ly.p_off % 4 == 0) ? 1 : 0;
-    if (l < L - 1) {
-      f.ldA = r16(ly.Np + 1) + padA;  // + the ones column (bias row of the next layer's update)
-      f.offD = (int)off;
-      off += 64LL * f.ldA * esz;
-      f.ldG = r16(ly.Np) + 4;
-      f.offG = (int)off;
-      off += 64LL * f.ldG * 4;
-    }
-    if (l >= 1) maxN = std::max(maxN, ly.N);
+    RcLayer& q = a.ly[l];
+    q.K = ly.K; q.N = ly.N; q.Kp = ly.Kp; q.Np = ly.Np;
+    q.act = ly.act; q.has_bias = ly.has_bias; q.rate = ly.rate;
+    q.p_off = ly.p_off; q.wsh_off = ly.wsh_off; q.wtsh_off = ly.wtsh_off;
+    q.DT = reinterpret_cast<void*>(ly.DT);
+    q.dZT = reinterpret_cast<void*>(ly.dZT);
   }
-  FusedArgs& a = fa_;
-  std::memset(&a, 0, sizeof(a));
-  a.offLg = (int)off; a.ldLg = 36; off += 64LL * 36 * 4;
-  a.lddZ = r16(maxN) + padA;
-  a.offdZ0 = (int)off; off += 64LL * a.lddZ * esz;
-  a.offdZ1 = (int)off; off += 64LL * a.lddZ * esz;
-  a.offY = (int)off; off += 64LL * 32 * 4;
-  a.offSrow = (int)off; off += 64 * 4;
-  if (off > 160 * 1024) return false;
-  a.lds_bytes = (int)off;
-  check(hipMalloc(&d_fly_, sizeof(FusedLayer) * L), "hipMalloc(fused layers)");
-  check(hipMemcpy(d_fly_, fl.data(), sizeof(FusedLayer) * L, hipMemcpyHostToDevice), "hipMemcpy(fused layers)");
-  const LayerCfg& l0 = c_.layers[0];
-  a.L = L;
-  a.nsplit = deferred ? 1 : std::max(1, c_.fused_split);
-  a.ly = d_fly_;
-  a.R = c_.R; a.B = c_.B; a.Bp = c_.Bp;
-  a.D0 = reinterpret_cast<const void*>(l0.D); a.sD0 = (long long)c_.B * l0.Np;
-  a.Z0 = reinterpret_cast<const float*>(l0.Z); a.sZ0 = (long long)c_.B * l0.N;
   a.Y = reinterpret_cast<const float*>(c_.Y); a.sY = c_.sY; a.ldy = c_.ldy;
   a.perm = reinterpret_cast<const int*>(c_.perm); a.sPerm = c_.sPerm;
   a.ntrain = reinterpret_cast<const int*>(c_.ntrain);
-  a.dZ0T = reinterpret_cast<void*>(l0.dZT); a.sdZ0T = (long long)l0.N * c_.Bp;
-  a.P = reinterpret_cast<float*>(c_.P); a.sP = c_.sP;
-  a.S = reinterpret_cast<float*>(c_.S); a.sS = c_.sS;
-  a.op = c_.op;
-  a.Wsh = reinterpret_cast<void*>(c_.Wsh); a.sWsh = c_.sWsh; a.wsh_par = c_.wsh_par;
-  a.WTsh = reinterpret_cast<void*>(c_.WTsh); a.sWTsh = c_.sWTsh; a.wtsh_par = c_.wtsh_par;
-  a.Bsh = deferred ? nullptr : reinterpret_cast<float*>(c_.Bsh); a.sBsh = c_.sBsh; a.bsh_par = c_.bsh_par;
-  if (deferred) {
-    a.dZ1T = reinterpret_cast<void*>(c_.layers[1].dZT);
-    a.sdZ1T = (long long)c_.layers[1].N * c_.Bp;
-  }
+  a.P = reinterpret_cast<const float*>(c_.P); a.sP = c_.sP;
+  a.Wsh = reinterpret_cast<const void*>(c_.Wsh); a.sWsh = c_.sWsh; a.wsh_par = c_.wsh_par;
+  a.WTsh = reinterpret_cast<const void*>(c_.WTsh); a.sWTsh = c_.sWTsh; a.wtsh_par = c_.wtsh_par;
   a.loss = c_.loss; a.nmet = c_.nmet;
   for (int i = 0; i < 4; ++i) a.met[i] = c_.met[i];
   a.acc = reinterpret_cast<double*>(c_.acc); a.acc_stride = c_.acc_stride;
   a.ctr = reinterpret_cast<long long*>(c_.ctr);
   a.seed = c_.seed;
-  // grouped launches around the tail: layer-0 forward (+ X^T), layer-0 update
-  ffwd_.assign(1, fwd_[0]);
-  fbwd_.assign(1, bwd_.back());
-  if (deferred) {
-    // layer 0 and layer 1 updates in one grouped launch: DW_1 reads D_0^T (kept in
-    // the forward launch) and the dZ_1^T the tail wrote
-    const Launch& b1 = bwd_[bwd_.size() - 2];  // {DW_1, DX_1}
-    Launch& u = fbwd_[0];
-    u.ga.p[1] = b1.ga.p[0];
-    u.ga.nprob = 2;
-    finalize(u);
-  } else {
-    ffwd_[0].ga.p[0].DT = nullptr;  // D_0^T is not needed: the tail reads D_0 into LDS
-  }
   return true;
 }
 
-void Executor::run_tail(hipStream_t s, int step_off) const {
-  FusedArgs a = fa_;
+void Executor::run_rowchain(hipStream_t s, int step_off, bool grad) const {
+  TableArgs ta = rc_.ta_fwd;
+  ta.step_off = step_off;
+  check(ea_gemm_table(&ta, c_.bf16, 0, s), "row-chain layer-0 slabs");
+  RcArgs a = rc_.rc;
   a.step_off = step_off;
-  check(ea_fused_tail(&a, c_.bf16, s), "fused_tail");
+  check(ea_rowchain(&a, c_.bf16, rc_.nbw, s), "row chain");
+  TableArgs tw = grad ? rc_.ta_grad : rc_.ta_dw;
+  tw.step_off = step_off;
+  check(ea_gemm_table(&tw, c_.bf16, 1, s), "row-chain weight gradients");
 }
 
 void Executor::run_step(hipStream_t s, int step_off) const {
-  if (fused_) {
-    run(ffwd_, s, step_off);
-    run_tail(s, step_off);
-    run(fbwd_, s, step_off);
+  if (rc_) {
+    run_rowchain(s, step_off, false);
   } else {
     run(fwd_, s, step_off);
     run(bwd_, s, step_off);
@@ -162,7 +182,6 @@ void Executor::destroy_graphs() {
 
 int Executor::pick_cfg(long long M, long long N, long long K) const {
   if (c_.force_cfg >= 0) return c_.force_cfg;
-  if (K <= c_.lat64_max_k && N >= 64 && M >= 128 && !(M >= 256 && N >= c_.thr_min_n && K >= c_.thr_min_k)) return 3;
   if (M >= 256 && N >= c_.thr_min_n && K >= c_.thr_min_k) {
     // 128x128 tiles while they give every CU at least two workgroups (256 CUs),
     // else 128x64 tiles (twice the workgroups; measured on MI355X, profiles/)
@@ -241,10 +260,6 @@ std::vector<Executor::Launch> Executor::build_forward(bool eval, long long chunk
       p.lda = eval ? src->ldx : c_.ldx;
       p.sA = eval ? src->sX : c_.sX;
       p.a_gather = 1;
-      if (!eval && c_.Xp) {  // the epoch's batch rows are contiguous in the permuted copy
-        p.A = reinterpret_cast<const void*>(c_.Xp);
-        p.a_rowstep = 1;
-      }
     } else {
       const LayerCfg& pv = c_.layers[l - 1];
       p.A = reinterpret_cast<const void*>(pv.D);
@@ -340,7 +355,7 @@ std::vector<Executor::Launch> Executor::build_forward(bool eval, long long chunk
         La.ga.nprob = 1;
       }
     }
-    if (l == 0 && !eval && L > 0 && !c_.XpT) {
+    if (l == 0 && !eval && L > 0) {
       // X^T of the batch for the layer-0 weight gradient, in the same launch
       Prob t = base_prob();
       t.kind = PK_GATHER_T;
@@ -379,13 +394,7 @@ void Executor::build() {
     const LayerCfg& ly = c_.layers[l];
     Prob w = base_prob();
     w.kind = PK_DW_UPDATE;
-    if (l == 0 && c_.XpT) {
-      // X^T of this step's batch = columns [step*B, step*B + Bp) of the epoch's
-      // permuted X^T: no per-step gather-transpose launch problem
-      w.A = reinterpret_cast<const void*>(c_.XpT);
-      w.sA = (long long)ly.Kp * c_.ldxpt;
-      w.a_colstep = 1;
-    } else if (l == 0) {
+    if (l == 0) {
       w.A = reinterpret_cast<const void*>(c_.XT);
       w.sA = (long long)ly.Kp * c_.Bp;
     } else {
@@ -393,7 +402,7 @@ void Executor::build() {
       w.A = reinterpret_cast<const void*>(pv.DT);
       w.sA = (long long)pv.N * c_.Bp;
     }
-    w.lda = (l == 0 && c_.XpT) ? c_.ldxpt : c_.Bp;
+    w.lda = c_.Bp;
     w.M = ly.K + (ly.has_bias ? 1 : 0);
     w.ones_row = ly.has_bias ? ly.K : -1;
     w.N = ly.N;
@@ -475,10 +484,10 @@ void Executor::advance(int nsteps, hipStream_t s) const {
 
 void Executor::train_launch(int idx, hipStream_t s) {
   // one launch of the active step plan, step_off 0, no counter advance
-  if (fused_) {
-    if (idx == (int)ffwd_.size()) { run_tail(s, 0); return; }
-    const Launch& L = idx < (int)ffwd_.size() ? ffwd_[idx] : fbwd_[idx - ffwd_.size() - 1];
-    check(ea_gemm_grouped(&L.ga, c_.bf16, L.cfg, s), "train_launch");
+  if (rc_) {
+    if (idx == 0) check(ea_gemm_table(&rc_.ta_fwd, c_.bf16, 0, s), "train_launch");
+    else if (idx == 1) check(ea_rowchain(&rc_.rc, c_.bf16, rc_.nbw, s), "train_launch");
+    else check(ea_gemm_table(&rc_.ta_dw, c_.bf16, 1, s), "train_launch");
     return;
   }
   const int nf = (int)fwd_.size();
@@ -504,17 +513,18 @@ void Executor::grad_launch(int idx, hipStream_t s) {
 
 void Executor::set_stamps(uintptr_t buf) {
   long long* p = reinterpret_cast<long long*>(buf);
-  for (auto* v : {&fwd_, &bwd_, &ffwd_, &fbwd_})
+  for (auto* v : {&fwd_, &bwd_})
     for (auto& L : *v) L.ga.stamps = p;
-  fa_.stamps = p;
+  rc_.ta_fwd.stamps = rc_.ta_dw.stamps = rc_.ta_grad.stamps = p;
+  rc_.rc.stamps = p;
 }
 
 std::vector<int> Executor::launch_blocks() const {
   std::vector<int> v;
-  if (fused_) {
-    for (auto& L : ffwd_) v.push_back(L.ga.total_blocks);
-    v.push_back(c_.R * fa_.nsplit);
-    for (auto& L : fbwd_) v.push_back(L.ga.total_blocks);
+  if (rc_) {
+    v.push_back(rc_.ta_fwd.total_blocks);
+    v.push_back(c_.R * cdiv(c_.B, RC_ROWS));
+    v.push_back(rc_.ta_dw.total_blocks);
     return v;
   }
   for (auto& L : fwd_) v.push_back(L.ga.total_blocks);
@@ -522,14 +532,17 @@ std::vector<int> Executor::launch_blocks() const {
   return v;
 }
 
+std::vector<int> Executor::table_begins(int launch) const {
+  std::vector<int> v;
+  if (!rc_ || launch == 1) return v;
+  const TableArgs& ta = launch == 0 ? rc_.ta_fwd : rc_.ta_dw;
+  for (int i = 0; i < ta.nprob; ++i) v.push_back(ta.begin[i]);
+  return v;
+}
+
 std::vector<int> Executor::launch_cfgs() const {
   std::vector<int> v;
-  if (fused_) {
-    for (auto& L : ffwd_) v.push_back(L.cfg);
-    v.push_back(-1);  // fused tail
-    for (auto& L : fbwd_) v.push_back(L.cfg);
-    return v;
-  }
+  if (rc_) return {0, -1, 3};  // table launches (64x32 / 64x64 tiles), the row chain (-1)
   for (auto& L : fwd_) v.push_back(L.cfg);
   for (auto& L : bwd_) v.push_back(L.cfg);
   return v;
@@ -541,6 +554,10 @@ void Executor::train_step(hipStream_t s) {
 }
 
 void Executor::forward_backward(hipStream_t s) {
+  if (rc_) {
+    run_rowchain(s, 0, true);
+    return;
+  }
   run(fwd_, s, 0);
   for (auto L : bwd_) {
     for (int i = 0; i < L.ga.nprob; ++i)
@@ -581,9 +598,6 @@ FlatArgs Executor::flat_args() const {
   a.WTsh = reinterpret_cast<void*>(c_.WTsh);
   a.sWTsh = c_.sWTsh;
   a.wtsh_par = c_.wtsh_par;
-  a.Bsh = reinterpret_cast<float*>(c_.Bsh);
-  a.sBsh = c_.sBsh;
-  a.bsh_par = c_.bsh_par;
   a.ctr = reinterpret_cast<long long*>(c_.ctr);
   a.ntrain = reinterpret_cast<const int*>(c_.ntrain);
   a.B = c_.B;

@@ -4,8 +4,11 @@
 // (reference elephas/worker.py:26-49 SparkWorker.train, :76-131
 // AsynchronousSparkWorker.train) with a plan of grouped MFMA launches:
 //
-//   step = [FWD_0 + gather X^T] [FWD_1] ... [FWD_{L-1} + loss]   (L launches)
-//          [DW_{L-1} + DX_{L-1}] ... [DW_0 (+ counter advance)]  (L launches)
+//   grouped plan:   [FWD_0 + gather X^T] [FWD_1] ... [FWD_{L-1} + loss]   (L launches)
+//                   [DW_{L-1} + DX_{L-1}] ... [DW_0]                      (L launches)
+//   row-chain plan  (small MLPs, csrc/kernels/rowchain.hip; 3 launches):
+//                   [layer-0 split-K slabs + gather X^T] [row chain: layers 1..L-1
+//                   forward, loss, dZ_{L-1} .. dZ_0] [DW of every layer]
 //
 // The step reads its batch index, dropout counter and optimizer iteration from
 // device counters, so one captured hipGraph of a step is replayed for every
@@ -43,26 +46,21 @@ struct ExecCfg {
   uintptr_t perm = 0; long long sPerm = 0;
   uintptr_t ntrain = 0, vstart = 0, vcount = 0;
   uintptr_t XT = 0;
-  // optional per-epoch pre-permuted copies of the training shard (B % 8 == 0):
-  // Xp [R][nmax][ldx] row-major, XpT [R][ldx][ldxpt] transposed
-  uintptr_t Xp = 0, XpT = 0; long long ldxpt = 0;
   // parameters
   uintptr_t P = 0; long long sP = 0, nparams = 0;
   uintptr_t G = 0; long long sG = 0;
   uintptr_t S = 0; long long sS = 0;
   uintptr_t Wsh = 0; long long sWsh = 0, wsh_par = 0;
   uintptr_t WTsh = 0; long long sWTsh = 0, wtsh_par = 0;
-  uintptr_t Bsh = 0; long long sBsh = 0, bsh_par = 0;  // fp32 bias images (fused tail)
   OptParams op{};
   int loss = 0, nmet = 0, met[4] = {0, 0, 0, 0};
   uintptr_t acc = 0; int acc_stride = 6;
   uintptr_t ctr = 0;
   int force_cfg = -1;  // -1 auto, 0 LAT, 1 THR, 2 THR-N64
   int thr_min_n = 256;
-  int lat64_max_k = 0;  // reductions this shallow use the 64x64 split-K-2 tile (0 = off)
   int thr_min_k = 64;  // smallest reduction depth for the 128-row THR tiles (Otto DW, K = batch 128: 135 -> 127 us/step)
-  int fused = -1;      // fused small-MLP tail: -1 auto (when eligible), 0 off, 1 required
-  int fused_split = 16; // workgroups per replica in the fused tail
+  int rowchain = -1;   // row-chain step plan: -1 when eligible, 0 off, 1 required
+  int rc_split = 0;    // layer-0 split-K slabs of the row-chain plan (0 = auto)
 };
 
 struct EvalSource {
@@ -96,10 +94,10 @@ class Executor {
   void replay(int graph_id, hipStream_t s);
   void destroy_graphs();
 
-  // GEMM launches per step (a captured chunk adds one 1-block counter advance)
-  int launches_per_step() const { return fused_ ? (int)ffwd_.size() + 1 + (int)fbwd_.size() : (int)fwd_.size() + (int)bwd_.size(); }
-  bool fused() const { return fused_; }
-  int fused_lds_bytes() const { return fused_ ? fa_.lds_bytes : 0; }
+  // launches per step (a captured chunk adds one 1-block counter advance)
+  int launches_per_step() const { return rc_.on ? 3 : (int)fwd_.size() + (int)bwd_.size(); }
+  bool rowchain() const { return rc_.on; }
+  int rowchain_split() const { return rc_.on ? rc_.nsplitk : 0; }
   std::vector<int> launch_cfgs() const;
   // diagnostics: bind a [blocks_max][16] int64 buffer for in-kernel stamps (0 = off)
   void set_stamps(uintptr_t buf);
@@ -111,6 +109,8 @@ class Executor {
   int grad_launch_layer(int idx) const;
   void grad_launch(int idx, hipStream_t s);
   std::vector<int> launch_blocks() const;
+  // row-chain plan: first block of every problem of table launch i (0: A, 2: C)
+  std::vector<int> table_begins(int launch) const;
 
  private:
   struct Launch {
@@ -119,13 +119,19 @@ class Executor {
   };
   ExecCfg c_;
   std::vector<Launch> fwd_, bwd_;
-  // fused plan: [FWD_0 + X^T gather] [fused tail, one block per replica] [DW_0 update]
-  bool fused_ = false;
-  std::vector<Launch> ffwd_, fbwd_;
-  FusedArgs fa_{};
-  FusedLayer* d_fly_ = nullptr;
-  bool build_fused();
-  void run_tail(hipStream_t s, int step_off) const;
+  // row-chain plan: table launch A {layer-0 partial slabs, X^T gather}, row chain B,
+  // table launch C {DW of every layer} (update, or gradient for the all-reduce path)
+  struct RowChain {
+    bool on = false;
+    int nbw = 2, nsplitk = 1;
+    TableArgs ta_fwd{}, ta_dw{}, ta_grad{};
+    RcArgs rc{};
+    explicit operator bool() const { return on; }
+  } rc_;
+  Prob* d_probs_ = nullptr;   // device tables of the row-chain launches
+  float* d_zp_ = nullptr;     // layer-0 split-K slabs [R][nsplitk][B][N0]
+  bool build_rowchain();
+  void run_rowchain(hipStream_t s, int step_off, bool grad) const;
   void run_step(hipStream_t s, int step_off) const;
   std::vector<std::pair<hipGraph_t, hipGraphExec_t>> graphs_;
 

@@ -24,10 +24,9 @@ SOURCES = [
     "kernels/gemm_cfg0_bf16.hip",
     "kernels/gemm_cfg1_bf16.hip",
     "kernels/gemm_cfg2_bf16.hip",
-    "kernels/gemm_cfg3_bf16.hip",
     "kernels/gemm_f32.hip",
     "kernels/flat.hip",
-    "kernels/fused.hip",
+    "kernels/rowchain.hip",
     "runtime/executor.cpp",
     "runtime/rwlock.cpp",
     "runtime/param_server.cpp",

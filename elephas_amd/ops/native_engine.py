@@ -12,10 +12,11 @@ T is bf16 under the 'mixed_bfloat16' policy and fp32 otherwise.  The fused
 update epilogue writes the next step's shadow parity while this step's DX
 GEMMs still read the current one, so DW and DX of a layer share one launch.
 
-One training step is 2L grouped launches; the step is captured once as a
-hipGraph (natively, in csrc/runtime/executor.cpp) and replayed for every step
-of every epoch because batch index, dropout counter and optimizer iteration are
-read from device counters.
+A training step is 3 launches on the row-chain plan (small MLPs: every layer but
+the last <= 256 wide, a last layer <= 32 wide -- csrc/kernels/rowchain.hip) and 2L
+grouped launches otherwise; the step is captured once as a hipGraph (natively, in
+csrc/runtime/executor.cpp) and replayed for every step of every epoch because
+batch index, dropout counter and optimizer iteration are read from device counters.
 """
 from __future__ import annotations
 
@@ -41,13 +42,12 @@ class NativeTrainer(TrainerBase):
     GRAPH_CHUNK = 16
 
     def __init__(self, model, plan, R: int = 1, batch_size: int = 32, device=None, seed: Optional[int] = None,
-                 policy: Optional[str] = None, eval_batch: int = 2048, fused: Optional[int] = None):
+                 policy: Optional[str] = None, eval_batch: int = 2048, rowchain: Optional[int] = None):
         super().__init__(model, plan, R, batch_size)
         self.C = native.require()
-        # fused small-MLP tail kernel (csrc/kernels/fused.hip): None -> $ELEPHAS_AMD_FUSED
-        # (default 0: the grouped per-layer launches measure faster on MI355X, see
-        # profiles/README.md), -1 when eligible, 1 required
-        self.fused_mode = int(os.environ.get("ELEPHAS_AMD_FUSED", "0")) if fused is None else int(fused)
+        # row-chain step plan (3 launches, csrc/kernels/rowchain.hip): None ->
+        # $ELEPHAS_AMD_ROWCHAIN (default -1: whenever the model is eligible), 0 off, 1 required
+        self.rowchain_mode = int(os.environ.get("ELEPHAS_AMD_ROWCHAIN", "-1")) if rowchain is None else int(rowchain)
         if not plan.native_ok:
             raise ValueError(f"model is not supported by the native engine: {plan.reason}")
         self.dev = torch.device(device) if device is not None else config.get_device()
@@ -93,10 +93,6 @@ class NativeTrainer(TrainerBase):
             self.G = torch.zeros(R, self.n, dtype=torch.float32, device=dev)
             self.Wsh = torch.zeros(R, 2, max(wsh, 1), dtype=self.T, device=dev)
             self.WTsh = torch.zeros(R, 2, max(wtsh, 1), dtype=self.T, device=dev)
-            # fp32 bias images per parity for the fused tail (indexed like P); only
-            # small MLPs are eligible, so the [R, 2, n] mirror stays small
-            self.Bsh = torch.zeros(R, 2, self.n, dtype=torch.float32, device=dev) \
-                if self.fused_mode != 0 and self.n <= (4 << 20) else None
             self.ctr = torch.zeros(2 + R, dtype=torch.int64, device=dev)
             self.acc = torch.zeros(R, 6, dtype=torch.float64, device=dev)
             self.acc_val = torch.zeros(R, 6, dtype=torch.float64, device=dev)
@@ -110,15 +106,6 @@ class NativeTrainer(TrainerBase):
             self.ntrain = torch.zeros(R, dtype=torch.int32, device=dev)
             self.vstart = torch.zeros(R, dtype=torch.int32, device=dev)
             self.vcount = torch.zeros(R, dtype=torch.int32, device=dev)
-        # optional per-epoch pre-permuted copies of the shards (ELEPHAS_AMD_XP=1): layer 0
-        # reads contiguous batch rows and its weight update a column window of X^T, so
-        # the step has no perm-indirect gather and no gather-transpose workgroups
-        # (-3.3 us of kernel time per MNIST step), but the one-pass permute kernel per
-        # epoch costs about as much at ~105 steps per epoch: measured 67.0 vs 65.7
-        # us/step on MNIST, equal on Otto (profiles/README.md) -- off by default
-        self.xp_layout = (self.B % 8 == 0 and self.fused_mode == 0 and self.bf16 and
-                          os.environ.get("ELEPHAS_AMD_XP", "0") == "1")
-        self.Xp = self.XpT = None
         self.ntrain_h = [0] * R
         self.vcount_h = [0] * R
         self.active = [True] * R
@@ -160,24 +147,19 @@ class NativeTrainer(TrainerBase):
             force_cfg=int(os.environ.get("ELEPHAS_AMD_GEMM_CFG", "-1")),
             thr_min_k=int(os.environ.get("ELEPHAS_AMD_THR_MIN_K", "64")),
             thr_min_n=int(os.environ.get("ELEPHAS_AMD_THR_MIN_N", "256")),
-            lat64_max_k=int(os.environ.get("ELEPHAS_AMD_LAT64_MAX_K", "0")),
-            fused=self.fused_mode if ws is self.ws else 0,
-            fused_split=int(os.environ.get("ELEPHAS_AMD_FUSED_SPLIT", "16")),
+            rowchain=self.rowchain_mode if ws is self.ws else 0,
+            rc_split=int(os.environ.get("ELEPHAS_AMD_RC_SPLIT", "0")),
             layers=layers,
             X=self.X.data_ptr(), sX=self.nmax * self.Kp0, ldx=self.Kp0,
             Y=self.Y.data_ptr(), sY=self.nmax * self.ldy, ldy=self.ldy,
             perm=self.perm.data_ptr(), sPerm=self.nmax,
             ntrain=self.ntrain.data_ptr(), vstart=self.vstart.data_ptr(), vcount=self.vcount.data_ptr(),
             XT=ws["XT"].data_ptr(),
-            Xp=self.Xp.data_ptr() if (self.Xp is not None and ws is self.ws) else 0,
-            XpT=self.XpT.data_ptr() if (self.XpT is not None and ws is self.ws) else 0,
-            ldxpt=getattr(self, "ldxpt", 0),
             P=self.P.data_ptr(), sP=self.n, nparams=self.n,
             G=self.G.data_ptr(), sG=self.n,
             S=self.S.data_ptr(), sS=self.S.shape[1] * self.n,
             Wsh=self.Wsh.data_ptr(), sWsh=2 * self.Wsh.shape[2], wsh_par=self.Wsh.shape[2],
             WTsh=self.WTsh.data_ptr(), sWTsh=2 * self.WTsh.shape[2], wtsh_par=self.WTsh.shape[2],
-            Bsh=self.Bsh.data_ptr() if self.Bsh is not None else 0, sBsh=2 * self.n, bsh_par=self.n,
             opt=opt, loss=self.loss.native, metrics=[m.native for m in self.metrics],
             acc=self.acc.data_ptr(), acc_stride=6, ctr=self.ctr.data_ptr())
 
@@ -286,13 +268,9 @@ class NativeTrainer(TrainerBase):
         nmax = max(1, max(len(x) for x in xs))
         self._enter()
         with torch.cuda.stream(self.stream):
-            if nmax != self.nmax or (self.xp_layout and self.Xp is None):
+            if nmax != self.nmax:
                 self.nmax = nmax
                 self.X = torch.zeros(self.R, nmax, self.Kp0, dtype=self.T, device=self.dev)
-                if self.xp_layout:
-                    self.Xp = torch.zeros(self.R, nmax, self.Kp0, dtype=self.T, device=self.dev)
-                    self.ldxpt = pad8(nmax) + pad8(self.B)   # zero tail: last partial batch
-                    self.XpT = torch.zeros(self.R, self.Kp0, self.ldxpt, dtype=self.T, device=self.dev)
                 self.Y = torch.zeros(self.R, nmax, self.ldy, dtype=torch.float32, device=self.dev)
                 self.perm = torch.zeros(self.R, nmax, dtype=torch.int32, device=self.dev)
                 rebuild = True
@@ -334,9 +312,6 @@ class NativeTrainer(TrainerBase):
                 self.perm.copy_(torch.argsort(keys, dim=1).to(torch.int32))
             else:
                 self.perm.copy_(torch.arange(nmax, device=self.dev, dtype=torch.int32).expand(R, nmax))
-            if self.Xp is not None:   # one pass: Xp rows in epoch order + their transpose
-                self.C.permute_rows(self.X.data_ptr(), self.perm.data_ptr(), self.Xp.data_ptr(), self.XpT.data_ptr(),
-                                    R, nmax, self.Kp0, self.ldxpt, self.s)
 
     # ------------------------------------------------------------------ train
     def steps_per_epoch(self) -> int:
@@ -539,6 +514,6 @@ class NativeTrainer(TrainerBase):
         return self.exe.launches_per_step()
 
     @property
-    def fused(self) -> bool:
-        """True when training steps run the fused small-MLP tail kernel (csrc/kernels/fused.hip)."""
-        return bool(self.exe.fused())
+    def rowchain(self) -> bool:
+        """True when training steps run the 3-launch row-chain plan (csrc/kernels/rowchain.hip)."""
+        return bool(self.exe.rowchain())

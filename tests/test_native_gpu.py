@@ -195,13 +195,13 @@ def test_graph_replay_equals_eager():
     assert not np.array_equal(ws[0][0], ws[0][1])  # replicas draw different dropout masks
 
 
-def _fit_weights(model, policy, B, xs, ys, fused, epochs=1, val=0.0, R=None, seed=7):
+def _fit_weights(model, policy, B, xs, ys, rowchain, epochs=1, val=0.0, R=None, seed=7):
     from elephas_amd import config
     from elephas_amd.ops.plan import build_plan
     from elephas_amd.ops.native_engine import NativeTrainer
     config.set_policy(policy)
     R = R or len(xs)
-    t = NativeTrainer(model, build_plan(model), R, B, torch.device("cuda"), seed=seed, fused=fused)
+    t = NativeTrainer(model, build_plan(model), R, B, torch.device("cuda"), seed=seed, rowchain=rowchain)
     t.set_data(xs, ys, val, shuffle=True)
     np.random.seed(3)
     torch.manual_seed(5)   # epoch shuffles draw from the global CUDA generator
@@ -209,13 +209,14 @@ def _fit_weights(model, policy, B, xs, ys, fused, epochs=1, val=0.0, R=None, see
     return t, t.get_weights_flat(), h
 
 
-def _fused_case(case, fmode):
+def _plan_case(case):
     from elephas_amd.models.optimizers import SGD, Adam, RMSprop
     rng = np.random.default_rng(11)
-    if case == "mnist_bf16_dropout":
+    if case in ("mnist_bf16_dropout", "mnist_f32_dropout"):
         model = _mlp(784, [128, 128], 10, dropout=0.2)
         model.compile(SGD(learning_rate=0.1), "categorical_crossentropy", ["acc"])
-        policy, B, d, k, tol = "mixed_bfloat16", 64, 784, 10, 2e-2
+        policy, tol = ("mixed_bfloat16", 2e-2) if "bf16" in case else ("float32", 1e-4)
+        B, d, k = 64, 784, 10
         sizes = [300, 130, 40]            # third replica runs out of batches early
     elif case == "tanh_f32_adam":
         model = _mlp(30, [64, 48], 5, act="tanh", dropout=0.1)
@@ -243,12 +244,20 @@ def _fused_case(case, fmode):
             y = np.eye(k, dtype=np.float32)[rng.integers(0, k, n)]
         xs.append(x)
         ys.append(y)
-    tf, wf, hf = _fit_weights(model, policy, B, xs, ys, fused=fmode, epochs=2, val=0.1)
-    tg, wg, hg = _fit_weights(model, policy, B, xs, ys, fused=0, epochs=2, val=0.1)
-    assert tf.fused and not tg.fused
+    tf, wf, hf = _fit_weights(model, policy, B, xs, ys, rowchain=1, epochs=2, val=0.1)
+    tg, wg, hg = _fit_weights(model, policy, B, xs, ys, rowchain=0, epochs=2, val=0.1)
+    assert tf.rowchain and not tg.rowchain
     assert tf.launch_count() == 3
-    scale = np.abs(wg).max()
-    assert np.abs(wf - wg).max() <= tol * scale, (np.abs(wf - wg).max(), scale)
+    if policy == "float32":
+        scale = np.abs(wg).max()
+        assert np.abs(wf - wg).max() <= tol * scale, (np.abs(wf - wg).max(), scale)
+    else:
+        # bf16 weight images: the plans sum layer 0 in different orders, and a 1-ulp
+        # fp32 difference can flip a bf16 rounding that later steps carry on
+        # (the fp32 cases pin the plans' equivalence tightly); compare on average
+        w0 = np.concatenate([w.reshape(-1) for w in model.get_weights()])
+        err = np.abs(wf - wg).mean() / np.abs(wg - w0).mean()
+        assert err < tol, err
     for a, b in zip(hf, hg):
         if a is None:
             assert b is None
@@ -257,7 +266,7 @@ def _fused_case(case, fmode):
             assert np.allclose(a[key], b[key], rtol=5 * tol, atol=5 * tol), (key, a[key], b[key])
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3])
+@pytest.mark.parametrize("cfg", [0, 1, 2])
 @pytest.mark.parametrize("bf16", [1, 0])
 @pytest.mark.parametrize("M,N,K", [(64, 128, 784), (64, 10, 128), (785, 128, 64), (300, 200, 136), (512, 512, 512)])
 def test_plain_gemm_matches_torch_fp32(M, N, K, bf16, cfg):
@@ -285,8 +294,8 @@ def test_plain_gemm_rejects_misaligned_shapes():
         C.gemm_nt(A.data_ptr(), A.data_ptr(), A.data_ptr(), 4, 4, 10, 10, 10, 4, 0, 0, 0)
 
 
-@pytest.mark.parametrize("fused", [0, 1, 2])
-def test_training_is_bit_deterministic(fused):
+@pytest.mark.parametrize("rowchain", [0, 1])
+def test_training_is_bit_deterministic(rowchain):
     """Same seeds -> bit-identical weights (no races between the update epilogue
     and the GEMMs that read the weight shadows, no order-dependent reductions)."""
     from elephas_amd.models.optimizers import SGD
@@ -295,8 +304,8 @@ def test_training_is_bit_deterministic(fused):
     model.compile(SGD(learning_rate=0.1), "categorical_crossentropy", ["acc"])
     xs = [rng.random((n, 784), dtype=np.float32) for n in (300, 130, 40)]
     ys = [np.eye(10, dtype=np.float32)[rng.integers(0, 10, len(x))] for x in xs]
-    _, w1, _ = _fit_weights(model, "mixed_bfloat16", 64, xs, ys, fused=fused, epochs=2, val=0.1)
-    _, w2, _ = _fit_weights(model, "mixed_bfloat16", 64, xs, ys, fused=fused, epochs=2, val=0.1)
+    _, w1, _ = _fit_weights(model, "mixed_bfloat16", 64, xs, ys, rowchain=rowchain, epochs=2, val=0.1)
+    _, w2, _ = _fit_weights(model, "mixed_bfloat16", 64, xs, ys, rowchain=rowchain, epochs=2, val=0.1)
     assert np.array_equal(w1, w2), np.abs(w1 - w2).max()
 
 
@@ -420,30 +429,14 @@ def test_spark_model_granularities_native_vs_torch(gran, tmp_path):
     assert np.abs(ws[0] - ws[1]).max() < 2e-4, np.abs(ws[0] - ws[1]).max()
 
 
-@pytest.mark.parametrize("case", ["mnist_bf16_dropout", "tanh_f32_adam", "mse_f32", "sparse_bf16_rmsprop"])
-def test_deferred_tail_matches_grouped_path(case):
-    """Fused mode 2: one workgroup per replica runs layers 1..L-1 forward, loss and
-    input gradients in LDS; layer 1's update is deferred into layer 0's grouped
-    launch (3 launches per step, no cross-workgroup writes inside the tail)."""
-    _fused_case(case, 2)
-
-
-def test_permuted_epoch_layout_matches_gather_path(monkeypatch):
-    """ELEPHAS_AMD_XP=1 (per-epoch permuted X / X^T copies) trains bit-identically to
-    the per-step perm-gather path (same rows, same order, same math)."""
-    from elephas_amd.models.optimizers import SGD
-    rng = np.random.default_rng(5)
-    model = _mlp(784, [128, 128], 10, dropout=0.2)
-    model.compile(SGD(learning_rate=0.1), "categorical_crossentropy", ["acc"])
-    xs = [rng.random((n, 784), dtype=np.float32) for n in (300, 131, 64)]
-    ys = [np.eye(10, dtype=np.float32)[rng.integers(0, 10, len(x))] for x in xs]
-    ws = []
-    for xp in ("0", "1"):
-        monkeypatch.setenv("ELEPHAS_AMD_XP", xp)
-        t, w, _ = _fit_weights(model, "mixed_bfloat16", 64, xs, ys, fused=0, epochs=2, val=0.1)
-        assert (t.Xp is not None) == (xp == "1")
-        ws.append(w)
-    assert np.array_equal(ws[0], ws[1]), np.abs(ws[0] - ws[1]).max()
+@pytest.mark.parametrize("case", ["mnist_bf16_dropout", "mnist_f32_dropout", "tanh_f32_adam", "mse_f32",
+                                  "sparse_bf16_rmsprop"])
+def test_rowchain_matches_grouped_path(case):
+    """Row-chain plan (3 launches: layer-0 split-K slabs, one row-local chain kernel for
+    layers 1..L-1 forward / loss / input gradients, one DW launch for every layer) ==
+    the grouped 2L-launch plan: same dropout masks, same update rules, fp32
+    accumulation (only the layer-0 summation order differs)."""
+    _plan_case(case)
 
 
 @pytest.mark.parametrize("mode,freq", [("synchronous", "epoch"), ("asynchronous", "epoch"), ("asynchronous", "batch"),

@@ -5,8 +5,8 @@ import bench
 from elephas_amd import config
 from elephas_amd.ops.plan import build_plan
 from elephas_amd.ops.native_engine import NativeTrainer
-config.set_policy("mixed_bfloat16")
-# usage: stamps.py [replicas] [model] [batch]
+# usage: stamps.py [replicas] [model] [batch] [policy]
+config.set_policy(sys.argv[4] if len(sys.argv) > 4 else "float32")
 MODEL = sys.argv[2] if len(sys.argv) > 2 else "mnist"
 BATCH = int(sys.argv[3]) if len(sys.argv) > 3 else 64
 m = bench.build_model(MODEL)
@@ -26,17 +26,18 @@ names = ["start", "setup", "mainloop", "reduce", "end", "e5", "e6", "e7", "e8"]
 cfgs = t.exe.launch_cfgs()
 for rep in range(2):
     for i, nb in enumerate(blocks):
-        if cfgs[i] == -1:  # fused tail: 32 stamps per block
+        if cfgs[i] == -1:  # row chain: stamps 0..15 per block (rowchain.hip rstamp)
             buf.zero_()
             torch.cuda.synchronize()
             t.exe.train_launch(i, t.s)
             t.stream.synchronize()
-            st = buf[:nb * 32].view(nb, 32).cpu().numpy().astype(np.int64)
+            st = buf[:nb * 16].view(nb, 16).cpu().numpy().astype(np.int64)
             if rep == 1:
                 t0 = st[:, 0].min()
                 rel = np.where(st > 0, (st - t0) * 10.0, np.nan)
                 med = np.nanmedian(rel, axis=0)
-                print(f"launch {i} fused tail blocks {nb}: " + " ".join(f"{k}:{v:.0f}" for k, v in enumerate(med) if v == v), flush=True)
+                print(f"launch {i} row chain blocks {nb}: median(ns) " +
+                      " ".join(f"{k}:{v:.0f}" for k, v in enumerate(med) if v == v), flush=True)
             continue
         buf.zero_()
         torch.cuda.synchronize()
@@ -54,4 +55,11 @@ for rep in range(2):
             print(f"  est. s_memtime MHz {mhz:.0f}", flush=True)
             print(f"launch {i} blocks {nb}: median(ns) " + " ".join(f"{n}={v:.0f}" for n, v in zip(names, med)) +
                   f" | max end {mx[4]:.0f} | start spread {mx[0]:.0f}", flush=True)
+            begins = list(t.exe.table_begins(i)) if hasattr(t.exe, "table_begins") else []
+            for pi, b0 in enumerate(begins):
+                b1 = begins[pi + 1] if pi + 1 < len(begins) else nb
+                sub = rel[b0:b1]
+                print(f"    problem {pi} blocks [{b0},{b1}): median " +
+                      " ".join(f"{n}={v:.0f}" for n, v in zip(names, np.nanmedian(sub, axis=0))) +
+                      f" | p90 end {np.nanpercentile(sub[:, 4], 90):.0f} max end {np.nanmax(sub[:, 4]):.0f}", flush=True)
 t.exe.set_stamps(0)
