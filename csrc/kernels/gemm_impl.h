@@ -61,8 +61,11 @@ __device__ __forceinline__ void gather_transpose_block(const GA& ga, const Prob&
   // one block = 64 batch rows x 64 features; output XT[k][m] (ld = lddt)
   // tiles_m: batch blocks, tiles_n: feature blocks
   const int per_r = p.tiles_m * p.tiles_n;
-  const int r = lb / per_r;
-  const int t = lb % per_r;
+  // replica-minor block order: with R = 8 a replica's blocks share one XCD (blocks
+  // are dealt round-robin over the 8 XCDs), so its operands are fetched into one L2
+  (void)per_r;
+  const int r = lb % p.R;
+  const int t = lb / p.R;
   const int b0 = (t / p.tiles_n) * 64;
   const int k0 = (t % p.tiles_n) * 64;
   const long long step = ga.ctr[0] + ga.step_off;
@@ -177,9 +180,9 @@ __device__ __forceinline__ void row_softmax_cce_reg(const Prob& p, int lane, con
 
 template <typename T>
 __device__ __forceinline__ void loss_rows_block(const GroupArgs& ga, const Prob& p, int lb, float* smem) {
-  const int r = lb / p.tiles_m;
+  const int r = lb % p.R;  // replica-minor block order (XCD affinity)
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int row0 = (lb % p.tiles_m) * LOSS_RPB;
+  const int row0 = (lb / p.R) * LOSS_RPB;
   const long long step = ga.ctr[0] + ga.step_off;
   const int valid = batch_valid(p, r, step);
   const bool train = !p.eval_mode && p.D;
@@ -482,8 +485,12 @@ __device__ __forceinline__ void run_prob(const GA& ga, const Prob& p, const int 
     const int tk = partial ? p.tiles_k : 1;
     const int per_mn = p.tiles_m * p.tiles_n;
     const int per_r = per_mn * tk;
-    const int r = lb / per_r;
-    const int tkm = lb % per_r;
+    // replica-minor block order: block lb -> replica lb % R, tile lb / R. With R = 8
+    // every block of a replica runs on one XCD (round-robin dealing), so the operands
+    // the replica's tiles share (dZ^T, X^T, W) are fetched from HBM into ONE L2
+    (void)per_r;
+    const int r = lb % p.R;
+    const int tkm = lb / p.R;
     const int kch = partial ? tkm / per_mn : 0;
     const int t = partial ? tkm - kch * per_mn : tkm;
     const int tm = t / p.tiles_n, tn = t % p.tiles_n;

@@ -175,8 +175,9 @@ __global__ __launch_bounds__(256) void rowchain_kernel(RcArgs a) {
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int i16 = lane & 15, g = lane >> 4;
   const int tiles = (a.B + RB - 1) / RB;
-  const int r = blockIdx.x / tiles;
-  const int m0 = (blockIdx.x - r * tiles) * RB;
+  (void)tiles;
+  const int r = blockIdx.x % a.R;  // replica-minor: a replica's row blocks share one XCD
+  const int m0 = (blockIdx.x / a.R) * RB;
   const long long s0 = a.ctr[0];
   const long long step = s0 + a.step_off;
   const long long cnt = (long long)a.ntrain[r] - step * a.B;
