@@ -587,13 +587,34 @@ __device__ __forceinline__ void opt_update_v(const OptParams& p, float (&w)[NV],
 }
 
 // ------------------------------------------------------------ step counters
+// Uniform reads of launch-invariant device words (step counters, per-replica row
+// counts): through the constant address space they are scalar loads (the cache is
+// invalidated at every dispatch, as for kernel arguments), issued together at the
+// top of the kernel instead of as vector loads, each waited for on its own.
+// Only for words nothing in the reading kernel writes.
+template <typename T> __device__ __forceinline__ T ld_inv(const T* p) {
+  return *(const __attribute__((address_space(4))) T*)(unsigned long long)p;
+}
+
+// a whole launch-invariant struct, dword by dword (unused words are dropped)
+template <typename T> __device__ __forceinline__ T ld_inv_struct(const T* p) {
+  static_assert(sizeof(T) % 4 == 0, "dword-sized struct");
+  T out;
+  const __attribute__((address_space(4))) unsigned* src =
+      (const __attribute__((address_space(4))) unsigned*)(unsigned long long)p;
+  unsigned* dst = reinterpret_cast<unsigned*>(&out);
+#pragma unroll
+  for (int i = 0; i < (int)(sizeof(T) / 4); ++i) dst[i] = src[i];
+  return out;
+}
+
 // see GroupArgs::step_off (args.h)
 __device__ __forceinline__ long long iter_at(const long long* ctr, const int* ntrain, int B, int r, long long s0,
                                              int off) {
-  const long long nb = ((long long)ntrain[r] + B - 1) / B;
+  const long long nb = ((long long)ld_inv(ntrain + r) + B - 1) / B;
   long long d = nb - s0;
   d = d < 0 ? 0 : (d > off ? off : d);
-  return ctr[2 + r] + d;
+  return ld_inv(ctr + 2 + r) + d;
 }
 
 }  // namespace ea

@@ -38,16 +38,16 @@ namespace ea {
 // ------------------------------------------------------------------ helpers
 __device__ __forceinline__ int batch_valid(const Prob& p, int r, long long step) {
   if (p.eval_mode) {
-    long long c = (long long)p.vcount[r] - p.chunk * p.B;
+    long long c = (long long)ld_inv(p.vcount + r) - p.chunk * p.B;
     return (int)(c < 0 ? 0 : (c > p.B ? p.B : c));
   }
-  long long c = (long long)p.ntrain[r] - step * p.B;
+  long long c = (long long)ld_inv(p.ntrain + r) - step * p.B;
   return (int)(c < 0 ? 0 : (c > p.B ? p.B : c));
 }
 
 // absolute data row for batch row m of replica r
 __device__ __forceinline__ long long batch_row(const Prob& p, int r, long long step, int m) {
-  if (p.eval_mode) return (long long)p.vstart[r] + p.chunk * p.B + m;
+  if (p.eval_mode) return (long long)ld_inv(p.vstart + r) + p.chunk * p.B + m;
   return (long long)p.perm[(long long)r * p.sPerm + step * p.B + m];
 }
 
@@ -68,7 +68,7 @@ __device__ __forceinline__ void gather_transpose_block(const GA& ga, const Prob&
   const int t = lb / p.R;
   const int b0 = (t / p.tiles_n) * 64;
   const int k0 = (t % p.tiles_n) * 64;
-  const long long step = ga.ctr[0] + ga.step_off;
+  const long long step = ld_inv(ga.ctr) + ga.step_off;
   const int valid = batch_valid(p, r, step);
   const T* A = reinterpret_cast<const T*>(p.A) + (long long)r * p.sA;
   T* XT = reinterpret_cast<T*>(p.DT) + (long long)r * p.sDT;
@@ -183,7 +183,7 @@ __device__ __forceinline__ void loss_rows_block(const GroupArgs& ga, const Prob&
   const int r = lb % p.R;  // replica-minor block order (XCD affinity)
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int row0 = (lb / p.R) * LOSS_RPB;
-  const long long step = ga.ctr[0] + ga.step_off;
+  const long long step = ld_inv(ga.ctr) + ga.step_off;
   const int valid = batch_valid(p, r, step);
   const bool train = !p.eval_mode && p.D;
   // LDS-staged transposed store (bf16 only: 8 rows x 2 B = one 16-byte store)
@@ -497,9 +497,9 @@ __device__ __forceinline__ void run_prob(const GA& ga, const Prob& p, const int 
     const int koff = partial ? kch * p.kchunk : 0;
     const int Keff = partial ? min(p.kchunk, p.K - koff) : p.K;
     const int m0 = tm * BM, n0 = tn * BN;
-    const long long step = ga.ctr[0] + ga.step_off;
+    const long long step = ld_inv(ga.ctr) + ga.step_off;
     // (every launcher passes a valid ntrain: the plain-GEMM entry points it at zeros)
-    const long long iter = iter_at(ga.ctr, p.ntrain, p.B, r, ga.ctr[0], ga.step_off);
+    const long long iter = iter_at(ga.ctr, p.ntrain, p.B, r, ld_inv(ga.ctr), ga.step_off);
     const int valid = (p.kind == PK_PLAIN) ? p.M : batch_valid(p, r, step);
     const bool skip_update = (p.kind == PK_DW_UPDATE) && valid == 0;
     stamp(ga, 1);
@@ -1039,8 +1039,13 @@ __global__ __launch_bounds__(256) void gemm_table(TableArgs ta) {
 #pragma unroll
   for (int j = 1; j < TABLE_MAX; ++j) i += (j < ta.nprob && bid >= ta.begin[j]) ? 1 : 0;
   i = __builtin_amdgcn_readfirstlane(i);
-  const Prob* __restrict__ p = ta.probs + i;
-  run_prob<T, WM, WN, WAVES_M, WAVES_N, KSPLIT, KM, (KM == KM_DW) ? 2 : 0>(ta, *p, bid - ta.begin[i], smem);
+  // Read the problem through the constant address space (as kernel arguments are):
+  // those loads are scalar and invariant, so hipcc keeps or rematerialises the
+  // fields; through a plain global pointer every field read after an epilogue store
+  // became a vector load with its own full memory round trip (the compiler cannot
+  // tell the table from the stored-to buffers)
+  const Prob p = ld_inv_struct(ta.probs + i);
+  run_prob<T, WM, WN, WAVES_M, WAVES_N, KSPLIT, KM, (KM == KM_DW) ? 2 : 0>(ta, p, bid - ta.begin[i], smem);
   stamp(ta, 4);
   stamp_clk(ta, 11);
 }

@@ -178,9 +178,9 @@ __global__ __launch_bounds__(256) void rowchain_kernel(RcArgs a) {
   (void)tiles;
   const int r = blockIdx.x % a.R;  // replica-minor: a replica's row blocks share one XCD
   const int m0 = (blockIdx.x / a.R) * RB;
-  const long long s0 = a.ctr[0];
+  const long long s0 = ld_inv(a.ctr);
   const long long step = s0 + a.step_off;
-  const long long cnt = (long long)a.ntrain[r] - step * a.B;
+  const long long cnt = (long long)ld_inv(a.ntrain + r) - step * a.B;
   const int valid = (int)(cnt < 0 ? 0 : (cnt > a.B ? a.B : cnt));
   if (valid == 0) return;  // no batch for this replica this step: DW skips its update too
   const long long iter = iter_at(a.ctr, a.ntrain, a.B, r, s0, a.step_off);
