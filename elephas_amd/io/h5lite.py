@@ -9,6 +9,17 @@ Attributes larger than one object-header message (64 KiB) are stored as a
 uint8 dataset ``__attr__<name>`` next to the object, and read back
 transparently (libhdf5 would need dense attribute storage for them).
 
+Reads, in addition, what h5py writes with libhdf5's default (earliest) file
+format -- i.e. files produced by TF/Keras ``model.save('x.h5')`` and Elephas:
+  * superblock versions 0/1, object header version 1
+  * old-style groups: symbol-table message -> v1 B-tree (group nodes) -> symbol
+    table nodes, link names in the group's local heap
+  * chunked datasets (v1 B-tree of raw-data chunks) with the deflate (gzip),
+    shuffle and fletcher32 filters
+  * variable-length strings (h5py ``str`` attributes) through the global heap
+Not read: dense (fractal-heap) link/attribute storage, which only the
+``libver='latest'`` format writes for groups or objects with many entries.
+
 The API is the h5py subset that Keras' HDF5 format and the reference use
 (reference elephas/spark_model.py:117-125, 377-381; ml_model.py:61-70,130-132,
 178-185, 265-266): ``File(path, mode)``, ``.attrs[...]``, ``create_group``,
@@ -113,7 +124,13 @@ def _parse_dtype(buf: bytes, off: int):
         return dt, 8 + 4
     if cls == 3:
         return np.dtype(f"S{size}"), 8
+    if cls == 9 and (bits[0] & 0x0F) == 1:  # variable-length string: {u32 len, u64 heap addr, u32 index}
+        return VLEN_STR, 8 + 12
     raise NotImplementedError(f"HDF5 datatype class {cls} (version {ver}) is not supported by h5lite")
+
+
+# marker for variable-length strings: elements are 16-byte global-heap references
+VLEN_STR = np.dtype([("len", "<u4"), ("addr", "<u8"), ("idx", "<u4")])
 
 
 def _space_msg(shape) -> bytes:
@@ -511,12 +528,14 @@ class _Reader:
                 k, v = self._attr(p)
                 attrs._d[k] = v
         if 0x08 in types:  # dataset
-            shape, dt, raw = None, None, None
+            shape, dt, raw, chunked, filters = None, None, None, None, []
             for mtype, p, size in msgs:
                 if mtype == 0x01:
                     shape = _parse_space(b, p)
                 elif mtype == 0x03:
                     dt, _ = _parse_dtype(b, p)
+                elif mtype == 0x0B:
+                    filters = self._filters(p)
                 elif mtype == 0x08:
                     ver, cls = b[p], b[p + 1]
                     if ver != 3:
@@ -527,12 +546,23 @@ class _Reader:
                     elif cls == 0:
                         ln = struct.unpack_from("<H", b, p + 2)[0]
                         raw = b[p + 4:p + 4 + ln]
+                    elif cls == 2:
+                        nd = b[p + 2]
+                        bt = struct.unpack_from("<Q", b, p + 3)[0]
+                        cdims = struct.unpack_from("<" + "I" * nd, b, p + 11)
+                        chunked = (bt, cdims)
                     else:
-                        raise NotImplementedError("chunked datasets are not supported by h5lite")
+                        raise NotImplementedError(f"layout class {cls}")
             shape = shape or ()
             n = int(np.prod(shape)) if shape else 1
-            arr = np.frombuffer(raw, dtype=dt, count=n if raw else 0)
-            arr = arr.reshape(shape) if raw else np.zeros(shape, dtype=dt)
+            if chunked is not None:
+                arr = self._read_chunked(chunked[0], chunked[1], shape, dt, filters)
+            else:
+                arr = np.frombuffer(raw, dtype=dt, count=n if raw else 0)
+                arr = arr.reshape(shape) if raw else np.zeros(shape, dtype=dt)
+            if dt == VLEN_STR:
+                arr = self._vlen_strings(arr)
+                dt = arr.dtype
             ds = Dataset(name, arr.astype(dt.newbyteorder("=")) if dt.kind in "iuf" else arr.copy())
             ds.attrs = attrs
             return ds
@@ -583,6 +613,8 @@ class _Reader:
         shape = shape if shape is not None else (0,)
         n = int(np.prod(shape)) if shape else 1
         arr = np.frombuffer(b, dtype=dt, count=n, offset=q).reshape(shape).copy()
+        if dt == VLEN_STR:
+            return name, self._vlen_strings(arr)
         if dt.kind in "iuf":
             arr = arr.astype(dt.newbyteorder("="))
         return name, arr
@@ -608,8 +640,135 @@ class _Reader:
             return name, None
         return name, struct.unpack_from("<Q", b, q)[0]
 
+    # -------------------------------------------------- old-style (v1) structures
     def _symbol_table(self, p, g, name):
-        raise NotImplementedError("old-style (symbol table) groups are not supported by h5lite")
+        """Symbol-table message: v1 B-tree of the group's symbol table nodes + the
+        local heap holding the link names."""
+        b = self.b
+        btree, heap = struct.unpack_from("<QQ", b, p)
+        if b[heap:heap + 4] != b"HEAP":
+            raise OSError("bad local heap signature")
+        data_addr = struct.unpack_from("<Q", b, heap + 24)[0]
+        for snod in self._btree_children(btree, 0):
+            if b[snod:snod + 4] != b"SNOD":
+                raise OSError("bad symbol table node signature")
+            nsym = struct.unpack_from("<H", b, snod + 6)[0]
+            q = snod + 8
+            for _ in range(nsym):
+                noff, ohdr = struct.unpack_from("<QQ", b, q)
+                q += 40  # name offset, header address, cache type, reserved, scratch pad
+                end = b.index(b"\x00", data_addr + noff)
+                lname = b[data_addr + noff:end].decode("utf-8")
+                g._children[lname] = self.read_obj(ohdr, name.rstrip("/") + "/" + lname)
+
+    def _btree_nodes(self, addr, node_type, ndims=0):
+        """Leaf entries (key, child address) of a v1 B-tree (type 0: group nodes,
+        type 1: raw-data chunks with ndims-dimensional keys)."""
+        b = self.b
+        if b[addr:addr + 4] != b"TREE":
+            raise OSError("bad v1 B-tree signature")
+        ntype, level = b[addr + 4], b[addr + 5]
+        if ntype != node_type:
+            raise OSError(f"unexpected B-tree node type {ntype}")
+        used = struct.unpack_from("<H", b, addr + 6)[0]
+        q = addr + 24
+        ksize = 8 if node_type == 0 else 8 + 8 * ndims
+        out = []
+        for _ in range(used):
+            key = b[q:q + ksize]
+            child = struct.unpack_from("<Q", b, q + ksize)[0]
+            q += ksize + 8
+            if level == 0:
+                out.append((key, child))
+            else:
+                out.extend(self._btree_nodes(child, node_type, ndims))
+        return out
+
+    def _btree_children(self, addr, node_type):
+        return [c for _, c in self._btree_nodes(addr, node_type)]
+
+    def _filters(self, p):
+        """Filter pipeline message (versions 1 and 2) -> [(filter id, client values)]."""
+        b = self.b
+        ver, nf = b[p], b[p + 1]
+        q = p + (8 if ver == 1 else 2)
+        out = []
+        for _ in range(nf):
+            fid = struct.unpack_from("<H", b, q)[0]
+            q += 2
+            nlen = 0
+            if ver == 1 or fid >= 256:
+                nlen = struct.unpack_from("<H", b, q)[0]
+                q += 2
+            flags, nval = struct.unpack_from("<HH", b, q)
+            q += 4
+            if ver == 1:
+                nlen = (nlen + 7) // 8 * 8
+            q += nlen
+            vals = struct.unpack_from("<" + "I" * nval, b, q)
+            q += 4 * nval
+            if ver == 1 and nval % 2:
+                q += 4
+            out.append((fid, vals))
+        return out
+
+    def _read_chunked(self, btree, cdims, shape, dt, filters):
+        """Assemble a chunked dataset from the raw-data chunk B-tree (the last chunk
+        dimension is the element size), undoing the filter pipeline per chunk."""
+        import zlib
+        nd = len(cdims) - 1
+        csh = tuple(int(c) for c in cdims[:nd])
+        if not shape:
+            shape = ()
+        full = tuple(-(-int(s) // c) * c for s, c in zip(shape, csh)) if nd else ()
+        out = np.zeros(full, dtype=dt)
+        if btree == UNDEF:
+            return out[tuple(slice(0, s) for s in shape)] if nd else out
+        esz = dt.itemsize
+        for key, addr in self._btree_nodes(btree, 1, len(cdims)):
+            csize, fmask = struct.unpack_from("<II", key, 0)
+            offs = struct.unpack_from("<" + "Q" * len(cdims), key, 8)[:nd]
+            raw = self.b[addr:addr + csize]
+            for i, (fid, vals) in reversed(list(enumerate(filters))):
+                if fmask & (1 << i):
+                    continue  # filter skipped for this chunk
+                if fid == 1:
+                    raw = zlib.decompress(raw)
+                elif fid == 2:  # shuffle: byte planes -> elements
+                    n = len(raw) // esz
+                    raw = np.frombuffer(raw, np.uint8)[:n * esz].reshape(esz, n).T.tobytes()
+                elif fid == 3:  # fletcher32: trailing checksum
+                    raw = raw[:-4]
+                else:
+                    raise NotImplementedError(f"HDF5 filter {fid} is not supported by h5lite")
+            blk = np.frombuffer(raw, dtype=dt, count=int(np.prod(csh))).reshape(csh)
+            out[tuple(slice(o, o + c) for o, c in zip(offs, csh))] = blk
+        return out[tuple(slice(0, s) for s in shape)]
+
+    def _vlen_strings(self, refs):
+        """Global-heap references of variable-length strings -> fixed-length bytes array."""
+        b = self.b
+        vals = []
+        for ref in refs.reshape(-1):
+            ln, addr, idx = int(ref["len"]), int(ref["addr"]), int(ref["idx"])
+            if addr == 0 or ln == 0:
+                vals.append(b"")
+                continue
+            if b[addr:addr + 4] != b"GCOL":
+                raise OSError("bad global heap signature")
+            csize = struct.unpack_from("<Q", b, addr + 8)[0]
+            q, end, found = addr + 16, addr + csize, b""
+            while q + 16 <= end:
+                oid, _, _, osz = struct.unpack_from("<HHIQ", b, q)
+                if oid == 0:  # free space: end of the collection's objects
+                    break
+                if oid == idx:
+                    found = b[q + 16:q + 16 + min(ln, osz)]
+                    break
+                q += 16 + (osz + 7) // 8 * 8
+            vals.append(found)
+        n = max([len(v) for v in vals] + [1])
+        return np.array(vals, dtype=f"S{n}").reshape(refs.shape)
 
 
 def read_file(path: str) -> Group:

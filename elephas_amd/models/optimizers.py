@@ -95,6 +95,11 @@ class Optimizer:
     def n_state(self) -> int:
         return 0
 
+    def slot_names(self) -> List[str]:
+        """Keras 2.10 slot-variable names of the state planes, in engine plane order
+        (HDF5 ``optimizer_weights``: '<optimizer>/<layer>/<kernel|bias>/<slot>:0')."""
+        return []
+
     def init_state(self, params: List[torch.Tensor]) -> List[List[torch.Tensor]]:
         return [[torch.zeros_like(p) for _ in range(self.n_state())] for p in params]
 
@@ -117,6 +122,9 @@ class SGD(Optimizer):
 
     def n_state(self):
         return 1 if self._hyper["momentum"] > 0 else 0
+
+    def slot_names(self):
+        return ["momentum"] if self._hyper["momentum"] > 0 else []
 
     @torch.no_grad()
     def apply_torch(self, params, grads, state, iteration):
@@ -151,6 +159,10 @@ class RMSprop(Optimizer):
 
     def n_state(self):
         return 1 + (1 if self._hyper["momentum"] > 0 else 0) + (1 if self._hyper["centered"] else 0)
+
+    def slot_names(self):
+        h = self._hyper
+        return ["rms"] + (["momentum"] if h["momentum"] > 0 else []) + (["mg"] if h["centered"] else [])
 
     @torch.no_grad()
     def apply_torch(self, params, grads, state, iteration):
@@ -194,6 +206,9 @@ class Adam(Optimizer):
     def n_state(self):
         return 3 if self._hyper["amsgrad"] else 2
 
+    def slot_names(self):
+        return ["m", "v"] + (["vhat"] if self._hyper["amsgrad"] else [])
+
     @torch.no_grad()
     def apply_torch(self, params, grads, state, iteration):
         h = self._hyper
@@ -228,6 +243,9 @@ class Adagrad(Optimizer):
     def n_state(self):
         return 1
 
+    def slot_names(self):
+        return ["accumulator"]
+
     def init_state(self, params):
         return [[torch.full_like(p, self._hyper["initial_accumulator_value"])] for p in params]
 
@@ -240,6 +258,9 @@ class Adagrad(Optimizer):
 
 
 class Adamax(Optimizer):
+    def slot_names(self):
+        return ["m", "v"]
+
     _defaults = {"learning_rate": 0.001, "beta_1": 0.9, "beta_2": 0.999, "epsilon": 1e-7}
 
     def __init__(self, learning_rate=0.001, beta_1=0.9, beta_2=0.999, epsilon=1e-07, name="Adamax", **kwargs):
@@ -268,6 +289,9 @@ class Adamax(Optimizer):
 
 
 class Adadelta(Optimizer):
+    def slot_names(self):
+        return ["accum_grad", "accum_var"]
+
     _defaults = {"learning_rate": 0.001, "rho": 0.95, "epsilon": 1e-7}
 
     def __init__(self, learning_rate=0.001, rho=0.95, epsilon=1e-07, name="Adadelta", **kwargs):
@@ -291,6 +315,9 @@ class Adadelta(Optimizer):
 
 
 class Nadam(Optimizer):
+    def slot_names(self):
+        return ["m", "v"]
+
     _defaults = {"learning_rate": 0.001, "beta_1": 0.9, "beta_2": 0.999, "epsilon": 1e-7}
 
     def __init__(self, learning_rate=0.001, beta_1=0.9, beta_2=0.999, epsilon=1e-07, name="Nadam", **kwargs):

@@ -194,6 +194,10 @@ class Model:
         if t is None:
             t = make_trainer(self, 1, key)
             self._trainers = {key: t}  # one live trainer: it owns the optimizer state
+            pending = getattr(self, "_pending_optimizer_state", None)
+            if pending is not None:  # optimizer weights restored from an HDF5 checkpoint
+                t.set_state_flat(pending[0][None], [pending[1]])
+                self._pending_optimizer_state = None
         elif getattr(t, "_weight_epoch", None) != weight_epoch():
             # the host weights changed since the trainer last saw them (a repeated
             # predict / evaluate on unchanged weights skips this upload: 150 MB on Wide)
