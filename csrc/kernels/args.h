@@ -91,7 +91,12 @@ struct Prob {
 struct GroupArgs {
   Prob p[2];
   int nprob;
-  int total_blocks;
+  // grid (R, total_blocks): blockIdx.x = replica, blockIdx.y = tile of the launch.
+  // Blocks are dealt to the 8 XCDs round-robin in x-fastest order, so with R = 8 a
+  // replica's tiles share one XCD's L2 (and the replica index is a scalar register:
+  // no integer division on the vector ALU)
+  int R;
+  int total_blocks;   // tiles per replica; problem i owns tiles [p[i].block_begin, ...)
   long long* ctr;           // [0]=step in epoch, [1]=arrive counter, [2..2+R)=iter per replica
   unsigned long long seed;
   // Step counters: ctr[0] = base step-in-epoch, ctr[2 + r] = base optimizer
@@ -112,7 +117,8 @@ constexpr int TABLE_MAX = 4;
 struct TableArgs {
   const Prob* probs;
   int nprob;
-  int begin[TABLE_MAX];
+  int begin[TABLE_MAX];   // first tile (per replica) of every problem
+  int R;                  // grid (R, total_blocks) as GroupArgs
   int total_blocks;
   long long* ctr;
   unsigned long long seed;

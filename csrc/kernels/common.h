@@ -593,7 +593,12 @@ __device__ __forceinline__ void opt_update_v(const OptParams& p, float (&w)[NV],
 // top of the kernel instead of as vector loads, each waited for on its own.
 // Only for words nothing in the reading kernel writes.
 template <typename T> __device__ __forceinline__ T ld_inv(const T* p) {
-  return *(const __attribute__((address_space(4))) T*)(unsigned long long)p;
+  // the address is forced into SGPRs: hipcc otherwise sometimes forms it on the
+  // vector ALU (e.g. from a copy of the workgroup id) and emits a vector load
+  const unsigned long long u = (unsigned long long)p;
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)u);
+  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(u >> 32));
+  return *(const __attribute__((address_space(4))) T*)(((unsigned long long)hi << 32) | lo);
 }
 
 // a whole launch-invariant struct, dword by dword (unused words are dropped)

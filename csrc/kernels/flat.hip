@@ -121,9 +121,9 @@ __device__ __forceinline__ TileV find_tile(const FlatArgs& a, int t, int& lt) {
 template <typename T, bool UPDATE>
 __global__ __launch_bounds__(256) void shadow_tiles_kernel(FlatArgs a, int tiles_per_replica) {
   __shared__ float tile[64][65];
-  const int r = blockIdx.x % a.R;  // replica-minor block order (XCD affinity, see gemm_impl.h)
+  const int r = __builtin_amdgcn_readfirstlane(blockIdx.x % a.R);  // replica-minor (XCD affinity, gemm_impl.h)
   int lt;
-  const TileV g = find_tile(a, blockIdx.x / a.R, lt);
+  const TileV g = find_tile(a, __builtin_amdgcn_readfirstlane(blockIdx.x / a.R), lt);
   const int k0 = (lt / g.tn) * 64, n0 = (lt % g.tn) * 64;
   long long iter = a.ctr[2 + r];
   if (UPDATE && (long long)a.ntrain[r] - a.ctr[0] * a.B <= 0) return;  // replica has no batch this step

@@ -25,9 +25,9 @@ extern "C" hipError_t ea_gemm_grouped(const ea::GroupArgs* ga, int bf16, int cfg
     // dZ^T stage (bf16, LOSS_RPB rows) + the 4-wave x 6 partial-sum reduction
     const size_t lds = (size_t)(LOSS_RPB * LOSS_LDS_MAX_N * 2 + 15) / 16 * 16 + 32 * sizeof(float);
     if (bf16)
-      hipLaunchKernelGGL(loss_rows_kernel<__bf16>, dim3(ga->total_blocks), dim3(256), lds, s, *ga);
+      hipLaunchKernelGGL(loss_rows_kernel<__bf16>, dim3(ga->R, ga->total_blocks), dim3(256), lds, s, *ga);
     else
-      hipLaunchKernelGGL(loss_rows_kernel<float>, dim3(ga->total_blocks), dim3(256), lds, s, *ga);
+      hipLaunchKernelGGL(loss_rows_kernel<float>, dim3(ga->R, ga->total_blocks), dim3(256), lds, s, *ga);
     return hipGetLastError();
   }
   if (!bf16) return ea_gemm_launch_f32(ga, cfg, s);

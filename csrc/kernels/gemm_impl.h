@@ -20,7 +20,7 @@
 //   THR : 128x128 tile, 2x2 waves, no split-K   (MFMA-bound wide layers)
 //
 // Several independent problems (e.g. DW_l and DX_l of the same layer) run in one
-// grouped launch; blockIdx.x selects the problem.
+// grouped launch; blockIdx.y (the tile) selects the problem, blockIdx.x is the replica.
 //
 // This header holds the kernel templates; each tile config is instantiated in a
 // translation unit of its own (gemm_cfg*.hip, compiled in parallel) and
@@ -57,15 +57,9 @@ template <typename T> __device__ __forceinline__ void st(void* base, long long i
 
 // ------------------------------------------------------- gather-transpose
 template <typename T, typename GA>
-__device__ __forceinline__ void gather_transpose_block(const GA& ga, const Prob& p, int lb, float* sm) {
+__device__ __forceinline__ void gather_transpose_block(const GA& ga, const Prob& p, int r, int t, float* sm) {
   // one block = 64 batch rows x 64 features; output XT[k][m] (ld = lddt)
   // tiles_m: batch blocks, tiles_n: feature blocks
-  const int per_r = p.tiles_m * p.tiles_n;
-  // replica-minor block order: with R = 8 a replica's blocks share one XCD (blocks
-  // are dealt round-robin over the 8 XCDs), so its operands are fetched into one L2
-  (void)per_r;
-  const int r = lb % p.R;
-  const int t = lb / p.R;
   const int b0 = (t / p.tiles_n) * 64;
   const int k0 = (t % p.tiles_n) * 64;
   const long long step = ld_inv(ga.ctr) + ga.step_off;
@@ -179,10 +173,9 @@ __device__ __forceinline__ void row_softmax_cce_reg(const Prob& p, int lane, con
 }
 
 template <typename T>
-__device__ __forceinline__ void loss_rows_block(const GroupArgs& ga, const Prob& p, int lb, float* smem) {
-  const int r = lb % p.R;  // replica-minor block order (XCD affinity)
+__device__ __forceinline__ void loss_rows_block(const GroupArgs& ga, const Prob& p, int r, int lb, float* smem) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int row0 = (lb / p.R) * LOSS_RPB;
+  const int row0 = lb * LOSS_RPB;
   const long long step = ld_inv(ga.ctr) + ga.step_off;
   const int valid = batch_valid(p, r, step);
   const bool train = !p.eval_mode && p.D;
@@ -302,11 +295,13 @@ __device__ __forceinline__ void st8(void* base, long long idx, const float (&v)[
 // (W = 16/32/64 by output width), reductions are W-lane shuffles.
 // diagnostics: wall-clock stamps (100 MHz s_memrealtime) of block-relative phases
 template <typename GA> __device__ __forceinline__ void stamp(const GA& ga, int k) {
-  if (ga.stamps && threadIdx.x == 0) ga.stamps[(long long)blockIdx.x * 16 + k] = (long long)__builtin_amdgcn_s_memrealtime();
+  if (ga.stamps && threadIdx.x == 0)
+    ga.stamps[((long long)blockIdx.y * gridDim.x + blockIdx.x) * 16 + k] = (long long)__builtin_amdgcn_s_memrealtime();
 }
 // shader-clock counter (slots 10..15) to estimate the SCLK the kernel runs at
 template <typename GA> __device__ __forceinline__ void stamp_clk(const GA& ga, int k) {
-  if (ga.stamps && threadIdx.x == 0) ga.stamps[(long long)blockIdx.x * 16 + k] = (long long)__builtin_amdgcn_s_memtime();
+  if (ga.stamps && threadIdx.x == 0)
+    ga.stamps[((long long)blockIdx.y * gridDim.x + blockIdx.x) * 16 + k] = (long long)__builtin_amdgcn_s_memtime();
 }
 
 // ------------------------------------------------------- LDS-staged main loop
@@ -470,14 +465,14 @@ constexpr unsigned KM_PARTIAL = KB(PK_PARTIAL);
 // wave) uses a shallow ring so three workgroups fit on a CU
 template <typename T, int WM, int WN, int WAVES_M, int WAVES_N, int KSPLIT, unsigned KM = KM_ALL, int PF_ = 0,
           typename GA>
-__device__ __forceinline__ void run_prob(const GA& ga, const Prob& p, const int lb, float* smem) {
+__device__ __forceinline__ void run_prob(const GA& ga, const Prob& p, const int r, const int lb, float* smem) {
   static_assert(WAVES_M * WAVES_N * KSPLIT == 4, "4 waves per block");
   constexpr int BM = WAVES_M * WM * 16;
   constexpr int BN = WAVES_N * WN * 16;
   constexpr int LDC = BN + 4;  // 16-byte aligned rows for float4 LDS access
   constexpr int EPL = KT<T>::EPL, KC = KT<T>::KC;
   if ((KM & KB(PK_GATHER_T)) && p.kind == PK_GATHER_T) {
-    gather_transpose_block<T>(ga, p, lb, smem);
+    gather_transpose_block<T>(ga, p, r, lb, smem);
   } else {
     // split-K over workgroups (PK_PARTIAL): chunk kc covers reduction elements
     // [kc * kchunk, kc * kchunk + Keff) and writes its own fp32 slab
@@ -485,12 +480,10 @@ __device__ __forceinline__ void run_prob(const GA& ga, const Prob& p, const int 
     const int tk = partial ? p.tiles_k : 1;
     const int per_mn = p.tiles_m * p.tiles_n;
     const int per_r = per_mn * tk;
-    // replica-minor block order: block lb -> replica lb % R, tile lb / R. With R = 8
-    // every block of a replica runs on one XCD (round-robin dealing), so the operands
-    // the replica's tiles share (dZ^T, X^T, W) are fetched from HBM into ONE L2
+    // r = blockIdx.x (GroupArgs: replica-minor grid, XCD affinity); lb = this
+    // replica's tile within the problem
     (void)per_r;
-    const int r = lb % p.R;
-    const int tkm = lb / p.R;
+    const int tkm = lb;
     const int kch = partial ? tkm / per_mn : 0;
     const int t = partial ? tkm - kch * per_mn : tkm;
     const int tm = t / p.tiles_n, tn = t % p.tiles_n;
@@ -1006,11 +999,11 @@ __global__ __launch_bounds__(256) void gemm_grouped(GroupArgs ga) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   stamp(ga, 0);
   stamp_clk(ga, 10);
-  const int bid = blockIdx.x;
+  const int r = blockIdx.x, bid = blockIdx.y;
   if (KM1 != KM_NONE && ga.nprob > 1 && bid >= ga.p[1].block_begin)
-    run_prob<T, WM, WN, WAVES_M, WAVES_N, KSPLIT, KM1>(ga, ga.p[1], bid - ga.p[1].block_begin, smem);
+    run_prob<T, WM, WN, WAVES_M, WAVES_N, KSPLIT, KM1>(ga, ga.p[1], r, bid - ga.p[1].block_begin, smem);
   else
-    run_prob<T, WM, WN, WAVES_M, WAVES_N, KSPLIT, KM0>(ga, ga.p[0], bid - ga.p[0].block_begin, smem);
+    run_prob<T, WM, WN, WAVES_M, WAVES_N, KSPLIT, KM0>(ga, ga.p[0], r, bid - ga.p[0].block_begin, smem);
 
   stamp(ga, 4);
   stamp_clk(ga, 11);
@@ -1023,7 +1016,7 @@ __global__ __launch_bounds__(256) void gemm_grouped(GroupArgs ga) {
 template <typename T>
 __global__ __launch_bounds__(256) void loss_rows_kernel(GroupArgs ga) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  loss_rows_block<T>(ga, ga.p[0], blockIdx.x - ga.p[0].block_begin, smem);
+  loss_rows_block<T>(ga, ga.p[0], blockIdx.x, blockIdx.y - ga.p[0].block_begin, smem);
 }
 
 // Grouped launch over a device table of problems (row-chain plan, up to
@@ -1034,7 +1027,7 @@ __global__ __launch_bounds__(256) void gemm_table(TableArgs ta) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   stamp(ta, 0);
   stamp_clk(ta, 10);
-  const int bid = blockIdx.x;
+  const int r = blockIdx.x, bid = blockIdx.y;
   int i = 0;
 #pragma unroll
   for (int j = 1; j < TABLE_MAX; ++j) i += (j < ta.nprob && bid >= ta.begin[j]) ? 1 : 0;
@@ -1045,7 +1038,7 @@ __global__ __launch_bounds__(256) void gemm_table(TableArgs ta) {
   // became a vector load with its own full memory round trip (the compiler cannot
   // tell the table from the stored-to buffers)
   const Prob p = ld_inv_struct(ta.probs + i);
-  run_prob<T, WM, WN, WAVES_M, WAVES_N, KSPLIT, KM, (KM == KM_DW) ? 2 : 0>(ta, p, bid - ta.begin[i], smem);
+  run_prob<T, WM, WN, WAVES_M, WAVES_N, KSPLIT, KM, (KM == KM_DW) ? 2 : 0>(ta, p, r, bid - ta.begin[i], smem);
   stamp(ta, 4);
   stamp_clk(ta, 11);
 }
@@ -1088,7 +1081,7 @@ template <typename T, int WM, int WN, int WAVES_M, int WAVES_N, int KSPLIT, unsi
 static bool launch_if(const GroupArgs& ga, size_t lds, hipStream_t s, hipError_t& err) {
   if (!(KM0 & KB(ga.p[0].kind))) return false;
   if (ga.nprob > 1 && !(KM1 & KB(ga.p[1].kind))) return false;
-  hipLaunchKernelGGL((gemm_grouped<T, WM, WN, WAVES_M, WAVES_N, KSPLIT, KM0, KM1>), dim3(ga.total_blocks),
+  hipLaunchKernelGGL((gemm_grouped<T, WM, WN, WAVES_M, WAVES_N, KSPLIT, KM0, KM1>), dim3(ga.R, ga.total_blocks),
                      dim3(256), lds, s, ga);
   err = hipGetLastError();
   return true;
@@ -1110,7 +1103,7 @@ static hipError_t launch_cfg(const GroupArgs& ga, hipStream_t s) {
         return e;
     }
   }
-  hipLaunchKernelGGL((gemm_grouped<T, WM, WN, WAVES_M, WAVES_N, KSPLIT>), dim3(ga.total_blocks), dim3(256), lds, s,
+  hipLaunchKernelGGL((gemm_grouped<T, WM, WN, WAVES_M, WAVES_N, KSPLIT>), dim3(ga.R, ga.total_blocks), dim3(256), lds, s,
                      ga);
   return hipGetLastError();
 }
@@ -1127,10 +1120,10 @@ static hipError_t launch_table(const TableArgs& ta, int dw, hipStream_t s) {
   if (ta.total_blocks <= 0) return hipSuccess;
   if (dw) {
     const size_t lds = lds_bytes<T, 4, 2, 1, 2, 2>(false);
-    hipLaunchKernelGGL((gemm_table<T, 4, 2, 1, 2, 2, KM_DW>), dim3(ta.total_blocks), dim3(256), lds, s, ta);
+    hipLaunchKernelGGL((gemm_table<T, 4, 2, 1, 2, 2, KM_DW>), dim3(ta.R, ta.total_blocks), dim3(256), lds, s, ta);
   } else {
     const size_t lds = lds_bytes<T, 4, 2, 1, 1, 4>(false);
-    hipLaunchKernelGGL((gemm_table<T, 4, 2, 1, 1, 4, KM_PARTIAL | KM_GATHER>), dim3(ta.total_blocks), dim3(256), lds,
+    hipLaunchKernelGGL((gemm_table<T, 4, 2, 1, 1, 4, KM_PARTIAL | KM_GATHER>), dim3(ta.R, ta.total_blocks), dim3(256), lds,
                        s, ta);
   }
   return hipGetLastError();

@@ -142,29 +142,31 @@ __device__ __forceinline__ void lds_barrier() {
   asm volatile("" ::: "memory");
 }
 
-// the generic loss (every Keras loss / activation / metric pairing) is a call, not
-// inlined: it is ~20k instructions that the softmax + CCE path never executes
-__device__ __attribute__((noinline)) void rc_loss_generic(const Prob& q, int r, int m0, float* sLg, const float* sY,
-                                                          const int* sRow, float inv_valid, float (&sums)[6]) {
-  loss_tile_lds<RB, 36, 32>(q, r, m0, sLg, sY, sRow, true, inv_valid, sums);
-}
-
 __device__ __forceinline__ void rstamp(const RcArgs& a, int k) {
-  if (a.stamps && threadIdx.x == 0) a.stamps[(long long)blockIdx.x * 16 + k] = (long long)__builtin_amdgcn_s_memrealtime();
+  if (a.stamps && threadIdx.x == 0)
+    a.stamps[((long long)blockIdx.y * gridDim.x + blockIdx.x) * 16 + k] = (long long)__builtin_amdgcn_s_memrealtime();
 }
 
 }  // namespace
 
 // T: compute dtype; L: Dense layers (2..4); NBW: 16-column blocks per wave of the
-// widest hidden layer (2: widths <= 128, 4: <= 256)
-template <typename T, int L, int NBW>
+// widest hidden layer (2: widths <= 128, 4: <= 256); GEN: the generic loss path
+// (every Keras loss / activation / metric pairing, ~20k instructions) instead of
+// the softmax + (sparse) categorical cross-entropy one -- picked on the host
+template <typename T, int L, int NBW, bool GEN>
 __global__ __launch_bounds__(256) void rowchain_kernel(RcArgs a) {
-  constexpr int NKMAX = NBW * 64 / KT<T>::KC;  // reduction chunks of the widest layer
+  constexpr int EPL = KT<T>::EPL, KC = KT<T>::KC;
+  constexpr int NKMAX = NBW * 64 / KC;  // reduction chunks of the widest layer
   constexpr int PF = NKMAX < 8 ? NKMAX : 8;      // NBW 2: the whole reduction in flight
   constexpr int LD = NBW * 64 + (sizeof(T) == 2 ? 8 : 4);  // LDS row stride: conflict-free fragment reads
+  constexpr int LDG = NBW * 64 + 4;                         // fp32 rows of G_0
   constexpr int NH = L - 1;                                 // activations D_0 .. D_{L-2} kept in LDS
+  constexpr int NKF = (NKMAX + 3) / 4;                      // last-layer forward chunks per wave (K split 4 ways)
+  constexpr int NKL = (32 + KC - 1) / KC;                   // last-layer input-gradient chunks (Np_last <= 32)
+  constexpr int CPT = NBW * 4;                              // phase 0: columns per thread (16 threads per row)
   __shared__ __attribute__((aligned(16))) T sD[NH][RB * LD];
   __shared__ __attribute__((aligned(16))) T sdZ[2][RB * LD];
+  __shared__ __attribute__((aligned(16))) float sG0[RB * LDG];
   __shared__ __attribute__((aligned(16))) float sRed[4][RB * 32];
   __shared__ __attribute__((aligned(16))) float sLg[RB * 36];
   __shared__ __attribute__((aligned(16))) float sY[RB * 32];
@@ -174,10 +176,10 @@ __global__ __launch_bounds__(256) void rowchain_kernel(RcArgs a) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int i16 = lane & 15, g = lane >> 4;
-  const int tiles = (a.B + RB - 1) / RB;
-  (void)tiles;
-  const int r = blockIdx.x % a.R;  // replica-minor: a replica's row blocks share one XCD
-  const int m0 = (blockIdx.x / a.R) * RB;
+  // grid (R, row blocks), x fastest: a replica's row blocks share one XCD and the
+  // replica index is a scalar register (uniform loads indexed by it stay scalar)
+  const int r = blockIdx.x;
+  const int m0 = blockIdx.y * RB;
   const long long s0 = ld_inv(a.ctr);
   const long long step = s0 + a.step_off;
   const long long cnt = (long long)ld_inv(a.ntrain + r) - step * a.B;
@@ -188,18 +190,55 @@ __global__ __launch_bounds__(256) void rowchain_kernel(RcArgs a) {
   const T* Wcur = reinterpret_cast<const T*>(a.Wsh) + (long long)r * a.sWsh + rpar * a.wsh_par;
   const T* WTcur = reinterpret_cast<const T*>(a.WTsh) + (long long)r * a.sWTsh + rpar * a.wtsh_par;
   const float* Pr = a.P + (long long)r * a.sP;
+  const RcLayer LL = a.ly[L - 1];
 
-  // layer 1's weights start streaming now, under the slab loads below (the last
-  // layer has a K-split loop of its own)
+  // ---- everything that does not depend on this step's data is requested up front,
+  //      under the slab loads: the batch rows' targets, the first hidden layer's
+  //      weight ring, the last layer's forward and input-gradient fragments, biases
+  int prow[2];
+  {
+    const int* pr = a.perm + (long long)r * a.sPerm + step * a.B + m0;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int row = (tid >> 5) + 8 * i;
+      const bool in = m0 + row < valid;
+      const int v = pr[in ? row : 0];
+      prow[i] = in ? v : -1;
+    }
+  }
   Ring<T, NBW, PF> ring;
   if constexpr (L > 2) ring_start(ring, WTcur + a.ly[1].wtsh_off, a.ly[1].Kp, a.ly[1].Kp, a.ly[1].N, w, lane);
-
-  // G_l = act'(z_l) * keep / (1 - rate), owned by the lane that owns the element
-  float G[NH][NBW][4];
-
-  // biases of layers 1 .. L-1 (fp32 master), loaded now: nothing below waits a memory
-  // round trip for them
-  float hb[L][NBW];
+  uint4 wl[NKF][2];  // last layer forward: B^T rows = its <= 32 outputs, chunks w + 4i
+  {
+    const T* BT = WTcur + LL.wtsh_off;
+#pragma unroll
+    for (int i = 0; i < NKF; ++i) {
+      const int kk = (w + 4 * i) * KC + g * EPL;
+      const bool kin = kk < LL.Kp;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int col = j * 16 + i16;
+        const uint4 v = *reinterpret_cast<const uint4*>(BT + (long long)(col < LL.N ? col : 0) * LL.Kp + (kin ? kk : 0));
+        wl[i][j] = (kin && col < LL.N) ? v : zero4();
+      }
+    }
+  }
+  uint4 xl[NKL][NBW];  // last layer input gradient: B^T rows = its K inputs, reduction over Np_last
+  {
+    const T* BT = Wcur + LL.wsh_off;
+#pragma unroll
+    for (int i = 0; i < NKL; ++i) {
+      const int kk = i * KC + g * EPL;
+      const bool kin = kk < LL.Np;
+#pragma unroll
+      for (int j = 0; j < NBW; ++j) {
+        const int col = (w + 4 * j) * 16 + i16;
+        const uint4 v = *reinterpret_cast<const uint4*>(BT + (long long)(col < LL.K ? col : 0) * LL.Np + (kin ? kk : 0));
+        xl[i][j] = (kin && col < LL.K) ? v : zero4();
+      }
+    }
+  }
+  float hb[L][NBW];  // hidden-layer biases in the lanes that own the columns
 #pragma unroll
   for (int l = 1; l < L - 1; ++l) {
     const RcLayer ly = a.ly[l];
@@ -214,88 +253,107 @@ __global__ __launch_bounds__(256) void rowchain_kernel(RcArgs a) {
   }
   float lastb;
   {
-    const RcLayer ly = a.ly[L - 1];
     const int c = tid & 31;
-    const bool cv = c < ly.N && ly.has_bias;
-    const float v = Pr[ly.p_off + (long long)ly.K * ly.N + (cv ? c : 0)];
+    const bool cv = c < LL.N && LL.has_bias;
+    const float v = Pr[LL.p_off + (long long)LL.K * LL.N + (cv ? c : 0)];
     lastb = cv ? v : 0.f;
   }
 
-  // ---- phase 0: z_0 = sum of the split-K slabs + bias -> D_0 (LDS), D_0^T, G_0;
-  //      the targets of this workgroup's rows
+  float yv[2];  // this thread's two target values (rows (tid >> 5) + 8i, column tid & 31)
+
+  // G_l (l >= 1) = act'(z_l) * keep / (1 - rate), owned by the lane that owns the
+  // element in both the forward and the input-gradient GEMM; G_0 goes through LDS
+  float G[L][NBW][4];
+
+  // ---- phase 0: z_0 = sum of the split-K slabs + bias -> D_0 (LDS) and G_0 (LDS);
+  //      one row and CPT consecutive columns per thread: 16-byte slab loads, all
+  //      issued before the first add
   {
     const RcLayer l0 = a.ly[0];
-    const float* Zr = a.Zp + (long long)r * a.sZp;
+    const int row = tid >> 4, c0 = (tid & 15) * CPT;
+    const int m = m0 + row;
+    const bool rv = m < valid;
+    const float* Zr = a.Zp + (long long)r * a.sZp + (long long)(rv ? m : 0) * l0.Np;
     const float* bias = Pr + l0.p_off + (long long)l0.K * l0.N;
-    const int nb = (l0.N + 15) >> 4;
-    float z[NBW * 4];
+    float4 sv[RC_MAXSPLIT][CPT / 4];
 #pragma unroll
-    for (int j = 0; j < NBW; ++j) {
-      const int col = (w + 4 * j) * 16 + i16;
-      const bool cv = (w + 4 * j < nb) && col < l0.N;
-      const float bv = (cv && l0.has_bias) ? bias[col] : 0.f;
+    for (int kc = 0; kc < RC_MAXSPLIT; ++kc) {
+      const float* slab = Zr + (long long)(kc < a.nsplitk ? kc : 0) * a.sZpk;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) z[j * 4 + q] = bv;
-      if (w + 4 * j < nb) {
-        // every slab load is issued before the first add (a data-dependent loop exit
-        // would serialise one memory round trip per slab)
-        float sv[RC_MAXSPLIT][4];
-#pragma unroll
-        for (int kc = 0; kc < RC_MAXSPLIT; ++kc) {
-          const float* slab = Zr + (long long)(kc < a.nsplitk ? kc : 0) * a.sZpk;
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const int m = m0 + 4 * g + q;
-            const bool in = cv && m < valid;
-            sv[kc][q] = slab[in ? (long long)m * l0.N + col : 0];
-          }
-        }
-#pragma unroll
-        for (int kc = 0; kc < RC_MAXSPLIT; ++kc)
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const bool in = cv && m0 + 4 * g + q < valid && kc < a.nsplitk;
-            z[j * 4 + q] += in ? sv[kc][q] : 0.f;
-          }
+      for (int v = 0; v < CPT / 4; ++v) {
+        const int c = c0 + 4 * v;
+        sv[kc][v] = *reinterpret_cast<const float4*>(slab + (c < l0.Np ? c : 0));
       }
     }
-    // targets (rows in epoch order through perm) and the row-valid map
+    float z[CPT];
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+      const int c = c0 + i;
+      const bool cv = c < l0.N && l0.has_bias;
+      const float bv = bias[cv ? c : 0];
+      z[i] = cv ? bv : 0.f;
+    }
+    // the targets of this workgroup's rows (perm rows requested at entry): loaded now,
+    // stored to LDS only before the loss, so nothing waits for this second round trip
     {
       const int ldy = (int)a.ldy;
       const float* Yb = a.Y + (long long)r * a.sY;
-      const int* pr = a.perm + (long long)r * a.sPerm + step * a.B + m0;
-      for (int e = tid; e < RB * 32; e += 256) {
-        const int row = e >> 5, j = e & 31;
-        const bool in = m0 + row < valid && j < ldy;
-        const int dr = in ? pr[row] : 0;
-        sY[e] = in ? Yb[(long long)dr * ldy + j] : 0.f;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int e = tid + 256 * i, j = e & 31;
+        const bool in = prow[i] >= 0 && j < ldy;
+        yv[i] = Yb[in ? (long long)prow[i] * ldy + j : 0];
+        if (!in) prow[i] = -1;
       }
       if (tid < RB) sRow[tid] = m0 + tid < valid ? 1 : -1;
     }
-    float o[NBW * 4], gg[NBW * 4];
-    act_fg_v<NBW * 4>(l0.act, z, o, gg);
+#pragma unroll
+    for (int kc = 0; kc < RC_MAXSPLIT; ++kc) {
+      if (kc >= a.nsplitk) break;  // uniform; every load above is already in flight
+#pragma unroll
+      for (int v = 0; v < CPT / 4; ++v) {
+        z[4 * v + 0] += sv[kc][v].x;
+        z[4 * v + 1] += sv[kc][v].y;
+        z[4 * v + 2] += sv[kc][v].z;
+        z[4 * v + 3] += sv[kc][v].w;
+      }
+    }
+    float o[CPT], gg[CPT], dv[CPT], gv[CPT];
+    act_fg_v<CPT>(l0.act, z, o, gg);
     const float keep_scale = l0.rate > 0.f ? 1.f / (1.f - l0.rate) : 1.f;
     const uint32_t dbase = dropout_base(a.seed, r, 0, iter);
-    T* DT0 = reinterpret_cast<T*>(l0.DT) + (long long)r * l0.N * a.Bp;
 #pragma unroll
-    for (int j = 0; j < NBW; ++j) {
-      if (w + 4 * j >= nb) continue;
-      const int col = (w + 4 * j) * 16 + i16;
-      float dv[4];
+    for (int i = 0; i < CPT; ++i) {
+      const int c = c0 + i;
+      const bool live = c < l0.N && rv;
+      const float u = (live && l0.rate > 0.f) ? dropout_u1(dbase, m, c) : 1.f;
+      const bool keep = live && u >= l0.rate;
+      dv[i] = keep ? o[i] * keep_scale : 0.f;
+      gv[i] = keep ? gg[i] * keep_scale : 0.f;
+    }
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int m = m0 + 4 * g + q;
-        const bool live = col < l0.N && m < valid;
-        const float u = (live && l0.rate > 0.f) ? dropout_u1(dbase, m, col) : 1.f;
-        const bool keep = live && u >= l0.rate;
-        dv[q] = keep ? o[j * 4 + q] * keep_scale : 0.f;
-        G[0][j][q] = keep ? gg[j * 4 + q] * keep_scale : 0.f;
-        sD[0][(4 * g + q) * LD + col] = from_f<T>(dv[q]);
+    for (int i = 0; i < CPT; i += 4) {
+      if (c0 + i < NBW * 64) {
+        *reinterpret_cast<float4*>(sG0 + row * LDG + c0 + i) = make_float4(gv[i], gv[i + 1], gv[i + 2], gv[i + 3]);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) sD[0][row * LD + c0 + i + k] = from_f<T>(dv[i + k]);
       }
-      if (col < l0.N && m0 + 4 * g < a.Bp) st4t<T>(DT0 + (long long)col * a.Bp + m0 + 4 * g, dv);
     }
   }
   lds_barrier();
+  // D_0^T (layer 1's weight-gradient operand) from the LDS tile: 4 rows per store
+  {
+    const RcLayer l0 = a.ly[0];
+    T* DT0 = reinterpret_cast<T*>(l0.DT) + (long long)r * l0.N * a.Bp;
+    for (int e = tid; e < l0.N * (RB / 4); e += 256) {
+      const int c = e / (RB / 4), rq = (e - c * (RB / 4)) * 4;
+      if (m0 + rq >= a.Bp) continue;
+      float v[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v[k] = to_f<T>(sD[0][(rq + k) * LD + c]);
+      st4t<T>(DT0 + (long long)c * a.Bp + m0 + rq, v);
+    }
+  }
   rstamp(a, 1);
 
   // ---- forward through the hidden layers 1 .. L-2
@@ -305,9 +363,12 @@ __global__ __launch_bounds__(256) void rowchain_kernel(RcArgs a) {
     f32x4 acc[NBW];
     ring_run<T, NBW, PF, NKMAX>(ring, sD[l - 1], LD, acc, w, lane);
     rstamp(a, 2);
-    // the next hidden layer's weights stream in under this epilogue
+    // the ring's next weights stream in under this epilogue and the loss: the next
+    // hidden layer's W^T, or after the last one the row-major W_{L-2} of the backward
     if (l + 1 < L - 1)
       ring_start(ring, WTcur + a.ly[l + 1].wtsh_off, a.ly[l + 1].Kp, a.ly[l + 1].Kp, a.ly[l + 1].N, w, lane);
+    else
+      ring_start(ring, Wcur + a.ly[L - 2].wsh_off, a.ly[L - 2].Np, a.ly[L - 2].Np, a.ly[L - 2].K, w, lane);
     const int nb = (ly.N + 15) >> 4;
     float z[NBW * 4], o[NBW * 4], gg[NBW * 4];
 #pragma unroll
@@ -339,45 +400,33 @@ __global__ __launch_bounds__(256) void rowchain_kernel(RcArgs a) {
   }
   rstamp(a, 3);
 
-  // ---- last layer (N <= 32): the 4 waves split the reduction, partial tiles
-  //      summed through LDS, then the loss over whole rows
+  // ---- last layer (N <= 32): the 4 waves split the reduction over their
+  //      preloaded fragments, partial tiles summed through LDS, then the loss
   {
-    constexpr int l = L - 1;
-    const RcLayer ly = a.ly[l];
-    constexpr int EPL = KT<T>::EPL, KC = KT<T>::KC;
-    const T* BT = WTcur + ly.wtsh_off;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) sY[tid + 256 * i] = prow[i] >= 0 ? yv[i] : 0.f;
+    const RcLayer ly = LL;
     const int nks = (ly.Kp + KC - 1) / KC;
     const int nb = (ly.N + 15) >> 4;  // 1 or 2
     f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
-    const T* bp[2];
+    const T* arow = sD[L - 2] + i16 * LD + g * EPL;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int col = j * 16 + i16;
-      bp[j] = BT + (long long)(col < ly.N ? col : 0) * ly.Kp;
-    }
-    const T* arow = sD[l - 1] + i16 * LD + g * EPL;
-    for (int ks = w; ks < nks; ks += 4) {
-      const int kk = ks * KC + g * EPL;
-      const bool kin = kk < ly.Kp;
-      uint4 b[2];
+    for (int i = 0; i < NKF; ++i) {
+      const int ks = w + 4 * i;
+      if (ks < nks) {
+        const bool kin = ks * KC + g * EPL < ly.Kp;
+        const uint4 av = *reinterpret_cast<const uint4*>(arow + (kin ? ks * KC : 0));
+        const uint4 a0 = kin ? av : zero4();
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const uint4 v = *reinterpret_cast<const uint4*>(bp[j] + (kin ? kk : 0));
-        b[j] = (kin && j < nb) ? v : zero4();
+        for (int j = 0; j < 2; ++j)
+          if (j < nb) mma16<T>(acc[j], a0, wl[i][j]);
       }
-      const uint4 av = *reinterpret_cast<const uint4*>(arow + (kin ? ks * KC : 0));
-      const uint4 av0 = kin ? av : zero4();
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-        if (j < nb) mma16<T>(acc[j], av0, b[j]);
     }
     rstamp(a, 4);
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int q = 0; q < 4; ++q) sRed[w][(4 * g + q) * 32 + j * 16 + i16] = acc[j][q];
-    // the backward's first weights (layer L-1, row-major image) stream in now
-    ring_start(ring, Wcur + ly.wsh_off, ly.Np, ly.Np, ly.K, w, lane);
     lds_barrier();
     for (int e = tid; e < RB * 32; e += 256) {  // column e & 31 == tid & 31: lastb
       const int row = e >> 5, c = e & 31;
@@ -401,14 +450,15 @@ __global__ __launch_bounds__(256) void rowchain_kernel(RcArgs a) {
     q.B = a.B;
     const float inv_valid = 1.f / (float)valid;
     float sums[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    if (softmax_cce_fast(q)) {
+    constexpr bool fast = !GEN;
+    if constexpr (GEN) {
+      loss_tile_lds<RB, 36, 32>(q, r, m0, sLg, sY, sRow, true, inv_valid, sums);
+    } else if (w == 0) {  // one quad per row: the 16 rows are wave 0
       if (ly.N <= 16) loss_tile_cce<4, RB, 36, 32>(q, r, m0, sLg, sY, sRow, true, inv_valid, sums);
       else loss_tile_cce<8, RB, 36, 32>(q, r, m0, sLg, sY, sRow, true, inv_valid, sums);
-    } else {
-      rc_loss_generic(q, r, m0, sLg, sY, sRow, inv_valid, sums);
     }
     rstamp(a, 6);
-    if (a.acc) {
+    if (a.acc && (!fast || w == 0)) {
 #pragma unroll
       for (int i = 0; i < 6; ++i) {
         if (i < 2 + a.nmet) {
@@ -437,16 +487,33 @@ __global__ __launch_bounds__(256) void rowchain_kernel(RcArgs a) {
   }
   rstamp(a, 7);
 
-  // ---- backward: dZ_{l-1} = (dZ_l . W_l^T) * G_{l-1} for l = L-1 .. 1
+  // ---- backward: dZ_{l-1} = (dZ_l . W_l^T) * G_{l-1} for l = L-1 .. 1; the last
+  //      layer's fragments were loaded at entry, the others stream through the ring
   int cur = 0;
 #pragma unroll
   for (int l = L - 1; l >= 1; --l) {
     const RcLayer ly = a.ly[l];
     const RcLayer pv = a.ly[l - 1];
     f32x4 acc[NBW];
-    ring_run<T, NBW, PF, NKMAX>(ring, sdZ[cur], LD, acc, w, lane);
+    if (l == L - 1) {
+#pragma unroll
+      for (int j = 0; j < NBW; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const T* arow = sdZ[cur] + i16 * LD + g * EPL;
+      const int nb = (ly.K + 15) >> 4;
+#pragma unroll
+      for (int i = 0; i < NKL; ++i) {
+        const bool kin = i * KC + g * EPL < ly.Np;
+        const uint4 av = *reinterpret_cast<const uint4*>(arow + (kin ? i * KC : 0));
+        const uint4 a0 = kin ? av : zero4();
+#pragma unroll
+        for (int j = 0; j < NBW; ++j)
+          if (w + 4 * j < nb) mma16<T>(acc[j], a0, xl[i][j]);
+      }
+    } else {
+      ring_run<T, NBW, PF, NKMAX>(ring, sdZ[cur], LD, acc, w, lane);
+      if (l > 1) ring_start(ring, Wcur + a.ly[l - 1].wsh_off, a.ly[l - 1].Np, a.ly[l - 1].Np, a.ly[l - 1].K, w, lane);
+    }
     rstamp(a, 8 + 2 * (L - 1 - l));
-    if (l > 1) ring_start(ring, Wcur + a.ly[l - 1].wsh_off, a.ly[l - 1].Np, a.ly[l - 1].Np, a.ly[l - 1].K, w, lane);
     const int nb = (ly.K + 15) >> 4;
     T* dZT = reinterpret_cast<T*>(pv.dZT) + (long long)r * pv.N * a.Bp;
 #pragma unroll
@@ -456,7 +523,8 @@ __global__ __launch_bounds__(256) void rowchain_kernel(RcArgs a) {
       float v[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        v[q] = col < pv.N ? acc[j][q] * G[l - 1][j][q] : 0.f;
+        const float gq = (l - 1 >= 1) ? G[l - 1][j][q] : sG0[(4 * g + q) * LDG + (col < NBW * 64 ? col : 0)];
+        v[q] = col < pv.N ? acc[j][q] * gq : 0.f;
         if (l > 1) sdZ[cur ^ 1][(4 * g + q) * LD + col] = from_f<T>(v[q]);
       }
       if (col < pv.N && m0 + 4 * g < a.Bp) st4t<T>(dZT + (long long)col * a.Bp + m0 + 4 * g, v);
@@ -471,22 +539,31 @@ __global__ __launch_bounds__(256) void rowchain_kernel(RcArgs a) {
 
 using namespace ea;
 
-// grid: R x ceil(B / 16) workgroups of 256 threads
+// grid: (R, ceil(B / 16)) workgroups of 256 threads
 extern "C" hipError_t ea_rowchain(const RcArgs* a, int bf16, int nbw, hipStream_t s) {
   if (a->L < 2 || a->L > RC_MAXL || (nbw != 2 && nbw != 4)) return hipErrorInvalidValue;
-  const dim3 grid(a->R * ((a->B + RC_ROWS - 1) / RC_ROWS));
-#define EA_RC(TT, LL, NB) hipLaunchKernelGGL((rowchain_kernel<TT, LL, NB>), grid, dim3(256), 0, s, *a)
-#define EA_RC_L(TT, NB)   \
-  switch (a->L) {         \
-    case 2: EA_RC(TT, 2, NB); break; \
-    case 3: EA_RC(TT, 3, NB); break; \
-    default: EA_RC(TT, 4, NB); break; \
+  const dim3 grid(a->R, (a->B + RC_ROWS - 1) / RC_ROWS);
+  // the loss_tile_cce path: softmax + (sparse) CCE with accuracy / CCE metrics
+  bool fast = a->ly[a->L - 1].act == ACT_SOFTMAX && (a->loss == LOSS_CCE || a->loss == LOSS_SPARSE_CCE) &&
+              a->ly[a->L - 1].N <= 32;
+  for (int i = 0; i < a->nmet; ++i)
+    fast = fast && (a->met[i] == MET_ACC_CAT || a->met[i] == MET_ACC_SPARSE || a->met[i] == LOSS_CCE ||
+                    a->met[i] == LOSS_SPARSE_CCE);
+#define EA_RC(TT, LL, NB, GN) hipLaunchKernelGGL((rowchain_kernel<TT, LL, NB, GN>), grid, dim3(256), 0, s, *a)
+#define EA_RC_L(TT, NB, GN)           \
+  switch (a->L) {                     \
+    case 2: EA_RC(TT, 2, NB, GN); break; \
+    case 3: EA_RC(TT, 3, NB, GN); break; \
+    default: EA_RC(TT, 4, NB, GN); break; \
   }
+#define EA_RC_G(TT, NB) \
+  if (fast) { EA_RC_L(TT, NB, false) } else { EA_RC_L(TT, NB, true) }
   if (bf16) {
-    if (nbw == 2) { EA_RC_L(__bf16, 2) } else { EA_RC_L(__bf16, 4) }
+    if (nbw == 2) { EA_RC_G(__bf16, 2) } else { EA_RC_G(__bf16, 4) }
   } else {
-    if (nbw == 2) { EA_RC_L(float, 2) } else { EA_RC_L(float, 4) }
+    if (nbw == 2) { EA_RC_G(float, 2) } else { EA_RC_G(float, 4) }
   }
+#undef EA_RC_G
 #undef EA_RC_L
 #undef EA_RC
   return hipGetLastError();

@@ -204,6 +204,7 @@ PYBIND11_MODULE(_C, m) {
     p.tiles_m = (M + ea_gemm_tile_m(cfg) - 1) / ea_gemm_tile_m(cfg);
     p.tiles_n = (N + ea_gemm_tile_n(cfg) - 1) / ea_gemm_tile_n(cfg);
     ga.nprob = 1;
+    ga.R = 1;
     ga.total_blocks = p.tiles_m * p.tiles_n;
     static long long* dctr = nullptr;
     if (!dctr) {

@@ -61,14 +61,14 @@ bool Executor::build_rowchain() {
   ns = cdiv(l0.Kp, kchunk);
   rc_.nsplitk = ns;
   rc_.nbw = wmax <= 128 ? 2 : 4;
-  const long long slab = (long long)c_.B * l0.N;
+  const long long slab = (long long)c_.B * l0.Np;  // rows padded to 8: 16-byte slab reads
   check(hipMalloc(&d_zp_, sizeof(float) * (size_t)c_.R * ns * slab), "hipMalloc(row-chain slabs)");
   check(hipMemset(d_zp_, 0, sizeof(float) * (size_t)c_.R * ns * slab), "hipMemset(row-chain slabs)");
 
   // tile geometry of the table launches: 64x32 (layer 0), 64x64 (weight gradients)
-  auto blocks = [&](const Prob& p) {
-    if (p.kind == PK_GATHER_T) return p.R * cdiv(p.B, 64) * cdiv(p.K, 64);
-    return p.R * p.tiles_m * p.tiles_n * std::max(1, p.tiles_k);
+  auto blocks = [&](const Prob& p) {  // tiles per replica (grid (R, tiles))
+    if (p.kind == PK_GATHER_T) return cdiv(p.B, 64) * cdiv(p.K, 64);
+    return p.tiles_m * p.tiles_n * std::max(1, p.tiles_k);
   };
   auto table = [&](TableArgs& ta, Prob* host, int n, Prob* dev, int cfg) {
     const int bm = ea_gemm_tile_m(cfg), bn = ea_gemm_tile_n(cfg);
@@ -90,6 +90,7 @@ bool Executor::build_rowchain() {
     }
     ta.probs = dev;
     ta.nprob = n;
+    ta.R = c_.R;
     ta.total_blocks = begin;
     ta.ctr = reinterpret_cast<long long*>(c_.ctr);
     ta.seed = c_.seed;
@@ -104,7 +105,7 @@ bool Executor::build_rowchain() {
   z.tiles_k = ns;
   z.kchunk = kchunk;
   z.D = d_zp_;
-  z.ldd = l0.N;
+  z.ldd = l0.Np;
   z.sD = ns * slab;
   z.sPart = slab;
   z.Z = nullptr;
@@ -231,8 +232,9 @@ void Executor::finalize(Launch& L) const {
       p.tiles_n = cdiv(p.N, bn);
     }
     p.block_begin = begin;
-    begin += p.R * p.tiles_m * p.tiles_n;
+    begin += p.tiles_m * p.tiles_n;  // tiles per replica: grid (R, tiles)
   }
+  L.ga.R = c_.R;
   L.ga.total_blocks = begin;
   L.ga.ctr = reinterpret_cast<long long*>(c_.ctr);
   L.ga.seed = c_.seed;
@@ -522,13 +524,13 @@ void Executor::set_stamps(uintptr_t buf) {
 std::vector<int> Executor::launch_blocks() const {
   std::vector<int> v;
   if (rc_) {
-    v.push_back(rc_.ta_fwd.total_blocks);
+    v.push_back(c_.R * rc_.ta_fwd.total_blocks);
     v.push_back(c_.R * cdiv(c_.B, RC_ROWS));
-    v.push_back(rc_.ta_dw.total_blocks);
+    v.push_back(c_.R * rc_.ta_dw.total_blocks);
     return v;
   }
-  for (auto& L : fwd_) v.push_back(L.ga.total_blocks);
-  for (auto& L : bwd_) v.push_back(L.ga.total_blocks);
+  for (auto& L : fwd_) v.push_back(c_.R * L.ga.total_blocks);
+  for (auto& L : bwd_) v.push_back(c_.R * L.ga.total_blocks);
   return v;
 }
 
@@ -536,7 +538,7 @@ std::vector<int> Executor::table_begins(int launch) const {
   std::vector<int> v;
   if (!rc_ || launch == 1) return v;
   const TableArgs& ta = launch == 0 ? rc_.ta_fwd : rc_.ta_dw;
-  for (int i = 0; i < ta.nprob; ++i) v.push_back(ta.begin[i]);
+  for (int i = 0; i < ta.nprob; ++i) v.push_back(ta.begin[i] * c_.R);  // linear block ids
   return v;
 }
 

@@ -23,8 +23,13 @@ from .trainer import TrainerBase, prepare_features, prepare_targets, split_point
 
 
 class TorchTrainer(TrainerBase):
-    def __init__(self, model, plan, R: int = 1, batch_size: int = 32, device=None, seed: Optional[int] = None):
+    def __init__(self, model, plan, R: int = 1, batch_size: int = 32, device=None, seed: Optional[int] = None,
+                 hash_dropout_seed: Optional[int] = None):
         super().__init__(model, plan, R, batch_size)
+        # None: dropout masks from torch's generator; an int: the native engine's
+        # counter-hash masks for that executor seed (ops/dropout_hash.py), so the two
+        # engines can be compared step for step with dropout on
+        self.hash_dropout_seed = hash_dropout_seed
         self.device = torch.device(device) if device is not None else torch.device("cpu")
         self.like = model.get_weights()
         self.gen = torch.Generator(device="cpu")
@@ -86,10 +91,12 @@ class TorchTrainer(TrainerBase):
     def forward(self, r: int, x: torch.Tensor, training: bool, ps=None):
         h = x
         wi = 0
+        dense = -1  # index of the Dense layer whose output the ops act on (the kernels' `layer`)
         pre, last_act = None, None
         ps = self.params[r] if ps is None else ps
         for op in self.plan.ops:
             if isinstance(op, Dense):
+                dense += 1
                 h = h @ ps[wi]
                 wi += 1
                 if op.use_bias:
@@ -102,7 +109,12 @@ class TorchTrainer(TrainerBase):
                 h = op.activation(h)
             elif isinstance(op, Dropout):
                 if training and op.rate > 0:
-                    keep = torch.rand(h.shape, generator=self.gen).to(h.device) >= op.rate
+                    if self.hash_dropout_seed is not None:
+                        from .dropout_hash import keep_mask
+                        keep = torch.from_numpy(keep_mask(self.hash_dropout_seed, r, dense, self.iters[r],
+                                                          h.shape[0], h.shape[1], op.rate)).to(h.device)
+                    else:
+                        keep = torch.rand(h.shape, generator=self.gen).to(h.device) >= op.rate
                     h = h * keep.to(h.dtype) / (1.0 - op.rate)
             elif isinstance(op, Flatten):
                 h = h.reshape(h.shape[0], -1)

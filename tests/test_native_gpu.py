@@ -592,3 +592,43 @@ def test_ps_pull_refresh_matches_two_step_pull():
     w0, w1 = ts[0].get_weights_flat(), ts[1].get_weights_flat()
     assert np.abs(w0 - theta.cpu().numpy()).max() > 0
     np.testing.assert_array_equal(w0, w1)
+
+
+@pytest.mark.parametrize("rowchain", [0, 1])
+def test_native_dropout_matches_fp32_reference_with_same_masks(rowchain):
+    """Native dropout (masks regenerated from the counter hash in the forward AND the
+    backward kernels) == the fp32 torch autograd engine drawing the same masks
+    (ops/dropout_hash.py): weights and per-step losses agree over several steps of 2
+    replicas, on both step plans -- so the masks, their fwd/bwd identity and the
+    1 / (1 - rate) scaling are those of tf.nn.dropout (reference conftest.py:13,16)."""
+    from elephas_amd import config
+    from elephas_amd.models.optimizers import SGD
+    from elephas_amd.ops.plan import build_plan
+    from elephas_amd.ops.native_engine import NativeTrainer
+    from elephas_amd.ops.torch_engine import TorchTrainer
+    config.set_policy("float32")
+    model = _mlp(40, [48, 32], 6, dropout=0.3)
+    model.compile(SGD(0.2), "categorical_crossentropy", ["acc"])
+    plan = build_plan(model)
+    xs, ys = [], []
+    for r in range(2):
+        x, y = _data(96, 40, 6, seed=20 + r)
+        xs.append(x)
+        ys.append(y)
+    nat = NativeTrainer(model, plan, 2, 32, torch.device("cuda"), seed=12345, rowchain=rowchain)
+    ref = TorchTrainer(model, plan, 2, 32, torch.device("cuda"), hash_dropout_seed=12345)
+    w0 = nat.get_weights_flat()[0].copy()
+    for t in (nat, ref):
+        t.set_data(xs, ys, 0.0, shuffle=False)
+    hn = nat.fit(2)
+    hr = ref.fit(2)
+    wn, wr = nat.get_weights_flat(), ref.get_weights_flat()
+    err = np.abs(wn - wr).max() / np.abs(wr - w0).max()
+    assert err < 1e-4, err
+    for a, b in zip(hn, hr):
+        np.testing.assert_allclose(a["loss"], b["loss"], rtol=1e-4)
+    # without the shared masks the runs differ: the comparison above has teeth
+    free = TorchTrainer(model, plan, 2, 32, torch.device("cuda"), seed=3)
+    free.set_data(xs, ys, 0.0, shuffle=False)
+    free.fit(2)
+    assert np.abs(free.get_weights_flat() - wr).max() / np.abs(wr - w0).max() > 1e-2
