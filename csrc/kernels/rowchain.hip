@@ -206,6 +206,34 @@ __global__ __launch_bounds__(256) void rowchain_kernel(RcArgs a) {
       prow[i] = in ? v : -1;
     }
   }
+  // layer-0 slabs and bias first: phase 0 waits only for these (the wait counter
+  // drains in issue order), the weight streams issued next stay in flight under it
+  const int row = tid >> 4, c0 = (tid & 15) * CPT;
+  const int m = m0 + row;
+  const bool rv = m < valid;
+  float4 sv[RC_MAXSPLIT][CPT / 4];
+  float z[CPT];
+  {
+    const RcLayer l0 = a.ly[0];
+    const float* Zr = a.Zp + (long long)r * a.sZp + (long long)(rv ? m : 0) * l0.Np;
+    const float* bias = Pr + l0.p_off + (long long)l0.K * l0.N;
+#pragma unroll
+    for (int kc = 0; kc < RC_MAXSPLIT; ++kc) {
+      const float* slab = Zr + (long long)(kc < a.nsplitk ? kc : 0) * a.sZpk;
+#pragma unroll
+      for (int v = 0; v < CPT / 4; ++v) {
+        const int c = c0 + 4 * v;
+        sv[kc][v] = *reinterpret_cast<const float4*>(slab + (c < l0.Np ? c : 0));
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+      const int c = c0 + i;
+      const bool cv = c < l0.N && l0.has_bias;
+      const float bv = bias[cv ? c : 0];
+      z[i] = cv ? bv : 0.f;
+    }
+  }
   Ring<T, NBW, PF> ring;
   if constexpr (L > 2) ring_start(ring, WTcur + a.ly[1].wtsh_off, a.ly[1].Kp, a.ly[1].Kp, a.ly[1].N, w, lane);
   uint4 wl[NKF][2];  // last layer forward: B^T rows = its <= 32 outputs, chunks w + 4i
@@ -270,29 +298,6 @@ __global__ __launch_bounds__(256) void rowchain_kernel(RcArgs a) {
   //      issued before the first add
   {
     const RcLayer l0 = a.ly[0];
-    const int row = tid >> 4, c0 = (tid & 15) * CPT;
-    const int m = m0 + row;
-    const bool rv = m < valid;
-    const float* Zr = a.Zp + (long long)r * a.sZp + (long long)(rv ? m : 0) * l0.Np;
-    const float* bias = Pr + l0.p_off + (long long)l0.K * l0.N;
-    float4 sv[RC_MAXSPLIT][CPT / 4];
-#pragma unroll
-    for (int kc = 0; kc < RC_MAXSPLIT; ++kc) {
-      const float* slab = Zr + (long long)(kc < a.nsplitk ? kc : 0) * a.sZpk;
-#pragma unroll
-      for (int v = 0; v < CPT / 4; ++v) {
-        const int c = c0 + 4 * v;
-        sv[kc][v] = *reinterpret_cast<const float4*>(slab + (c < l0.Np ? c : 0));
-      }
-    }
-    float z[CPT];
-#pragma unroll
-    for (int i = 0; i < CPT; ++i) {
-      const int c = c0 + i;
-      const bool cv = c < l0.N && l0.has_bias;
-      const float bv = bias[cv ? c : 0];
-      z[i] = cv ? bv : 0.f;
-    }
     // the targets of this workgroup's rows (perm rows requested at entry): loaded now,
     // stored to LDS only before the loss, so nothing waits for this second round trip
     {
@@ -318,6 +323,7 @@ __global__ __launch_bounds__(256) void rowchain_kernel(RcArgs a) {
         z[4 * v + 3] += sv[kc][v].w;
       }
     }
+    rstamp(a, 12);  // slabs summed
     float o[CPT], gg[CPT], dv[CPT], gv[CPT];
     act_fg_v<CPT>(l0.act, z, o, gg);
     const float keep_scale = l0.rate > 0.f ? 1.f / (1.f - l0.rate) : 1.f;
@@ -340,7 +346,9 @@ __global__ __launch_bounds__(256) void rowchain_kernel(RcArgs a) {
       }
     }
   }
+  rstamp(a, 13);  // D_0 / G_0 in LDS
   lds_barrier();
+  rstamp(a, 14);
   // D_0^T (layer 1's weight-gradient operand) from the LDS tile: 4 rows per store
   {
     const RcLayer l0 = a.ly[0];
