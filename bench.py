@@ -108,9 +108,8 @@ def main():
                     help="batch granularity: per-layer gradient buckets all-reduced beside the backward")
     ap.add_argument("--dropout", type=float, default=None, help="override the model's dropout (diagnostics)")
     ap.add_argument("--out", default=None, help="also append the JSON line to this file")
-    ap.add_argument("--async-threads", action="store_true",
-                    help="async/hogwild: one Python thread + executor per worker instead of the lockstep "
-                         "replica executor (worker.BatchedAsynchronousWorker)")
+    ap.add_argument("--async-groups", type=int, default=None,
+                    help="async/hogwild: independently progressing worker groups per GPU (default: one per worker)")
     ap.add_argument("--mode", default="synchronous", choices=["synchronous", "asynchronous", "hogwild"],
                     help="asynchronous / hogwild: every worker pulls from and pushes to the HBM "
                          "parameter server around each step (frequency='batch', BASELINE config #3)")
@@ -238,7 +237,11 @@ def main():
             torch.cuda.synchronize()
         dist.barrier()
 
-    # warmup (includes hipGraph capture)
+    # warmup (includes hipGraph capture of both chunk shapes)
+    if gpu and not args.no_graph:
+        t.prepare_graphs(allreduce_path=batch_mode and world > 1 and not args.overlap)
+    if gpu and args.validation_split > 0:
+        t._eval_exe()   # the epoch-end validation executor exists before the timed region
     run(args.warmup)
     average()
     sync()
@@ -366,118 +369,76 @@ def bench_infer(args, model, dist, rank, world, dev):
 
 
 def bench_async(args, model, dist, rank, world, dev):
-    """Async / hogwild DP through the device parameter server (reference worker.py:114-127,
-    frequency='batch'): W worker threads per GPU, each step = pull theta from the PS (HBM on
-    rank 0; other ranks over xGMI IPC) -> one optimizer step -> push theta_pulled - theta.
-    'asynchronous' serialises pulls/pushes with the writer-priority RW lock, 'hogwild' not."""
-    import threading
+    """Async / hogwild DP through the sharded device parameter server (reference
+    worker.py:114-127, frequency='batch'): the W workers of a GPU are split into G
+    independently progressing groups (worker.BatchedAsynchronousWorker, one executor +
+    HIP stream each); every group-step is ONE hipGraph replay of pull (gather theta from
+    the shards, chunk-consistent in 'asynchronous') -> refresh -> train -> push (fp32
+    atomic adds into the owners' shards over xGMI).  No host lock, no host sync."""
     import torch
     from elephas_amd.ops.native_engine import NativeTrainer
-    from elephas_amd.ops.plan import build_plan
+    from elephas_amd.ops.plan import build_plan, flatten_weights
     from elephas_amd.parameter.client import DeviceClient
-    from elephas_amd.parameter.server import DeviceServer
-    from elephas_amd.utils.serialization import model_to_dict
+    from elephas_amd.worker import BatchedAsynchronousWorker, _Group
     dims, drop, classes, rows, _ = MODELS[args.model]
     W, B = args.workers_per_gpu, args.batch
-    ps = None
+    G = max(1, min(W, args.async_groups or W))
+    init = flatten_weights(model.get_weights())
+    client = DeviceClient().connect(len(init), args.mode)
     if rank == 0:
-        ps = DeviceServer(model_to_dict(model), 0, args.mode)
-        client = DeviceClient(server=ps)
-        handle = ps.handle() if world > 1 else None
-    else:
-        handle, client = None, None
-    handle = dist.broadcast_object(handle, 0)
-    if rank != 0:
-        client = DeviceClient(handle=handle)
+        src = torch.from_numpy(init).to(dev)
+        client.ps.set(src.data_ptr(), torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+    dist.barrier()
     plan = build_plan(model)
     rng = np.random.default_rng(1000 + rank)
     centers = rng.normal(0, 1, size=(classes, dims[0])).astype(np.float32)
-    trainers = []
+    dx, dy = [], []
     for w in range(W):
         y = rng.integers(0, classes, rows)
         x = centers[y] + rng.normal(0, 2.0, size=(rows, dims[0])).astype(np.float32)
-        x = ((x - x.min()) / (x.max() - x.min())).astype(np.float32)
-        t = NativeTrainer(model, plan, 1, B, dev, seed=4321 + 97 * rank + w)
-        t.set_data([x], [np.eye(classes, dtype=np.float32)[y]], args.validation_split, shuffle=True)
+        dx.append(((x - x.min()) / (x.max() - x.min())).astype(np.float32))
+        dy.append(np.eye(classes, dtype=np.float32)[y])
+    bounds = [W * g // G for g in range(G + 1)]
+    worker = BatchedAsynchronousWorker(None, None, client, {}, "batch", None, None, None, None)
+    groups = []
+    for g in range(G):
+        lo, hi = bounds[g], bounds[g + 1]
+        t = NativeTrainer(model, plan, hi - lo, B, dev, seed=4321 + 97 * rank + g)
+        t.set_data(dx[lo:hi], dy[lo:hi], args.validation_split, shuffle=True)
         t.begin_epoch()
-        trainers.append(t)
-    spe = int(math.ceil(trainers[0].ntrain_h[0] / B))
-    errors = []
-    if not args.async_threads:
-        # lockstep replicas (the SparkModel GPU path, worker.BatchedAsynchronousWorker):
-        # one pull into all W replicas, one grouped step, one push of the summed deltas
-        xs = [t.X for t in trainers]
-        del trainers
-        t = NativeTrainer(model, plan, W, B, dev, seed=4321 + 97 * rank)
-        rngd = np.random.default_rng(1000 + rank)
-        centers = rngd.normal(0, 1, size=(classes, dims[0])).astype(np.float32)
-        dx, dy = [], []
-        for w in range(W):
-            y = rngd.integers(0, classes, rows)
-            x = centers[y] + rngd.normal(0, 2.0, size=(rows, dims[0])).astype(np.float32)
-            dx.append(((x - x.min()) / (x.max() - x.min())).astype(np.float32))
-            dy.append(np.eye(classes, dtype=np.float32)[y])
-        t.set_data(dx, dy, args.validation_split, shuffle=True)
-        t.begin_epoch()
-        state = {"pos": 0}
-        before = torch.empty(t.P.shape[1], dtype=torch.float32, device=t.P.device)
-
-        def run_lockstep(k):
-            for _ in range(k):
-                if state["pos"] >= spe:
-                    t.begin_epoch()
-                    state["pos"] = 0
-                with torch.cuda.stream(t.stream):   # one kernel: theta -> all W replicas' P + images, before
-                    client.pull_refresh(t, before.data_ptr())
-                t.run_steps(1, use_graph=True)
-                with torch.cuda.stream(t.stream):   # one kernel: theta += sum_w P[w] - W * before
-                    client.push_replicas(t.P.data_ptr(), t.P.stride(0), W, before.data_ptr(), t.s)
-                state["pos"] += 1
-            t.stream.synchronize()
-
-    def worker(t, k):
-        try:
-            done = 0
-            while done < k:
-                if t._pos >= spe:
-                    t.begin_epoch()
-                    t._pos = 0
-                with torch.cuda.stream(t.stream):
-                    client.pull_into(t.P.data_ptr(), t.s)
-                    t.sync_shadows()
-                    before = t.P.clone()
-                t.run_steps(1, use_graph=True)
-                with torch.cuda.stream(t.stream):
-                    delta = before - t.P
-                    client.push_from(delta.data_ptr(), t.s)
-                t._pos += 1
-                done += 1
-            t.stream.synchronize()
-        except BaseException as e:  # noqa: BLE001 - surfaced below
-            errors.append(e)
+        grp = _Group(t, [True] * (hi - lo))
+        if not args.no_graph:
+            grp.capture(worker)
+        groups.append(grp)
+    spe = groups[0].t.steps_per_epoch()
+    state = {"pos": 0}
 
     def run(k):
-        ths = [threading.Thread(target=worker, args=(t, k)) for t in trainers]
-        for th in ths:
-            th.start()
-        for th in ths:
-            th.join()
-        if errors:
-            raise errors[0]
+        while k > 0:
+            if state["pos"] >= spe:
+                for grp in groups:
+                    grp.t.begin_epoch()
+                state["pos"] = 0
+            n = min(k, spe - state["pos"])
+            for grp in groups:            # every group enqueues n rounds on its own stream
+                grp.steps(worker, n)
+            state["pos"] += n
+            k -= n
 
-    if args.async_threads:
-        for t in trainers:
-            t._pos = 0
-    else:
-        run = run_lockstep
+    def sync():
+        for grp in groups:
+            grp.t.stream.synchronize()
+        torch.cuda.synchronize()
+        dist.barrier()
+
     run(args.warmup)
-    torch.cuda.synchronize()
-    dist.barrier()
+    sync()
     t0 = time.perf_counter()
     run(args.steps)
-    torch.cuda.synchronize()
-    dist.barrier()
+    sync()
     dt = time.perf_counter() - t0
+    client.check()
     dt_max = max(dist.all_gather_object(dt))
     if rank == 0:
         value = W * B * args.steps * world / dt_max
@@ -490,13 +451,14 @@ def bench_async(args, model, dist, rank, world, dev):
             "data": "synthetic, random-init weights",
             "config": {"model": args.model, "global_batch": B * W * world, "seq_len": None,
                        "parallelism": f"{args.mode}-dp{world}", "workers_per_gpu": W, "batch_per_worker": B,
-                       "frequency": "batch", "ps": "device (HBM, rank 0; xGMI IPC for other ranks)",
-                       "workers": "python threads" if args.async_threads else "lockstep replicas of one executor"},
+                       "frequency": "batch", "groups_per_gpu": G,
+                       "ps": f"sharded over {world} GPU(s), 4096-parameter chunks, IPC-mapped",
+                       "exchange": "hipGraph per group-step (pull, refresh, train, push)" if groups[0].graph
+                       else "eager launches"},
         }
         print(json.dumps(line), flush=True)
     dist.barrier()
-    if ps is not None:
-        ps.close()
+    client.close()
     if dist.is_initialized():
         import torch.distributed as tdist
         tdist.destroy_process_group()

@@ -296,48 +296,6 @@ extern "C" hipError_t ea_ps_sub(float* p, const float* d, long long n, float sca
   return hipGetLastError();
 }
 
-// Batched async workers (worker.BatchedAsynchronousWorker): the R lockstep replicas
-// of a rank pull theta once and push the sum of their deltas.
-//   pull : P[r] = theta (every replica) and before = theta, one pass over theta
-//   push : theta += sum_r P[r] - R * before    (= theta - sum_r (before - P[r]))
-// replacing a D2D copy + broadcast + clone (pull) and reduce + scale + subtract +
-// apply (push) -- 3 and 4 launches -- on every batch.
-__global__ __launch_bounds__(256) void ps_pull_replicas_kernel(const float* __restrict__ src, float* P, long long sP,
-                                                               int R, float* before, long long n) {
-  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
-    const float v = src[i];
-    before[i] = v;
-    for (int r = 0; r < R; ++r) P[(long long)r * sP + i] = v;
-  }
-}
-
-__global__ __launch_bounds__(256) void ps_push_replicas_kernel(float* p, const float* P, long long sP, int R,
-                                                               const float* __restrict__ before, long long n,
-                                                               int atomic) {
-  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
-    // sum of per-replica differences: each P[r] - before is (nearly) exact because
-    // the two are close (Sterbenz); -R*before + sum P[r] would round every add at
-    // ulp(R*|w|) and lose the small deltas
-    const float b = before[i];
-    float d = 0.f;
-    for (int r = 0; r < R; ++r) d += P[(long long)r * sP + i] - b;
-    if (atomic) atomicAdd(p + i, d);
-    else p[i] += d;
-  }
-}
-
-extern "C" hipError_t ea_ps_pull_replicas(const float* src, float* P, long long sP, int R, float* before, long long n,
-                                          hipStream_t s) {
-  hipLaunchKernelGGL(ps_pull_replicas_kernel, dim3(grid_for(n)), dim3(256), 0, s, src, P, sP, R, before, n);
-  return hipGetLastError();
-}
-
-extern "C" hipError_t ea_ps_push_replicas(float* p, const float* P, long long sP, int R, const float* before,
-                                          long long n, int atomic, hipStream_t s) {
-  hipLaunchKernelGGL(ps_push_replicas_kernel, dim3(grid_for(n)), dim3(256), 0, s, p, P, sP, R, before, n, atomic);
-  return hipGetLastError();
-}
-
 extern "C" hipError_t ea_sub(const float* a, const float* b, float* out, long long n, hipStream_t s) {
   hipLaunchKernelGGL(sub_kernel, dim3(grid_for(n)), dim3(256), 0, s, a, b, out, n);
   return hipGetLastError();

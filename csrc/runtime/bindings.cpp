@@ -10,7 +10,8 @@
 #include <cstring>
 
 #include "executor.h"
-#include "param_server.h"
+#include "rwlock.h"
+#include "peer.h"
 #include "host_loader.h"
 
 namespace py = pybind11;
@@ -235,68 +236,53 @@ PYBIND11_MODULE(_C, m) {
         "sub");
   });
 
-  // ---- device parameter server (async / hogwild), see param_server.h
-  py::class_<DeviceParameterServer>(m, "DeviceParameterServer")
-      .def(py::init<long long, int, int, const std::string&>(), py::arg("n"), py::arg("locked"), py::arg("device"),
-           py::arg("lock_name") = "")
-      .def("pull", [](DeviceParameterServer& ps, uintptr_t dst, uintptr_t s) {
-        py::gil_scoped_release rel;
-        ps.pull(reinterpret_cast<float*>(dst), S(s));
+  // ---- peer-memory collectives and the sharded device PS (peer.h)
+  py::class_<PeerAllReduce>(m, "PeerAllReduce")
+      .def(py::init<int, int, long long, int, double>(), py::arg("rank"), py::arg("world"), py::arg("cap_elems"),
+           py::arg("device"), py::arg("timeout_s") = 20.0)
+      .def("handle", [](PeerAllReduce& p) { return py::bytes(p.handle()); })
+      .def("open", [](PeerAllReduce& p, std::vector<py::bytes> hs) {
+        std::vector<std::string> v;
+        for (auto& h : hs) v.emplace_back(std::string(h));
+        p.open(v);
       })
-      .def("push", [](DeviceParameterServer& ps, uintptr_t delta, uintptr_t s) {
+      .def("all_reduce", [](PeerAllReduce& p, uintptr_t in, uintptr_t out, long long n, uintptr_t s, int algo) {
         py::gil_scoped_release rel;
-        ps.push(reinterpret_cast<const float*>(delta), S(s));
+        p.all_reduce(reinterpret_cast<const float*>(in), reinterpret_cast<float*>(out), n, S(s), algo);
+      }, py::arg("inp"), py::arg("out"), py::arg("n"), py::arg("stream"), py::arg("algo") = -1)
+      .def("error", &PeerAllReduce::error)
+      .def("clear_error", &PeerAllReduce::clear_error)
+      .def_property_readonly("capacity", &PeerAllReduce::capacity)
+      .def_property_readonly("calls", &PeerAllReduce::calls)
+      .def_property("twoshot_min_bytes", &PeerAllReduce::twoshot_min_bytes, &PeerAllReduce::set_twoshot_min_bytes);
+  py::class_<ShardedParameterServer>(m, "ShardedParameterServer")
+      .def(py::init<int, int, long long, int, int, long long, double>(), py::arg("rank"), py::arg("world"),
+           py::arg("n"), py::arg("consistent"), py::arg("device"), py::arg("chunk") = 4096, py::arg("timeout_s") = 30.0)
+      .def("handle", [](ShardedParameterServer& p) { return py::bytes(p.handle()); })
+      .def("open", [](ShardedParameterServer& p, std::vector<py::bytes> hs) {
+        std::vector<std::string> v;
+        for (auto& h : hs) v.emplace_back(std::string(h));
+        p.open(v);
       })
-      .def("pull_replicas", [](DeviceParameterServer& ps, uintptr_t P, long long sP, int R, uintptr_t before, uintptr_t s) {
-        py::gil_scoped_release rel;
-        ps.pull_replicas(reinterpret_cast<float*>(P), sP, R, reinterpret_cast<float*>(before), S(s));
+      .def("set", [](ShardedParameterServer& p, uintptr_t src, uintptr_t s) {
+        p.set(reinterpret_cast<const float*>(src), S(s));
       })
-      .def("push_replicas", [](DeviceParameterServer& ps, uintptr_t P, long long sP, int R, uintptr_t before, uintptr_t s) {
-        py::gil_scoped_release rel;
-        ps.push_replicas(reinterpret_cast<const float*>(P), sP, R, reinterpret_cast<const float*>(before), S(s));
+      .def("pull", [](ShardedParameterServer& p, uintptr_t dst, uintptr_t s) {
+        p.pull(reinterpret_cast<float*>(dst), S(s));
       })
-      .def("set", [](DeviceParameterServer& ps, uintptr_t src, uintptr_t s) {
-        py::gil_scoped_release rel;
-        ps.set(reinterpret_cast<const float*>(src), S(s));
+      .def("push_replicas", [](ShardedParameterServer& p, uintptr_t P, long long sP, int R, uintptr_t before,
+                               uintptr_t s) {
+        p.push_replicas(reinterpret_cast<const float*>(P), sP, R, reinterpret_cast<const float*>(before), S(s));
       })
-      .def("ipc_handle", [](DeviceParameterServer& ps) { return py::bytes(ps.ipc_handle()); })
-      .def("data_ptr", [](DeviceParameterServer& ps) { return reinterpret_cast<uintptr_t>(ps.data()); })
-      .def_property_readonly("n", &DeviceParameterServer::size)
-      .def_property_readonly("pushes", &DeviceParameterServer::pushes)
-      .def_property_readonly("pulls", &DeviceParameterServer::pulls);
-  py::class_<RemoteParameterServer>(m, "RemoteParameterServer")
-      .def(py::init([](py::bytes h, long long n, int locked, std::string lock_name) {
-             return new RemoteParameterServer(std::string(h), n, locked, lock_name);
-           }),
-           py::arg("handle"), py::arg("n"), py::arg("locked"), py::arg("lock_name"))
-      .def("pull", [](RemoteParameterServer& ps, uintptr_t dst, uintptr_t s) {
-        py::gil_scoped_release rel;
-        ps.pull(reinterpret_cast<float*>(dst), S(s));
+      .def("push_delta", [](ShardedParameterServer& p, uintptr_t d, uintptr_t s) {
+        p.push_delta(reinterpret_cast<const float*>(d), S(s));
       })
-      .def("push", [](RemoteParameterServer& ps, uintptr_t delta, uintptr_t s) {
-        py::gil_scoped_release rel;
-        ps.push(reinterpret_cast<const float*>(delta), S(s));
-      })
-      .def("pull_replicas", [](RemoteParameterServer& ps, uintptr_t P, long long sP, int R, uintptr_t before, uintptr_t s) {
-        py::gil_scoped_release rel;
-        ps.pull_replicas(reinterpret_cast<float*>(P), sP, R, reinterpret_cast<float*>(before), S(s));
-      })
-      .def("push_replicas", [](RemoteParameterServer& ps, uintptr_t P, long long sP, int R, uintptr_t before, uintptr_t s) {
-        py::gil_scoped_release rel;
-        ps.push_replicas(reinterpret_cast<const float*>(P), sP, R, reinterpret_cast<const float*>(before), S(s));
-      });
-  // parameter-server pull fused with the executor's shadow refresh: one kernel reads
-  // theta and writes every replica's P, both W / W^T parities and `before`
-  m.def("ps_pull_refresh", [](DeviceParameterServer& ps, Executor& exe, uintptr_t before, uintptr_t s) {
-    if (exe.covered_params() != ps.size()) throw std::invalid_argument("ps_pull_refresh: parameter count mismatch");
-    py::gil_scoped_release rel;
-    ps.pull_with(S(s), [&](float* theta) { exe.refresh_from(theta, reinterpret_cast<float*>(before), S(s)); });
-  });
-  m.def("ps_pull_refresh", [](RemoteParameterServer& ps, Executor& exe, uintptr_t before, uintptr_t s) {
-    if (exe.covered_params() != ps.size()) throw std::invalid_argument("ps_pull_refresh: parameter count mismatch");
-    py::gil_scoped_release rel;
-    ps.pull_with(S(s), [&](float* theta) { exe.refresh_from(theta, reinterpret_cast<float*>(before), S(s)); });
-  });
+      .def("error", &ShardedParameterServer::error)
+      .def("clear_error", &ShardedParameterServer::clear_error)
+      .def("shard_begin", &ShardedParameterServer::shard_begin)
+      .def_property_readonly("n", &ShardedParameterServer::size)
+      .def_property_readonly("consistent", &ShardedParameterServer::consistent)
+      .def_property_readonly("nchunks", &ShardedParameterServer::nchunks);
   m.def("shm_rwlock_create", &shm_rwlock_create);
   m.def("shm_rwlock_destroy", &shm_rwlock_destroy);
 

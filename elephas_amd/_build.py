@@ -27,9 +27,10 @@ SOURCES = [
     "kernels/gemm_f32.hip",
     "kernels/flat.hip",
     "kernels/rowchain.hip",
+    "kernels/peer.hip",
     "runtime/executor.cpp",
+    "runtime/peer.cpp",
     "runtime/rwlock.cpp",
-    "runtime/param_server.cpp",
     "runtime/host_loader.cpp",
     "runtime/bindings.cpp",
 ]

@@ -331,12 +331,19 @@ class NativeTrainer(TrainerBase):
             for _ in range(nsteps):
                 self.exe.train_step(self.s)
             return
-        g = min(self.GRAPH_CHUNK, nsteps)
-        full, rest = divmod(nsteps, g)
+        # fixed chunk shapes: only two graphs ever exist per executor, so no capture
+        # lands inside a timed loop whose step count differs from the warmup's
+        full, rest = divmod(nsteps, self.GRAPH_CHUNK)
         if full:
-            self.exe.replay_n(self._graph(g, 0), full, self.s)
+            self.exe.replay_n(self._graph(self.GRAPH_CHUNK, 0), full, self.s)
         if rest:
             self.exe.replay_n(self._graph(1, 0), rest, self.s)
+
+    def prepare_graphs(self, allreduce_path: bool = False):
+        """Capture (without running) every graph run_steps / run_steps_allreduce use."""
+        keys = [(1, 1), (1, 2)] if allreduce_path else [(self.GRAPH_CHUNK, 0), (1, 0)]
+        for n, mode in keys:
+            self._graph(n, mode)
 
     def run_steps_allreduce(self, nsteps: int, allreduce, use_graph: bool = True):
         """Per-step gradient all-reduce path: [fwd+bwd -> G] -> allreduce(G) -> [apply]."""
@@ -401,28 +408,40 @@ class NativeTrainer(TrainerBase):
             self.exe = self.C.Executor(cfg)
 
     def fit(self, epochs, verbose=0, allreduce=None):
-        hist = [dict() if self.active[r] else None for r in range(self.R)]
+        hist = self.new_history()
         self._enter()
-        steps = self.steps_per_epoch()
         for epoch in range(int(epochs)):
-            self.begin_epoch()
-            if allreduce is None:
-                self.run_steps(steps)
-            else:
-                self.run_steps_allreduce(steps, allreduce)
-            sums = self._host(self.acc) if steps > 0 else np.zeros((self.R, 6))
-            val = self._val_sums() if max(self.vcount_h) > 0 else None
-            for r in range(self.R):
-                if not self.active[r]:
-                    continue
-                h = self._history_from_sums(sums[r]) if self.ntrain_h[r] > 0 else {}
-                if val is not None and self.vcount_h[r] > 0:
-                    h.update(self._history_from_sums(val[r], "val_"))
-                for k, v in h.items():
-                    hist[r].setdefault(k, []).append(v)
-                if verbose:
-                    self.print_epoch(epoch, epochs, h, r)
+            self.launch_epoch(allreduce)
+            self.collect_epoch(hist, epoch, epochs, verbose)
         self._exit()
+        return hist
+
+    def new_history(self):
+        return [dict() if self.active[r] else None for r in range(self.R)]
+
+    def launch_epoch(self, allreduce=None):
+        """Enqueue one epoch (reshuffle + every step) on self.stream; no host sync."""
+        self.begin_epoch()
+        steps = self.steps_per_epoch()
+        if allreduce is None:
+            self.run_steps(steps)
+        else:
+            self.run_steps_allreduce(steps, allreduce)
+
+    def collect_epoch(self, hist, epoch, epochs, verbose=0):
+        """Append the launched epoch's loss / metrics and validation pass to ``hist``."""
+        sums = self._host(self.acc) if self.steps_per_epoch() > 0 else np.zeros((self.R, 6))
+        val = self._val_sums() if max(self.vcount_h) > 0 else None
+        for r in range(self.R):
+            if not self.active[r]:
+                continue
+            h = self._history_from_sums(sums[r]) if self.ntrain_h[r] > 0 else {}
+            if val is not None and self.vcount_h[r] > 0:
+                h.update(self._history_from_sums(val[r], "val_"))
+            for k, v in h.items():
+                hist[r].setdefault(k, []).append(v)
+            if verbose:
+                self.print_epoch(epoch, epochs, h, r)
         return hist
 
     def _val_sums(self):

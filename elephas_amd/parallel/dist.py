@@ -66,10 +66,17 @@ def _comm_device() -> torch.device:
 
 
 def all_reduce_sum_(t: torch.Tensor) -> torch.Tensor:
-    """In-place sum across ranks; moves through the backend's device if needed."""
+    """In-place sum across ranks; moves through the backend's device if needed.
+    fp32 CUDA tensors of an RCCL job go through the peer-memory all-reduce
+    (parallel/p2p.py) up to its size limit."""
     if not is_initialized() or world_size() == 1:
         return t
     dev = _comm_device()
+    if t.is_cuda and dev.type == "cuda":
+        from . import p2p
+        peer = p2p.get()
+        if peer is not None and peer.eligible(t):
+            return peer.all_reduce_(t)
     if t.device == dev or (t.device.type == dev.type == "cuda"):
         dist.all_reduce(t)
         return t

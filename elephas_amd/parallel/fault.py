@@ -54,5 +54,10 @@ def maybe_inject(phase: str, rank: int) -> None:
         raise InjectedFault(f"injected fault: rank {rank}, phase {phase}, occurrence {n}")
 
 
+def injection_active() -> bool:
+    """True when a fault is configured (hooks must then run eagerly, not from a graph)."""
+    return _spec() is not None
+
+
 def reset() -> None:
     _counts.clear()

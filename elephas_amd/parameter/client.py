@@ -78,66 +78,77 @@ class SocketClient(BaseParameterClient):
 
 
 class DeviceClient(BaseParameterClient):
-    """Client of a DeviceServer: same-process (direct) or another process (HIP IPC over xGMI)."""
+    """This rank's endpoint of the sharded device parameter server.
+
+    ``connect`` is collective over the job's ranks (every rank allocates its shard
+    and maps every other rank's through HIP IPC); afterwards every call enqueues
+    kernels on the given stream and returns without synchronising it.
+    """
 
     client_type = "device"
 
-    def __init__(self, port: int = 4000, server=None, handle=None, like=None):
+    def __init__(self, port: int = 4000, like=None):
         self.port = port
-        self.server = server
-        self.remote = None
         self.like = like
-        if handle is not None:
-            self.attach(handle)
+        self.ps = None
+        self.n = None
 
-    def attach(self, handle):
+    def connect(self, n: int, mode: str, server=None, rank: int = None, world: int = None, device: int = None,
+                allgather=None, chunk: int = 4096):
+        import torch
         from ..ops import native
-        h, n, locked, lock_name = handle
-        self.remote = native.require().RemoteParameterServer(h, n, locked, lock_name)
-        self.n = n
+        from ..parallel import dist
+        from ..parallel.p2p import exchange_handles
+        rank = dist.rank() if rank is None else rank
+        world = dist.world_size() if world is None else world
+        device = torch.cuda.current_device() if device is None else device
+        consistent = 1 if mode == "asynchronous" else 0
+        self.ps = native.require().ShardedParameterServer(rank, world, int(n), consistent, device, chunk)
+        self.ps.open(exchange_handles(self.ps.handle(), allgather))
+        self.n = int(n)
+        if server is not None:
+            server.native = self.ps
+            self.like = server._like
+        return self
 
-    def bind(self, server):
-        self.server = server
-        self.like = server._like
+    def close(self):
+        self.ps = None
 
-    def _ps(self):
-        if self.server is not None:
-            return self.server.ps
-        if self.remote is not None:
-            return self.remote
-        raise RuntimeError("DeviceClient is not bound to a server")
+    def _native(self):
+        if self.ps is None:
+            raise RuntimeError("DeviceClient is not connected (DeviceClient.connect is collective)")
+        return self.ps
 
-    # flat device-buffer API (hot path)
+    # flat device-buffer API (hot path; stream-ordered, no host synchronisation)
     def pull_into(self, dst_ptr: int, stream: int) -> None:
-        self._ps().pull(dst_ptr, stream)
+        self._native().pull(dst_ptr, stream)
 
     def push_from(self, delta_ptr: int, stream: int) -> None:
-        self._ps().push(delta_ptr, stream)
-
-    # R lockstep replicas (rows of a [R, n] fp32 buffer, row stride sP elements)
-    def pull_replicas(self, P_ptr: int, sP: int, R: int, before_ptr: int, stream: int) -> None:
-        """P[r] = theta for every replica and before = theta (one kernel)."""
-        self._ps().pull_replicas(P_ptr, sP, R, before_ptr, stream)
+        """theta -= delta (the reference's update semantics)."""
+        self._native().push_delta(delta_ptr, stream)
 
     def pull_refresh(self, trainer, before_ptr: int) -> None:
-        """Pull fused with the trainer's weight-image refresh: ONE kernel reads theta and
-        writes every replica's fp32 master, both bf16 W / W^T parities and `before`."""
-        from ..ops import native
-        native.require().ps_pull_refresh(self._ps(), trainer.exe, before_ptr, trainer.s)
+        """before = theta (one gather kernel), then every replica's fp32 master and both
+        weight-image parities from it (one kernel)."""
+        self._native().pull(before_ptr, trainer.s)
+        trainer.exe.refresh_from(before_ptr, 0, trainer.s)
 
     def push_replicas(self, P_ptr: int, sP: int, R: int, before_ptr: int, stream: int) -> None:
-        """theta -= sum_r (before - P[r]) (one kernel)."""
-        self._ps().push_replicas(P_ptr, sP, R, before_ptr, stream)
+        """theta += sum_r (P[r] - before) (one kernel)."""
+        self._native().push_replicas(P_ptr, sP, R, before_ptr, stream)
 
-    # list-of-arrays API (reference compatibility)
+    def check(self) -> None:
+        e = self._native().error()
+        if e:
+            raise RuntimeError(f"device parameter server: a wait timed out (error word {e})")
+
+    # list-of-arrays API (reference compatibility; synchronous)
     def get_parameters(self):
-        if self.server is not None:
-            return self.server.get_weights()
         import torch
         from ..ops.plan import unflatten_weights
         buf = torch.empty(self.n, dtype=torch.float32, device="cuda")
         s = torch.cuda.current_stream()
-        self.remote.pull(buf.data_ptr(), s.cuda_stream)
+        self.pull_into(buf.data_ptr(), s.cuda_stream)
         s.synchronize()
         return unflatten_weights(buf.cpu().numpy(), self.like) if self.like else buf.cpu().numpy()
 

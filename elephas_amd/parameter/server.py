@@ -3,11 +3,14 @@
 Three transports behind the reference's server API
 (reference elephas/parameter/server.py:17-233):
   * ``DeviceServer``  (MI355X-native, default on GPU): the master parameters
-    are one flat fp32 vector in HBM (``_C.DeviceParameterServer``); workers on
-    the same process pull/push device-to-device, workers in other processes
-    map it through a HIP IPC handle and update it with peer RMW kernels over
-    xGMI.  'asynchronous' takes a writer-priority RW lock around every pull and
-    push; 'hogwild' takes none.
+    are one flat fp32 vector sharded in 4096-parameter chunks over the GPUs of
+    the job (``_C.ShardedParameterServer``, csrc/kernels/peer.hip); every rank
+    maps every shard through HIP IPC.  A pull is one gather kernel, a push one
+    kernel of fp32 atomic adds into the owners' memory over xGMI -- no host
+    lock, no stream synchronisation, capturable in a hipGraph.  Pushes are
+    never lost in either mode; 'asynchronous' pulls are chunk-consistent (a
+    pulled chunk never holds half of a push, per-chunk began/ended counters),
+    'hogwild' pulls read whatever is there.
   * ``HttpServer`` / ``SocketServer`` (host, cross-process compat transports
     with the reference's routes and opcodes).  Payloads are ``.npz`` archives
     read with ``allow_pickle=False`` instead of pickle.
@@ -22,7 +25,6 @@ import io
 import logging
 import socket
 import threading
-import uuid
 from typing import List, Optional
 
 import numpy as np
@@ -238,22 +240,19 @@ class SocketServer(BaseParameterServer):
 
 
 class DeviceServer(BaseParameterServer):
-    """HBM-resident flat parameter vector with device pull/push (see module doc)."""
+    """Rank 0's handle on the sharded HBM parameter server (see module doc).
+
+    The native state (``_C.ShardedParameterServer``: theta cut into chunks spread
+    over every rank's GPU memory) is created collectively by ``DeviceClient.connect``
+    on every rank when a fit starts; before that the server holds the weights on
+    the host like the other transports.
+    """
 
     def __init__(self, model, port: int, mode: str, **kwargs):
         super().__init__(model, port, mode, **kwargs)
-        from ..ops import native
-        from ..ops.plan import flatten_weights
-        import torch
-        self.C = native.require()
         self._like = self.master_network.get_weights()
         self.n = int(sum(w.size for w in self._like))
-        self.device = torch.cuda.current_device()
-        self.lock_name = kwargs.get("lock_name") or f"/elephas_amd_ps_{uuid.uuid4().hex[:12]}"
-        self.C.shm_rwlock_create(self.lock_name)
-        self.ps = self.C.DeviceParameterServer(max(self.n, 1), 1 if mode == "asynchronous" else 0, self.device,
-                                               self.lock_name)
-        self.set_weights(self._like)
+        self.native = None      # this rank's ShardedParameterServer once connected
         self.running = False
 
     def start(self):
@@ -263,31 +262,26 @@ class DeviceServer(BaseParameterServer):
         self.running = False
 
     def close(self):
-        if getattr(self, "lock_name", None):
-            self.C.shm_rwlock_destroy(self.lock_name)
-            self.lock_name = None
-
-    def __del__(self):
-        try:
-            self.close()
-        except Exception:
-            pass
+        self.native = None
 
     def set_weights(self, weights):
+        if self.native is None:
+            self.master_network.set_weights(weights)
+            return
         import torch
         from ..ops.plan import flatten_weights
-        flat = torch.from_numpy(flatten_weights(list(weights))).cuda(self.device)
-        self.ps.set(flat.data_ptr(), torch.cuda.current_stream(self.device).cuda_stream)
+        flat = torch.from_numpy(flatten_weights(list(weights))).cuda()
+        s = torch.cuda.current_stream()
+        self.native.set(flat.data_ptr(), s.cuda_stream)
+        s.synchronize()
 
     def get_weights(self):
+        if self.native is None:
+            return self.master_network.get_weights()
         import torch
         from ..ops.plan import unflatten_weights
-        buf = torch.empty(self.n, dtype=torch.float32, device=f"cuda:{self.device}")
-        s = torch.cuda.current_stream(self.device)
-        self.ps.pull(buf.data_ptr(), s.cuda_stream)
+        buf = torch.empty(self.n, dtype=torch.float32, device="cuda")
+        s = torch.cuda.current_stream()
+        self.native.pull(buf.data_ptr(), s.cuda_stream)
         s.synchronize()
         return unflatten_weights(buf.cpu().numpy(), self._like)
-
-    def handle(self):
-        """(IPC handle bytes, n, locked, lock name) for RemoteParameterServer in other processes."""
-        return bytes(self.ps.ipc_handle()), self.n, 1 if self.mode == "asynchronous" else 0, self.lock_name

@@ -405,15 +405,11 @@ class SparkModel:
             self.start_server()
         client = self.client
         if self._ps_type == "device":
+            # collective: every rank allocates its shard of theta and maps the others'
+            client.like = init
+            client.connect(len(flatten_weights(init)), self.mode, server=ps if dist.rank() == 0 else None)
             if dist.rank() == 0:
-                client.bind(ps)
-                handle = ps.handle() if dist.world_size() > 1 else None
-            else:
-                handle = None
-            handle = dist.broadcast_object(handle, 0)
-            if dist.rank() != 0:
-                client.like = init
-                client.attach(handle)
+                ps.set_weights(init)
         dist.barrier()
         print(">>> Initialize workers")
         errors = []
@@ -431,12 +427,14 @@ class SparkModel:
         print(">>> Distribute load")
         try:
             if self._ps_type == "device" and self._native_ok() and local:
-                # MI355X path: the rank's partitions as replicas of one native executor
-                # exchanging with the HBM parameter server in lockstep (worker.py)
+                # MI355X path: the rank's partitions as independently progressing groups of
+                # native replicas, each on its own stream, exchanging with the sharded device
+                # parameter server through stream-ordered kernels (worker.py)
                 try:
                     BatchedAsynchronousWorker(model_json, init, client, train_config, self.frequency,
                                               self.master_optimizer, self.master_loss, self.master_metrics,
-                                              self.custom_objects).train_partitions(local)
+                                              self.custom_objects,
+                                              groups=self.kwargs.get("async_groups")).train_partitions(local)
                 except BaseException as e:  # noqa: BLE001 - voted on below, then raised
                     errors.append(e)
                 local = []
@@ -461,10 +459,18 @@ class SparkModel:
             if dist.backend() == "nccl":
                 t = t.cuda()
             dist.broadcast_(t, 0)
+            final = unflatten_weights(t.cpu().numpy(), init)
         finally:
             if dist.rank() == 0:
                 self.stop_server()   # always, also when a worker failed
-        return unflatten_weights(t.cpu().numpy(), init)
+            if self._ps_type == "device":
+                # every rank has left the broadcast: nobody reads a shard any more
+                if ps is not None:
+                    ps.close()
+                client.close()
+        if ps is not None and self._ps_type == "device":
+            ps.set_weights(final)    # host copy of the final weights (the shards are gone)
+        return final
 
 
 class SparkMLlibModel(SparkModel):

@@ -218,28 +218,38 @@ class BatchedAsynchronousWorker:
     """GPU path of the asynchronous / hogwild workers for all of a rank's partitions.
 
     The reference runs one AsynchronousSparkWorker per partition in its own process
-    (worker.py:52-131). On an MI355X the rank's partitions are replicas of ONE native
-    executor that advance in lockstep: per epoch (frequency='epoch') or per batch
-    (frequency='batch') every replica pulls the same theta from the parameter server,
-    trains, and the replicas' deltas are pushed as one sum -- one admissible
-    interleaving of the reference's independent workers (all pull, all push), with one
-    pull and one push per exchange instead of one per worker, and the pushes of a
-    rank applied atomically under the server's write lock in 'asynchronous' mode.
-    Replicas without a batch in a step (shorter partitions) push a zero delta, as do
-    partitions with n <= batch_size (reference worker.py:116).
+    (worker.py:52-131), each progressing on its own against a concurrently served
+    parameter server.  Here a rank's partitions are split into ``groups`` (default:
+    one per partition) that progress just as independently: every group is its own
+    native executor on its own HIP stream, and its exchange with the sharded device
+    parameter server (parameter/client.py DeviceClient) is stream-ordered kernels --
+    pull (gather theta, chunk-consistent in 'asynchronous' mode) -> refresh every
+    replica's weights -> train -> push (fp32 atomic adds of sum_r(P[r] - before)) --
+    with no host lock and no host synchronisation.  The host only enqueues, so the
+    groups' pulls and pushes interleave on the GPU in whatever order the hardware
+    runs them; within a group the replicas move in lockstep and push one summed
+    delta.  For frequency='batch' a group's whole pull/step/push is ONE hipGraph
+    replay per batch.  Replicas without a batch in a step (shorter partitions) push
+    a zero delta, as do partitions with n <= batch_size (reference worker.py:116).
     """
 
     def __init__(self, json, parameters, client, train_config, frequency, master_optimizer, master_loss,
-                 master_metrics, custom_objects):
+                 master_metrics, custom_objects, groups: Optional[int] = None):
         self.json, self.parameters, self.client = json, parameters, client
         self.train_config = dict(train_config)
         self.frequency = frequency
         self.master_optimizer, self.master_loss, self.master_metrics = master_optimizer, master_loss, master_metrics
         self.custom_objects = custom_objects or {}
+        self.groups = groups
         self.model = None
+        self.histories = []
+
+    def _n_groups(self, nparts: int) -> int:
+        import os
+        g = self.groups if self.groups else int(os.environ.get("ELEPHAS_AMD_ASYNC_GROUPS", "0") or 0)
+        return max(1, min(nparts, g if g > 0 else nparts))
 
     def train_partitions(self, partitions):
-        import torch
         from .ops.engine import make_trainer
         if self.frequency not in ("epoch", "batch"):
             raise ValueError("frequency parameter can be `epoch` or `batch, got {}".format(self.frequency))
@@ -251,58 +261,131 @@ class BatchedAsynchronousWorker:
         tc = self.train_config
         epochs, bs = int(tc.get("epochs", 1)), int(tc.get("batch_size", 32))
         verbose, vs = int(tc.get("verbose", 0)), float(tc.get("validation_split", 0.0))
-        xs, ys = zip(*[partition_to_numpy(p) for p in parts])
-        R = len(parts)
-        t = make_trainer(self.model, R, bs, engine="native")
-        if self.frequency == "epoch":
+        data = [partition_to_numpy(p) for p in parts]
+        G = self._n_groups(len(parts))
+        bounds = [len(parts) * g // G for g in range(G + 1)]
+        groups = []
+        for g in range(G):
+            xs, ys = zip(*data[bounds[g]:bounds[g + 1]])
+            t = make_trainer(self.model, len(xs), bs, engine="native")
             active = [len(x) > bs for x in xs]   # inactive replicas push a zero delta
-            t.set_data(list(xs), list(ys), vs, active=active, shuffle=True)
-            for _ in range(epochs):
-                before = self._pull(t)
-                if any(active):
-                    t.fit(1, verbose=verbose)
-                self._push(t, before)
+            if self.frequency == "epoch":
+                t.set_data(list(xs), list(ys), vs, active=active, shuffle=True)
+            else:
+                t.set_data(list(xs), list(ys), 0.0, active=active, shuffle=False)
+            groups.append(_Group(t, active))
+        if self.frequency == "epoch":
+            for e in range(epochs):
+                for g in groups:          # enqueue every group's epoch, then read histories
+                    self._pull(g)
+                    if any(g.active):
+                        g.t.launch_epoch()
+                    self._push(g)
+                for g in groups:
+                    if any(g.active):
+                        g.t.collect_epoch(g.hist, e, epochs, verbose)
         else:
-            active = [len(x) > bs for x in xs]
-            if not any(active):
-                return t
-            t.set_data(list(xs), list(ys), 0.0, active=active, shuffle=False)
-            nb = t.steps_per_epoch()
+            live = [g for g in groups if any(g.active)]
+            for g in live:
+                g.capture(self)
             for _ in range(epochs):
-                t.begin_epoch()
-                for _ in range(nb):
-                    before = self._pull(t)
-                    t.run_steps(1, use_graph=True)
-                    self._push(t, before)
-        t.stream.synchronize()
-        return t
+                for g in live:                 # each group runs its epoch on its own stream
+                    g.t.begin_epoch()
+                    g.steps(self, g.t.steps_per_epoch())
+        for g in groups:
+            g.t.stream.synchronize()
+        if hasattr(self.client, "check"):
+            self.client.check()
+        self.histories = [h for g in groups for h in g.hist]
+        self.trainers = [g.t for g in groups]
+        return groups[0].t
 
-    def _pull(self, t):
+    def _pull(self, g):
         import torch
         from .parallel import dist, fault
         fault.maybe_inject("pull", dist.rank())
+        t = g.t
         with torch.cuda.stream(t.stream):
             if hasattr(self.client, "pull_refresh"):
-                before = getattr(self, "_before", None)
-                if before is None or before.numel() != t.P.shape[1] or before.device != t.P.device:
-                    before = self._before = torch.empty(t.P.shape[1], dtype=torch.float32, device=t.P.device)
-                self.client.pull_refresh(t, before.data_ptr())
-                return before
+                self.client.pull_refresh(t, g.before.data_ptr())
+                return
             self.client.pull_into(t.P[0].data_ptr(), t.s)
             if t.R > 1:
                 t.P[1:].copy_(t.P[0].expand(t.R - 1, -1))
             t.sync_shadows()
-            return t.P[0].clone()
+            g.before.copy_(t.P[0])
 
-    def _push(self, t, before):
+    def _push(self, g):
         import torch
         from .parallel import dist, fault
         fault.maybe_inject("push", dist.rank())
+        t = g.t
         with torch.cuda.stream(t.stream):
             if hasattr(self.client, "push_replicas"):
-                self.client.push_replicas(t.P.data_ptr(), t.P.stride(0), t.R, before.data_ptr(), t.s)
+                self.client.push_replicas(t.P.data_ptr(), t.P.stride(0), t.R, g.before.data_ptr(), t.s)
                 return
             # sum_r (theta_pulled - theta_r), each difference formed before summing (exact
             # for close values; R*before - sum P rounds at ulp(R*|w|) and loses the deltas)
-            delta = (before.unsqueeze(0) - t.P).sum(0)
+            delta = (g.before.unsqueeze(0) - t.P).sum(0)
             self.client.push_from(delta.data_ptr(), t.s)
+
+
+class _Group:
+    """One independently progressing set of lockstep replicas (BatchedAsynchronousWorker).
+
+    frequency='batch': ``steps(n)`` runs n rounds of pull -> train step -> push on the
+    group's own stream, replayed from hipGraphs holding CHUNK rounds and 1 round, so the
+    host issues one launch per CHUNK batches per group and the groups' streams run
+    side by side on the GPU."""
+
+    CHUNK = 16
+
+    def __init__(self, t, active):
+        import torch
+        self.t, self.active = t, active
+        self.hist = t.new_history()
+        self.before = torch.empty(t.P.shape[1], dtype=torch.float32, device=t.P.device)
+        self.graphs = {}
+
+    @property
+    def graph(self):
+        return bool(self.graphs)
+
+    def capture(self, worker):
+        """Capture the CHUNK-round and 1-round graphs; eager launches if capture fails."""
+        import os
+        import torch
+        from .parallel import fault
+        if os.environ.get("ELEPHAS_AMD_ASYNC_GRAPH", "1") == "0" or fault.injection_active():
+            return
+        try:
+            for k in (self.CHUNK, 1):
+                g = torch.cuda.CUDAGraph()
+                self.t.stream.synchronize()
+                with torch.cuda.graph(g, stream=self.t.stream):
+                    for _ in range(k):
+                        worker._pull(self)
+                        self.t.exe.train_step(self.t.s)
+                        worker._push(self)
+                self.graphs[k] = g
+        except Exception:  # noqa: BLE001 - eager launches are equivalent, just slower
+            self.graphs = {}
+
+    def steps(self, worker, n):
+        """Enqueue n pull/step/push rounds (no host synchronisation)."""
+        import torch
+        if self.graphs:
+            full, rest = divmod(n, self.CHUNK)
+            with torch.cuda.stream(self.t.stream):
+                for _ in range(full):
+                    self.graphs[self.CHUNK].replay()
+                for _ in range(rest):
+                    self.graphs[1].replay()
+            return
+        for _ in range(n):
+            worker._pull(self)
+            self.t.run_steps(1, use_graph=True)
+            worker._push(self)
+
+    def step(self, worker):
+        self.steps(worker, 1)

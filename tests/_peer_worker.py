@@ -1,0 +1,196 @@
+"""One rank of the multi-process peer-memory GPU tests (tests/test_peer_gpu.py).
+
+Started as a child process per rank; every rank uses cuda:0 (two processes sharing
+one MI355X: HIP IPC maps the other process's buffers exactly as it maps another
+GPU's), a gloo process group exchanges the IPC handles.  Prints one JSON line.
+Usage: python tests/_peer_worker.py SCENARIO   (RANK / WORLD_SIZE / MASTER_* in env)
+"""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def _gloo():
+    import torch.distributed as dist
+    from datetime import timedelta
+    dist.init_process_group("gloo", timeout=timedelta(seconds=120))
+    return dist
+
+
+def _allgather(dist):
+    def f(obj):
+        out = [None] * dist.get_world_size()
+        dist.all_gather_object(out, obj)
+        return out
+    return f
+
+
+def allreduce(dist, rank, world):
+    """Every algorithm and size class against the fp32 rank-order sum; outputs of all
+    ranks must be bit-identical."""
+    import torch
+    from elephas_amd.parallel.p2p import PeerAllReduce
+    ag = _allgather(dist)
+    pa = PeerAllReduce(rank, world, 0, cap_elems=65536, allgather=ag)
+    res = {"self_test": pa.ok, "cases": []}
+    s = torch.cuda.Stream()
+    for n in (1, 5, 1000, 4096, 65536, 118_282, 200_003):
+        for algo in (0, 1, -1):
+            xs = [torch.from_numpy(np.random.default_rng(1000 * r + n + algo).normal(size=n).astype(np.float32))
+                  for r in range(world)]
+            want = xs[0].clone()
+            for r in range(1, world):
+                want += xs[r]
+            x = xs[rank].cuda()
+            s.wait_stream(torch.cuda.current_stream())
+            pa.all_reduce_(x, algo=algo, stream=s)
+            s.synchronize()
+            got = x.cpu()
+            digests = ag(float(got.double().sum()))
+            res["cases"].append(dict(n=n, algo=algo, exact=bool(torch.equal(got, want)),
+                                     same_on_all_ranks=len(set(digests)) == 1))
+    # misaligned view (goes through the aligned bounce buffer)
+    base = torch.arange(1001, dtype=torch.float32, device="cuda") * (rank + 1)
+    v = base[1:]
+    pa.all_reduce_(v)
+    torch.cuda.synchronize()
+    res["misaligned_ok"] = bool(torch.equal(v.cpu(), torch.arange(1, 1001, dtype=torch.float32)
+                                            * sum(r + 1 for r in range(world))))
+    res["error"] = int(pa.impl.error())
+    return res
+
+
+def bench(dist, rank, world):
+    """us per call of the peer all-reduce vs RCCL-less baseline (two processes on one
+    GPU: the peer reads are local HBM reads, so this bounds the kernel's fixed cost,
+    not the xGMI transfer time)."""
+    import torch
+    from elephas_amd.parallel.p2p import PeerAllReduce
+    pa = PeerAllReduce(rank, world, 0, allgather=_allgather(dist))
+    out = {}
+    for nbytes in (473_128, 2_312_228, 16 << 20):
+        n = nbytes // 4
+        x = torch.ones(n, dtype=torch.float32, device="cuda")
+        for algo in (0, 1):
+            for _ in range(20):
+                pa.all_reduce_(x, algo=algo)
+            torch.cuda.synchronize()
+            dist.barrier()
+            iters = 200
+            t0 = time.perf_counter()
+            for _ in range(iters):
+                pa.all_reduce_(x, algo=algo)
+            torch.cuda.synchronize()
+            dt = (time.perf_counter() - t0) / iters
+            out[f"{nbytes}B_{'two' if algo else 'one'}shot_us"] = round(dt * 1e6, 2)
+            dist.barrier()
+    out["error"] = int(pa.impl.error())
+    return out
+
+
+def ps(dist, rank, world):
+    """Both ranks push concurrently into the sharded PS (each owns half the chunks):
+    no update is lost and asynchronous pulls are chunk-consistent."""
+    import torch
+    from elephas_amd.ops import native
+    from elephas_amd.parallel.p2p import exchange_handles
+    C = native.require()
+    n, K = 50_000, 40
+    p = C.ShardedParameterServer(rank, world, n, 1, 0, 4096)
+    p.open(exchange_handles(p.handle(), _allgather(dist)))
+    if rank == 0:
+        z = torch.zeros(n, dtype=torch.float32, device="cuda")
+        torch.cuda.synchronize()
+        p.set(z.data_ptr(), torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+    dist.barrier()
+    d = torch.full((n,), -float(rank + 1), dtype=torch.float32, device="cuda")
+    snaps = torch.empty(K, n, dtype=torch.float32, device="cuda")
+    sp, sq = torch.cuda.Stream(), torch.cuda.Stream()
+    torch.cuda.synchronize()
+    for k in range(K):
+        p.push_delta(d.data_ptr(), sp.cuda_stream)
+        p.pull(snaps[k].data_ptr(), sq.cuda_stream)
+    torch.cuda.synchronize()
+    dist.barrier()
+    fin = torch.empty(n, dtype=torch.float32, device="cuda")
+    p.pull(fin.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    want = float(K * sum(r + 1 for r in range(world)))
+    torn = 0
+    for c0 in range(0, n, 4096):
+        blk = snaps[:, c0:c0 + 4096]
+        torn += int((blk != blk[:, :1]).any(1).sum())
+    res = dict(final_exact=bool(torch.equal(fin, torch.full_like(fin, want))), torn_chunks=torn,
+               shard_begin=[int(p.shard_begin(r)) for r in range(world)], error=int(p.error()))
+    dist.barrier()   # nobody frees its shard while a peer may still read it
+    return res
+
+
+def spark_async(dist, rank, world, mode):
+    """SparkModel asynchronous / hogwild fit with two ranks sharing the GPU: sharded
+    device PS across the two processes, two independent worker groups per rank.
+    Learnable synthetic data: accuracy must rise well above chance on every rank and
+    the final weights must be identical on both ranks."""
+    import torch
+    from elephas_amd import config
+    from elephas_amd.data import SparkContext
+    from elephas_amd.models import Sequential, Dense, Dropout
+    from elephas_amd.models.optimizers import SGD
+    from elephas_amd.parallel import dist as edist
+    from elephas_amd.spark_model import SparkModel
+    from elephas_amd.utils.rdd_utils import to_simple_rdd
+    config.set_policy("float32")
+    rng = np.random.default_rng(5)
+    centers = rng.normal(0, 1, size=(10, 64)).astype(np.float32)
+    y = rng.integers(0, 10, 4000)
+    x = (centers[y] + rng.normal(0, 0.7, size=(4000, 64))).astype(np.float32)
+    yo = np.eye(10, dtype=np.float32)[y]
+    np.random.seed(0)
+    m = Sequential()
+    m.add(Dense(64, activation="relu", input_dim=64))
+    m.add(Dropout(0.1))
+    m.add(Dense(10, activation="softmax"))
+    m.compile(SGD(learning_rate=0.05), "categorical_crossentropy", ["acc"])
+    acc0 = m.evaluate(x, yo)[1]
+    sm = SparkModel(m, mode=mode, frequency="batch", parameter_server_mode="device", num_workers=4,
+                    async_groups=2)
+    sm.fit(to_simple_rdd(SparkContext.getOrCreate(), x, yo), epochs=2, batch_size=32, verbose=0,
+           validation_split=0.0)
+    w = np.concatenate([a.ravel() for a in sm.master_network.get_weights()])
+    digests = _allgather(dist)(float(np.float64(w).sum()))
+    acc = sm.master_network.evaluate(x, yo)[1]
+    edist.barrier()
+    return dict(acc0=float(acc0), acc=float(acc), finite=bool(np.isfinite(w).all()),
+                same_on_all_ranks=len(set(digests)) == 1)
+
+
+def main():
+    scenario = sys.argv[1]
+    dist = _gloo()
+    rank, world = dist.get_rank(), dist.get_world_size()
+    import torch
+    torch.cuda.set_device(0)
+    if scenario == "allreduce":
+        res = allreduce(dist, rank, world)
+    elif scenario == "bench":
+        res = bench(dist, rank, world)
+    elif scenario == "ps":
+        res = ps(dist, rank, world)
+    elif scenario in ("spark_asynchronous", "spark_hogwild"):
+        res = spark_async(dist, rank, world, scenario.split("_", 1)[1])
+    else:
+        raise SystemExit(f"unknown scenario {scenario}")
+    print("RESULT " + json.dumps(dict(rank=rank, **res)), flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

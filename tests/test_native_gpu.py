@@ -522,47 +522,86 @@ def test_host_loader_uploads(threads):
     assert not got[:, 781:].any()
 
 
-@pytest.mark.parametrize("locked", [0, 1])
-def test_ps_replica_pull_push(locked):
-    """Fused lockstep-replica exchange with the HBM parameter server:
-    pull_replicas writes theta into every replica row and `before`; push_replicas
-    applies theta += sum_r P[r] - R * before (fp32 reference)."""
+@pytest.mark.parametrize("consistent", [0, 1])
+def test_ps_replica_pull_push(consistent):
+    """Sharded device PS (one rank): pull gathers theta exactly; push_replicas applies
+    theta += sum_r (P[r] - before) (fp64 reference); push_delta applies theta -= d."""
     from elephas_amd.ops import native
     C = native.require()
     n, R = 118_282, 8
-    ps = C.DeviceParameterServer(n, locked, 0, "")
+    ps = C.ShardedParameterServer(0, 1, n, consistent, 0)
+    assert ps.nchunks == (n + 4095) // 4096
     rng = np.random.default_rng(9)
     theta = torch.from_numpy(rng.normal(size=n).astype(np.float32)).cuda()
     s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
     ps.set(theta.data_ptr(), s.cuda_stream)
-    P = torch.zeros(R, n + 6, dtype=torch.float32, device="cuda")[:, :n]   # padded row stride
     before = torch.empty(n, dtype=torch.float32, device="cuda")
-    s.wait_stream(torch.cuda.current_stream())   # zero-fill (current stream) before the pull (stream s)
-    ps.pull_replicas(P.data_ptr(), P.stride(0), R, before.data_ptr(), s.cuda_stream)
+    ps.pull(before.data_ptr(), s.cuda_stream)
     s.synchronize()
     assert torch.equal(before, theta)
-    assert torch.equal(P, theta.expand(R, n))
-    P.add_(torch.from_numpy(rng.normal(size=(R, n)).astype(np.float32)).cuda() * 1e-2)
-    want = (theta.double() + P.double().sum(0) - R * before.double()).float()
-    s.wait_stream(torch.cuda.current_stream())   # the perturbation of P before the push reads it
+    P = torch.zeros(R, n + 6, dtype=torch.float32, device="cuda")[:, :n]   # padded row stride
+    P.copy_(theta.expand(R, n) + torch.from_numpy(rng.normal(size=(R, n)).astype(np.float32)).cuda() * 1e-2)
+    want = (theta.double() + (P.double() - before.double()).sum(0)).float()
+    s.wait_stream(torch.cuda.current_stream())   # P is written on the current stream
     ps.push_replicas(P.data_ptr(), P.stride(0), R, before.data_ptr(), s.cuda_stream)
-    s.synchronize()
     got = torch.empty(n, dtype=torch.float32, device="cuda")
     ps.pull(got.data_ptr(), s.cuda_stream)
     s.synchronize()
     torch.testing.assert_close(got, want, rtol=0, atol=1e-5)
+    d = torch.from_numpy(rng.normal(size=n).astype(np.float32)).cuda()
+    s.wait_stream(torch.cuda.current_stream())
+    ps.push_delta(d.data_ptr(), s.cuda_stream)
+    ps.pull(got.data_ptr(), s.cuda_stream)
+    s.synchronize()
+    torch.testing.assert_close(got, want - d, rtol=0, atol=1e-5)
+    assert ps.error() == 0
 
 
-def test_ps_pull_refresh_matches_two_step_pull():
-    """The fused pull (theta -> every replica's master + both weight-image parities +
-    `before`, one kernel) leaves the executor in the same state as pull + refresh:
-    the next training steps give bit-identical weights."""
+def test_ps_concurrent_streams_lose_no_update():
+    """Eight streams push integer deltas into the same chunks concurrently while four
+    others pull: every push lands exactly once (fp32 atomics, integers exact) and an
+    'asynchronous' pull never sees a chunk with half of a push applied (each push adds
+    the same value to every element of the vector, so a consistent chunk is constant)."""
     from elephas_amd.ops import native
+    C = native.require()
+    n, K = 40_000, 25
+    ps = C.ShardedParameterServer(0, 1, n, 1, 0, 4096)
+    zero = torch.zeros(n, dtype=torch.float32, device="cuda")
+    torch.cuda.synchronize()
+    ps.set(zero.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    ones = torch.full((n,), -1.0, dtype=torch.float32, device="cuda")   # theta -= -1 per push
+    pushers = [torch.cuda.Stream() for _ in range(8)]
+    pullers = [torch.cuda.Stream() for _ in range(4)]
+    snaps = [torch.empty(K, n, dtype=torch.float32, device="cuda") for _ in pullers]
+    torch.cuda.synchronize()
+    for k in range(K):
+        for st in pushers:
+            ps.push_delta(ones.data_ptr(), st.cuda_stream)
+        for st, sn in zip(pullers, snaps):
+            ps.pull(sn[k].data_ptr(), st.cuda_stream)
+    torch.cuda.synchronize()
+    assert ps.error() == 0
+    final = torch.empty(n, dtype=torch.float32, device="cuda")
+    ps.pull(final.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert torch.equal(final, torch.full_like(final, 8.0 * K))
+    for sn in snaps:
+        for c0 in range(0, n, 4096):
+            blk = sn[:, c0:c0 + 4096]
+            assert torch.equal(blk, blk[:, :1].expand_as(blk)), "torn chunk in an asynchronous pull"
+
+
+def test_ps_pull_refresh_then_steps_match_set_weights():
+    """DeviceClient.pull_refresh (gather kernel + refresh of every replica's master and
+    both weight-image parities) leaves the executor in the same state as uploading the
+    same weights with set_weights_flat: the next steps give bit-identical weights."""
     from elephas_amd.ops.plan import build_plan
     from elephas_amd.ops.native_engine import NativeTrainer
     from elephas_amd.models import optimizers as O
+    from elephas_amd.parameter.client import DeviceClient
     from elephas_amd import config
-    C = native.require()
     config.set_policy("mixed_bfloat16")
     model = _mlp(784, [128, 128], 10, dropout=0.2)
     model.compile(O.SGD(0.1), "categorical_crossentropy", ["acc"])
@@ -570,25 +609,23 @@ def test_ps_pull_refresh_matches_two_step_pull():
     x, y = _data(512, 784, 10)
     ts = [NativeTrainer(model, build_plan(model), R, 64, torch.device("cuda"), seed=77) for _ in range(2)]
     n = ts[0].P.shape[1]
-    ps = C.DeviceParameterServer(n, 1, 0, "")
+    client = DeviceClient().connect(n, "asynchronous", rank=0, world=1, allgather=lambda h: [h])
     theta = torch.from_numpy(np.random.default_rng(3).normal(size=n).astype(np.float32) * 0.05).cuda()
-    s = torch.cuda.Stream()
-    ps.set(theta.data_ptr(), s.cuda_stream)
-    befores = []
+    torch.cuda.synchronize()
+    client.ps.set(theta.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    before = torch.empty(n, dtype=torch.float32, device="cuda")
     for i, t in enumerate(ts):
         t.set_data([x] * R, [y] * R, 0.0, shuffle=False)
         t.begin_epoch()
-        before = torch.empty(n, dtype=torch.float32, device="cuda")
-        with torch.cuda.stream(t.stream):
-            if i == 0:
-                C.ps_pull_refresh(ps, t.exe, before.data_ptr(), t.s)
-            else:
-                ps.pull_replicas(t.P.data_ptr(), t.P.stride(0), R, before.data_ptr(), t.s)
-                t.sync_shadows()
+        if i == 0:
+            with torch.cuda.stream(t.stream):
+                client.pull_refresh(t, before.data_ptr())
+        else:
+            t.set_weights_flat(theta.cpu().numpy())
         t.stream.synchronize()
-        befores.append(before)
         t.run_steps(2, use_graph=False)
-    assert torch.equal(befores[0], theta) and torch.equal(befores[1], theta)
+    assert torch.equal(before, theta)
     w0, w1 = ts[0].get_weights_flat(), ts[1].get_weights_flat()
     assert np.abs(w0 - theta.cpu().numpy()).max() > 0
     np.testing.assert_array_equal(w0, w1)
