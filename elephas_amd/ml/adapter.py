@@ -24,11 +24,7 @@ def df_to_simple_rdd(df, categorical: bool = False, nb_classes: Optional[int] = 
     df.createOrReplaceTempView("temp_table")
     selected_df = spark_session.sql(f"SELECT {features_col} AS features, {label_col} as label from temp_table")
     lp_rdd = selected_df.rdd.map(lambda row: LabeledPoint(row.label, Vectors.fromML(row.features)))
-    lp_rdd = RDDLike.keep_partitions(lp_rdd, df)
+    nparts = df.rdd.getNumPartitions()
+    if lp_rdd.getNumPartitions() != nparts:   # one worker per partition of the input DataFrame
+        lp_rdd = lp_rdd.repartition(nparts)
     return lp_to_simple_rdd(lp_rdd, categorical, nb_classes)
-
-
-class RDDLike:
-    @staticmethod
-    def keep_partitions(rdd, df):
-        return rdd

@@ -175,25 +175,32 @@ class ElephasTransformer(Model, HasKerasModelConfig, HasLabelCol, HasOutputCol, 
     def get_model(self):
         return model_from_json(self.get_keras_model_config(), self.get_custom_objects())
 
-    def _predict_fn(self):
-        model = self.get_model()
-        model.set_weights(self.weights)
-        return model.predict
-
     def _transform(self, df: DataFrame) -> DataFrame:
+        """Append the network's predictions as ``outputCol`` (reference ml_model.py:223-242
+        maps the prediction over the DataFrame's partitions).  The rows are split in
+        contiguous blocks over the ranks of the job, each rank predicts its block on its
+        GPU in ``inference_batch_size`` chunks, and one tensor all-gather (RCCL) puts the
+        predictions back in row order on every rank -- the SparkModel.predict path."""
+        from .parallel import dist
         output_col = self.getOutputCol()
         new_schema = copy.deepcopy(df.schema)
         rows = df.collect()
-        predict = self._predict_fn()
+        model = self.get_model()
+        model.set_weights(self.weights)
         features_col = self.getFeaturesCol()
-        feats = np.array([from_vector(r[features_col]) for r in rows]) if rows else np.zeros((0, 1))
-        bs = self.get_inference_batch_size()
-        if len(feats) == 0:
-            preds = np.zeros((0, 1))
-        elif bs is not None and bs > 0:
-            preds = np.vstack([predict(feats[i:i + bs]) for i in range(0, len(feats), bs)])
+        n = len(rows)
+        lo, hi = dist.block_range(n)
+        out_shape = tuple(model.output_shape[1:])
+        if hi > lo:
+            feats = np.array([from_vector(r[features_col]) for r in rows[lo:hi]])
+            bs = self.get_inference_batch_size()
+            if bs is not None and bs > 0:
+                local = np.vstack([model.predict(feats[i:i + bs]) for i in range(0, len(feats), bs)])
+            else:
+                local = model.predict(feats)
         else:
-            preds = predict(feats)
+            local = np.zeros((0,) + out_shape, np.float32)
+        preds = dist.all_gather_rows(np.asarray(local, np.float32).reshape((-1,) + out_shape), n)
         if getattr(self, "model_type", None) == ModelType.REGRESSION:
             values = [float(np.asarray(p).reshape(-1)[0]) for p in preds]
             output_col_field = StructField(output_col, DoubleType(), True)

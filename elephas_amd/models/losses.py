@@ -133,6 +133,11 @@ FUNCTIONS = {
     "cosine_similarity": cosine_similarity, "categorical_hinge": categorical_hinge,
 }
 
+def registered_names():
+    """Every built-in loss name and alias (alias -> canonical via ``canonical``)."""
+    return list(FUNCTIONS) + list(ALIASES)
+
+
 # keras convenience aliases as module attributes
 mse = MSE = mean_squared_error
 mae = MAE = mean_absolute_error

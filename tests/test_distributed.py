@@ -122,3 +122,43 @@ def test_all_gather_rows_uneven_blocks(tmp_path):
     want = np.arange(11, dtype=np.float32)[:, None] * np.ones((1, 5), np.float32)
     for r in range(3):
         np.testing.assert_array_equal(np.load(tmp_path / f"g{r}.npy"), want)
+
+
+def _transform_worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    import torch.distributed as tdist
+    tdist.init_process_group("gloo", rank=rank, world_size=world)
+    from elephas_amd import config
+    config.set_device("cpu")
+    out = _transform_local()
+    np.save(os.path.join(out_dir, f"t{rank}.npy"), out)
+    tdist.barrier()
+    tdist.destroy_process_group()
+
+
+def _transform_local():
+    from elephas_amd.data import SparkContext
+    from elephas_amd.ml.adapter import to_data_frame
+    from elephas_amd.ml_model import ElephasTransformer
+    from elephas_amd.utils.model_utils import ModelType
+    x, y = _data()
+    m = _model()
+    df = to_data_frame(SparkContext(master="local[4]"), x[:101], y[:101], categorical=True)
+    tr = ElephasTransformer(weights=m.get_weights(), model_type=ModelType.CLASSIFICATION)
+    tr.set_keras_model_config(m.to_json())
+    tr.set_inference_batch_size(16)
+    out = tr.transform(df)
+    return np.asarray([r[tr.getOutputCol()] for r in out.collect()])
+
+
+def test_transform_three_ranks_equals_single_process(tmp_path):
+    """ElephasTransformer.transform splits the rows over the ranks (uneven blocks of
+    101 rows), predicts each block locally and gathers them in row order: every rank
+    gets exactly the single-process output (reference ml_model.py:223-242)."""
+    port = _free_port()
+    mp.start_processes(_transform_worker, args=(3, port, str(tmp_path)), nprocs=3, join=True, start_method="spawn")
+    want = _transform_local()
+    assert want.shape == (101, 3)
+    for r in range(3):
+        np.testing.assert_allclose(np.load(tmp_path / f"t{r}.npy"), want, rtol=0, atol=1e-6)
