@@ -458,13 +458,12 @@ __device__ __forceinline__ float opt_update(const OptParams& p, float w, float g
     case OPT_RMSPROP: {
       float ms = p.rho * S[si] + (1.f - p.rho) * g * g;
       S[si] = ms;
-      float upd = lr * g / (sqrtf(ms) + p.eps);
-      if (p.mom > 0.f) {
-        float m = p.mom * S[si + p.s_plane] + upd;
+      if (p.mom > 0.f) {  // tf ApplyRMSProp: epsilon inside the square root
+        float m = p.mom * S[si + p.s_plane] + lr * g / sqrtf(ms + p.eps);
         S[si + p.s_plane] = m;
         return w - m;
       }
-      return w - upd;
+      return w - lr * g / (sqrtf(ms) + p.eps);
     }
     case OPT_ADAM: {
       const float t = (float)(iter + 1);
@@ -543,13 +542,12 @@ __device__ __forceinline__ void opt_update_v(const OptParams& p, float (&w)[NV],
       _Pragma("unroll") for (int q = 0; q < NV; ++q) {
         const float ms = p.rho * s0[q] + (1.f - p.rho) * g[q] * g[q];
         s0[q] = ms;
-        const float upd = lr * g[q] / (sqrtf(ms) + p.eps);
-        if (p.mom > 0.f) {
-          const float m = p.mom * s1[q] + upd;
+        if (p.mom > 0.f) {  // tf ApplyRMSProp: epsilon inside the square root
+          const float m = p.mom * s1[q] + lr * g[q] / sqrtf(ms + p.eps);
           s1[q] = m;
           w[q] -= m;
         } else {
-          w[q] -= upd;
+          w[q] -= lr * g[q] / (sqrtf(ms) + p.eps);
         }
       }
       break;

@@ -179,13 +179,13 @@ class RMSprop(Optimizer):
                 mg = s[idx]
                 mg.mul_(h["rho"]).add_((1 - h["rho"]) * g)
                 denom = ms - mg * mg
-            upd = lr * g / (torch.sqrt(denom) + h["epsilon"])
             if h["momentum"] > 0:
+                # tf.raw_ops.ResourceApply(Centered)RMSProp: epsilon inside the square root
                 mom = s[1]
-                mom.mul_(h["momentum"]).add_(upd)
+                mom.mul_(h["momentum"]).add_(lr * g / torch.sqrt(denom + h["epsilon"]))
                 p.sub_(mom)
             else:
-                p.sub_(upd)
+                p.sub_(lr * g / (torch.sqrt(denom) + h["epsilon"]))
 
 
 class Adam(Optimizer):

@@ -48,13 +48,31 @@ class PeerAllReduce:
         self.device = torch.cuda.current_device() if device is None else int(device)
         cap = cap_elems or int(os.environ.get("ELEPHAS_AMD_P2P_CAP_ELEMS", str(4 << 20)))
         self.max_bytes = int(os.environ.get("ELEPHAS_AMD_P2P_MAX_BYTES", str(64 << 20)))
-        self.impl = self.C.PeerAllReduce(self.rank, self.world, cap, self.device, timeout_s)
-        tsm = os.environ.get("ELEPHAS_AMD_P2P_TWOSHOT_MIN_BYTES")
-        if tsm:
-            self.impl.twoshot_min_bytes = int(tsm)
-        self.impl.open(exchange_handles(self.impl.handle(), allgather))
+        gather = allgather or dist.all_gather_object
+        # every step is voted on by all ranks, so a rank whose allocation / IPC mapping
+        # fails never leaves its peers waiting in a kernel for it
+        self.impl, handle = None, b""
+        try:
+            self.impl = self.C.PeerAllReduce(self.rank, self.world, cap, self.device, timeout_s)
+            handle = bytes(self.impl.handle())
+        except Exception:  # noqa: BLE001
+            self.impl = None
+        handles = exchange_handles(handle, allgather)
+        opened = False
+        if self.impl is not None and all(handles):
+            try:
+                self.impl.open(handles)
+                opened = True
+            except Exception:  # noqa: BLE001
+                opened = False
+        self.ok = all(gather(opened))
+        if self.ok and self.impl is not None:
+            tsm = os.environ.get("ELEPHAS_AMD_P2P_TWOSHOT_MIN_BYTES")
+            if tsm:
+                self.impl.twoshot_min_bytes = int(tsm)
+            if verify:
+                self.ok = self._self_test(allgather)
         self._tmp = None
-        self.ok = self._self_test(allgather) if verify else True
 
     def _self_test(self, allgather) -> bool:
         """One-shot and two-shot all-reduce of known vectors on every rank, then a vote:

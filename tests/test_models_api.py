@@ -143,6 +143,75 @@ def test_adam_rule_matches_keras_formula():
     assert np.allclose(w.numpy(), _numpy_adam(np.ones(5, np.float32), gs), atol=1e-6)
 
 
+# Independent numpy transcriptions of the Keras 2.10 optimizer_v2 update rules
+# (keras/optimizers/optimizer_v2/*.py and the tf.raw_ops.ResourceApply* kernels they
+# call); lr_t = lr / (1 + decay * iterations) with iterations counted from 0.
+def _keras_rule(name, hp):
+    def sgd(w, g, st, it):
+        lr = hp["lr"] / (1 + hp.get("decay", 0) * it)
+        mom = hp.get("momentum", 0)
+        if mom == 0:
+            return w - lr * g
+        st["m"] = mom * st.get("m", 0) - lr * g
+        return w + mom * st["m"] - lr * g if hp.get("nesterov") else w + st["m"]
+
+    def rmsprop(w, g, st, it):
+        lr = hp["lr"] / (1 + hp.get("decay", 0) * it)
+        rho, eps, mom = hp.get("rho", 0.9), hp.get("eps", 1e-7), hp.get("momentum", 0)
+        st["ms"] = st.get("ms", 0) + (g * g - st.get("ms", 0)) * (1 - rho)
+        denom = st["ms"]
+        if hp.get("centered"):
+            st["mg"] = st.get("mg", 0) + (g - st.get("mg", 0)) * (1 - rho)
+            denom = denom - st["mg"] ** 2
+        if mom:                                   # ResourceApplyRMSProp: eps inside sqrt
+            st["mom"] = mom * st.get("mom", 0) + lr * g / np.sqrt(denom + eps)
+            return w - st["mom"]
+        return w - lr * g / (np.sqrt(denom) + eps)
+
+    def adagrad(w, g, st, it):
+        lr = hp["lr"] / (1 + hp.get("decay", 0) * it)
+        st["acc"] = st.get("acc", hp.get("init", 0.1)) + g * g
+        return w - lr * g / (np.sqrt(st["acc"]) + hp.get("eps", 1e-7))
+
+    def adamax(w, g, st, it):
+        lr = hp["lr"] / (1 + hp.get("decay", 0) * it)
+        b1, b2, eps = 0.9, 0.999, 1e-7
+        st["m"] = b1 * st.get("m", 0) + (1 - b1) * g
+        st["u"] = np.maximum(b2 * st.get("u", 0), np.abs(g))
+        return w - lr / (1 - b1 ** (it + 1)) * st["m"] / (st["u"] + eps)
+    return {"sgd": sgd, "rmsprop": rmsprop, "adagrad": adagrad, "adamax": adamax}[name]
+
+
+@pytest.mark.parametrize("name,opt,hp", [
+    ("sgd", lambda: O.SGD(0.05), {"lr": 0.05}),
+    ("sgd", lambda: O.SGD(0.05, momentum=0.9), {"lr": 0.05, "momentum": 0.9}),
+    ("sgd", lambda: O.SGD(0.01, decay=1e-2, momentum=0.9, nesterov=True),
+     {"lr": 0.01, "decay": 1e-2, "momentum": 0.9, "nesterov": True}),
+    ("rmsprop", lambda: O.RMSprop(0.01), {"lr": 0.01}),
+    ("rmsprop", lambda: O.RMSprop(0.01, momentum=0.5, decay=0.1), {"lr": 0.01, "momentum": 0.5, "decay": 0.1}),
+    ("rmsprop", lambda: O.RMSprop(0.01, centered=True), {"lr": 0.01, "centered": True}),
+    ("rmsprop", lambda: O.RMSprop(0.01, centered=True, momentum=0.3),
+     {"lr": 0.01, "centered": True, "momentum": 0.3}),
+    ("adagrad", lambda: O.Adagrad(0.1), {"lr": 0.1}),
+    ("adagrad", lambda: O.Adagrad(0.1, initial_accumulator_value=0.5, decay=0.05),
+     {"lr": 0.1, "init": 0.5, "decay": 0.05}),
+    ("adamax", lambda: O.Adamax(0.02), {"lr": 0.02}),
+])
+def test_optimizer_rules_match_keras_formulas(name, opt, hp):
+    """Every optimizer of the engines (the torch rule here; the native kernels are
+    checked against the torch engine on the GPU) against the Keras formulas, 4 steps."""
+    o = opt()
+    w = torch.linspace(-1, 1, 7)
+    st = o.init_state([w])
+    ref_w, ref_st = w.numpy().astype(np.float64).copy(), {}
+    rule = _keras_rule(name, hp)
+    for it in range(4):
+        g = np.random.default_rng(40 + it).normal(size=7).astype(np.float32)
+        o.apply_torch([w], [torch.tensor(g)], st[0:1], it)
+        ref_w = rule(ref_w, g.astype(np.float64), ref_st, it)
+    np.testing.assert_allclose(w.numpy(), ref_w, rtol=1e-5, atol=1e-6)
+
+
 def test_save_load_roundtrip(tmp_cwd, classification_model):
     classification_model.compile(O.RMSprop(), "categorical_crossentropy", ["acc"])
     classification_model.save("model.h5")
