@@ -113,7 +113,7 @@ def main():
     ap.add_argument("--mode", default="synchronous", choices=["synchronous", "asynchronous", "hogwild"],
                     help="asynchronous / hogwild: every worker pulls from and pushes to the HBM "
                          "parameter server around each step (frequency='batch', BASELINE config #3)")
-    ap.add_argument("--task", default="train", choices=["train", "predict", "evaluate"],
+    ap.add_argument("--task", default="train", choices=["train", "fit", "predict", "evaluate"],
                     help="predict / evaluate: distributed inference of the master network "
                          "(SparkModel.predict / evaluate path, BASELINE config #5)")
     ap.add_argument("--infer-rows", type=int, default=None, help="rows per GPU for --task predict/evaluate")
@@ -141,6 +141,8 @@ def main():
         d, dr, c, r, lr = MODELS[args.model]
         MODELS[args.model] = (d, args.dropout, c, r, lr)
     model = build_model(args.model)
+    if args.task == "fit":
+        return bench_fit(args, model, dist, rank, world, dev)
     if args.task != "train":
         return bench_infer(args, model, dist, rank, world, dev)
     if args.mode != "synchronous":
@@ -298,6 +300,70 @@ def main():
         if args.out:
             with open(args.out, "a") as f:
                 f.write(s + "\n")
+    if dist.is_initialized():
+        dist.barrier()
+        import torch.distributed as tdist
+        tdist.destroy_process_group()
+
+
+def bench_fit(args, model, dist, rank, world, dev):
+    """End-to-end SparkModel.fit wall time -- the reference's measured unit
+    (examples/mnist_mlp_spark_synchronous.py:47-57: 60,000 rows in local[8]
+    partitions, 1 epoch, batch 64, validation_split 0.1, mode='synchronous'), through
+    the public API: RDD partitions -> workers -> native executor -> averaging.
+    A "step" = one whole fit call; warmup fits absorb executor construction.
+    strong: the reference job (60k rows, 8 partitions) split over the GPUs;
+    weak: that job on every GPU."""
+    import torch
+    from elephas_amd.data import SparkContext
+    from elephas_amd.spark_model import SparkModel
+    from elephas_amd.utils.rdd_utils import to_simple_rdd
+    dims, _, classes, _, _ = MODELS[args.model]
+    parts = 8 if args.scaling == "strong" else 8 * world
+    rows = 60000 if args.scaling == "strong" else 60000 * world
+    rng = np.random.default_rng(2024)
+    centers = rng.normal(0, 1, size=(classes, dims[0])).astype(np.float32)
+    y = rng.integers(0, classes, rows)
+    x = np.clip(centers[y] * 0.25 + 0.5 + rng.normal(0, 0.25, size=(rows, dims[0])), 0, 1).astype(np.float32)
+    yo = np.eye(classes, dtype=np.float32)[y]
+    rdd = to_simple_rdd(SparkContext(master=f"local[{parts}]"), x, yo)
+    sm = SparkModel(model, mode="synchronous")
+    kw = dict(epochs=1, batch_size=args.batch, verbose=0, validation_split=args.validation_split)
+
+    def sync():
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+        dist.barrier()
+
+    for _ in range(max(args.warmup, 0)):
+        sm.fit(rdd, **kw)
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        sm.fit(rdd, **kw)
+    sync()
+    dt = time.perf_counter() - t0
+    dt_max = max(dist.all_gather_object(dt))
+    samples = sm.metrics["samples"] * args.steps
+    if rank == 0:
+        acc = sm.master_network.evaluate(x[:10000], yo[:10000])[1]
+        line = {
+            "metric": "samples/sec (whole node) MNIST-MLP 784-128-128-10 SparkModel.fit wall (end to end)",
+            "value": round(samples / dt_max, 1), "unit": "samples/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(dt_max / args.steps * 1e3, 4), "higher_is_better": True,
+            "scaling": args.scaling, "vs_baseline": None,
+            "dtype": "bf16" if args.policy == "mixed_bfloat16" else "fp32",
+            "data": "synthetic MNIST-shaped, learnable (class centers + noise), random-init weights",
+            "config": {"model": "MNIST-MLP 784-128-128-10", "rows": rows, "partitions": parts, "epochs": 1,
+                       "batch": args.batch, "validation_split": args.validation_split, "mode": "synchronous",
+                       "seq_len": None, "global_batch": args.batch * parts, "parallelism": f"dp{world}",
+                       "phases_ms_last_fit": {k: round(v * 1e3, 3) for k, v in sm.metrics["phases"].items()},
+                       "train_accuracy_after": round(float(acc), 4)},
+        }
+        print(json.dumps(line), flush=True)
+        if args.out:
+            with open(args.out, "a") as f:
+                f.write(json.dumps(line) + "\n")
     if dist.is_initialized():
         dist.barrier()
         import torch.distributed as tdist

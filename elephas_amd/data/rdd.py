@@ -9,8 +9,11 @@ Spark's observable semantics that the reference relies on
   * ``repartition(n)`` redistributes round-robin (order is not preserved,
     which is why the reference index-tags predictions: spark_model.py:257-266);
   * ``zipWithIndex`` numbers elements in partition order; ``sortBy`` sorts.
-Training never iterates these Python lists on the hot path: partitions are
-stacked into device-resident shards (elephas_amd/parallel/workers.py).
+Partitions built from numpy arrays (``to_simple_rdd``, ``parallelize`` of a
+``ColumnarPartition``) stay COLUMNAR: a partition is a pair of array views
+(features, labels) that behaves like a list of (x, y) tuples for the generic
+operations, while the training path hands the arrays straight to the pinned
+loader (worker.partition_to_numpy) -- no per-row Python objects, no copies.
 """
 from __future__ import annotations
 
@@ -129,10 +132,56 @@ class SparkContext:
         self.stop()
 
 
+class ColumnarPartition:
+    """Rows ``(x[i], y[i])`` of two row-aligned numpy arrays, without per-row objects.
+
+    Sequence protocol (len / iteration / indexing / slicing) so every RDD operation
+    that treats a partition as a list of pairs keeps working; ``x`` / ``y`` are the
+    zero-copy views the MI355X training path uploads."""
+
+    __slots__ = ("x", "y")
+
+    def __init__(self, x, y):
+        if len(x) != len(y):
+            raise ValueError("features and labels must have the same number of rows")
+        self.x, self.y = x, y
+
+    def __len__(self):
+        return len(self.x)
+
+    def __iter__(self):
+        return zip(self.x, self.y)
+
+    def __getitem__(self, i):
+        if isinstance(i, slice):
+            return ColumnarPartition(self.x[i], self.y[i])
+        return self.x[i], self.y[i]
+
+    def __bool__(self):
+        return len(self.x) > 0
+
+    def __eq__(self, other):
+        return list(self) == list(other)
+
+    def __repr__(self):
+        return f"ColumnarPartition({len(self)} rows)"
+
+
+def _columnar(parts) -> bool:
+    return bool(parts) and all(isinstance(p, ColumnarPartition) for p in parts)
+
+
 class RDD:
     def __init__(self, partitions: List[list], ctx: Optional[SparkContext] = None):
-        self._parts = [list(p) for p in partitions]
+        self._parts = [p if isinstance(p, ColumnarPartition) else list(p) for p in partitions]
         self.ctx = ctx or SparkContext.getOrCreate()
+
+    @classmethod
+    def from_arrays(cls, x, y, num_slices: int, ctx: Optional[SparkContext] = None) -> "RDD":
+        """``parallelize`` of row-aligned arrays: contiguous columnar slices (views)."""
+        n, k = len(x), max(1, int(num_slices))
+        return cls([ColumnarPartition(x[i * n // k:(i + 1) * n // k], y[i * n // k:(i + 1) * n // k])
+                    for i in range(k)], ctx)
 
     # ---- structure
     @property
@@ -146,7 +195,8 @@ class RDD:
         return RDD([[list(p)] for p in self._parts], self.ctx)
 
     def partitions(self) -> List[list]:
-        return [list(p) for p in self._parts]
+        """The partitions (columnar ones as zero-copy ColumnarPartition views)."""
+        return [p if isinstance(p, ColumnarPartition) else list(p) for p in self._parts]
 
     def cache(self):
         return self
@@ -182,6 +232,13 @@ class RDD:
 
     def repartition(self, numPartitions: int) -> "RDD":
         n = max(1, int(numPartitions))
+        if _columnar(self._parts):
+            # round-robin over the global row order, as below, on the arrays
+            import numpy as np
+            x = np.concatenate([p.x for p in self._parts]) if len(self._parts) > 1 else self._parts[0].x
+            y = np.concatenate([p.y for p in self._parts]) if len(self._parts) > 1 else self._parts[0].y
+            return RDD([ColumnarPartition(np.ascontiguousarray(x[i::n]), np.ascontiguousarray(y[i::n]))
+                        for i in range(n)], self.ctx)
         parts = [[] for _ in range(n)]
         for i, x in enumerate(itertools.chain.from_iterable(self._parts)):
             parts[i % n].append(x)
@@ -244,6 +301,14 @@ class RDD:
     # ---- actions
     def collect(self) -> list:
         return [x for p in self._parts for x in p]
+
+    def to_arrays(self):
+        """(features, labels) of a columnar RDD as two arrays (partition order)."""
+        import numpy as np
+        if not _columnar(self._parts):
+            items = self.collect()
+            return np.asarray([a for a, _ in items]), np.asarray([b for _, b in items])
+        return np.concatenate([p.x for p in self._parts]), np.concatenate([p.y for p in self._parts])
 
     def count(self) -> int:
         return sum(len(p) for p in self._parts)

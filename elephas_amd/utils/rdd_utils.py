@@ -8,9 +8,14 @@ from ..mllib.adapter import from_vector, to_vector
 
 
 def to_simple_rdd(sc, features: np.ndarray, labels: np.ndarray):
-    """numpy features/labels -> RDD of (x, y) pairs (``parallelize``: contiguous slices)."""
-    pairs = [(x, y) for x, y in zip(features, labels)]
-    return sc.parallelize(pairs)
+    """numpy features/labels -> RDD of (x, y) pairs (``parallelize``: contiguous slices).
+
+    The partitions are columnar views of the two arrays (data/rdd.py ColumnarPartition):
+    they iterate as (x, y) pairs like the reference's, but the training path uploads
+    the arrays directly instead of rebuilding them row by row."""
+    from ..data.rdd import RDD
+    features, labels = np.asarray(features), np.asarray(labels)
+    return RDD.from_arrays(features, labels, sc.defaultParallelism, sc)
 
 
 def to_labeled_point(sc, features: np.ndarray, labels: np.ndarray, categorical: bool = False):

@@ -31,6 +31,11 @@ def _value(parameters):
 
 
 def partition_to_numpy(data):
+    """A partition's (features, labels) arrays: the views of a columnar partition as
+    they are, else stacked from its (x, y) rows."""
+    from .data.rdd import ColumnarPartition
+    if isinstance(data, ColumnarPartition):
+        return np.asarray(data.x), np.asarray(data.y)
     items = list(data)
     if not items:
         return np.zeros((0,)), np.zeros((0,))

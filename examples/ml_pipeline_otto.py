@@ -28,7 +28,7 @@ sc = spark_session.sparkContext
 
 def synth_csv(path, n, seed=0):
     rng = np.random.default_rng(seed)
-    centers = rng.gamma(0.6, 2.0, size=(9, 93))
+    centers = rng.gamma(0.6, 2.0, size=(1, 93)) * np.exp(rng.normal(0, 0.25, size=(9, 93)))  # Otto-like overlap
     y = rng.integers(0, 9, n)
     x = rng.poisson(centers[y])
     with open(path, "w") as f:

@@ -100,3 +100,32 @@ def test_metrics():
     assert 0 < m.weightedPrecision <= 1
     r = RegressionMetrics(sc.parallelize([(1.0, 1.0), (2.0, 2.5), (3.0, 2.5)]))
     assert abs(r.meanAbsoluteError - 1 / 3) < 1e-9 and r.r2 < 1
+
+
+def test_columnar_partitions_match_row_partitions():
+    """to_simple_rdd keeps numpy views per partition (no per-row objects) and behaves
+    exactly like the list-of-pairs RDD: contiguous slices, round-robin repartition,
+    collect order; the training path gets the arrays back without a copy."""
+    import numpy as np
+    from elephas_amd.data import SparkContext, ColumnarPartition
+    from elephas_amd.data.rdd import RDD
+    from elephas_amd.utils.rdd_utils import to_simple_rdd
+    from elephas_amd.worker import partition_to_numpy
+    sc = SparkContext(master="local[3]")
+    x = np.arange(22 * 4, dtype=np.float32).reshape(22, 4)
+    y = np.arange(22) % 3
+    col = to_simple_rdd(sc, x, y)
+    rows = RDD([list(p) for p in col.partitions()], sc)          # the row-wise equivalent
+    assert all(isinstance(p, ColumnarPartition) for p in col.partitions())
+    px, py = partition_to_numpy(col.partitions()[1])
+    assert np.shares_memory(px, x) and px.shape == (7, 4)
+    for a, b in ((col, rows), (col.repartition(5), rows.repartition(5))):
+        assert a.getNumPartitions() == b.getNumPartitions()
+        for pa, pb in zip(a.partitions(), b.partitions()):
+            assert len(pa) == len(pb)
+            for (xa, ya), (xb, yb) in zip(pa, pb):
+                assert np.array_equal(xa, xb) and ya == yb
+    assert col.count() == 22 and len(col.collect()) == 22
+    xs, ys = col.repartition(4).to_arrays()
+    assert sorted(map(tuple, xs.tolist())) == sorted(map(tuple, x.tolist()))
+    assert col.map(lambda r: r[1]).collect() == list(y)

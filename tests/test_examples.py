@@ -45,3 +45,23 @@ def test_notebook_cells_run(tmp_path, monkeypatch):
         src = src.replace("61878", "600").replace("set_epochs(20)", "set_epochs(1)")
         exec(compile(src, "cell", "exec"), g)
     assert 0.0 <= g["metrics"].precision() <= 1.0
+
+
+def test_notebook_otto_pipeline_learns(tmp_path, monkeypatch):
+    """Learnability bar for the Otto pipeline (the reference's only quality number is
+    train precision 0.764 on the real Otto CSV, Spark_ML_Pipeline.ipynb:531; that CSV is
+    not available offline, so parity with 0.764 is unpinned).  The notebook's synthetic
+    Otto-shaped data has overlapping classes (shared Poisson rates, +-25 % per class);
+    6000 rows x 4 epochs of the notebook's model and Adam config must reach precision
+    0.75 (measured 0.83 on the CPU engine; untrained: ~0.11)."""
+    import json
+    nb = json.load(open(os.path.join(EX, "Spark_ML_Pipeline.ipynb")))
+    monkeypatch.chdir(tmp_path)
+    g = {}
+    for c in nb["cells"]:
+        if c["cell_type"] != "code":
+            continue
+        src = "".join(c["source"]).replace("os.path.abspath('..')", repr(ROOT))
+        src = src.replace("61878", "6000").replace("set_epochs(20)", "set_epochs(4)")
+        exec(compile(src, "cell", "exec"), g)
+    assert g["metrics"].precision() >= 0.75
