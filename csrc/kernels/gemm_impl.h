@@ -516,7 +516,7 @@ __device__ __forceinline__ void run_prob(const GA& ga, const Prob& p, const int 
       pf_vec[ps] = false;
       if constexpr (DW_PF) {
         const int gm = m0 + ps * RPP + t_row, gn0 = n0 + t_c0;
-        pf_vec[ps] = p.kind == PK_DW_UPDATE && !skip_update && gm < p.M && gn0 + 8 <= p.N &&
+        pf_vec[ps] = p.kind == PK_DW_UPDATE && gm < p.M && gn0 + 8 <= p.N &&
                      ((p.p_off + (long long)gm * p.N + gn0) & 3) == 0 && (p.op.s_plane & 3) == 0;
         if (pf_vec[ps]) {
           const long long pidx = p.p_off + (long long)gm * p.N + gn0;
@@ -542,10 +542,16 @@ __device__ __forceinline__ void run_prob(const GA& ga, const Prob& p, const int 
 #pragma unroll
       for (int j = 0; j < WN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    if (!skip_update) {
+    // Weight-gradient-only launches: the operands are activation workspaces (no batch
+    // gather, no weight-image parity), so no operand address depends on the step
+    // counters -- the loads are issued without waiting for the counter round trip
+    // (a skipped update only wastes its loads; its epilogue is skipped below).
+    constexpr bool CTR_FREE = (KM & ~KM_DW) == 0u;
+    const bool a_gather = CTR_FREE ? false : (bool)p.a_gather;
+    if (CTR_FREE || !skip_update) {
       const T* A = reinterpret_cast<const T*>(p.A) + (long long)r * p.sA + koff;
       const T* BTp = reinterpret_cast<const T*>(p.BT) + (long long)r * p.sB +
-                     (p.bt_shadow ? (iter & 1) * p.bt_par : 0) + koff;
+                     ((!CTR_FREE && p.bt_shadow) ? (iter & 1) * p.bt_par : 0) + koff;
       // Every fragment load is an unconditional, in-bounds 16-byte global load
       // (invalid rows read row 0, k past the end reads k=0) followed by a value
       // select, so hipcc emits global_load_dwordx4 and never a pointer select
@@ -559,7 +565,7 @@ __device__ __forceinline__ void run_prob(const GA& ga, const Prob& p, const int 
         if (m == p.ones_row) {
           aones_m |= 1u << i;
         } else if (m < p.M) {
-          if (p.a_gather) {
+          if (a_gather) {
             if (m < valid) {
               arow[i] = A + batch_row(p, r, step, m) * p.lda;
               amask |= 1u << i;
@@ -598,7 +604,7 @@ __device__ __forceinline__ void run_prob(const GA& ga, const Prob& p, const int 
           if (m == p.ones_row) {
             aones |= 1u << t;
           } else if (m < p.M) {
-            if (p.a_gather) {
+            if (a_gather) {
               if (m < valid) arow_ld[t] = Ab + batch_row(p, r, step, m) * p.lda;
             } else {
               arow_ld[t] = Ab + (long long)m * p.lda;

@@ -180,42 +180,17 @@ __global__ __launch_bounds__(256) void rowchain_kernel(RcArgs a) {
   // replica index is a scalar register (uniform loads indexed by it stay scalar)
   const int r = blockIdx.x;
   const int m0 = blockIdx.y * RB;
-  const long long s0 = ld_inv(a.ctr);
-  const long long step = s0 + a.step_off;
-  const long long cnt = (long long)ld_inv(a.ntrain + r) - step * a.B;
-  const int valid = (int)(cnt < 0 ? 0 : (cnt > a.B ? a.B : cnt));
-  if (valid == 0) return;  // no batch for this replica this step: DW skips its update too
-  const long long iter = iter_at(a.ctr, a.ntrain, a.B, r, s0, a.step_off);
-  const long long rpar = iter & 1;
-  const T* Wcur = reinterpret_cast<const T*>(a.Wsh) + (long long)r * a.sWsh + rpar * a.wsh_par;
-  const T* WTcur = reinterpret_cast<const T*>(a.WTsh) + (long long)r * a.sWTsh + rpar * a.wtsh_par;
   const float* Pr = a.P + (long long)r * a.sP;
-  const RcLayer LL = a.ly[L - 1];
-
-  // ---- everything that does not depend on this step's data is requested up front,
-  //      under the slab loads: the batch rows' targets, the first hidden layer's
-  //      weight ring, the last layer's forward and input-gradient fragments, biases
-  int prow[2];
-  {
-    const int* pr = a.perm + (long long)r * a.sPerm + step * a.B + m0;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int row = (tid >> 5) + 8 * i;
-      const bool in = m0 + row < valid;
-      const int v = pr[in ? row : 0];
-      prow[i] = in ? v : -1;
-    }
-  }
-  // layer-0 slabs and bias first: phase 0 waits only for these (the wait counter
-  // drains in issue order), the weight streams issued next stay in flight under it
+  // layer-0 slabs and bias FIRST, before the step counter is read: none of their
+  // addresses depend on it, so their round trip overlaps the counter's instead of
+  // following it (phase 0 waits only for these; the wait counter drains in issue order)
   const int row = tid >> 4, c0 = (tid & 15) * CPT;
   const int m = m0 + row;
-  const bool rv = m < valid;
   float4 sv[RC_MAXSPLIT][CPT / 4];
   float z[CPT];
   {
     const RcLayer l0 = a.ly[0];
-    const float* Zr = a.Zp + (long long)r * a.sZp + (long long)(rv ? m : 0) * l0.Np;
+    const float* Zr = a.Zp + (long long)r * a.sZp + (long long)(m < a.B ? m : 0) * l0.Np;
     const float* bias = Pr + l0.p_off + (long long)l0.K * l0.N;
 #pragma unroll
     for (int kc = 0; kc < RC_MAXSPLIT; ++kc) {
@@ -232,6 +207,32 @@ __global__ __launch_bounds__(256) void rowchain_kernel(RcArgs a) {
       const bool cv = c < l0.N && l0.has_bias;
       const float bv = bias[cv ? c : 0];
       z[i] = cv ? bv : 0.f;
+    }
+  }
+  const long long s0 = ld_inv(a.ctr);
+  const long long step = s0 + a.step_off;
+  const long long cnt = (long long)ld_inv(a.ntrain + r) - step * a.B;
+  const int valid = (int)(cnt < 0 ? 0 : (cnt > a.B ? a.B : cnt));
+  if (valid == 0) return;  // no batch for this replica this step: DW skips its update too
+  const long long iter = iter_at(a.ctr, a.ntrain, a.B, r, s0, a.step_off);
+  const long long rpar = iter & 1;
+  const T* Wcur = reinterpret_cast<const T*>(a.Wsh) + (long long)r * a.sWsh + rpar * a.wsh_par;
+  const T* WTcur = reinterpret_cast<const T*>(a.WTsh) + (long long)r * a.sWTsh + rpar * a.wtsh_par;
+  const RcLayer LL = a.ly[L - 1];
+  const bool rv = m < valid;
+
+  // ---- everything that does not depend on this step's data is requested up front,
+  //      under the slab loads: the batch rows' targets, the first hidden layer's
+  //      weight ring, the last layer's forward and input-gradient fragments, biases
+  int prow[2];
+  {
+    const int* pr = a.perm + (long long)r * a.sPerm + step * a.B + m0;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int row = (tid >> 5) + 8 * i;
+      const bool in = m0 + row < valid;
+      const int v = pr[in ? row : 0];
+      prow[i] = in ? v : -1;
     }
   }
   Ring<T, NBW, PF> ring;
