@@ -104,6 +104,8 @@ def main():
     ap.add_argument("--granularity", default="fit", choices=["fit", "batch"])
     ap.add_argument("--validation-split", type=float, default=0.1)
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--rccl", action="store_true",
+                    help="batch granularity: all-reduce through torch.distributed/RCCL (no peer-memory kernels)")
     ap.add_argument("--overlap", action="store_true",
                     help="batch granularity: per-layer gradient buckets all-reduced beside the backward")
     ap.add_argument("--dropout", type=float, default=None, help="override the model's dropout (diagnostics)")
@@ -187,6 +189,10 @@ def main():
 
     if batch_mode and gpu and (world > 1 or args.overlap):
         t.set_grad_scale(1.0 / world)   # mean of the ranks' gradients after the sum all-reduce
+    channel = None
+    if batch_mode and gpu and world > 1 and not args.overlap and not args.no_graph and not args.rccl:
+        from elephas_amd.parallel import p2p   # per-step peer all-reduce captured with the step
+        channel = p2p.graph_channel(t.G.numel())
 
     state = {"step_in_epoch": steps_per_epoch, "epochs": 0, "val_passes": 0}
 
@@ -205,7 +211,9 @@ def main():
                 state["epochs"] += 1
             n = min(k, steps_per_epoch - state["step_in_epoch"])
             if gpu:
-                if batch_mode and args.overlap:
+                if channel is not None:
+                    t.run_steps_allreduce_graph(n, channel)
+                elif batch_mode and args.overlap:
                     t.run_steps_allreduce_overlap(n, dist.all_reduce_sum_)
                 elif batch_mode and world > 1:
                     t.run_steps_allreduce(n, allreduce_grads, use_graph=not args.no_graph)
@@ -288,6 +296,8 @@ def main():
                 "batch_per_worker": B,
                 "rows_per_worker": rows,
                 "sync": "reference (one-shot averaging per fit)" if not batch_mode else "per-step gradient all-reduce",
+                "allreduce": ("peer-memory kernel in the step's hipGraph" if channel is not None
+                              else ("torch.distributed" if world > 1 else None)),
                 "optimizer": "SGD(lr=%g)" % MODELS[args.model][4],
                 "engine": "native HIP executor + hipGraph" if gpu else "torch CPU reference",
                 "launches_per_step": launches,

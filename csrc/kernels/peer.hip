@@ -121,8 +121,21 @@ __device__ __forceinline__ void sum_span(const PeerArgs& a, int parity, long lon
   }
 }
 
+// Epoch of this call for workgroup b: the host's counter, or (graph mode: the same
+// kernel replayed from a hipGraph with frozen arguments) one past the epoch this
+// rank's workgroup b flagged last -- identical on every rank because every rank
+// makes the same calls with the same sizes.
+__device__ __forceinline__ unsigned call_epoch(const PeerArgs& a, int b) {
+  if (!a.dev_epoch) return a.epoch;
+  __shared__ unsigned e;
+  if (threadIdx.x == 0) e = __hip_atomic_load(flag_ptr(a.base[a.rank], 0, b), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+  __syncthreads();
+  return e;
+}
+
 __global__ __launch_bounds__(256) void allreduce_oneshot_kernel(PeerArgs a) {
   const int b = blockIdx.x;
+  a.epoch = call_epoch(a, b);
   const int parity = a.epoch & 1;
   const long long lo = (long long)b * a.chunk;
   const long long hi = lo + a.chunk < a.n ? lo + a.chunk : a.n;
@@ -136,6 +149,7 @@ __global__ __launch_bounds__(256) void allreduce_oneshot_kernel(PeerArgs a) {
 // slice p = [p*slice, min(n, (p+1)*slice)); block b owns sub-chunk b of every slice.
 __global__ __launch_bounds__(256) void allreduce_twoshot_kernel(PeerArgs a) {
   const int b = blockIdx.x;
+  a.epoch = call_epoch(a, b);
   const int parity = a.epoch & 1;
   char* mine = a.base[a.rank];
   auto span = [&](int p, long long& lo, long long& hi) {

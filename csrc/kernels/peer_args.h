@@ -21,6 +21,7 @@ struct PeerArgs {
   long long slice;              // two-shot: elements per rank slice (multiple of 4)
   unsigned long long timeout_ticks;  // 100 MHz wall-clock ticks
   unsigned epoch;
+  int dev_epoch;                // 1: each workgroup derives the epoch from its own last flag
   int world, rank;
 };
 

@@ -250,6 +250,9 @@ PYBIND11_MODULE(_C, m) {
         py::gil_scoped_release rel;
         p.all_reduce(reinterpret_cast<const float*>(in), reinterpret_cast<float*>(out), n, S(s), algo);
       }, py::arg("inp"), py::arg("out"), py::arg("n"), py::arg("stream"), py::arg("algo") = -1)
+      .def("all_reduce_graph", [](PeerAllReduce& p, uintptr_t in, uintptr_t out, long long n, uintptr_t s, int algo) {
+        p.all_reduce_graph(reinterpret_cast<const float*>(in), reinterpret_cast<float*>(out), n, S(s), algo);
+      }, py::arg("inp"), py::arg("out"), py::arg("n"), py::arg("stream"), py::arg("algo") = -1)
       .def("error", &PeerAllReduce::error)
       .def("clear_error", &PeerAllReduce::clear_error)
       .def_property_readonly("capacity", &PeerAllReduce::capacity)

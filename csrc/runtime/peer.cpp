@@ -89,6 +89,21 @@ PeerAllReduce::PeerAllReduce(int rank, int world, long long cap_elems, int devic
       timeout_ticks_(ticks_for(timeout_s, device)) {}
 
 void PeerAllReduce::all_reduce(const float* in, float* out, long long n, hipStream_t s, int algo) {
+  if (graph_n_ >= 0) throw std::runtime_error("PeerAllReduce: object is in graph mode");
+  launch(in, out, n, s, algo, false);
+}
+
+void PeerAllReduce::all_reduce_graph(const float* in, float* out, long long n, hipStream_t s, int algo) {
+  if (n > cap_) throw std::invalid_argument("PeerAllReduce::all_reduce_graph: n exceeds the staging capacity");
+  if (epoch_ != 0) throw std::runtime_error("PeerAllReduce: host-epoch calls were made on this object");
+  if (graph_n_ >= 0 && (graph_n_ != n || graph_algo_ != algo))
+    throw std::invalid_argument("PeerAllReduce::all_reduce_graph: every call needs the same n and algo");
+  graph_n_ = n;
+  graph_algo_ = algo;
+  launch(in, out, n, s, algo, true);
+}
+
+void PeerAllReduce::launch(const float* in, float* out, long long n, hipStream_t s, int algo, bool dev_epoch) {
   if (!buf_.opened()) throw std::runtime_error("PeerAllReduce: peers not opened");
   if ((reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(out)) & 15)
     throw std::invalid_argument("PeerAllReduce: buffers must be 16-byte aligned");
@@ -110,7 +125,8 @@ void PeerAllReduce::all_reduce(const float* in, float* out, long long n, hipStre
     a.world = W;
     a.rank = buf_.rank();
     a.timeout_ticks = timeout_ticks_;
-    a.epoch = ++epoch_;
+    a.dev_epoch = dev_epoch ? 1 : 0;
+    a.epoch = dev_epoch ? 0u : ++epoch_;
     // work per workgroup: >= 1024 elements, <= PEER_MAX_BLOCKS workgroups
     const long long span = two ? (m + W - 1) / W : m;
     long long chunk = (span + PEER_MAX_BLOCKS - 1) / PEER_MAX_BLOCKS;

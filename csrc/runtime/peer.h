@@ -59,6 +59,10 @@ class PeerAllReduce {
   void open(const std::vector<std::string>& handles) { buf_.open(handles); }
   // out = sum over ranks of in (may alias); algo: -1 auto, 0 one-shot, 1 two-shot
   void all_reduce(const float* in, float* out, long long n, hipStream_t s, int algo = -1);
+  // Graph-capturable form: the epoch is derived on the device, so one captured call
+  // can be replayed any number of times.  Every call on this object must then use
+  // graph mode with the same n and algo (n <= capacity), on every rank.
+  void all_reduce_graph(const float* in, float* out, long long n, hipStream_t s, int algo = -1);
   unsigned error() const { return buf_.error(); }
   void clear_error() { buf_.clear_error(); }
   long long capacity() const { return cap_; }
@@ -67,9 +71,12 @@ class PeerAllReduce {
   long long twoshot_min_bytes() const { return twoshot_min_bytes_; }
 
  private:
+  void launch(const float* in, float* out, long long n, hipStream_t s, int algo, bool dev_epoch);
   PeerBuffer buf_;
   long long cap_;
   unsigned epoch_ = 0;
+  long long graph_n_ = -1;
+  int graph_algo_ = -2;
   unsigned long long timeout_ticks_;
   long long twoshot_min_bytes_ = 1LL << 20;
 };

@@ -359,6 +359,31 @@ class NativeTrainer(TrainerBase):
             else:
                 self.exe.apply(self.s)
 
+    def run_steps_allreduce_graph(self, nsteps: int, channel, algo: int = -1):
+        """Per-step gradient all-reduce with the whole step -- forward/backward, the peer
+        all-reduce of G over IPC-mapped buffers (parallel/p2p.py graph channel), the
+        optimizer apply -- captured as ONE hipGraph of GRAPH_CHUNK steps (and one of 1
+        step), so the host launches one graph per 16 steps.  R == 1 (one replica per rank)."""
+        if self.R != 1:
+            raise ValueError("run_steps_allreduce_graph: one replica per rank")
+        graphs = self._graphs.setdefault(("peer_ar", id(channel)), {})
+        full, rest = divmod(nsteps, self.GRAPH_CHUNK)
+        for k, reps in ((self.GRAPH_CHUNK, full), (1, rest)):
+            if reps == 0:
+                continue
+            if k not in graphs:
+                g = torch.cuda.CUDAGraph()
+                self.stream.synchronize()
+                with torch.cuda.graph(g, stream=self.stream):
+                    for _ in range(k):
+                        self.exe.forward_backward(self.s)
+                        channel.all_reduce_graph_(self.G[0], algo=algo, stream=self.stream)
+                        self.exe.apply(self.s)
+                graphs[k] = g
+            with torch.cuda.stream(self.stream):
+                for _ in range(reps):
+                    graphs[k].replay()
+
     def run_steps_allreduce_overlap(self, nsteps: int, allreduce_bucket, comm_stream=None):
         """Per-step gradient path with the all-reduce bucketed per layer and overlapped
         with the rest of the backward: as soon as the launch that completes layer l's

@@ -117,6 +117,16 @@ class PeerAllReduce:
         self.impl.all_reduce(t.data_ptr(), t.data_ptr(), n, s.cuda_stream, algo)
         return t
 
+    def all_reduce_graph_(self, t: torch.Tensor, algo: int = -1, stream: Optional[torch.cuda.Stream] = None
+                          ) -> torch.Tensor:
+        """In-place sum whose launch can be captured in a hipGraph and replayed: the call
+        epoch lives on the device.  A channel (``graph_channel``) serves one fixed size."""
+        if not (self.eligible(t) and t.data_ptr() % 16 == 0):
+            raise ValueError("all_reduce_graph_: needs a 16-byte aligned contiguous fp32 CUDA tensor")
+        s = stream or torch.cuda.current_stream(t.device)
+        self.impl.all_reduce_graph(t.data_ptr(), t.data_ptr(), t.numel(), s.cuda_stream, algo)
+        return t
+
     def check(self) -> None:
         """Raise if a peer wait timed out (synchronous read of the error word)."""
         e = self.impl.error()
@@ -149,6 +159,15 @@ def get() -> Optional[PeerAllReduce]:
         _peer = _DISABLED
         return None
     return _peer
+
+
+def graph_channel(n: int) -> Optional[PeerAllReduce]:
+    """A dedicated peer all-reduce of exactly n floats for graph-captured per-step
+    gradient exchange (collective; None when the peer path is unavailable).  The
+    mechanism was validated by the job-wide instance's self-test."""
+    if get() is None:
+        return None
+    return PeerAllReduce(cap_elems=int(n), verify=False)
 
 
 class _Disabled:

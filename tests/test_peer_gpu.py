@@ -58,6 +58,15 @@ def test_peer_allreduce_two_processes():
         assert not bad, bad
 
 
+def test_per_step_allreduce_in_graph_matches_eager_gloo():
+    """The per-step DP path with the peer all-reduce captured inside the step's hipGraph
+    (16 steps per replay, device-side call epochs) gives bit-identical weights to the
+    eager path that all-reduces the same gradients through gloo, on both ranks."""
+    for r in _run("step_graph"):
+        assert r["error"] == 0 and r["same_on_all_ranks"] and r["moved"] > 0, r
+        assert r["bit_equal"], r
+
+
 def test_sharded_ps_two_processes():
     """Sharded device PS over two processes: concurrent pushes from both ranks are all
     applied (integer deltas, exact), asynchronous pulls never see a torn chunk."""
