@@ -220,6 +220,16 @@ class NativeTrainer(TrainerBase):
                 avg.mul_(1.0 / world)
             self.exe.refresh_from(avg.data_ptr(), 0, self.s)
 
+    def reset_for_fit(self, flat, seed: Optional[int] = None):
+        """Reuse this trainer (buffers, uploaded shards, eval executor) for a new fit the
+        way the reference starts every fit with a freshly built worker model: weights =
+        ``flat``, zero optimizer state and iterations, a fresh dropout seed (the training
+        executor is rebuilt around the same buffers; its graphs are recaptured lazily)."""
+        self.seed = int(seed) if seed is not None else int(np.random.randint(1, 2**62))
+        self._build_executor()
+        self.reset_optimizer_state()
+        self.set_weights_flat(flat)
+
     def reset_optimizer_state(self):
         with torch.cuda.stream(self.stream):
             self.S.fill_(float(self.opt_hp.get("state_init", 0.0)))

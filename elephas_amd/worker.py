@@ -52,6 +52,63 @@ def _build_model(json_str, custom_objects, optimizer, loss, metrics, weights):
     return model
 
 
+def _data_key(xs, ys, vs, active, shuffle):
+    """Identity of a rank's partitions for the trainer cache: the arrays' objects, buffer
+    addresses and shapes plus a strided sample of their contents (cheap; catches the
+    common in-place edits of a dataset between fits, not every possible one)."""
+    key = [float(vs), tuple(bool(a) for a in active), bool(shuffle)]
+    for a in list(xs) + list(ys):
+        a = np.asarray(a)
+        if a.size == 0:
+            key.append((a.shape,))
+            continue
+        flat = a.reshape(-1)
+        step = max(1, flat.size // 4096)
+        key.append((id(a), a.__array_interface__["data"][0], a.shape, a.dtype.str,
+                    hash(np.ascontiguousarray(flat[::step]).tobytes()), hash(flat[-64:].tobytes())))
+    return tuple(key)
+
+
+class _TrainerCache:
+    """The last native trainer a SparkWorker built (one per process): a following fit
+    of the same model / optimizer / loss / metrics / batch size / replica count reuses its
+    device buffers, executor plan and -- for unchanged partitions -- its uploaded shards."""
+
+    def __init__(self):
+        self._key, self._entry = None, None
+
+    @staticmethod
+    def _key_of(worker, R, engine):
+        import json
+        from . import config
+        bs, _, _, _, _ = worker._cfg()
+        enc = lambda o: json.dumps(o, sort_keys=True, default=lambda v: getattr(v, "__name__", repr(v)))
+        custom = tuple((k, id(v)) for k, v in sorted((worker.custom_objects or {}).items()))
+        return (worker.json, enc(worker.master_optimizer), enc(worker.master_loss), enc(worker.master_metrics),
+                custom, int(R), int(bs), config.get_policy(), str(config.get_device()), engine)
+
+    def lookup(self, worker, R, engine):
+        if self._entry is None or self._key != self._key_of(worker, R, engine):
+            return None
+        return self._entry
+
+    def store(self, worker, R, engine, trainer, model, data_key):
+        if not hasattr(trainer, "reset_for_fit"):   # only the native engine is reused
+            self._key, self._entry = None, None
+            return
+        self._key, self._entry = self._key_of(worker, R, engine), (trainer, model, data_key)
+
+    def set_data_key(self, data_key):
+        if self._entry is not None:
+            self._entry = (self._entry[0], self._entry[1], data_key)
+
+    def clear(self):
+        self._key, self._entry = None, None
+
+
+_trainer_cache = _TrainerCache()
+
+
 class SparkWorker:
     """Synchronous worker (reference worker.py:11-49)."""
 
@@ -91,8 +148,6 @@ class SparkWorker:
         """Build the shared executor with one replica per partition and load the
         shards (no training). Returns (trainer, active)."""
         from .ops.engine import make_trainer
-        self.model = _build_model(self.json, self.custom_objects, self.master_optimizer, self.master_loss,
-                                  self.master_metrics, _value(self.parameters))
         bs, epochs, verbose, vs, shuffle = self._cfg()
         xs, ys = [], []
         for p in partitions:
@@ -100,9 +155,26 @@ class SparkWorker:
             xs.append(x)
             ys.append(y)
         active = [len(x) > bs for x in xs]   # reference worker.py:41 (`if n > batch_size: fit`)
+        hit = _trainer_cache.lookup(self, len(partitions), engine)
+        if hit is not None:
+            # same model / optimizer / shapes as the previous fit: reset the cached native
+            # trainer instead of rebuilding it, and keep its device shards if the
+            # partitions are the very same arrays (columnar RDDs of an unchanged dataset)
+            trainer, model, data_key = hit
+            self.model = model
+            trainer.reset_for_fit(flatten_weights(list(_value(self.parameters))), seed)
+            key = _data_key(xs, ys, vs, active, shuffle)
+            if partitions and (key is None or key != data_key):
+                trainer.set_data(xs, ys, vs, active=active, shuffle=shuffle)
+                _trainer_cache.set_data_key(key)
+            return trainer, active
+        self.model = _build_model(self.json, self.custom_objects, self.master_optimizer, self.master_loss,
+                                  self.master_metrics, _value(self.parameters))
         trainer = make_trainer(self.model, max(1, len(partitions)), bs, engine=engine, seed=seed)
         if partitions:
             trainer.set_data(xs, ys, vs, active=active, shuffle=shuffle)
+        _trainer_cache.store(self, len(partitions), engine, trainer, self.model,
+                             _data_key(xs, ys, vs, active, shuffle) if partitions else None)
         return trainer, active
 
     def train_partitions(self, partitions: Sequence[list], engine: Optional[str] = None, seed: Optional[int] = None):

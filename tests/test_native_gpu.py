@@ -670,3 +670,50 @@ def test_native_dropout_matches_fp32_reference_with_same_masks(rowchain):
     free.set_data(xs, ys, 0.0, shuffle=False)
     free.fit(2)
     assert np.abs(free.get_weights_flat() - wr).max() / np.abs(wr - w0).max() > 1e-2
+
+
+def test_spark_model_refit_reuses_trainer_exactly():
+    """A second SparkModel.fit of the same model reuses the cached native trainer (same
+    object; shards kept for the same columnar RDD, re-uploaded for a new one) and gives
+    bit-identical weights to a fit on a freshly built trainer from the same start."""
+    from elephas_amd import config, worker
+    from elephas_amd.data import SparkContext
+    from elephas_amd.models.optimizers import SGD
+    from elephas_amd.spark_model import SparkModel
+    from elephas_amd.utils.rdd_utils import to_simple_rdd
+    config.set_policy("float32")
+    x, y = _data(1200, 64, 5, seed=4)
+    sc = SparkContext(master="local[4]")
+    rdd = to_simple_rdd(sc, x, y)
+    kw = dict(epochs=2, batch_size=32, verbose=0, validation_split=0.1, shuffle=False)
+
+    def new_model(weights=None):
+        m = _mlp(64, [48, 32], 5)
+        m.compile(SGD(learning_rate=0.05, momentum=0.9), "categorical_crossentropy", ["acc"])
+        if weights is not None:
+            m.set_weights(weights)
+        return m
+    worker._trainer_cache.clear()
+    sm = SparkModel(new_model(), mode="synchronous")
+    sm.fit(rdd, **kw)
+    first = worker._trainer_cache._entry[0]
+    w1 = sm.master_network.get_weights()
+    sm.fit(rdd, **kw)                                  # reuses trainer and shards
+    assert worker._trainer_cache._entry[0] is first
+    w2 = sm.master_network.get_weights()
+    worker._trainer_cache.clear()
+    fresh = SparkModel(new_model(w1), mode="synchronous")
+    fresh.fit(rdd, **kw)
+    for a, b in zip(w2, fresh.master_network.get_weights()):
+        np.testing.assert_array_equal(a, b)
+    # a different dataset through the cached trainer: re-uploaded, same as fresh again
+    x2, y2 = _data(1200, 64, 5, seed=9)
+    rdd2 = to_simple_rdd(sc, x2, y2)
+    w3_start = fresh.master_network.get_weights()
+    fresh.fit(rdd2, **kw)
+    w3 = fresh.master_network.get_weights()
+    worker._trainer_cache.clear()
+    ref = SparkModel(new_model(w3_start), mode="synchronous")
+    ref.fit(rdd2, **kw)
+    for a, b in zip(w3, ref.master_network.get_weights()):
+        np.testing.assert_array_equal(a, b)
