@@ -211,7 +211,9 @@ def _fit_weights(model, policy, B, xs, ys, rowchain, epochs=1, val=0.0, R=None, 
 
 
 def _plan_case(case):
+    from elephas_amd.models import initializers
     from elephas_amd.models.optimizers import SGD, Adam, RMSprop
+    initializers.set_seed(2024)   # the initial weights must not depend on which tests ran before
     rng = np.random.default_rng(11)
     if case in ("mnist_bf16_dropout", "mnist_f32_dropout"):
         model = _mlp(784, [128, 128], 10, dropout=0.2)
@@ -254,11 +256,15 @@ def _plan_case(case):
         assert np.abs(wf - wg).max() <= tol * scale, (np.abs(wf - wg).max(), scale)
     else:
         # bf16 weight images: the plans sum layer 0 in different orders, and a 1-ulp
-        # fp32 difference can flip a bf16 rounding that later steps carry on
-        # (the fp32 cases pin the plans' equivalence tightly); compare on average
-        w0 = np.concatenate([w.reshape(-1) for w in model.get_weights()])
-        err = np.abs(wf - wg).mean() / np.abs(wg - w0).mean()
-        assert err < tol, err
+        # fp32 difference flips the bf16 rounding of some weight images, which later
+        # steps carry on (tools/plan_flake_probe.py: both plans are bit-deterministic,
+        # the gap between them depends on the initial weights, 1e-10 .. 0.2 of the mean
+        # update after 10 steps at lr 0.1). The fp32 cases pin the plans' equivalence
+        # tightly; here the plans must agree within a few bf16 ulps: the mean weight gap
+        # below 2^-6 of the mean weight magnitude (worst of 15 initialisations: 4.5e-3;
+        # a wrong mask or update rule on any layer is tens of percent)
+        err = np.abs(wf - wg).mean() / np.abs(wg).mean()
+        assert err < 2.0 ** -6, err
     for a, b in zip(hf, hg):
         if a is None:
             assert b is None
