@@ -137,8 +137,17 @@ def broadcast_object(obj: Any, src: int = 0) -> Any:
 
 
 def barrier() -> None:
+    """Host barrier.  On an RCCL job whose peer-memory all-reduce is up, a 1-element
+    peer all-reduce + device sync: every rank's kernel waits for every peer's flag,
+    which a peer only raises after reaching this call (~10 us instead of an RCCL
+    barrier's all-reduce round trip through the proxy threads)."""
     if is_initialized() and world_size() > 1:
         if dist.get_backend() == "nccl":
+            from . import p2p
+            peer = p2p.current()
+            if peer is not None:
+                peer.barrier()
+                return
             dist.barrier(device_ids=[torch.cuda.current_device()])
         else:
             dist.barrier()

@@ -73,6 +73,7 @@ class PeerAllReduce:
             if verify:
                 self.ok = self._self_test(allgather)
         self._tmp = None
+        self._bar = None
 
     def _self_test(self, allgather) -> bool:
         """One-shot and two-shot all-reduce of known vectors on every rank, then a vote:
@@ -127,6 +128,16 @@ class PeerAllReduce:
         self.impl.all_reduce_graph(t.data_ptr(), t.data_ptr(), t.numel(), s.cuda_stream, algo)
         return t
 
+    def barrier(self) -> None:
+        """All ranks reach this call before any returns (1-element all-reduce + sync)."""
+        if self._bar is None:
+            self._bar = torch.zeros(4, dtype=torch.float32, device=f"cuda:{self.device}")
+        s = torch.cuda.current_stream(self.device)
+        self.impl.all_reduce(self._bar.data_ptr(), self._bar.data_ptr(), 4, s.cuda_stream, 0)
+        s.synchronize()
+        if self.impl.error():
+            raise RuntimeError("peer barrier: a wait for a peer rank timed out")
+
     def check(self) -> None:
         """Raise if a peer wait timed out (synchronous read of the error word)."""
         e = self.impl.error()
@@ -178,6 +189,12 @@ class _Disabled:
 
 
 _DISABLED = _Disabled()
+
+
+def current() -> Optional[PeerAllReduce]:
+    """The job-wide instance if it has been created and passed its self-test (never
+    creates it: a barrier must not become the first collective)."""
+    return _peer if isinstance(_peer, PeerAllReduce) else None
 
 
 def reset() -> None:

@@ -62,6 +62,12 @@ def allreduce(dist, rank, world):
     torch.cuda.synchronize()
     res["misaligned_ok"] = bool(torch.equal(v.cpu(), torch.arange(1, 1001, dtype=torch.float32)
                                             * sum(r + 1 for r in range(world))))
+    # peer barrier: a rank that arrives late holds every other rank in the barrier
+    t0 = time.perf_counter()
+    if rank == 1:
+        time.sleep(0.3)
+    pa.barrier()
+    res["barrier_waited"] = time.perf_counter() - t0
     res["error"] = int(pa.impl.error())
     return res
 

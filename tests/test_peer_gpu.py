@@ -54,6 +54,7 @@ def test_peer_allreduce_two_processes():
     rank-order sum bit for bit, and all ranks agree; a misaligned view works too."""
     for r in _run("allreduce"):
         assert r["self_test"] and r["error"] == 0 and r["misaligned_ok"], r
+        assert r["barrier_waited"] >= 0.25, r     # the peer barrier waited for the late rank
         bad = [c for c in r["cases"] if not (c["exact"] and c["same_on_all_ranks"])]
         assert not bad, bad
 
