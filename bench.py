@@ -47,7 +47,7 @@ MODELS = {
     # name: (layers, dropout, classes, rows per worker, lr)
     "mnist": ([784, 128, 128], 0.2, 10, 7500, 0.1),
     "otto": ([93, 512, 512, 512], 0.5, 9, 7735, 0.01),
-    "wide": ([4096, 4096, 4096], 0.0, 1000, 4096, 0.01),
+    "wide": ([4096, 4096, 4096], 0.0, 1000, 16384, 0.01),   # 16 batches of 1024 per epoch
 }
 
 
