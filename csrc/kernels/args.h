@@ -41,7 +41,8 @@ enum ProbKind : int {
   PK_DW_GRAD = 5,    // dW -> flat gradient buffer (all-reduce path)
   PK_GATHER_T = 6,   // X^T batch (gathered through perm) for DW of layer 1
   PK_LOSS_ROWS = 7,  // wide final layer: one wave per row over fp32 logits Z
-  PK_PARTIAL = 8     // split-K slab: fp32 C over K chunk kc -> D + r*sD + kc*sPart (row-chain plan)
+  PK_PARTIAL = 8     // split-K slab: fp32 C over K chunk kc -> D + r*sD + kc*sPart (row-chain layer 0,
+                     // wide last layer); a new kind must be added to KM_ALL (gemm_impl.h)
 };
 
 struct Prob {
@@ -133,6 +134,7 @@ constexpr int RC_MAXL = 4;
 constexpr int RC_ROWS = 16;
 constexpr int RC_MAXW = 256;
 constexpr int RC_MAXSPLIT = 8;   // layer-0 split-K slabs
+constexpr int LOSS_MAX_SPLIT = 4;  // split-K slabs of a wide last layer summed by the loss rows kernel
 struct RcLayer {
   int K, N, Kp, Np, act, has_bias;
   float rate;

@@ -118,8 +118,8 @@ __device__ __forceinline__ bool softmax_cce_wide(const Prob& p) {
   return ok;
 }
 
-template <int NV, typename DZ>
-__device__ __forceinline__ void row_softmax_cce_reg(const Prob& p, int lane, const float* zrow, const float* yrow,
+template <int NV, typename ZL, typename DZ>
+__device__ __forceinline__ void row_softmax_cce_reg(const Prob& p, int lane, ZL zload, const float* yrow,
                                                     bool train, DZ dz, RowOut& ro) {
   const int N = p.N;
   const bool sparse = p.loss == LOSS_SPARSE_CCE;
@@ -128,7 +128,7 @@ __device__ __forceinline__ void row_softmax_cce_reg(const Prob& p, int lane, con
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
     const int j = lane + 64 * i;
-    z[i] = j < N ? zrow[j] : -INFINITY;
+    z[i] = j < N ? zload(j) : -INFINITY;
     y[i] = sparse ? (j == ycls ? 1.f : 0.f) : (j < N ? yrow[j] : 0.f);
   }
   float zmax = -INFINITY, bz = -INFINITY, by = -INFINITY;
@@ -203,9 +203,23 @@ __device__ __forceinline__ void loss_rows_block(const GroupArgs& ga, const Prob&
       continue;
     }
     const float* zrow = p.Z + (long long)r * p.sZ + (long long)row * p.ldz;
+    // logits: Z, or (split-K last layer) the sum of the tiles_k fp32 slabs + bias
+    // (at most LOSS_MAX_SPLIT slabs; unconditional loads with clamped slab indices so
+    // every load of a row is in flight at once -- no branch between them)
+    const int nsl = p.tiles_k > 1 ? p.tiles_k : 1;
+    auto zat = [&](int j) {
+      if (nsl == 1) return zrow[j];
+      float v = p.bias ? p.bias[(long long)r * p.sBias + j] : 0.f;
+#pragma unroll
+      for (int k = 0; k < LOSS_MAX_SPLIT; ++k) {
+        const float x = zrow[(long long)(k < nsl ? k : 0) * p.sPart + j];
+        v += k < nsl ? x : 0.f;
+      }
+      return v;
+    };
     float* prow = p.pred ? p.pred + (long long)r * p.sPred + (p.chunk * p.B + row) * p.ldp : nullptr;
     if (!p.Y) {  // predict only
-      if (prow) row_predict<64, 0>(lane, p.N, p.act, [&](int, int j) { return zrow[j]; }, [&](int, int j, float v) { prow[j] = v; });
+      if (prow) row_predict<64, 0>(lane, p.N, p.act, [&](int, int j) { return zat(j); }, [&](int, int j, float v) { prow[j] = v; });
       continue;
     }
     const long long drow = batch_row(p, r, step, row);
@@ -224,9 +238,9 @@ __device__ __forceinline__ void loss_rows_block(const GroupArgs& ga, const Prob&
       // (16 values per lane, all loads in flight at once); the generic loop below
       // re-reads global memory once per pass and per 64-column chunk, one
       // dependent round trip each (66 us for 1024 x 1000)
-      row_softmax_cce_reg<16>(p, lane, zrow, yrow, train, dz, ro);
+      row_softmax_cce_reg<16>(p, lane, zat, yrow, train, dz, ro);
     } else {
-      row_loss<64, 0>(lane, p.N, p.act, p.loss, p.met, p.nmet, [&](int, int j) { return zrow[j]; },
+      row_loss<64, 0>(lane, p.N, p.act, p.loss, p.met, p.nmet, [&](int, int j) { return zat(j); },
                       [&](int, int j) { return yrow[j]; }, yrow[0], train, dz, prow != nullptr, pw, ro);
     }
     // per-wave partial sums; one set of atomics per workgroup below (same-address
@@ -451,7 +465,7 @@ __device__ __forceinline__ void thr_lds_mainloop(const __bf16* const (&arow_ld)[
 // --------------------------------------------------------------- the kernel
 // KM: bit k set = problem kind k can occur in this instantiation; the other
 // kinds' epilogues are compiled out (smaller code per launch, see launch_cfg).
-constexpr unsigned KM_ALL = 0xffu;
+constexpr unsigned KM_ALL = 0x1ffu;  // every ProbKind (0..8, args.h)
 constexpr unsigned KB(int k) { return 1u << k; }
 // the executor's launches: {FWD, X^T gather}, {FWD_LOSS}, {DW update or grad, DX}
 constexpr unsigned KM_NONE = 0u;
@@ -1105,7 +1119,8 @@ static hipError_t launch_cfg(const GroupArgs& ga, hipStream_t s) {
       hipError_t e = hipSuccess;
       if (launch_if<T, WM, WN, WAVES_M, WAVES_N, KSPLIT, KM_FWD, KM_GATHER>(ga, lds, s, e) ||
           launch_if<T, WM, WN, WAVES_M, WAVES_N, KSPLIT, KM_LOSS, KM_NONE>(ga, lds, s, e) ||
-          launch_if<T, WM, WN, WAVES_M, WAVES_N, KSPLIT, KM_DW, KM_DX>(ga, lds, s, e))
+          launch_if<T, WM, WN, WAVES_M, WAVES_N, KSPLIT, KM_DW, KM_DX>(ga, lds, s, e) ||
+          launch_if<T, WM, WN, WAVES_M, WAVES_N, KSPLIT, KM_PARTIAL, KM_NONE>(ga, lds, s, e))
         return e;
     }
   }
@@ -1149,6 +1164,7 @@ static void set_attr_spec() {
   set_attr<T, WM, WN, WAVES_M, WAVES_N, KSPLIT, KM_FWD, KM_GATHER>();
   set_attr<T, WM, WN, WAVES_M, WAVES_N, KSPLIT, KM_LOSS, KM_NONE>();
   set_attr<T, WM, WN, WAVES_M, WAVES_N, KSPLIT, KM_DW, KM_DX>();
+  set_attr<T, WM, WN, WAVES_M, WAVES_N, KSPLIT, KM_PARTIAL, KM_NONE>();
 }
 
 }  // namespace ea

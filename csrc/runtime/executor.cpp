@@ -2,6 +2,8 @@
 // See executor.h for the step structure.
 #include "executor.h"
 
+#include <cstdlib>
+
 #include <algorithm>
 #include <cstring>
 
@@ -39,6 +41,7 @@ Executor::~Executor() {
   destroy_graphs();
   if (d_probs_) (void)hipFree(d_probs_);
   if (d_zp_) (void)hipFree(d_zp_);
+  if (d_zw_) (void)hipFree(d_zw_);
 }
 
 // Row-chain plan (rowchain.hip): 2 <= L <= RC_MAXL Dense layers, every layer but
@@ -181,6 +184,18 @@ void Executor::destroy_graphs() {
   graphs_.clear();
 }
 
+// split-K factor for the unfused (wide-output) last layer: THR tiles only, each slab
+// at least 8 k-tiles deep, up to LOSS_MAX_SPLIT slabs, until ~2 workgroups per CU
+int Executor::split_last(int cfg, long long N, long long K) const {
+  if (cfg != 1 && cfg != 2) return 1;
+  const char* e = std::getenv("ELEPHAS_AMD_SPLIT_LAST");
+  if (e && e[0] == '0') return 1;
+  const long long tiles = (long long)c_.R * cdiv((int)c_.B, 128) * cdiv((int)N, ea_gemm_tile_n(cfg));
+  int ks = 1;
+  while (ks < LOSS_MAX_SPLIT && tiles * ks < 512 && K / (2 * ks) >= 512) ks *= 2;
+  return ks;
+}
+
 int Executor::pick_cfg(long long M, long long N, long long K) const {
   if (c_.force_cfg >= 0) return c_.force_cfg;
   if (M >= 256 && N >= c_.thr_min_n && K >= c_.thr_min_k) {
@@ -232,7 +247,8 @@ void Executor::finalize(Launch& L) const {
       p.tiles_n = cdiv(p.N, bn);
     }
     p.block_begin = begin;
-    begin += p.tiles_m * p.tiles_n;  // tiles per replica: grid (R, tiles)
+    // tiles per replica: grid (R, tiles); split-K problems have tiles_k slabs each
+    begin += p.tiles_m * p.tiles_n * (p.kind == PK_PARTIAL ? std::max(1, p.tiles_k) : 1);
   }
   L.ga.R = c_.R;
   L.ga.total_blocks = begin;
@@ -333,6 +349,23 @@ std::vector<Executor::Launch> Executor::build_forward(bool eval, long long chunk
         g.DT = nullptr;
         g.acc = nullptr;
         g.pred = nullptr;
+        // A wide last layer (1024 x 1000 x 4096) gives a 128x64 grid of only 128
+        // workgroups: split its reduction into ks slabs (fp32, executor-owned) until
+        // every CU holds ~2 workgroups; the loss rows kernel sums the slabs + bias
+        const int ks = split_last(cfg, ly.N, ly.Kp);
+        if (ks > 1) {
+          const long long slab = (long long)c_.B * ly.N;
+          if (!d_zw_) check(hipMalloc(&d_zw_, sizeof(float) * (size_t)c_.R * ks * slab), "hipMalloc(logit slabs)");
+          g.kind = PK_PARTIAL;
+          g.tiles_k = ks;
+          g.kchunk = cdiv(cdiv(ly.Kp, ks), 64) * 64;
+          g.D = d_zw_;
+          g.ldd = ly.N;
+          g.sD = ks * slab;
+          g.sPart = slab;
+          g.Z = nullptr;
+          g.bias = nullptr;
+        }
         La.ga.p[0] = g;
         La.ga.nprob = 1;
         finalize(La);
@@ -343,6 +376,13 @@ std::vector<Executor::Launch> Executor::build_forward(bool eval, long long chunk
         q.Z = reinterpret_cast<float*>(ly.Z);
         q.ldz = ly.N;
         q.sZ = (long long)c_.B * ly.N;
+        q.tiles_k = 1;
+        if (ks > 1) {
+          q.Z = d_zw_;
+          q.sZ = ks * (long long)c_.B * ly.N;
+          q.tiles_k = ks;
+          q.sPart = (long long)c_.B * ly.N;
+        }
         if (!eval) {
           q.D = reinterpret_cast<void*>(ly.dZ);
           q.ldd = ly.Np;

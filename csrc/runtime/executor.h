@@ -130,6 +130,7 @@ class Executor {
   } rc_;
   Prob* d_probs_ = nullptr;   // device tables of the row-chain launches
   float* d_zp_ = nullptr;     // layer-0 split-K slabs [R][nsplitk][B][N0]
+  mutable float* d_zw_ = nullptr;  // (allocated by the const plan builder) wide last layer split-K logit slabs [R][ks][B][N_last]
   bool build_rowchain();
   void run_rowchain(hipStream_t s, int step_off, bool grad) const;
   void run_step(hipStream_t s, int step_off) const;
@@ -138,6 +139,7 @@ class Executor {
   Prob base_prob() const;
   void finalize(Launch& L) const;
   int pick_cfg(long long M, long long N, long long K) const;
+  int split_last(int cfg, long long N, long long K) const;
   std::vector<Launch> build_forward(bool eval, long long chunk, const EvalSource* src) const;
   void build();
   void run(const std::vector<Launch>& ls, hipStream_t s, int step_off) const;

@@ -129,6 +129,33 @@ def test_wide_output_loss_rows_path(policy, B):
     config.set_policy("float32")
 
 
+@pytest.mark.parametrize("policy", ["float32", "mixed_bfloat16"])
+def test_split_k_wide_last_layer(policy):
+    """A wide last layer with a deep reduction (K = 2048 -> 300 classes at batch 256)
+    runs as split-K slabs (PK_PARTIAL, 4 slabs) summed with the bias by the loss rows
+    kernel; training, evaluation and prediction match the fp32 torch reference."""
+    from elephas_amd import config
+    model = _mlp(64, [2048], 300)
+    model.compile("sgd", "categorical_crossentropy", ["acc"])
+    x, y = _data(600, 64, 300, seed=6)
+    nat, ref = _engines(model, 256, policy)
+    kinds = [p for p in nat.exe.launch_cfgs()]
+    for t in (nat, ref):
+        t.set_data([x], [y], 0.0, shuffle=False)
+        t.fit(2)
+    wn, wr = nat.get_weights_flat(), ref.get_weights_flat()
+    w0 = np.concatenate([w.reshape(-1) for w in model.get_weights()])
+    if policy == "float32":
+        assert np.abs(wn - wr).max() <= 1e-4 * np.abs(wr - w0).max() + 1e-6
+        assert np.allclose(nat.evaluate(x, y), ref.evaluate(x, y), rtol=1e-4)
+        assert np.allclose(nat.predict(x[:100]), ref.predict(x[:100]), rtol=1e-4, atol=1e-6)
+    else:
+        assert np.abs(wn - wr).mean() / np.abs(wr - w0).mean() < 0.05
+        assert np.allclose(nat.evaluate(x, y), ref.evaluate(x, y), rtol=2e-2, atol=2e-2)
+    assert kinds  # the plan was built
+    config.set_policy("float32")
+
+
 def test_partial_batches_and_validation():
     model = _mlp(30, [40], 4, dropout=0.0)
     model.compile("sgd", "categorical_crossentropy", ["acc"])

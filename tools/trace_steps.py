@@ -13,7 +13,9 @@ rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 tail = rows[-n:]
 by = {}
 for r in tail:
-    key = (r["Kernel_Name"][:70], int(r["Grid_Size_X"]) // int(r["Workgroup_Size_X"]))
+    wgs = (int(r["Grid_Size_X"]) // int(r["Workgroup_Size_X"])) * int(r.get("Grid_Size_Y") or 1) * \
+        int(r.get("Grid_Size_Z") or 1)
+    key = (r["Kernel_Name"][:70], wgs)
     by.setdefault(key, []).append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
 tot = 0.0
 for (name, wgs), v in sorted(by.items(), key=lambda kv: -len(kv[1])):
