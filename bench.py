@@ -313,6 +313,8 @@ def main():
     if dist.is_initialized():
         dist.barrier()
         import torch.distributed as tdist
+        from elephas_amd.parallel import p2p
+        p2p.shutdown()   # peer buffers freed only after every rank is done with them
         tdist.destroy_process_group()
 
 
@@ -377,6 +379,8 @@ def bench_fit(args, model, dist, rank, world, dev):
     if dist.is_initialized():
         dist.barrier()
         import torch.distributed as tdist
+        from elephas_amd.parallel import p2p
+        p2p.shutdown()   # peer buffers freed only after every rank is done with them
         tdist.destroy_process_group()
 
 
@@ -441,6 +445,8 @@ def bench_infer(args, model, dist, rank, world, dev):
     if dist.is_initialized():
         dist.barrier()
         import torch.distributed as tdist
+        from elephas_amd.parallel import p2p
+        p2p.shutdown()   # peer buffers freed only after every rank is done with them
         tdist.destroy_process_group()
 
 
@@ -537,6 +543,8 @@ def bench_async(args, model, dist, rank, world, dev):
     client.close()
     if dist.is_initialized():
         import torch.distributed as tdist
+        from elephas_amd.parallel import p2p
+        p2p.shutdown()   # peer buffers freed only after every rank is done with them
         tdist.destroy_process_group()
 
 

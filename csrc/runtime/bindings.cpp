@@ -255,6 +255,7 @@ PYBIND11_MODULE(_C, m) {
       }, py::arg("inp"), py::arg("out"), py::arg("n"), py::arg("stream"), py::arg("algo") = -1)
       .def("error", &PeerAllReduce::error)
       .def("clear_error", &PeerAllReduce::clear_error)
+      .def("release", &PeerAllReduce::release)
       .def_property_readonly("capacity", &PeerAllReduce::capacity)
       .def_property_readonly("calls", &PeerAllReduce::calls)
       .def_property("twoshot_min_bytes", &PeerAllReduce::twoshot_min_bytes, &PeerAllReduce::set_twoshot_min_bytes);
@@ -282,6 +283,7 @@ PYBIND11_MODULE(_C, m) {
       })
       .def("error", &ShardedParameterServer::error)
       .def("clear_error", &ShardedParameterServer::clear_error)
+      .def("release", &ShardedParameterServer::release)
       .def("shard_begin", &ShardedParameterServer::shard_begin)
       .def_property_readonly("n", &ShardedParameterServer::size)
       .def_property_readonly("consistent", &ShardedParameterServer::consistent)

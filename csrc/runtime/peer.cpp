@@ -42,12 +42,16 @@ PeerBuffer::PeerBuffer(int rank, int world, long long data_bytes, int device)
   if (world == 1) opened_ = true;
 }
 
+// A buffer other ranks have mapped is freed only after release(): a peer's kernel may
+// still be reading it (the last collective's reads trail its flag wait), and freeing
+// mapped memory under a running kernel faults the reader.  Without release() the
+// process exit reclaims it.
 PeerBuffer::~PeerBuffer() {
   for (int r = 0; r < world_; ++r) {
-    if (!bases_[r]) continue;
-    if (r == rank_) (void)hipFree(bases_[r]);
-    else (void)hipIpcCloseMemHandle(bases_[r]);
+    if (!bases_[r] || r == rank_) continue;
+    (void)hipIpcCloseMemHandle(bases_[r]);
   }
+  if (bases_[rank_] && (world_ == 1 || released_)) (void)hipFree(bases_[rank_]);
 }
 
 std::string PeerBuffer::handle() const {

@@ -43,11 +43,15 @@ class PeerBuffer {
   // error word written by kernels whose wait timed out (0 = none); synchronous read
   unsigned error() const;
   void clear_error();
+  // the caller guarantees no rank will touch this buffer again (every rank has
+  // synchronised its device and passed a process-group barrier): free it on destruction
+  void release() { released_ = true; }
 
  private:
   int rank_, world_, device_;
   long long data_bytes_;
   bool opened_ = false;
+  bool released_ = false;
   std::vector<char*> bases_;
 };
 
@@ -65,6 +69,7 @@ class PeerAllReduce {
   void all_reduce_graph(const float* in, float* out, long long n, hipStream_t s, int algo = -1);
   unsigned error() const { return buf_.error(); }
   void clear_error() { buf_.clear_error(); }
+  void release() { buf_.release(); }
   long long capacity() const { return cap_; }
   long long calls() const { return epoch_; }
   void set_twoshot_min_bytes(long long b) { twoshot_min_bytes_ = b; }
@@ -96,6 +101,7 @@ class ShardedParameterServer {
   void push_delta(const float* delta, hipStream_t s);  // theta -= delta (reference update semantics)
   unsigned error() const { return buf_.error(); }
   void clear_error() { buf_.clear_error(); }
+  void release() { buf_.release(); }
   long long size() const { return n_; }
   int consistent() const { return consistent_; }
   long long nchunks() const { return nchunks_; }

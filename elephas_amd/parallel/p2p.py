@@ -197,6 +197,27 @@ def current() -> Optional[PeerAllReduce]:
     return _peer if isinstance(_peer, PeerAllReduce) else None
 
 
+def shutdown() -> None:
+    """Tear the job-wide peer all-reduce down safely (collective; call before
+    destroy_process_group): every rank drains its device, a process-group barrier
+    (RCCL / gloo, not the peer kernels) proves no rank will read a peer buffer again,
+    then the buffers are unmapped and freed.  Without it the buffers live until exit."""
+    global _peer
+    if not isinstance(_peer, PeerAllReduce):
+        _peer = None
+        return
+    import torch.distributed as tdist
+    torch.cuda.synchronize(_peer.device)
+    if dist.is_initialized():
+        if dist.backend() == "nccl":
+            tdist.barrier(device_ids=[torch.cuda.current_device()])
+        else:
+            tdist.barrier()
+    _peer.impl.release()
+    _peer.impl = None
+    _peer = None
+
+
 def reset() -> None:
     global _peer
     _peer = None

@@ -111,7 +111,14 @@ class DeviceClient(BaseParameterClient):
             self.like = server._like
         return self
 
-    def close(self):
+    def close(self, release: bool = False):
+        """Drop this rank's endpoint.  ``release``: the caller guarantees every rank has
+        finished every pull / push (e.g. after a collective that follows the final
+        stream synchronisation), so this rank's shard can be freed; otherwise it stays
+        allocated until process exit (freeing memory a peer may still be reading faults
+        the reader)."""
+        if self.ps is not None and release:
+            self.ps.release()
         self.ps = None
 
     def _native(self):

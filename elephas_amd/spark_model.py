@@ -464,10 +464,11 @@ class SparkModel:
             if dist.rank() == 0:
                 self.stop_server()   # always, also when a worker failed
             if self._ps_type == "device":
-                # every rank has left the broadcast: nobody reads a shard any more
+                # after a completed broadcast every rank has synchronised its pulls and
+                # pushes and rank 0 its final pull: the shards can be freed
                 if ps is not None:
                     ps.close()
-                client.close()
+                client.close(release="final" in locals())
         if ps is not None and self._ps_type == "device":
             ps.set_weights(final)    # host copy of the final weights (the shards are gone)
         return final
