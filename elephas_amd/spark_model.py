@@ -13,9 +13,12 @@ Mapping of the reference's distribution:
     flat parameter vector; theta <- theta0 - sum_i(delta_i)/N == mean_i(theta_i)
     with N the number of partitions (empty / tiny partitions count, as in the
     reference).
-  * parameter server (async / hogwild) -> device-resident flat vector on rank 0
-    ('device' transport, IPC-mapped into other ranks over xGMI), or the
-    http/socket compatibility transports.
+  * parameter server (async / hogwild) -> the flat vector sharded over the GPUs
+    ('device' transport: every shard IPC-mapped into every rank; single-kernel
+    pulls / atomic pushes on the workers' streams), or the http/socket
+    compatibility transports.
+  * small all-reduces -> peer-memory kernels over xGMI (parallel/p2p.py), RCCL
+    above 64 MB.
   * distributed predict / evaluate -> contiguous shards per rank, ordered
     gather / sample-weighted all-reduce of [sum loss, sum metrics, n].
 """
