@@ -39,7 +39,9 @@ def init_from_env(backend: str = None, timeout_s: int = None) -> bool:
         return False
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     if backend is None:
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        # ELEPHAS_AMD_DIST_BACKEND=gloo: rehearsal of a multi-rank GPU job on ONE GPU
+        # (RCCL refuses two ranks on one device; the peer kernels do not)
+        backend = os.environ.get("ELEPHAS_AMD_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
     if backend == "nccl":
         local = int(os.environ.get("LOCAL_RANK", "0"))
         torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
@@ -72,7 +74,7 @@ def all_reduce_sum_(t: torch.Tensor) -> torch.Tensor:
     if not is_initialized() or world_size() == 1:
         return t
     dev = _comm_device()
-    if t.is_cuda and dev.type == "cuda":
+    if t.is_cuda:
         from . import p2p
         peer = p2p.get()
         if peer is not None and peer.eligible(t):

@@ -158,7 +158,9 @@ def get() -> Optional[PeerAllReduce]:
     global _peer
     if _peer is not None:
         return _peer
-    if not enabled() or not dist.is_initialized() or dist.world_size() < 2 or dist.backend() != "nccl":
+    rehearsal = os.environ.get("ELEPHAS_AMD_P2P_ANY_BACKEND") == "1" and torch.cuda.is_available()
+    if not enabled() or not dist.is_initialized() or dist.world_size() < 2 or \
+            (dist.backend() != "nccl" and not rehearsal):
         return None
     local = int(os.environ.get("LOCAL_WORLD_SIZE", str(dist.world_size())))
     if dist.world_size() > 8 or local != dist.world_size():   # IPC maps peers of one node only
