@@ -203,7 +203,7 @@ def main():
         while k > 0:
             if state["step_in_epoch"] >= steps_per_epoch:
                 if state["epochs"] > 0 and args.validation_split > 0 and gpu:
-                    t._val_sums()
+                    t.launch_val()   # enqueued like fit() does: no host sync at the epoch end
                     state["val_passes"] += 1
                 if gpu:
                     t.begin_epoch()

@@ -445,9 +445,29 @@ class NativeTrainer(TrainerBase):
     def fit(self, epochs, verbose=0, allreduce=None):
         hist = self.new_history()
         self._enter()
-        for epoch in range(int(epochs)):
-            self.launch_epoch(allreduce)
-            self.collect_epoch(hist, epoch, epochs, verbose)
+        epochs = int(epochs)
+        if verbose or allreduce is not None:
+            # per-epoch host reads (progress lines; the all-reduce path is host-driven anyway)
+            for epoch in range(epochs):
+                self.launch_epoch(allreduce)
+                self.collect_epoch(hist, epoch, epochs, verbose)
+        else:
+            # every epoch enqueued back to back: the epoch-end loss / metric sums and the
+            # validation pass land in per-epoch device slots, read with ONE host copy at
+            # the end (no host synchronisation -- and no GPU bubble -- per epoch)
+            has_val = max(self.vcount_h) > 0
+            with torch.cuda.stream(self.stream):
+                slots = torch.zeros(epochs, 2, self.R, 6, dtype=torch.float64, device=self.dev)
+            for epoch in range(epochs):
+                self.launch_epoch()
+                with torch.cuda.stream(self.stream):
+                    slots[epoch, 0].copy_(self.acc)
+                if has_val:
+                    self.launch_val(slots[epoch, 1])
+            host = self._host(slots)
+            for epoch in range(epochs):
+                self._append_history(hist, host[epoch, 0] if self.steps_per_epoch() > 0 else None,
+                                     host[epoch, 1] if has_val else None, epoch, epochs, 0)
         self._exit()
         return hist
 
@@ -465,8 +485,13 @@ class NativeTrainer(TrainerBase):
 
     def collect_epoch(self, hist, epoch, epochs, verbose=0):
         """Append the launched epoch's loss / metrics and validation pass to ``hist``."""
-        sums = self._host(self.acc) if self.steps_per_epoch() > 0 else np.zeros((self.R, 6))
+        sums = self._host(self.acc) if self.steps_per_epoch() > 0 else None
         val = self._val_sums() if max(self.vcount_h) > 0 else None
+        return self._append_history(hist, sums, val, epoch, epochs, verbose)
+
+    def _append_history(self, hist, sums, val, epoch, epochs, verbose):
+        if sums is None:
+            sums = np.zeros((self.R, 6))
         for r in range(self.R):
             if not self.active[r]:
                 continue
@@ -479,8 +504,10 @@ class NativeTrainer(TrainerBase):
                 self.print_epoch(epoch, epochs, h, r)
         return hist
 
-    def _val_sums(self):
-        """Validation tails of the training shards (per replica), dropout off."""
+    def launch_val(self, dst: Optional[torch.Tensor] = None):
+        """Enqueue the validation pass over the tails of the training shards (per
+        replica, dropout off) into acc_val, and a copy of it into ``dst`` (a [R, 6]
+        fp64 device tensor) if given; no host synchronisation."""
         exe = self._eval_exe()
         with torch.cuda.stream(self.stream):
             self.acc_val.zero_()
@@ -491,6 +518,12 @@ class NativeTrainer(TrainerBase):
                        acc=self.acc_val.data_ptr())
             for c in range(nch):
                 exe.eval_chunk(c, src, self.s)
+            if dst is not None:
+                dst.copy_(self.acc_val)
+
+    def _val_sums(self):
+        """Validation tails of the training shards (per replica), dropout off."""
+        self.launch_val()
         return self._host(self.acc_val)
 
     def _host(self, t: torch.Tensor) -> np.ndarray:
