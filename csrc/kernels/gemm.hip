@@ -7,17 +7,20 @@ extern "C" {
 hipError_t ea_gemm_launch_lat_bf16(const ea::GroupArgs* ga, hipStream_t s);
 hipError_t ea_gemm_launch_thr_bf16(const ea::GroupArgs* ga, hipStream_t s);
 hipError_t ea_gemm_launch_thr64_bf16(const ea::GroupArgs* ga, hipStream_t s);
+hipError_t ea_gemm_launch_big_bf16(const ea::GroupArgs* ga, hipStream_t s);
 hipError_t ea_gemm_launch_f32(const ea::GroupArgs* ga, int cfg, hipStream_t s);
 hipError_t ea_gemm_table_lat_bf16(const ea::TableArgs* ta, int dw, hipStream_t s);
 hipError_t ea_gemm_table_f32(const ea::TableArgs* ta, int dw, hipStream_t s);
 void ea_gemm_init_lat_bf16();
 void ea_gemm_init_thr_bf16();
 void ea_gemm_init_thr64_bf16();
+void ea_gemm_init_big_bf16();
 void ea_gemm_init_f32();
 }
 
 // cfg: 0 = LAT (64x32, split-K 4), 1 = THR (128x128), 2 = THR-N64 (128x64: twice the
-// workgroups for grids that would otherwise leave CUs with a single workgroup)
+// workgroups for grids that would otherwise leave CUs with a single workgroup),
+// 4 = BIG (256x256, 8 ping-pong waves, bf16 only: gemm_big.h)
 extern "C" hipError_t ea_gemm_grouped(const ea::GroupArgs* ga, int bf16, int cfg, hipStream_t s) {
   using namespace ea;
   if (ga->total_blocks <= 0) return hipSuccess;
@@ -30,7 +33,8 @@ extern "C" hipError_t ea_gemm_grouped(const ea::GroupArgs* ga, int bf16, int cfg
       hipLaunchKernelGGL(loss_rows_kernel<float>, dim3(ga->R, ga->total_blocks), dim3(256), lds, s, *ga);
     return hipGetLastError();
   }
-  if (!bf16) return ea_gemm_launch_f32(ga, cfg, s);
+  if (!bf16) return ea_gemm_launch_f32(ga, cfg == 4 ? 1 : cfg, s);
+  if (cfg == 4) return ea_gemm_launch_big_bf16(ga, s);
   if (cfg == 0) return ea_gemm_launch_lat_bf16(ga, s);
   if (cfg == 2) return ea_gemm_launch_thr64_bf16(ga, s);
   return ea_gemm_launch_thr_bf16(ga, s);
@@ -48,12 +52,15 @@ extern "C" void ea_gemm_init() {
   ea_gemm_init_lat_bf16();
   ea_gemm_init_thr_bf16();
   ea_gemm_init_thr64_bf16();
+  ea_gemm_init_big_bf16();
   ea_gemm_init_f32();
   done = true;
 }
 
 // cfg 3: the 64x64 tile of the row-chain weight-gradient table launch (not a
 // grouped-launch config)
-extern "C" int ea_gemm_tile_m(int cfg) { return (cfg == 0 || cfg == 3) ? 64 : 128; }
-extern "C" int ea_gemm_tile_n(int cfg) { return cfg == 0 ? 32 : ((cfg == 2 || cfg == 3) ? 64 : 128); }
+extern "C" int ea_gemm_tile_m(int cfg) { return cfg == 4 ? 256 : ((cfg == 0 || cfg == 3) ? 64 : 128); }
+extern "C" int ea_gemm_tile_n(int cfg) {
+  return cfg == 4 ? 256 : (cfg == 0 ? 32 : ((cfg == 2 || cfg == 3) ? 64 : 128));
+}
 extern "C" int ea_gather_tile() { return 64; }

@@ -1,0 +1,37 @@
+// Grouped GEMM instantiation: the 256x256 8-wave ping-pong tile (gemm_big.h), bf16,
+// one variant per kind set a launch can hold.
+#include "gemm_big.h"
+
+namespace ea {
+template <unsigned KM0, unsigned KM1>
+static bool big_if(const GroupArgs& ga, hipStream_t s, hipError_t& e) {
+  if (!(KM0 & KB(ga.p[0].kind))) return false;
+  if (ga.nprob > 1 && !(KM1 & KB(ga.p[1].kind))) return false;
+  hipLaunchKernelGGL((gemm_big<KM0, KM1>), dim3(ga.R, ga.total_blocks), dim3(BIG_NT), BIG_LDS, s, ga);
+  e = hipGetLastError();
+  return true;
+}
+template <unsigned KM0, unsigned KM1> static void big_attr() {
+  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_big<KM0, KM1>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, BIG_LDS);
+}
+constexpr unsigned KM_PLAIN_ = KB(PK_PLAIN);
+}  // namespace ea
+
+extern "C" hipError_t ea_gemm_launch_big_bf16(const ea::GroupArgs* ga, hipStream_t s) {
+  using namespace ea;
+  if (ga->total_blocks <= 0) return hipSuccess;
+  hipError_t e = hipSuccess;
+  if (big_if<KM_PLAIN_, KM_NONE>(*ga, s, e) || big_if<KM_FWD, KM_NONE>(*ga, s, e) ||
+      big_if<KM_DW, KM_DX>(*ga, s, e) || big_if<KM_DX, KM_NONE>(*ga, s, e))
+    return e;
+  return hipErrorInvalidValue;  // a kind the big tile has no epilogue for (loss, gather, split-K)
+}
+
+extern "C" void ea_gemm_init_big_bf16() {
+  using namespace ea;
+  big_attr<KM_PLAIN_, KM_NONE>();
+  big_attr<KM_FWD, KM_NONE>();
+  big_attr<KM_DW, KM_DX>();
+  big_attr<KM_DX, KM_NONE>();
+}

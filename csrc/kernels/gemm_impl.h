@@ -462,7 +462,6 @@ __device__ __forceinline__ void thr_lds_mainloop(const __bf16* const (&arow_ld)[
   __syncthreads();  // the epilogue reuses the staging LDS
 }
 
-// --------------------------------------------------------------- the kernel
 // KM: bit k set = problem kind k can occur in this instantiation; the other
 // kinds' epilogues are compiled out (smaller code per launch, see launch_cfg).
 constexpr unsigned KM_ALL = 0x1ffu;  // every ProbKind (0..8, args.h)
@@ -473,6 +472,325 @@ constexpr unsigned KM_FWD = KB(PK_FWD), KM_GATHER = KB(PK_GATHER_T);
 constexpr unsigned KM_LOSS = KB(PK_FWD_LOSS);
 constexpr unsigned KM_DW = KB(PK_DW_UPDATE) | KB(PK_DW_GRAD), KM_DX = KB(PK_DX);
 constexpr unsigned KM_PARTIAL = KB(PK_PARTIAL);
+
+// ------------------------------------------------------------- epilogues
+// The fused Dense-layer epilogues over a finished fp32 C tile [BM][BN + 4] in LDS
+// (tile rows m0.., columns n0.. of problem p), run by NT threads: each thread owns
+// 8 contiguous columns of one row per pass. Shared by the 256-thread tiles of
+// run_prob and the 512-thread 256x256 tile (gemm_big.h, two 128-row halves).
+// PFP / DW_PF: optimizer operands the caller prefetched before its main loop.
+template <typename T, int BM, int BN, int NT, unsigned KM, int PFP, bool DW_PF, typename GA>
+__device__ __forceinline__ void tile_epilogue(const GA& ga, const Prob& p, const int r, const int m0, const int n0,
+                                              const int kch, const int valid, const long long iter,
+                                              const long long step, const bool skip_update, float* smem,
+                                              const bool (&pf_vec)[PFP], const float (&pf_w)[PFP][8],
+                                              const float (&pf_s0)[PFP][8], const float (&pf_s1)[PFP][8]) {
+  constexpr int LDC = BN + 4;
+  constexpr int CPR = BN / 8;   // 8-column chunks per row
+  constexpr int RPP = NT / CPR; // rows per pass
+  constexpr int PASSES = BM / RPP;
+  static_assert(PASSES * RPP == BM, "epilogue passes");
+  // 512-thread tiles run the epilogue with the other half's accumulators still live
+  // (gemm_big.h): passes stay rolled so the epilogue fits the remaining registers
+  constexpr int EUNR = NT == 256 ? PASSES : 1;
+  const int t_row = threadIdx.x / CPR, t_c0 = (threadIdx.x % CPR) * 8;
+  (void)step; (void)kch; (void)valid; (void)iter; (void)skip_update; (void)pf_vec;
+  float* C = smem;  // final tile [BM][LDC]
+  stamp(ga, 3);
+
+  // Epilogue thread mapping: each thread owns 8 contiguous columns of one row
+  // per pass and issues all of its global loads before any store, so the
+  // loads of a pass overlap instead of serialising behind possibly-aliasing
+  // stores.
+  auto lds8 = [&](int row, int c0, float (&v)[8]) {
+    const float4 a = *reinterpret_cast<const float4*>(C + row * LDC + c0);
+    const float4 b = *reinterpret_cast<const float4*>(C + row * LDC + c0 + 4);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+  };
+  auto sts8 = [&](int row, int c0, const float (&v)[8]) {
+    *reinterpret_cast<float4*>(C + row * LDC + c0) = make_float4(v[0], v[1], v[2], v[3]);
+    *reinterpret_cast<float4*>(C + row * LDC + c0 + 4) = make_float4(v[4], v[5], v[6], v[7]);
+  };
+  // transposed store of the tile (D^T, dZ^T, W^T): each thread moves 8 consecutive
+  // rows of one column (8 LDS reads -> one 16-byte bf16 store, or two for fp32);
+  // the BM/8 threads of a column are consecutive, so a column's rows are one
+  // contiguous run in memory. Every destination here has ld % 8 == 0 and an
+  // 8-element-aligned base (Bp / Kp padding), checked on the host.
+  auto store_transposed = [&](void* base, long long off, long long ld, int nrows) {
+    constexpr int RC = BM / 8;  // 8-row chunks per column
+    for (int e = threadIdx.x; e < RC * BN; e += NT) {
+      const int rc = e % RC, col = e / RC, row = rc * 8, gm = m0 + row, gn = n0 + col;
+      if (gn >= p.N || gm >= nrows) continue;
+      float v[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v[q] = C[(row + q) * LDC + col];
+      const long long idx = off + (long long)gn * ld + gm;
+      if (gm + 8 <= nrows) {
+        st8<T>(base, idx, v);
+      } else {
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+          if (gm + q < nrows) st<T>(base, idx + q, v[q]);
+      }
+    }
+  };
+
+  switch (p.kind) {
+    case PK_PARTIAL: {
+      if constexpr (!(KM & KB(PK_PARTIAL))) break;
+      // raw fp32 slab of this K chunk; rows past the valid batch are zero (masked A)
+      float* out = reinterpret_cast<float*>(p.D) + (long long)r * p.sD + (long long)kch * p.sPart;
+#pragma unroll EUNR
+      for (int ps = 0; ps < PASSES; ++ps) {
+        const int row = ps * RPP + t_row, gm = m0 + row, gn0 = n0 + t_c0;
+        if (gm >= p.M || gn0 >= p.N) continue;
+        float v[8];
+        lds8(row, t_c0, v);
+        if (gn0 + 8 <= p.N && (p.ldd & 3) == 0) {
+          st8f(out + (long long)gm * p.ldd + gn0, v);
+        } else {
+#pragma unroll
+          for (int q = 0; q < 8; ++q)
+            if (gn0 + q < p.N) out[(long long)gm * p.ldd + gn0 + q] = v[q];
+        }
+      }
+      break;
+    }
+    case PK_PLAIN: {
+      if constexpr (!(KM & KB(PK_PLAIN))) break;
+      float* out = reinterpret_cast<float*>(p.D) + (long long)r * p.sD;
+#pragma unroll EUNR
+      for (int ps = 0; ps < PASSES; ++ps) {
+        const int row = ps * RPP + t_row, gm = m0 + row, gn0 = n0 + t_c0;
+        if (gm >= p.M) continue;
+        float v[8];
+        lds8(row, t_c0, v);
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+          if (gn0 + q < p.N) out[(long long)gm * p.ldd + gn0 + q] = v[q];
+      }
+      break;
+    }
+    case PK_FWD:
+    case PK_DX: {
+      if constexpr (!(KM & (KB(PK_FWD) | KB(PK_DX)))) break;
+      const bool fwd = p.kind == PK_FWD;
+      const float* __restrict__ bias = fwd && p.bias ? p.bias + (long long)r * p.sBias : nullptr;
+      float* __restrict__ Z = p.Z ? p.Z + (long long)r * p.sZ : nullptr;
+      const float keep_scale = p.rate > 0.f ? 1.f / (1.f - p.rate) : 1.f;
+      const bool drop = p.rate > 0.f && !p.eval_mode;
+#pragma unroll EUNR
+      for (int ps = 0; ps < PASSES; ++ps) {
+        const int row = ps * RPP + t_row, gm = m0 + row, gn0 = n0 + t_c0;
+        if (gm >= p.M || gn0 >= p.N) continue;
+        const bool rv = gm < valid;
+        float v[8], aux[8], zv[8], out[8], u[8];
+        lds8(row, t_c0, v);
+        if (drop) {  // t_c0 is a multiple of 8
+          dropout_u8(dropout_base(ga.seed, r, p.layer, iter), gm, gn0, u);
+        } else {
+#pragma unroll
+          for (int q = 0; q < 8; ++q) u[q] = 1.f;
+        }
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {  // loads first
+          const bool in = gn0 + q < p.N;
+          if (fwd) aux[q] = (bias && in) ? bias[gn0 + q] : 0.f;
+          else aux[q] = (in && rv) ? Z[(long long)gm * p.ldz + gn0 + q] : 0.f;
+        }
+        float av[8];
+        if (fwd) {
+#pragma unroll
+          for (int q = 0; q < 8; ++q) zv[q] = v[q] + aux[q];
+          act_f_v<8>(p.act, zv, av);
+        } else {
+          act_g_v<8>(p.act, aux, av);
+        }
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const bool live = gn0 + q < p.N && rv;
+          const bool keep = live && u[q] >= p.rate;
+          if (!live) zv[q] = 0.f;
+          out[q] = keep ? (fwd ? av[q] : v[q] * av[q]) * keep_scale : 0.f;
+        }
+        if (ps == 0) stamp(ga, 5);
+        if (fwd && Z) {
+#pragma unroll
+          for (int q = 0; q < 8; ++q)
+            if (gn0 + q < p.N) Z[(long long)gm * p.ldz + gn0 + q] = zv[q];
+        }
+        if (p.D) st8<T>(p.D, (long long)r * p.sD + (long long)gm * p.ldd + gn0, out);
+        sts8(row, t_c0, out);
+      }
+      stamp(ga, 6);
+      if (p.DT) {
+        __syncthreads();
+        stamp(ga, 7);
+        store_transposed(p.DT, (long long)r * p.sDT, p.lddt, p.M);
+      }
+      break;
+    }
+    case PK_FWD_LOSS: {
+      if constexpr ((KM & KB(PK_FWD_LOSS)) != 0u && NT == 256) {
+      // whole rows live in this tile (N <= BN, tiles_n == 1)
+      const float* __restrict__ bias = p.bias ? p.bias + (long long)r * p.sBias : nullptr;
+      int* srow = reinterpret_cast<int*>(smem + BM * LDC);   // data row of each tile row
+      float* Ys = smem + BM * LDC + BM;                       // staged targets [BM][BN]
+#pragma unroll EUNR
+      for (int ps = 0; ps < PASSES; ++ps) {
+        const int row = ps * RPP + t_row, gn0 = t_c0;
+        if (gn0 >= p.N) continue;
+        float v[8], b[8];
+        lds8(row, t_c0, v);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) b[q] = (bias && gn0 + q < p.N) ? bias[gn0 + q] : 0.f;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] += b[q];
+        sts8(row, t_c0, v);
+      }
+      stamp(ga, 5);
+      const int ldy = p.Y ? (int)p.ldy : 0;
+      for (int row = threadIdx.x; row < BM; row += NT) {
+        const int gm = m0 + row;
+        srow[row] = (gm < p.M && gm < valid) ? (int)batch_row(p, r, step, gm) : -1;
+      }
+      __syncthreads();
+      if (p.Y) {
+        const float* Yb = p.Y + (long long)r * p.sY;
+        for (int e = threadIdx.x; e < BM * ldy; e += NT) {
+          const int row = e / ldy, j = e % ldy;
+          const int dr = srow[row];
+          Ys[row * BN + j] = dr >= 0 ? Yb[(long long)dr * ldy + j] : 0.f;
+        }
+      }
+      __syncthreads();
+      stamp(ga, 6);
+      const bool train = !p.eval_mode && p.D;
+      const float inv_valid = valid > 0 ? 1.f / (float)valid : 0.f;
+      float sums[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      if (softmax_cce_fast(p)) {
+        if (p.N <= 16) loss_tile_cce<4, BM, LDC, BN>(p, r, m0, C, Ys, srow, train, inv_valid, sums);
+        else loss_tile_cce<8, BM, LDC, BN>(p, r, m0, C, Ys, srow, train, inv_valid, sums);
+      } else {
+        loss_tile_lds<BM, LDC, BN>(p, r, m0, C, Ys, srow, train, inv_valid, sums);
+      }
+      stamp(ga, 7);
+      if (p.acc && p.Y) {
+#pragma unroll
+        for (int q = 0; q < 6; ++q) {
+          if (q < 2 + p.nmet) {
+            const float s = row_sum<64>(sums[q]);
+            if ((threadIdx.x & 63) == 0 && s != 0.f)
+              atomicAdd(p.acc + (long long)r * p.acc_stride + q, (double)s);
+          }
+        }
+      }
+      stamp(ga, 8);
+      if (train) {
+        __syncthreads();  // dz rows were produced by lane groups
+#pragma unroll EUNR
+        for (int ps = 0; ps < PASSES; ++ps) {
+          const int row = ps * RPP + t_row, gm = m0 + row, gn0 = t_c0;
+          if (gm >= p.M || gn0 >= p.N) continue;
+          float v[8];
+          lds8(row, t_c0, v);
+#pragma unroll
+          for (int q = 0; q < 8; ++q)
+            if (gn0 + q >= p.N) v[q] = 0.f;
+          st8<T>(p.D, (long long)r * p.sD + (long long)gm * p.ldd + gn0, v);
+        }
+        if (p.DT) store_transposed(p.DT, (long long)r * p.sDT, p.lddt, p.M);
+      }
+      }  // if constexpr
+      break;
+    }
+    case PK_DW_UPDATE:
+    case PK_DW_GRAD: {
+      if constexpr (!(KM & (KB(PK_DW_UPDATE) | KB(PK_DW_GRAD)))) break;
+      if (skip_update) break;
+      const bool upd = p.kind == PK_DW_UPDATE;
+      float* __restrict__ P = p.P + (long long)r * p.sP;
+      float* __restrict__ S = p.S ? p.S + (long long)r * p.sS : nullptr;
+      float* __restrict__ G = p.G ? p.G + (long long)r * p.sG : nullptr;
+      const long long wpar = ((iter + 1) & 1);
+      const int krows = p.ones_row >= 0 ? p.ones_row : p.M;
+      const int np = S ? opt_planes(p.op) : 0;
+#pragma unroll EUNR
+      for (int ps = 0; ps < PASSES; ++ps) {
+        const int row = ps * RPP + t_row, gm = m0 + row, gn0 = n0 + t_c0;
+        if (gm >= p.M || gn0 >= p.N) continue;
+        float v[8];
+        lds8(row, t_c0, v);
+        const long long pidx = p.p_off + (long long)gm * p.N + gn0;
+        if (!upd) {
+#pragma unroll
+          for (int q = 0; q < 8; ++q)
+            if (gn0 + q < p.N) G[pidx + q] = valid > 0 ? v[q] * p.op.grad_scale : 0.f;
+          continue;
+        }
+        float w[8], s0[8], s1[8];
+        // whole 16-byte-aligned chunks (the common case) move as float4 pairs
+        const bool vec = gn0 + 8 <= p.N && (pidx & 3) == 0 && (p.op.s_plane & 3) == 0;
+        if (DW_PF && pf_vec[DW_PF ? ps : 0]) {
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            w[q] = pf_w[DW_PF ? ps : 0][q];
+            s0[q] = pf_s0[DW_PF ? ps : 0][q];
+            s1[q] = pf_s1[DW_PF ? ps : 0][q];
+          }
+        } else if (vec) {
+          ld8f(P + pidx, w);
+          if (np > 0) ld8f(S + pidx, s0); else zero8(s0);
+          if (np > 1) ld8f(S + p.op.s_plane + pidx, s1); else zero8(s1);
+        } else {
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {  // loads first
+            const bool in = gn0 + q < p.N;
+            w[q] = in ? P[pidx + q] : 0.f;
+            s0[q] = (in && np > 0) ? S[pidx + q] : 0.f;
+            s1[q] = (in && np > 1) ? S[p.op.s_plane + pidx + q] : 0.f;
+          }
+        }
+        {
+          float gq[8];
+#pragma unroll
+          for (int q = 0; q < 8; ++q) gq[q] = v[q] * p.op.grad_scale;
+          opt_update_v<8>(p.op, w, gq, s0, s1, iter);  // lanes past N are discarded below
+        }
+        if (ps == 0) stamp(ga, 5);
+        if (vec) {
+          st8f(P + pidx, w);
+          if (np > 0) st8f(S + pidx, s0);
+          if (np > 1) st8f(S + p.op.s_plane + pidx, s1);
+        } else {
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            if (gn0 + q < p.N) {
+              P[pidx + q] = w[q];
+              if (np > 0) S[pidx + q] = s0[q];
+              if (np > 1) S[p.op.s_plane + pidx + q] = s1[q];
+            } else {
+              w[q] = 0.f;
+            }
+          }
+        }
+        if (p.Wsh && gm < krows)
+          st8<T>(p.Wsh, (long long)r * p.sWsh + wpar * p.wsh_par + (long long)gm * p.ldwsh + gn0, w);
+        sts8(row, t_c0, w);
+      }
+      stamp(ga, 6);
+      if (upd && p.WTsh) {
+        __syncthreads();
+        stamp(ga, 7);
+        store_transposed(p.WTsh, (long long)r * p.sWTsh + wpar * p.wtsh_par, p.ldwtsh, krows);
+        stamp(ga, 8);
+      }
+      break;
+    }
+  }
+}
+
+// --------------------------------------------------------------- the kernel
 
 // PF_: k-steps of fragments in flight per wave in the register-direct loop (0 = by
 // tile size); the weight-gradient table launch (K = batch: one or two k-steps per
@@ -711,298 +1029,8 @@ __device__ __forceinline__ void run_prob(const GA& ga, const Prob& p, const int 
       }
       __syncthreads();
     }
-    float* C = smem;  // final tile [BM][LDC]
-    stamp(ga, 3);
-
-    // Epilogue thread mapping: each thread owns 8 contiguous columns of one row
-    // per pass and issues all of its global loads before any store, so the
-    // loads of a pass overlap instead of serialising behind possibly-aliasing
-    // stores.
-    auto lds8 = [&](int row, int c0, float (&v)[8]) {
-      const float4 a = *reinterpret_cast<const float4*>(C + row * LDC + c0);
-      const float4 b = *reinterpret_cast<const float4*>(C + row * LDC + c0 + 4);
-      v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
-    };
-    auto sts8 = [&](int row, int c0, const float (&v)[8]) {
-      *reinterpret_cast<float4*>(C + row * LDC + c0) = make_float4(v[0], v[1], v[2], v[3]);
-      *reinterpret_cast<float4*>(C + row * LDC + c0 + 4) = make_float4(v[4], v[5], v[6], v[7]);
-    };
-    // transposed store of the tile (D^T, dZ^T, W^T): each thread moves 8 consecutive
-    // rows of one column (8 LDS reads -> one 16-byte bf16 store, or two for fp32);
-    // the BM/8 threads of a column are consecutive, so a column's rows are one
-    // contiguous run in memory. Every destination here has ld % 8 == 0 and an
-    // 8-element-aligned base (Bp / Kp padding), checked on the host.
-    auto store_transposed = [&](void* base, long long off, long long ld, int nrows) {
-      constexpr int RC = BM / 8;  // 8-row chunks per column
-      for (int e = threadIdx.x; e < RC * BN; e += 256) {
-        const int rc = e % RC, col = e / RC, row = rc * 8, gm = m0 + row, gn = n0 + col;
-        if (gn >= p.N || gm >= nrows) continue;
-        float v[8];
-#pragma unroll
-        for (int q = 0; q < 8; ++q) v[q] = C[(row + q) * LDC + col];
-        const long long idx = off + (long long)gn * ld + gm;
-        if (gm + 8 <= nrows) {
-          st8<T>(base, idx, v);
-        } else {
-#pragma unroll
-          for (int q = 0; q < 8; ++q)
-            if (gm + q < nrows) st<T>(base, idx + q, v[q]);
-        }
-      }
-    };
-
-    switch (p.kind) {
-      case PK_PARTIAL: {
-        if constexpr (!(KM & KB(PK_PARTIAL))) break;
-        // raw fp32 slab of this K chunk; rows past the valid batch are zero (masked A)
-        float* out = reinterpret_cast<float*>(p.D) + (long long)r * p.sD + (long long)kch * p.sPart;
-#pragma unroll
-        for (int ps = 0; ps < PASSES; ++ps) {
-          const int row = ps * RPP + t_row, gm = m0 + row, gn0 = n0 + t_c0;
-          if (gm >= p.M || gn0 >= p.N) continue;
-          float v[8];
-          lds8(row, t_c0, v);
-          if (gn0 + 8 <= p.N && (p.ldd & 3) == 0) {
-            st8f(out + (long long)gm * p.ldd + gn0, v);
-          } else {
-#pragma unroll
-            for (int q = 0; q < 8; ++q)
-              if (gn0 + q < p.N) out[(long long)gm * p.ldd + gn0 + q] = v[q];
-          }
-        }
-        break;
-      }
-      case PK_PLAIN: {
-        if constexpr (!(KM & KB(PK_PLAIN))) break;
-        float* out = reinterpret_cast<float*>(p.D) + (long long)r * p.sD;
-#pragma unroll
-        for (int ps = 0; ps < PASSES; ++ps) {
-          const int row = ps * RPP + t_row, gm = m0 + row, gn0 = n0 + t_c0;
-          if (gm >= p.M) continue;
-          float v[8];
-          lds8(row, t_c0, v);
-#pragma unroll
-          for (int q = 0; q < 8; ++q)
-            if (gn0 + q < p.N) out[(long long)gm * p.ldd + gn0 + q] = v[q];
-        }
-        break;
-      }
-      case PK_FWD:
-      case PK_DX: {
-        if constexpr (!(KM & (KB(PK_FWD) | KB(PK_DX)))) break;
-        const bool fwd = p.kind == PK_FWD;
-        const float* __restrict__ bias = fwd && p.bias ? p.bias + (long long)r * p.sBias : nullptr;
-        float* __restrict__ Z = p.Z ? p.Z + (long long)r * p.sZ : nullptr;
-        const float keep_scale = p.rate > 0.f ? 1.f / (1.f - p.rate) : 1.f;
-        const bool drop = p.rate > 0.f && !p.eval_mode;
-#pragma unroll
-        for (int ps = 0; ps < PASSES; ++ps) {
-          const int row = ps * RPP + t_row, gm = m0 + row, gn0 = n0 + t_c0;
-          if (gm >= p.M || gn0 >= p.N) continue;
-          const bool rv = gm < valid;
-          float v[8], aux[8], zv[8], out[8], u[8];
-          lds8(row, t_c0, v);
-          if (drop) {  // t_c0 is a multiple of 8
-            dropout_u8(dropout_base(ga.seed, r, p.layer, iter), gm, gn0, u);
-          } else {
-#pragma unroll
-            for (int q = 0; q < 8; ++q) u[q] = 1.f;
-          }
-#pragma unroll
-          for (int q = 0; q < 8; ++q) {  // loads first
-            const bool in = gn0 + q < p.N;
-            if (fwd) aux[q] = (bias && in) ? bias[gn0 + q] : 0.f;
-            else aux[q] = (in && rv) ? Z[(long long)gm * p.ldz + gn0 + q] : 0.f;
-          }
-          float av[8];
-          if (fwd) {
-#pragma unroll
-            for (int q = 0; q < 8; ++q) zv[q] = v[q] + aux[q];
-            act_f_v<8>(p.act, zv, av);
-          } else {
-            act_g_v<8>(p.act, aux, av);
-          }
-#pragma unroll
-          for (int q = 0; q < 8; ++q) {
-            const bool live = gn0 + q < p.N && rv;
-            const bool keep = live && u[q] >= p.rate;
-            if (!live) zv[q] = 0.f;
-            out[q] = keep ? (fwd ? av[q] : v[q] * av[q]) * keep_scale : 0.f;
-          }
-          if (ps == 0) stamp(ga, 5);
-          if (fwd && Z) {
-#pragma unroll
-            for (int q = 0; q < 8; ++q)
-              if (gn0 + q < p.N) Z[(long long)gm * p.ldz + gn0 + q] = zv[q];
-          }
-          if (p.D) st8<T>(p.D, (long long)r * p.sD + (long long)gm * p.ldd + gn0, out);
-          sts8(row, t_c0, out);
-        }
-        stamp(ga, 6);
-        if (p.DT) {
-          __syncthreads();
-          stamp(ga, 7);
-          store_transposed(p.DT, (long long)r * p.sDT, p.lddt, p.M);
-        }
-        break;
-      }
-      case PK_FWD_LOSS: {
-        if constexpr (!(KM & KB(PK_FWD_LOSS))) break;
-        // whole rows live in this tile (N <= BN, tiles_n == 1)
-        const float* __restrict__ bias = p.bias ? p.bias + (long long)r * p.sBias : nullptr;
-        int* srow = reinterpret_cast<int*>(smem + BM * LDC);   // data row of each tile row
-        float* Ys = smem + BM * LDC + BM;                       // staged targets [BM][BN]
-#pragma unroll
-        for (int ps = 0; ps < PASSES; ++ps) {
-          const int row = ps * RPP + t_row, gn0 = t_c0;
-          if (gn0 >= p.N) continue;
-          float v[8], b[8];
-          lds8(row, t_c0, v);
-#pragma unroll
-          for (int q = 0; q < 8; ++q) b[q] = (bias && gn0 + q < p.N) ? bias[gn0 + q] : 0.f;
-#pragma unroll
-          for (int q = 0; q < 8; ++q) v[q] += b[q];
-          sts8(row, t_c0, v);
-        }
-        stamp(ga, 5);
-        const int ldy = p.Y ? (int)p.ldy : 0;
-        for (int row = threadIdx.x; row < BM; row += 256) {
-          const int gm = m0 + row;
-          srow[row] = (gm < p.M && gm < valid) ? (int)batch_row(p, r, step, gm) : -1;
-        }
-        __syncthreads();
-        if (p.Y) {
-          const float* Yb = p.Y + (long long)r * p.sY;
-          for (int e = threadIdx.x; e < BM * ldy; e += 256) {
-            const int row = e / ldy, j = e % ldy;
-            const int dr = srow[row];
-            Ys[row * BN + j] = dr >= 0 ? Yb[(long long)dr * ldy + j] : 0.f;
-          }
-        }
-        __syncthreads();
-        stamp(ga, 6);
-        const bool train = !p.eval_mode && p.D;
-        const float inv_valid = valid > 0 ? 1.f / (float)valid : 0.f;
-        float sums[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-        if (softmax_cce_fast(p)) {
-          if (p.N <= 16) loss_tile_cce<4, BM, LDC, BN>(p, r, m0, C, Ys, srow, train, inv_valid, sums);
-          else loss_tile_cce<8, BM, LDC, BN>(p, r, m0, C, Ys, srow, train, inv_valid, sums);
-        } else {
-          loss_tile_lds<BM, LDC, BN>(p, r, m0, C, Ys, srow, train, inv_valid, sums);
-        }
-        stamp(ga, 7);
-        if (p.acc && p.Y) {
-#pragma unroll
-          for (int q = 0; q < 6; ++q) {
-            if (q < 2 + p.nmet) {
-              const float s = row_sum<64>(sums[q]);
-              if ((threadIdx.x & 63) == 0 && s != 0.f)
-                atomicAdd(p.acc + (long long)r * p.acc_stride + q, (double)s);
-            }
-          }
-        }
-        stamp(ga, 8);
-        if (train) {
-          __syncthreads();  // dz rows were produced by lane groups
-#pragma unroll
-          for (int ps = 0; ps < PASSES; ++ps) {
-            const int row = ps * RPP + t_row, gm = m0 + row, gn0 = t_c0;
-            if (gm >= p.M || gn0 >= p.N) continue;
-            float v[8];
-            lds8(row, t_c0, v);
-#pragma unroll
-            for (int q = 0; q < 8; ++q)
-              if (gn0 + q >= p.N) v[q] = 0.f;
-            st8<T>(p.D, (long long)r * p.sD + (long long)gm * p.ldd + gn0, v);
-          }
-          if (p.DT) store_transposed(p.DT, (long long)r * p.sDT, p.lddt, p.M);
-        }
-        break;
-      }
-      case PK_DW_UPDATE:
-      case PK_DW_GRAD: {
-        if constexpr (!(KM & (KB(PK_DW_UPDATE) | KB(PK_DW_GRAD)))) break;
-        if (skip_update) break;
-        const bool upd = p.kind == PK_DW_UPDATE;
-        float* __restrict__ P = p.P + (long long)r * p.sP;
-        float* __restrict__ S = p.S ? p.S + (long long)r * p.sS : nullptr;
-        float* __restrict__ G = p.G ? p.G + (long long)r * p.sG : nullptr;
-        const long long wpar = ((iter + 1) & 1);
-        const int krows = p.ones_row >= 0 ? p.ones_row : p.M;
-        const int np = S ? opt_planes(p.op) : 0;
-#pragma unroll
-        for (int ps = 0; ps < PASSES; ++ps) {
-          const int row = ps * RPP + t_row, gm = m0 + row, gn0 = n0 + t_c0;
-          if (gm >= p.M || gn0 >= p.N) continue;
-          float v[8];
-          lds8(row, t_c0, v);
-          const long long pidx = p.p_off + (long long)gm * p.N + gn0;
-          if (!upd) {
-#pragma unroll
-            for (int q = 0; q < 8; ++q)
-              if (gn0 + q < p.N) G[pidx + q] = valid > 0 ? v[q] * p.op.grad_scale : 0.f;
-            continue;
-          }
-          float w[8], s0[8], s1[8];
-          // whole 16-byte-aligned chunks (the common case) move as float4 pairs
-          const bool vec = gn0 + 8 <= p.N && (pidx & 3) == 0 && (p.op.s_plane & 3) == 0;
-          if (DW_PF && pf_vec[DW_PF ? ps : 0]) {
-#pragma unroll
-            for (int q = 0; q < 8; ++q) {
-              w[q] = pf_w[DW_PF ? ps : 0][q];
-              s0[q] = pf_s0[DW_PF ? ps : 0][q];
-              s1[q] = pf_s1[DW_PF ? ps : 0][q];
-            }
-          } else if (vec) {
-            ld8f(P + pidx, w);
-            if (np > 0) ld8f(S + pidx, s0); else zero8(s0);
-            if (np > 1) ld8f(S + p.op.s_plane + pidx, s1); else zero8(s1);
-          } else {
-#pragma unroll
-            for (int q = 0; q < 8; ++q) {  // loads first
-              const bool in = gn0 + q < p.N;
-              w[q] = in ? P[pidx + q] : 0.f;
-              s0[q] = (in && np > 0) ? S[pidx + q] : 0.f;
-              s1[q] = (in && np > 1) ? S[p.op.s_plane + pidx + q] : 0.f;
-            }
-          }
-          {
-            float gq[8];
-#pragma unroll
-            for (int q = 0; q < 8; ++q) gq[q] = v[q] * p.op.grad_scale;
-            opt_update_v<8>(p.op, w, gq, s0, s1, iter);  // lanes past N are discarded below
-          }
-          if (ps == 0) stamp(ga, 5);
-          if (vec) {
-            st8f(P + pidx, w);
-            if (np > 0) st8f(S + pidx, s0);
-            if (np > 1) st8f(S + p.op.s_plane + pidx, s1);
-          } else {
-#pragma unroll
-            for (int q = 0; q < 8; ++q) {
-              if (gn0 + q < p.N) {
-                P[pidx + q] = w[q];
-                if (np > 0) S[pidx + q] = s0[q];
-                if (np > 1) S[p.op.s_plane + pidx + q] = s1[q];
-              } else {
-                w[q] = 0.f;
-              }
-            }
-          }
-          if (p.Wsh && gm < krows)
-            st8<T>(p.Wsh, (long long)r * p.sWsh + wpar * p.wsh_par + (long long)gm * p.ldwsh + gn0, w);
-          sts8(row, t_c0, w);
-        }
-        stamp(ga, 6);
-        if (upd && p.WTsh) {
-          __syncthreads();
-          stamp(ga, 7);
-          store_transposed(p.WTsh, (long long)r * p.sWTsh + wpar * p.wtsh_par, p.ldwtsh, krows);
-          stamp(ga, 8);
-        }
-        break;
-      }
-    }
+    tile_epilogue<T, BM, BN, 256, KM, PFP, DW_PF>(ga, p, r, m0, n0, kch, valid, iter, step, skip_update, smem, pf_vec,
+                                                pf_w, pf_s0, pf_s1);
   }
 
 }

@@ -189,7 +189,7 @@ PYBIND11_MODULE(_C, m) {
     // 16-byte aligned and K padded to whole chunks, or it reads out of bounds
     const int epl = bf16 ? 8 : 4;
     if (M <= 0 || N <= 0 || K <= 0 || (K % epl) || (lda % epl) || (ldb % epl) || lda < K || ldb < K || ldc < N ||
-        (A % 16) || (BT % 16) || (C % 4) || cfg < 0 || cfg > 2)
+        (A % 16) || (BT % 16) || (C % 4) || cfg < 0 || cfg > 4 || cfg == 3)
       throw std::invalid_argument("gemm_nt: K, lda, ldb must be multiples of 16 bytes, pointers 16-byte aligned");
     ea_gemm_init();
     GroupArgs ga;

@@ -24,6 +24,7 @@ SOURCES = [
     "kernels/gemm_cfg0_bf16.hip",
     "kernels/gemm_cfg1_bf16.hip",
     "kernels/gemm_cfg2_bf16.hip",
+    "kernels/gemm_big_bf16.hip",
     "kernels/gemm_f32.hip",
     "kernels/flat.hip",
     "kernels/rowchain.hip",
