@@ -490,9 +490,9 @@ __device__ __forceinline__ void tile_epilogue(const GA& ga, const Prob& p, const
   constexpr int RPP = NT / CPR; // rows per pass
   constexpr int PASSES = BM / RPP;
   static_assert(PASSES * RPP == BM, "epilogue passes");
-  // 512-thread tiles run the epilogue with the other half's accumulators still live
+  // the 256x256 tile runs the epilogue with the other half's accumulators still live
   // (gemm_big.h): passes stay rolled so the epilogue fits the remaining registers
-  constexpr int EUNR = NT == 256 ? PASSES : 1;
+  constexpr int EUNR = (NT == 256 && BM * BN <= 128 * 128) ? PASSES : 1;
   const int t_row = threadIdx.x / CPR, t_c0 = (threadIdx.x % CPR) * 8;
   (void)step; (void)kch; (void)valid; (void)iter; (void)skip_update; (void)pf_vec;
   float* C = smem;  // final tile [BM][LDC]

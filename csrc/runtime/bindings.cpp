@@ -66,6 +66,7 @@ static ExecCfg parse_cfg(const py::dict& d) {
   c.bf16 = get<int>(d, "bf16", 1);
   c.seed = get<unsigned long long>(d, "seed", 0);
   c.force_cfg = get<int>(d, "force_cfg", -1);
+  c.big = get<int>(d, "big", 0);
   c.thr_min_k = get<int>(d, "thr_min_k", 64);
   c.thr_min_n = get<int>(d, "thr_min_n", 256);
   c.rowchain = get<int>(d, "rowchain", -1);
@@ -184,7 +185,7 @@ PYBIND11_MODULE(_C, m) {
 
   // single PLAIN GEMM (C fp32 = A . BT^T) for kernel tests / generic matmul
   m.def("gemm_nt", [](uintptr_t A, uintptr_t BT, uintptr_t C, int M, int N, int K, long long lda, long long ldb,
-                      long long ldc, int bf16, int cfg, uintptr_t s) {
+                      long long ldc, int bf16, int cfg, uintptr_t s, uintptr_t stamps) {
     // the kernel issues unconditional 16-byte fragment loads along K: rows must be
     // 16-byte aligned and K padded to whole chunks, or it reads out of bounds
     const int epl = bf16 ? 8 : 4;
@@ -192,6 +193,7 @@ PYBIND11_MODULE(_C, m) {
         (A % 16) || (BT % 16) || (C % 4) || cfg < 0 || cfg > 4 || cfg == 3)
       throw std::invalid_argument("gemm_nt: K, lda, ldb must be multiples of 16 bytes, pointers 16-byte aligned");
     ea_gemm_init();
+    if (cfg == 4 && !bf16) cfg = 1;  // the 256x256 tile is bf16-only; fp32 runs the THR tile
     GroupArgs ga;
     std::memset(&ga, 0, sizeof(ga));
     Prob& p = ga.p[0];
@@ -207,6 +209,7 @@ PYBIND11_MODULE(_C, m) {
     ga.nprob = 1;
     ga.R = 1;
     ga.total_blocks = p.tiles_m * p.tiles_n;
+    ga.stamps = reinterpret_cast<long long*>(stamps);  // diagnostics (null = off)
     static long long* dctr = nullptr;
     if (!dctr) {
       chk(hipMalloc(&dctr, 64 * sizeof(long long)), "hipMalloc");
@@ -215,7 +218,8 @@ PYBIND11_MODULE(_C, m) {
     ga.ctr = dctr;
     p.ntrain = reinterpret_cast<const int*>(dctr);  // zero batch counts: the kernel reads ntrain[0]
     chk(ea_gemm_grouped(&ga, bf16, cfg, S(s)), "gemm_nt");
-  });
+  }, py::arg("A"), py::arg("BT"), py::arg("C"), py::arg("M"), py::arg("N"), py::arg("K"), py::arg("lda"),
+     py::arg("ldb"), py::arg("ldc"), py::arg("bf16"), py::arg("cfg"), py::arg("stream"), py::arg("stamps") = 0);
   m.def("tile_shape", [](int cfg) { return py::make_tuple(ea_gemm_tile_m(cfg), ea_gemm_tile_n(cfg)); });
 
   m.def("replica_average", [](uintptr_t P, long long sP, int R, long long n, uintptr_t out, int write_back,

@@ -197,7 +197,12 @@ int Executor::split_last(int cfg, long long N, long long K) const {
 }
 
 int Executor::pick_cfg(long long M, long long N, long long K) const {
-  if (c_.force_cfg >= 0) return c_.force_cfg;
+  if (c_.force_cfg >= 0) return (c_.force_cfg == 4 && !c_.bf16) ? 1 : c_.force_cfg;
+  // 256x256 ping-pong tiles (bf16) where they alone give every CU a workgroup
+  // (e.g. the 4096 x 4096 weight gradients of the Wide MLP: 256 tiles)
+  if (c_.bf16 && c_.big && M >= 1024 && N >= 1024 && K >= 512 &&
+      (long long)c_.R * cdiv((int)M, 256) * cdiv((int)N, 256) >= 240)
+    return 4;
   if (M >= 256 && N >= c_.thr_min_n && K >= c_.thr_min_k) {
     // 128x128 tiles while they give every CU at least two workgroups (256 CUs),
     // else 128x64 tiles (twice the workgroups; measured on MI355X, profiles/)
@@ -294,7 +299,8 @@ std::vector<Executor::Launch> Executor::build_forward(bool eval, long long chunk
     p.layer = l;
     p.act = ly.act;
     p.rate = ly.rate;
-    const int cfg = pick_cfg(c_.B, ly.N, ly.Kp);
+    int cfg = pick_cfg(c_.B, ly.N, ly.Kp);
+    if (cfg == 4 && last) cfg = 1;  // the big tile has no loss / split-K epilogue
     Launch La;
     std::memset(&La, 0, sizeof(La));
     La.cfg = cfg;
@@ -408,7 +414,7 @@ std::vector<Executor::Launch> Executor::build_forward(bool eval, long long chunk
       t.DT = reinterpret_cast<void*>(c_.XT);
       t.lddt = c_.Bp;
       t.sDT = (long long)ly.Kp * c_.Bp;
-      if (La.ga.nprob == 1 && La.ga.p[0].kind != PK_LOSS_ROWS) {
+      if (La.ga.nprob == 1 && La.ga.p[0].kind != PK_LOSS_ROWS && La.cfg != 4) {
         La.ga.p[1] = t;
         La.ga.nprob = 2;
       } else {
@@ -500,6 +506,21 @@ void Executor::build() {
       x.DT = reinterpret_cast<void*>(pv.dZT);
       x.lddt = c_.Bp;
       x.sDT = (long long)pv.N * c_.Bp;
+      const int cw = pick_cfg(w.M, w.N, w.K), cx = pick_cfg(x.M, x.N, x.K);
+      if ((cw == 4) != (cx == 4)) {
+        // one of the two products fills the chip with 256x256 tiles, the other
+        // would leave most CUs idle on them: two launches, each on its own tile
+        La.cfg = cw;
+        finalize(La);
+        bwd_.push_back(La);
+        std::memset(&La, 0, sizeof(La));
+        La.ga.p[0] = x;
+        La.ga.nprob = 1;
+        La.cfg = cx;
+        finalize(La);
+        bwd_.push_back(La);
+        continue;
+      }
       La.ga.p[1] = x;
       La.ga.nprob = 2;
       long long xw = (long long)x.M * x.N * x.K;

@@ -56,7 +56,8 @@ struct ExecCfg {
   int loss = 0, nmet = 0, met[4] = {0, 0, 0, 0};
   uintptr_t acc = 0; int acc_stride = 6;
   uintptr_t ctr = 0;
-  int force_cfg = -1;  // -1 auto, 0 LAT, 1 THR, 2 THR-N64
+  int force_cfg = -1;  // -1 auto, 0 LAT, 1 THR, 2 THR-N64, 4 BIG (256x256, bf16)
+  int big = 0;         // allow the 256x256 tile where its grid fills the chip (opt-in: measured slower on the Wide shapes)
   int thr_min_n = 256;
   int thr_min_k = 64;  // smallest reduction depth for the 128-row THR tiles (Otto DW, K = batch 128: 135 -> 127 us/step)
   int rowchain = -1;   // row-chain step plan: -1 when eligible, 0 off, 1 required

@@ -301,11 +301,12 @@ def _plan_case(case):
             assert np.allclose(a[key], b[key], rtol=5 * tol, atol=5 * tol), (key, a[key], b[key])
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 2])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 4])
 @pytest.mark.parametrize("bf16", [1, 0])
-@pytest.mark.parametrize("M,N,K", [(64, 128, 784), (64, 10, 128), (785, 128, 64), (300, 200, 136), (512, 512, 512)])
+@pytest.mark.parametrize("M,N,K", [(64, 128, 784), (64, 10, 128), (785, 128, 64), (300, 200, 136), (512, 512, 512),
+                                   (513, 770, 264)])
 def test_plain_gemm_matches_torch_fp32(M, N, K, bf16, cfg):
-    """Library entry of the MFMA GEMM (LAT / THR tiles) vs. a torch fp32 matmul."""
+    """Library entry of the MFMA GEMM (LAT / THR / 256x256 tiles) vs. a torch fp32 matmul."""
     from elephas_amd.ops import native
     C = native.require()
     torch.manual_seed(0)
@@ -344,12 +345,14 @@ def test_training_is_bit_deterministic(rowchain):
     assert np.array_equal(w1, w2), np.abs(w1 - w2).max()
 
 
-@pytest.mark.parametrize("cfg", ["1", "2"])
+@pytest.mark.parametrize("cfg", ["1", "2", "4"])
 @pytest.mark.parametrize("policy,tol", [("mixed_bfloat16", 5e-2), ("float32", 1e-3)])
 def test_throughput_tiles_match_reference(monkeypatch, policy, tol, cfg):
-    """Force the 128x128 THR tiles (LDS-staged glds main loop for bf16) on every
-    layer: gathered layer-0 rows, the ones row of the bias gradient, K / N / M
-    tails (K=100, N=70, B=48 of 64) and the fused SGD update must all match."""
+    """Force the 128x128 THR tiles (LDS-staged glds main loop for bf16) or the
+    256x256 8-wave tile (cfg 4: FWD / DX / DW epilogues over two 128-row halves,
+    the last layer and the X^T gather on their own launches) on every layer:
+    gathered layer-0 rows, the ones row of the bias gradient, K / N / M tails
+    (K=100, N=70, B=48 of 64) and the fused SGD update must all match."""
     from elephas_amd.models.optimizers import SGD
     monkeypatch.setenv("ELEPHAS_AMD_GEMM_CFG", cfg)
     model = _mlp(200, [136, 72], 70, dropout=0.0)
