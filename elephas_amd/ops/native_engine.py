@@ -342,17 +342,28 @@ class NativeTrainer(TrainerBase):
             for _ in range(nsteps):
                 self.exe.train_step(self.s)
             return
-        # fixed chunk shapes: only two graphs ever exist per executor, so no capture
-        # lands inside a timed loop whose step count differs from the warmup's
+        # fixed chunk shapes (GRAPH_CHUNK and its binary fractions, all captured by
+        # prepare_graphs), so no capture lands inside a timed loop whose step count
+        # differs from the warmup's; a remainder of r steps is popcount(r) graph
+        # launches instead of r (each graph boundary costs a launch gap on the GPU)
         full, rest = divmod(nsteps, self.GRAPH_CHUNK)
         if full:
             self.exe.replay_n(self._graph(self.GRAPH_CHUNK, 0), full, self.s)
-        if rest:
-            self.exe.replay_n(self._graph(1, 0), rest, self.s)
+        b = self.GRAPH_CHUNK // 2
+        while rest:
+            if rest >= b:
+                self.exe.replay_n(self._graph(b, 0), 1, self.s)
+                rest -= b
+            b //= 2
 
     def prepare_graphs(self, allreduce_path: bool = False):
         """Capture (without running) every graph run_steps / run_steps_allreduce use."""
-        keys = [(1, 1), (1, 2)] if allreduce_path else [(self.GRAPH_CHUNK, 0), (1, 0)]
+        chunks = []
+        b = self.GRAPH_CHUNK
+        while b >= 1:
+            chunks.append((b, 0))
+            b //= 2
+        keys = [(1, 1), (1, 2)] if allreduce_path else chunks
         for n, mode in keys:
             self._graph(n, mode)
 
