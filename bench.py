@@ -112,9 +112,13 @@ def main():
     ap.add_argument("--out", default=None, help="also append the JSON line to this file")
     ap.add_argument("--async-groups", type=int, default=None,
                     help="async/hogwild: independently progressing worker groups per GPU (default: one per worker)")
+    ap.add_argument("--frequency", default="batch", choices=["epoch", "batch"],
+                    help="async / hogwild exchange frequency (reference SparkModel frequency: its async "
+                         "examples use the default 'epoch')")
     ap.add_argument("--mode", default="synchronous", choices=["synchronous", "asynchronous", "hogwild"],
                     help="asynchronous / hogwild: every worker pulls from and pushes to the HBM "
-                         "parameter server around each step (frequency='batch', BASELINE config #3)")
+                         "parameter server around each step (--frequency batch) or epoch (--frequency "
+                         "epoch, the reference examples' setting); BASELINE config #3")
     ap.add_argument("--task", default="train", choices=["train", "fit", "predict", "evaluate"],
                     help="predict / evaluate: distributed inference of the master network "
                          "(SparkModel.predict / evaluate path, BASELINE config #5)")
@@ -452,11 +456,13 @@ def bench_infer(args, model, dist, rank, world, dev):
 
 def bench_async(args, model, dist, rank, world, dev):
     """Async / hogwild DP through the sharded device parameter server (reference
-    worker.py:114-127, frequency='batch'): the W workers of a GPU are split into G
+    worker.py:102-127, frequency 'batch' or 'epoch'): the W workers of a GPU are split into G
     independently progressing groups (worker.BatchedAsynchronousWorker, one executor +
-    HIP stream each); every group-step is ONE hipGraph replay of pull (gather theta from
-    the shards, chunk-consistent in 'asynchronous') -> refresh -> train -> push (fp32
-    atomic adds into the owners' shards over xGMI).  No host lock, no host sync."""
+    HIP stream each); with frequency='batch' every group-step is ONE hipGraph replay of
+    pull (gather theta from the shards, chunk-consistent in 'asynchronous') -> refresh ->
+    train -> push (fp32 atomic adds into the owners' shards over xGMI); with 'epoch' the
+    same pull / push bracket each epoch of graph-replayed training steps.  No host
+    lock, no host sync."""
     import torch
     from elephas_amd.ops.native_engine import NativeTrainer
     from elephas_amd.ops.plan import build_plan, flatten_weights
@@ -482,7 +488,8 @@ def bench_async(args, model, dist, rank, world, dev):
         dx.append(((x - x.min()) / (x.max() - x.min())).astype(np.float32))
         dy.append(np.eye(classes, dtype=np.float32)[y])
     bounds = [W * g // G for g in range(G + 1)]
-    worker = BatchedAsynchronousWorker(None, None, client, {}, "batch", None, None, None, None)
+    freq = args.frequency
+    worker = BatchedAsynchronousWorker(None, None, client, {}, freq, None, None, None, None)
     groups = []
     for g in range(G):
         lo, hi = bounds[g], bounds[g + 1]
@@ -491,22 +498,40 @@ def bench_async(args, model, dist, rank, world, dev):
         t.begin_epoch()
         grp = _Group(t, [True] * (hi - lo))
         if not args.no_graph:
-            grp.capture(worker)
+            if freq == "batch":
+                grp.capture(worker)
+            else:
+                t.prepare_graphs()
         groups.append(grp)
     spe = groups[0].t.steps_per_epoch()
     state = {"pos": 0}
 
     def run(k):
+        if freq == "epoch":
+            # reference worker.py:102-113: pull, train the epoch, push the epoch's delta;
+            # every call also starts with a pull and ends with a push, so the timed
+            # region holds complete exchanges
+            for grp in groups:
+                worker._pull(grp)
         while k > 0:
             if state["pos"] >= spe:
                 for grp in groups:
+                    if freq == "epoch":
+                        worker._push(grp)
+                        worker._pull(grp)
                     grp.t.begin_epoch()
                 state["pos"] = 0
             n = min(k, spe - state["pos"])
             for grp in groups:            # every group enqueues n rounds on its own stream
-                grp.steps(worker, n)
+                if freq == "epoch":
+                    grp.t.run_steps(n, use_graph=not args.no_graph)
+                else:
+                    grp.steps(worker, n)
             state["pos"] += n
             k -= n
+        if freq == "epoch":
+            for grp in groups:
+                worker._push(grp)
 
     def sync():
         for grp in groups:
@@ -533,10 +558,11 @@ def bench_async(args, model, dist, rank, world, dev):
             "data": "synthetic, random-init weights",
             "config": {"model": args.model, "global_batch": B * W * world, "seq_len": None,
                        "parallelism": f"{args.mode}-dp{world}", "workers_per_gpu": W, "batch_per_worker": B,
-                       "frequency": "batch", "groups_per_gpu": G,
+                       "frequency": freq, "groups_per_gpu": G,
                        "ps": f"sharded over {world} GPU(s), 4096-parameter chunks, IPC-mapped",
-                       "exchange": "hipGraph per group-step (pull, refresh, train, push)" if groups[0].graph
-                       else "eager launches"},
+                       "exchange": ("pull / push per epoch around hipGraph training chunks" if freq == "epoch"
+                                    else "hipGraph per group-step (pull, refresh, train, push)" if groups[0].graph
+                                    else "eager launches")},
         }
         print(json.dumps(line), flush=True)
     dist.barrier()
