@@ -40,11 +40,43 @@ def _attr_json(raw):
     return str(raw)
 
 
+# get_config() keys and the getters that produce them (reference ml_model.py:40-59);
+# the same dict round-trips through save() / load_ml_estimator() as constructor kwargs
+_ESTIMATOR_CONFIG = (
+    ("keras_model_config", "get_keras_model_config"), ("mode", "get_mode"), ("frequency", "get_frequency"),
+    ("num_workers", "get_num_workers"), ("categorical", "get_categorical_labels"), ("loss", "get_loss"),
+    ("metrics", "get_metrics"), ("validation_split", "get_validation_split"), ("featuresCol", "getFeaturesCol"),
+    ("labelCol", "getLabelCol"), ("epochs", "get_epochs"), ("batch_size", "get_batch_size"),
+    ("verbose", "get_verbosity"), ("nb_classes", "get_nb_classes"), ("outputCol", "getOutputCol"),
+)
+
+
+def _deprecated_col_setter(col: str):
+    """Spark 3 deprecated the column setters in favour of constructor kwargs; the
+    reference keeps them with a DeprecationWarning (ml_model.py:111-124)."""
+    def setter(self, value):
+        warnings.warn(f"set{col[0].upper()}{col[1:]} is deprecated in Spark 3.0.x+ - please supply {col} in the "
+                      f"constructor i.e; ElephasEstimator({col}='foo')", DeprecationWarning)
+        return self._set(**{col: value})
+    setter.__name__ = f"set{col[0].upper()}{col[1:]}"
+    return setter
+
+
+def _read_distributed_config(file_name: str, object_hook=None) -> dict:
+    """The ``distributed_config`` root attribute of an estimator / transformer file."""
+    f = h5lite.File(file_name, mode="r")
+    try:
+        return json.loads(_attr_json(f.attrs.get("distributed_config")), object_hook=object_hook)
+    finally:
+        f.close()
+
+
 class ElephasEstimator(Estimator, HasCategoricalLabels, HasValidationSplit, HasKerasModelConfig, HasFeaturesCol,
                        HasLabelCol, HasMode, HasEpochs, HasBatchSize, HasFrequency, HasVerbosity, HasNumberOfClasses,
                        HasNumberOfWorkers, HasOutputCol, HasLoss, HasMetrics, HasKerasOptimizerConfig,
                        HasCustomObjects, DefaultParamsReadable, DefaultParamsWritable):
-    """Spark-ML Estimator wrapping a Keras-compatible model config."""
+    """Spark-ML Estimator wrapping a Keras-compatible model config: ``fit(df)`` trains
+    a SparkModel on the native engine and returns an ``ElephasTransformer``."""
 
     @keyword_only
     def __init__(self, **kwargs):
@@ -53,29 +85,13 @@ class ElephasEstimator(Estimator, HasCategoricalLabels, HasValidationSplit, HasK
         self.set_params(**kwargs)
 
     def get_config(self):
-        return {"keras_model_config": self.get_keras_model_config(),
-                "mode": self.get_mode(),
-                "frequency": self.get_frequency(),
-                "num_workers": self.get_num_workers(),
-                "categorical": self.get_categorical_labels(),
-                "loss": self.get_loss(),
-                "metrics": self.get_metrics(),
-                "validation_split": self.get_validation_split(),
-                "featuresCol": self.getFeaturesCol(),
-                "labelCol": self.getLabelCol(),
-                "epochs": self.get_epochs(),
-                "batch_size": self.get_batch_size(),
-                "verbose": self.get_verbosity(),
-                "nb_classes": self.get_nb_classes(),
-                "outputCol": self.getOutputCol()}
+        return {key: getattr(self, getter)() for key, getter in _ESTIMATOR_CONFIG}
 
     def save(self, file_name: str):
         """HDF5 holding only the ``distributed_config`` attribute (reference :61-70)."""
+        conf = {"class_name": type(self).__name__, "config": self.get_config()}
         f = h5lite.File(file_name, mode="w")
-        f.attrs["distributed_config"] = json.dumps({
-            "class_name": self.__class__.__name__,
-            "config": self.get_config()
-        }).encode("utf8")
+        f.attrs["distributed_config"] = json.dumps(conf).encode("utf8")
         f.flush()
         f.close()
 
@@ -86,51 +102,39 @@ class ElephasEstimator(Estimator, HasCategoricalLabels, HasValidationSplit, HasK
     def get_model(self):
         return model_from_json(self.get_keras_model_config(), self.get_custom_objects())
 
+    # -- fit: DataFrame -> (features, label) RDD -> SparkModel -> transformer
+    def _training_rdd(self, df: DataFrame):
+        rdd = df_to_simple_rdd(df, categorical=self.get_categorical_labels(), nb_classes=self.get_nb_classes(),
+                               features_col=self.getFeaturesCol(), label_col=self.getLabelCol())
+        return rdd.repartition(self.get_num_workers())
+
+    def _compiled_model(self):
+        model = self.get_model()
+        model.compile(loss=self.get_loss(), optimizer=O.get(self.get_optimizer_config()),
+                      metrics=self.get_metrics(), custom_objects=self.get_custom_objects())
+        return model
+
     def _fit(self, df: DataFrame):
-        simple_rdd = df_to_simple_rdd(df, categorical=self.get_categorical_labels(), nb_classes=self.get_nb_classes(),
-                                      features_col=self.getFeaturesCol(), label_col=self.getLabelCol())
-        simple_rdd = simple_rdd.repartition(self.get_num_workers())
-        keras_model = model_from_json(self.get_keras_model_config(), self.get_custom_objects())
-        metrics = self.get_metrics()
-        loss = self.get_loss()
-        optimizer = O.get(self.get_optimizer_config())
-        keras_model.compile(loss=loss, optimizer=optimizer, metrics=metrics,
-                            custom_objects=self.get_custom_objects())
-        spark_model = SparkModel(model=keras_model, mode=self.get_mode(), frequency=self.get_frequency(),
+        rdd = self._training_rdd(df)
+        spark_model = SparkModel(model=self._compiled_model(), mode=self.get_mode(), frequency=self.get_frequency(),
                                  num_workers=self.get_num_workers(), custom_objects=self.get_custom_objects())
-        spark_model.fit(simple_rdd, epochs=self.get_epochs(), batch_size=self.get_batch_size(),
+        spark_model.fit(rdd, epochs=self.get_epochs(), batch_size=self.get_batch_size(),
                         verbose=self.get_verbosity(), validation_split=self.get_validation_split())
-        model_weights = spark_model.master_network.get_weights()
-        return ElephasTransformer(labelCol=self.getLabelCol(),
-                                  outputCol=self.getOutputCol(),
-                                  featuresCol=self.getFeaturesCol(),
-                                  keras_model_config=spark_model.master_network.to_json(),
-                                  weights=model_weights,
-                                  custom_objects=self.get_custom_objects(),
-                                  model_type=LossModelTypeMapper().get_model_type(loss),
+        trained = spark_model.master_network
+        return ElephasTransformer(labelCol=self.getLabelCol(), outputCol=self.getOutputCol(),
+                                  featuresCol=self.getFeaturesCol(), keras_model_config=trained.to_json(),
+                                  weights=trained.get_weights(), custom_objects=self.get_custom_objects(),
+                                  model_type=LossModelTypeMapper().get_model_type(self.get_loss()),
                                   history=spark_model.training_histories)
 
-    def setFeaturesCol(self, value):
-        warnings.warn("setFeaturesCol is deprecated in Spark 3.0.x+ - please supply featuresCol in the constructor "
-                      "i.e; ElephasEstimator(featuresCol='foo')", DeprecationWarning)
-        return self._set(featuresCol=value)
-
-    def setLabelCol(self, value):
-        warnings.warn("setLabelCol is deprecated in Spark 3.0.x+ - please supply labelCol in the constructor i.e;"
-                      " ElephasEstimator(labelCol='foo')", DeprecationWarning)
-        return self._set(labelCol=value)
-
-    def setOutputCol(self, value):
-        warnings.warn("setOutputCol is deprecated in Spark 3.0.x+ - please supply outputCol in the constructor i.e;"
-                      " ElephasEstimator(outputCol='foo')", DeprecationWarning)
-        return self._set(outputCol=value)
+    setFeaturesCol = _deprecated_col_setter("featuresCol")
+    setLabelCol = _deprecated_col_setter("labelCol")
+    setOutputCol = _deprecated_col_setter("outputCol")
 
 
 def load_ml_estimator(file_name: str) -> ElephasEstimator:
-    f = h5lite.File(file_name, mode="r")
-    elephas_conf = json.loads(_attr_json(f.attrs.get("distributed_config")))
-    config = elephas_conf.get("config")
-    return ElephasEstimator(**config)
+    """Rebuild an estimator from ElephasEstimator.save() (reference :129-133)."""
+    return ElephasEstimator(**_read_distributed_config(file_name).get("config"))
 
 
 class ElephasTransformer(Model, HasKerasModelConfig, HasLabelCol, HasOutputCol, HasFeaturesCol, HasCustomObjects,
@@ -140,10 +144,10 @@ class ElephasTransformer(Model, HasKerasModelConfig, HasLabelCol, HasOutputCol, 
     @keyword_only
     def __init__(self, **kwargs):
         super(ElephasTransformer, self).__init__()
-        if "weights" in kwargs.keys():
-            self.weights = kwargs.pop("weights")
-        if "model_type" in kwargs.keys():
-            self.model_type = kwargs.pop("model_type")
+        # weights / model_type / history are plain attributes, not Spark Params
+        for attr in ("weights", "model_type"):
+            if attr in kwargs:
+                setattr(self, attr, kwargs.pop(attr))
         self._history = kwargs.pop("history", [])
         self.set_params(**kwargs)
 
@@ -156,19 +160,17 @@ class ElephasTransformer(Model, HasKerasModelConfig, HasLabelCol, HasOutputCol, 
         return self._set(**kwargs)
 
     def get_config(self):
-        return {"keras_model_config": self.get_keras_model_config(),
-                "labelCol": self.getLabelCol(),
-                "featuresCol": self.getFeaturesCol(),
-                "outputCol": self.getOutputCol(),
-                "weights": [weight.tolist() for weight in getattr(self, "weights", [])],
+        return {"keras_model_config": self.get_keras_model_config(), "labelCol": self.getLabelCol(),
+                "featuresCol": self.getFeaturesCol(), "outputCol": self.getOutputCol(),
+                "weights": [np.asarray(w).tolist() for w in getattr(self, "weights", [])],
                 "model_type": getattr(self, "model_type", None)}
 
     def save(self, file_name: str):
+        """HDF5 with the ``distributed_config`` attribute: config, weights as lists and
+        the model type enum (reference :205-213)."""
+        conf = {"class_name": type(self).__name__, "config": self.get_config()}
         f = h5lite.File(file_name, mode="w")
-        f.attrs["distributed_config"] = json.dumps({
-            "class_name": self.__class__.__name__,
-            "config": self.get_config()
-        }, cls=ModelTypeEncoder).encode("utf8")
+        f.attrs["distributed_config"] = json.dumps(conf, cls=ModelTypeEncoder).encode("utf8")
         f.flush()
         f.close()
 
@@ -214,8 +216,8 @@ class ElephasTransformer(Model, HasKerasModelConfig, HasLabelCol, HasOutputCol, 
 
 
 def load_ml_transformer(file_name: str) -> ElephasTransformer:
-    f = h5lite.File(file_name, mode="r")
-    elephas_conf = json.loads(_attr_json(f.attrs.get("distributed_config")), object_hook=as_enum)
-    config = elephas_conf.get("config")
-    config["weights"] = [np.array(weight) for weight in config["weights"]]
+    """Rebuild a transformer from ElephasTransformer.save() (reference :265-269): the
+    model type comes back as its enum, the weights as arrays."""
+    config = _read_distributed_config(file_name, object_hook=as_enum).get("config")
+    config["weights"] = [np.array(w) for w in config["weights"]]
     return ElephasTransformer(**config)
