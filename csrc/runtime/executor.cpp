@@ -122,6 +122,9 @@ bool Executor::build_rowchain() {
     if (pu[l].kind != PK_DW_UPDATE) return false;
     pg[l] = pu[l];
     pg[l].kind = PK_DW_GRAD;
+    // (layer 0's update already skips its reader-less row-major image, build(): the
+    // split-K slab launch and the evaluation executor read W^T, the row chain reads W
+    // and W^T of layers >= 1 only)
   }
   table(rc_.ta_dw, pu, L, d_probs_ + TABLE_MAX, 3);
   table(rc_.ta_grad, pg, L, d_probs_ + 2 * TABLE_MAX, 3);
@@ -465,7 +468,9 @@ void Executor::build() {
     w.sS = c_.sS;
     w.G = reinterpret_cast<float*>(c_.G);
     w.sG = c_.sG;
-    w.Wsh = reinterpret_cast<void*>(c_.Wsh + ly.wsh_off * esz);
+    // layer 0 has no input gradient: its row-major image (the DX operand) has no reader
+    // (the FWD and evaluation launches read W^T), so its update skips that store
+    w.Wsh = (l == 0 && c_.rc_lean) ? nullptr : reinterpret_cast<void*>(c_.Wsh + ly.wsh_off * esz);
     w.sWsh = c_.sWsh;
     w.ldwsh = ly.Np;
     w.wsh_par = c_.wsh_par;

@@ -147,6 +147,7 @@ class NativeTrainer(TrainerBase):
             force_cfg=int(os.environ.get("ELEPHAS_AMD_GEMM_CFG", "-1")),
             big=int(os.environ.get("ELEPHAS_AMD_BIG", "0")),
             split_dwdx=int(os.environ.get("ELEPHAS_AMD_SPLIT_DWDX", "0")),
+            rc_lean=int(os.environ.get("ELEPHAS_AMD_RC_LEAN", "1")),
             thr_min_k=int(os.environ.get("ELEPHAS_AMD_THR_MIN_K", "64")),
             thr_min_n=int(os.environ.get("ELEPHAS_AMD_THR_MIN_N", "256")),
             rowchain=self.rowchain_mode if ws is self.ws else 0,
