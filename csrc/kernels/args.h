@@ -134,6 +134,7 @@ constexpr int RC_MAXL = 4;
 constexpr int RC_ROWS = 16;
 constexpr int RC_MAXW = 256;
 constexpr int RC_MAXSPLIT = 8;   // layer-0 split-K slabs
+constexpr int LOSS_RPB = 4;        // rows per workgroup of the wide-output loss rows kernel (one per wave)
 constexpr int LOSS_MAX_SPLIT = 4;  // split-K slabs of a wide last layer summed by the loss rows kernel
 struct RcLayer {
   int K, N, Kp, Np, act, has_bias;

@@ -100,7 +100,6 @@ __device__ __forceinline__ void gather_transpose_block(const GA& ga, const Prob&
 // last layer's weight update) is staged in LDS as [N][LOSS_RPB] and written with
 // one 16-byte store per class column instead of one scattered 2-byte store per
 // element (66 us -> see profiles/kernels_wide_b1024.txt for 1024 x 1000 bf16).
-constexpr int LOSS_RPB = 8;                       // rows per workgroup
 constexpr int LOSS_LDS_MAX_N = 64 * 65 * 4 / (LOSS_RPB * 2);  // fits the smallest launch's LDS (LAT)
 
 // Wide softmax + CCE row (one wave, NV values per lane in registers): the same
@@ -264,11 +263,12 @@ __device__ __forceinline__ void loss_rows_block(const GroupArgs& ga, const Prob&
   }
   if (stage_t) {
     __syncthreads();
-    // rows row0 .. row0+7 of dZ^T column j: 16 contiguous bytes (row0 % 8 == 0, lddt % 8 == 0)
+    // rows row0 .. row0+LOSS_RPB-1 of dZ^T column j: one 8-byte store (row0 % 4 == 0, lddt % 8 == 0)
+    static_assert(LOSS_RPB == 4, "one uint2 per column");
     unsigned short* out = reinterpret_cast<unsigned short*>(p.DT) + (long long)r * p.sDT + row0;
     for (int j = threadIdx.x; j < p.N; j += 256)
       if (row0 + LOSS_RPB <= p.lddt)
-        *reinterpret_cast<uint4*>(out + (long long)j * p.lddt) = *reinterpret_cast<const uint4*>(sdt + j * LOSS_RPB);
+        *reinterpret_cast<uint2*>(out + (long long)j * p.lddt) = *reinterpret_cast<const uint2*>(sdt + j * LOSS_RPB);
   }
 }
 

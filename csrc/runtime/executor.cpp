@@ -248,7 +248,7 @@ void Executor::finalize(Launch& L) const {
       p.tiles_m = cdiv(p.B, 64);
       p.tiles_n = cdiv(p.K, 64);
     } else if (p.kind == PK_LOSS_ROWS) {
-      p.tiles_m = cdiv(p.M, 8);  // LOSS_RPB rows per workgroup (gemm.hip)
+      p.tiles_m = cdiv(p.M, LOSS_RPB);  // rows per workgroup of the loss rows kernel
       p.tiles_n = 1;
     } else {
       p.tiles_m = cdiv(p.M, bm);
