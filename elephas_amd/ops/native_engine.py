@@ -39,7 +39,7 @@ def pad8(n: int) -> int:
 
 
 class NativeTrainer(TrainerBase):
-    GRAPH_CHUNK = 16
+    GRAPH_CHUNK = int(os.environ.get("ELEPHAS_AMD_GRAPH_CHUNK", "16"))  # steps per captured graph (a power of two)
 
     def __init__(self, model, plan, R: int = 1, batch_size: int = 32, device=None, seed: Optional[int] = None,
                  policy: Optional[str] = None, eval_batch: int = 2048, rowchain: Optional[int] = None):
