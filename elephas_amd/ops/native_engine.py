@@ -39,7 +39,9 @@ def pad8(n: int) -> int:
 
 
 class NativeTrainer(TrainerBase):
-    GRAPH_CHUNK = int(os.environ.get("ELEPHAS_AMD_GRAPH_CHUNK", "16"))  # steps per captured graph (a power of two)
+    # steps per captured graph: a power of two (run_steps splits a remainder into the
+    # binary fractions of it), ELEPHAS_AMD_GRAPH_CHUNK rounded down to one
+    GRAPH_CHUNK = 1 << (max(1, int(os.environ.get("ELEPHAS_AMD_GRAPH_CHUNK", "16"))).bit_length() - 1)
 
     def __init__(self, model, plan, R: int = 1, batch_size: int = 32, device=None, seed: Optional[int] = None,
                  policy: Optional[str] = None, eval_batch: int = 2048, rowchain: Optional[int] = None):
