@@ -238,7 +238,7 @@ def main():
         if batch_mode:
             return
         if gpu:
-            t.average_replicas(dist.all_reduce_sum_, world)
+            t.average_replicas(dist.all_reduce_sum_ if world > 1 else None, R * world)
         else:
             w = t.get_weights_flat().sum(0)
             tt = torch.from_numpy(w)

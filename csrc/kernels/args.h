@@ -161,6 +161,51 @@ struct RcArgs {
   long long* stamps;
 };
 
+// ------------------------------------------------- persistent replica-cluster step
+// A chunk of training steps of a 3-layer Dense stack (hidden widths 64 or 128, a last
+// layer of <= 16 units) in ONE launch (csrc/kernels/persist.hip): per replica, nk0 x nc0
+// layer-0 workgroups keep their W0 tile resident in LDS and nch = ceil(B/16) chain
+// workgroups run layers 1-2 for 16 batch rows each; they hand activations, gradients
+// and updated weights to each other through a per-replica workspace with flags.
+constexpr int PM_ROWS = 64;    // batch rows per replica (B <= 64)
+constexpr int PM_MAXH = 128;   // hidden widths: 64 or 128
+constexpr int PM_MAXC = 16;    // last layer units
+constexpr int PM_MAXWG = 64;   // workgroups of one kind per replica (one polling wave watches them)
+constexpr int PM_NTU = 2;      // layer-1 column tiles (and layer-2 row tiles) a chain workgroup owns
+enum PmFlag : int { PMF_PART = 0, PMF_BWD = 1, PMF_W = 2, PMF_N = 3 };
+struct PersistArgs {
+  int R, B, nsteps;
+  int K0, H0, H1, C;            // layer widths (H0, H1 in {64, 128}; C <= 16)
+  int nk0, nc0, kc0, cw;        // layer-0 tiles: nk0 k-chunks of kc0 rows x nc0 column blocks of cw
+  int nch, wgs;                 // chain workgroups per replica; workgroups per replica (nk0*nc0 + nch)
+  int act0, act1, act2;
+  float rate0, rate1;
+  int bias0, bias1, bias2;
+  long long p_off0, p_off1, p_off2;
+  const float* X; long long sX, ldx;
+  const float* Y; long long sY, ldy;
+  const int* perm; long long sPerm;
+  const int* ntrain;
+  float* P; long long sP;
+  float* S; long long sS;
+  OptParams op;
+  float* Wsh; long long sWsh, wsh_par;
+  float* WTsh; long long sWTsh, wtsh_par;
+  long long wsh_off[3], wtsh_off[3];
+  int Np[3], Kp[3];
+  int loss, nmet, met[4];
+  double* acc; int acc_stride;
+  long long* ctr;
+  unsigned long long seed;
+  float* ws; long long ws_stride;   // per-replica exchange workspace (floats)
+  long long o_part, o_dz0, o_a0, o_a1, o_dz1, o_dz2, o_w1, o_w2, o_b1, o_b2;
+  unsigned* flags;                  // [R][PMF_N][PM_MAXWG], zeroed before every launch
+  unsigned* err;                    // sticky error word (a timed-out wait), read by the host
+  long long timeout;                // spin limit in s_memrealtime ticks (100 MHz)
+  long long* stamps;                // diagnostics: [block][PM_STAMP_STEPS][16] s_memrealtime (null = off)
+};
+constexpr int PM_STAMP_STEPS = 8;
+
 constexpr int MAX_SEG = 16;
 
 struct Seg {

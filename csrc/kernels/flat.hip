@@ -192,13 +192,14 @@ static int shadow_tiles(const FlatArgs& a) {
   return t;
 }
 
-// mean over R replicas of P[r][i]; result written to every replica (and to out if given)
+// scale * sum over R replicas of P[r][i] (fp64 accumulation; scale 1/R = the mean);
+// result written to every replica if write_back (and to out if given)
 __global__ __launch_bounds__(256) void replica_average_kernel(float* P, long long sP, int R, long long n,
-                                                              float* out, int write_back) {
+                                                              float* out, int write_back, double scale) {
   for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
     double s = 0.0;
     for (int r = 0; r < R; ++r) s += P[(long long)r * sP + i];
-    const float m = (float)(s / R);
+    const float m = (float)(s * scale);
     if (out) out[i] = m;
     if (write_back)
       for (int r = 0; r < R; ++r) P[(long long)r * sP + i] = m;
@@ -280,8 +281,8 @@ extern "C" hipError_t ea_refresh_shadows(FlatArgs* a, int bf16, hipStream_t s) {
 }
 
 extern "C" hipError_t ea_replica_average(float* P, long long sP, int R, long long n, float* out, int write_back,
-                                         hipStream_t s) {
-  hipLaunchKernelGGL(replica_average_kernel, dim3(grid_for(n)), dim3(256), 0, s, P, sP, R, n, out, write_back);
+                                         double scale, hipStream_t s) {
+  hipLaunchKernelGGL(replica_average_kernel, dim3(grid_for(n)), dim3(256), 0, s, P, sP, R, n, out, write_back, scale);
   return hipGetLastError();
 }
 

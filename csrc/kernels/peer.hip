@@ -97,6 +97,13 @@ __device__ __forceinline__ void copy_span(const float* __restrict__ src, float* 
   for (long long i = v1 * 4 + threadIdx.x; i < hi; i += blockDim.x) dst[i] = src[i];
 }
 
+// A wait that timed out poisons the outputs it would have written with NaN (besides the
+// error word the host checks): a late peer never leaves a rank's local value looking
+// like a reduced one.
+__device__ __forceinline__ void poison_span(float* __restrict__ dst, long long lo, long long hi) {
+  for (long long i = lo + threadIdx.x; i < hi; i += blockDim.x) dst[i] = __builtin_nanf("");
+}
+
 // dst[i] = sum_{r < W} srcs[r][i] over [lo, hi), summed in rank order.
 __device__ __forceinline__ void sum_span(const PeerArgs& a, int parity, long long lo, long long hi, float* out,
                                          float* out2) {
@@ -142,7 +149,10 @@ __global__ __launch_bounds__(256) void allreduce_oneshot_kernel(PeerArgs a) {
   char* mine = a.base[a.rank];
   if (lo < hi) copy_span(a.in, stage_ptr(mine, a.cap, parity), lo, hi);
   signal(a, 0, b, a.epoch);
-  if (!wait_peers(a, 0, b, a.epoch)) return;
+  if (!wait_peers(a, 0, b, a.epoch)) {
+    if (lo < hi) poison_span(a.out, lo, hi);
+    return;
+  }
   if (lo < hi) sum_span(a, parity, lo, hi, a.out, nullptr);
 }
 
@@ -164,11 +174,22 @@ __global__ __launch_bounds__(256) void allreduce_twoshot_kernel(PeerArgs a) {
     if (lo < hi) copy_span(a.in, stage_ptr(mine, a.cap, parity), lo, hi);
   }
   signal(a, 0, b, a.epoch);
-  if (!wait_peers(a, 0, b, a.epoch)) return;
-  span(a.rank, lo, hi);
-  if (lo < hi) sum_span(a, parity, lo, hi, red_ptr(mine, a.cap, parity), a.out);
-  signal(a, 1, b, a.epoch);
-  if (!wait_peers(a, 1, b, a.epoch)) return;
+  // a timed-out wait raises no later flag (a peer must never read a slice this rank did
+  // not reduce): the peers' own waits time out and poison their outputs the same way
+  bool ok = wait_peers(a, 0, b, a.epoch);
+  if (ok) {
+    span(a.rank, lo, hi);
+    if (lo < hi) sum_span(a, parity, lo, hi, red_ptr(mine, a.cap, parity), a.out);
+    signal(a, 1, b, a.epoch);
+    ok = wait_peers(a, 1, b, a.epoch);
+  }
+  if (!ok) {
+    for (int p = 0; p < a.world; ++p) {
+      span(p, lo, hi);
+      if (lo < hi) poison_span(a.out, lo, hi);
+    }
+    return;
+  }
   for (int p = 0; p < a.world; ++p) {
     if (p == a.rank) continue;
     span(p, lo, hi);

@@ -1,0 +1,1004 @@
+// Persistent replica-cluster training kernel (MI355X / gfx950): a whole chunk of
+// training steps of a 3-layer Dense stack in ONE launch.
+//
+// Why: the MNIST step is latency-bound (profiles/README.md): the row-chain plan runs
+// it as three launches whose every phase is a dependent global round trip, and every
+// launch re-reads the weights it updates.  Here a replica's work is spread over a
+// fixed cluster of workgroups that stay resident for the whole chunk (one workgroup
+// per CU; block b serves replica b % R, so with R = 8 a replica's cluster shares one
+// XCD's L2 -- speed only, the protocol never depends on placement):
+//
+//   L0 workgroups (nk0 x nc0 per replica) each OWN a kc0 x cw tile of W0 (in LDS, for
+//     the whole chunk) and its optimizer state (registers).  Per step: wait for dZ_0,
+//     DW0 tile = X^T dZ_0, update the tile in place, then the NEXT step's split-K
+//     partial Z_0 tile = X_next . W0_tile (+ b0 on the first k-chunk) -> workspace.
+//     The next batch's X chunk streams into LDS (LDS-DMA) while they wait.
+//   chain workgroups (nch = B/16 per replica, 16 batch rows each): sum the partials
+//     (+ act, dropout), layer 1 and 2 forward, loss / metrics, input gradients down to
+//     dZ_0 -- row-local work, W1 / W2 read from LDS -- then publish dZ_0 and the weight
+//     gradient operands; in the time the L0 workgroups need for their part, each chain
+//     workgroup computes DW1 / DW2 for the layer-1 columns (layer-2 rows) it owns,
+//     updates them (masters and optimizer state in registers), publishes them, and
+//     loads the whole new W1 / W2 for the next step.
+//
+// Hand-offs follow the write-through form of the guide's inter-workgroup protocol
+// (cdna_hip_programming.md Guideline 16, R1): every handed-off byte is stored and
+// loaded with sc1 buffer instructions, each storing wave drains (s_waitcnt vmcnt(0)),
+// the workgroup barriers, one lane stores the flag (agent-scope relaxed = sc1); one
+// wave polls the producers' flags with sc1 loads.  Tags are the step index + 1 within
+// the launch; the flag block is zeroed by a memset node before every launch.  Every
+// spin is bounded (timeout -> sticky error word, the workgroup returns; the host
+// raises), and a launch that finds the error word set does nothing.
+//
+// Latency discipline (profiles/persist_*): every phase issues all of its global loads
+// (or LDS fragment reads) before the first use; handed-off rows are published from LDS
+// as coalesced 16-byte stores; per-lane buffer offsets stay few (the uniform parts go
+// in the SGPR soffset) so that the step loop does not spill.
+//
+// Semantics are those of the row-chain plan (reference elephas/worker.py:41-42 ->
+// one Keras fit step per batch): identical dropout masks (dropout_u1), batch windows,
+// optimizer iterations and loss epilogues; master weights and state are read from P / S
+// at the start of the launch and written back (with both weight-image parities) at
+// its end.
+#include "common.h"
+#include "loss_tile.h"
+
+namespace ea {
+
+namespace {
+
+using gu32 = __attribute__((address_space(1))) unsigned;
+using rsrc_t = __amdgpu_buffer_rsrc_t;
+typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
+
+constexpr int S17 = 17;   // LDS stride of 16-wide tiles
+constexpr int TU = 4;     // weight-gradient tiles per wave (<= 16 per workgroup)
+
+// LDS row strides are width + 1 (== 1 mod 32 for widths 64 / 128 / 32 / 16): the b32
+// fragment reads below -- 16 rows x k, or k x 16 columns, with k = kb + 16g + ks --
+// hit 32 distinct banks per half-wave.
+template <int H0, int H1>
+struct ChainLds {
+  static constexpr int L0S = H0 + 1, L1S = H1 + 1;
+  static constexpr int STAGE = 64 * L0S + 2 * 64 * 33 + 64 * S17;    // weight-gradient operands
+  static constexpr int W1 = (H0 * L1S > STAGE ? H0 * L1S : STAGE);  // W1, or the staging over it
+  static constexpr int o_w2 = W1;                     // [H1][17]
+  static constexpr int o_a0 = o_w2 + H1 * S17;        // [16][L0S]
+  static constexpr int o_g0 = o_a0 + 16 * L0S;        // [16][L0S]
+  static constexpr int o_z0 = o_g0 + 16 * L0S;        // [16][L0S] dZ_0 rows (published from here)
+  static constexpr int o_a1 = o_z0 + 16 * L0S;        // [16][L1S]
+  static constexpr int o_d1 = o_a1 + 16 * L1S;        // [16][L1S]
+  static constexpr int o_d2 = o_d1 + 16 * L1S;        // [16][17]
+  static constexpr int o_red = o_d2 + 16 * S17;       // [4][256]
+  static constexpr int o_lg = o_red + 1024;           // [16][36]
+  static constexpr int o_y = o_lg + 16 * 36;          // [16][32]
+  static constexpr int o_b1 = o_y + 16 * 32;          // [H1]
+  static constexpr int o_b2 = o_b1 + H1;              // [16]
+  static constexpr int o_row = o_b2 + 16;             // [16] ints
+  static constexpr int TOTAL = o_row + 16;
+};
+constexpr int L0_LDS = 2 * 64 * 129 + 128 * 33 + 64 * 33;
+constexpr int LDS_FLOATS = ((ChainLds<128, 128>::TOTAL > L0_LDS ? ChainLds<128, 128>::TOTAL : L0_LDS) + 3) & ~3;
+
+__device__ __forceinline__ f32x4 mma(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ f32x4 zero4f() { return f32x4{0.f, 0.f, 0.f, 0.f}; }
+
+// ---- write-through (sc1) accesses of handed-off bytes through a buffer resource of
+//      the replica's workspace: per-lane offset v + uniform offset s (SGPR), in floats
+__device__ __forceinline__ rsrc_t ws_rsrc(const float* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), (short)0, 0x7fffffff, 0x00020000);
+}
+__device__ __forceinline__ f32x4 ldw4(rsrc_t r, int v, int s) {
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, v * 4, s * 4, 16));
+}
+__device__ __forceinline__ void stw1(rsrc_t r, int v, int s, float x) {
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, x), r, v * 4, s * 4, 16);
+}
+__device__ __forceinline__ void stw4(rsrc_t r, int v, int s, f32x4 x) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, x), r, v * 4, s * 4, 16);
+}
+
+__device__ __forceinline__ unsigned* flag_at(const PersistArgs& a, int r, int kind) {
+  return a.flags + ((long long)r * PMF_N + kind) * PM_MAXWG;
+}
+
+// R1 publish: every storing wave drains its sc1 stores, the workgroup meets, one lane
+// raises the flag (agent-scope relaxed store = sc1)
+__device__ __forceinline__ void publish(unsigned* flag, unsigned tag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store((gu32*)(flag), tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// wave 0 polls flags[0 .. n) (lane q watches producer q) until every one reaches tag;
+// the whole workgroup leaves together.  false: timed out (error word set)
+__device__ __forceinline__ bool wait_all(const PersistArgs& a, const unsigned* flags, int n, unsigned tag,
+                                         unsigned code) {
+  int ok = 1;
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    const unsigned long long t0 = wall_clock64();
+    for (;;) {
+      const unsigned v = lane < n ? __hip_atomic_load((gu32*)(const_cast<unsigned*>(flags) + lane),
+                                                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                  : tag;
+      if (__all(v >= tag)) break;
+      if ((long long)(wall_clock64() - t0) > a.timeout) {
+        ok = 0;
+        if (lane == 0) __hip_atomic_store((gu32*)(a.err), code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  ok = __syncthreads_and(ok);
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no load moves above the poll
+  return ok != 0;
+}
+
+__device__ __forceinline__ float dropout_u1(uint32_t base, int row, int c) {
+  // the per-column-pair hash of dropout_u8 (common.h): the row-chain / grouped masks
+  const uint32_t h = fmix32(base ^ (((uint32_t)row << 16) | (uint32_t)(c >> 1)));
+  return (float)((c & 1) ? (h >> 16) : (h & 0xFFFFu)) * (1.0f / 65536.0f);
+}
+
+// diagnostics (tools/persist_stamps.py): s_memrealtime of phase k of step i (i < PM_STAMP_STEPS)
+__device__ __forceinline__ void pstamp(const PersistArgs& a, int i, int k) {
+  if (a.stamps && threadIdx.x == 0 && i >= 0 && i < PM_STAMP_STEPS)
+    a.stamps[((long long)blockIdx.x * PM_STAMP_STEPS + i) * 16 + k] = (long long)__builtin_amdgcn_s_memrealtime();
+}
+
+// global (sc1) rows [0, nrows) x columns [0, ncols) of a row-major block (row stride ld,
+// first element at uniform offset base) -> LDS tile (row stride lds).  ncols / 4 must
+// divide 256.  Every load of the thread is issued before the first LDS write.
+template <int NMAX>
+__device__ __forceinline__ void stage(rsrc_t rs, int base, int ld, int nrows, int ncols, float* dst, int lds) {
+  const int c4n = ncols >> 2, rpp = 256 / c4n;
+  const int row0 = threadIdx.x / c4n, c4 = threadIdx.x - row0 * c4n;
+  const int v = row0 * ld + 4 * c4;
+  f32x4 x[NMAX];
+#pragma unroll
+  for (int u = 0; u < NMAX; ++u)
+    if (row0 + u * rpp < nrows) x[u] = ldw4(rs, v, base + u * rpp * ld);
+#pragma unroll
+  for (int u = 0; u < NMAX; ++u) {
+    if (row0 + u * rpp < nrows) {
+      float* d = dst + (row0 + u * rpp) * lds + 4 * c4;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) d[q] = x[u][q];
+    }
+  }
+}
+
+// 16 LDS rows (stride lds) of W floats -> global rows at uniform offset base (row
+// stride W), as 16-byte write-through stores
+template <int W>
+__device__ __forceinline__ void publish_rows16(rsrc_t rs, int base, const float* src, int lds) {
+  constexpr int C4 = W / 4, TOT = 16 * C4, RPP = 256 / C4;
+  const int row0 = threadIdx.x / C4, c4 = threadIdx.x - row0 * C4;
+#pragma unroll
+  for (int u = 0; u < (TOT + 255) / 256; ++u) {
+    if (threadIdx.x + 256 * u < TOT) {
+      const float* s = src + (row0 + u * RPP) * lds + 4 * c4;
+      stw4(rs, row0 * W + 4 * c4, base + u * RPP * W, f32x4{s[0], s[1], s[2], s[3]});
+    }
+  }
+}
+
+// column sums of an LDS tile [64][ncols] (ncols <= 32) by all 256 threads: 8 row
+// groups of independent loads, one barrier, then the first ncols threads add the 8
+// partials (returned there).  Every thread must call it.
+__device__ __forceinline__ float col_sums(const float* tile, int ld, int ncols, float* red) {
+  const int tid = threadIdx.x, c = tid & 31, grp = tid >> 5;
+  float s = 0.f;
+  if (c < ncols) {
+#pragma unroll
+    for (int b = 0; b < 8; ++b) s += tile[(grp * 8 + b) * ld + c];
+  }
+  red[grp * 32 + c] = s;
+  __syncthreads();
+  float t = 0.f;
+  if (tid < ncols) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) t += red[q * 32 + tid];
+  }
+  return t;
+}
+
+struct Steps {
+  long long s0;
+  int ntr;
+  __device__ __forceinline__ int valid(const PersistArgs& a, int i) const {
+    const long long c = (long long)ntr - (s0 + i) * a.B;
+    return (int)(c < 0 ? 0 : (c > a.B ? a.B : c));
+  }
+};
+
+// ============================================================== layer-0 tiles
+template <int H0>
+__device__ __forceinline__ void l0_role(const PersistArgs& a, float* smem, int r, int kc, int cb, int q) {
+  constexpr int XS = 129;                       // X chunk rows (<= 128 columns)
+  const int tid = threadIdx.x, lane = tid & 63, i16 = lane & 15, g = lane >> 4;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int k0 = kc * a.kc0;
+  const int kreal = a.K0 - k0 < a.kc0 ? a.K0 - k0 : a.kc0;
+  const int KCP = (kreal + 63) & ~63;           // FWD reduction, zero padded to 64
+  const int cw = a.cw, n0 = cb * cw;
+  const int nct = cw >> 4, nrt = (kreal + 15) >> 4, ntiles = nrt * nct;
+  const int WS = cw + 1;
+  const int BR = a.nch * 16;                    // rows the chain workgroups produce
+  float* sX = smem;                             // [2][64][XS] X chunks of two steps
+  float* sW = sX + 2 * 64 * XS;                 // [128][WS]  the W0 tile (master, in place)
+  float* sdZ = sW + 128 * WS;                   // [64][WS]   dZ_0 columns of this tile
+  __shared__ float sB0[32];
+  __shared__ float sRedL[256];
+  const rsrc_t rs = ws_rsrc(a.ws + (long long)r * a.ws_stride);
+  float* P = a.P + (long long)r * a.sP;
+  float* S = a.S ? a.S + (long long)r * a.sS : nullptr;
+  const int np = S ? opt_planes(a.op) : 0;
+  const bool has_b = kc == 0 && a.bias0;
+  Steps st{ld_inv(a.ctr), ld_inv(a.ntrain + r)};
+
+  // ---- prologue: zero LDS (padding rows / columns stay zero), W0 tile and state
+  for (int e = tid; e < L0_LDS; e += 256) smem[e] = 0.f;
+  __syncthreads();
+  for (int e = tid; e < kreal * cw; e += 256) {
+    const int k = e / cw, n = e - k * cw;
+    sW[k * WS + n] = P[a.p_off0 + (long long)(k0 + k) * H0 + n0 + n];
+  }
+  int rt[TU], ct[TU];
+  float s0[TU * 4], s1[TU * 4];
+#pragma unroll
+  for (int u = 0; u < TU; ++u) {
+    const int t = w + 4 * u;
+    rt[u] = t < ntiles ? t / nct : 0;
+    ct[u] = t < ntiles ? t - rt[u] * nct : 0;
+#pragma unroll
+    for (int qq = 0; qq < 4; ++qq) {
+      const int k = rt[u] * 16 + 4 * g + qq, n = ct[u] * 16 + i16;
+      const bool in = t < ntiles && k < kreal;
+      const long long pi = a.p_off0 + (long long)(k0 + k) * H0 + n0 + n;
+      s0[4 * u + qq] = (in && np > 0) ? S[pi] : 0.f;
+      s1[4 * u + qq] = (in && np > 1) ? S[a.op.s_plane + pi] : 0.f;
+    }
+  }
+  float bw = 0.f, bs0 = 0.f, bs1 = 0.f;   // bias master / state (kc == 0, thread tid < cw)
+  const bool bown = has_b && tid < cw;
+  if (bown) {
+    const long long pi = a.p_off0 + (long long)a.K0 * H0 + n0 + tid;
+    bw = P[pi];
+    bs0 = np > 0 ? S[pi] : 0.f;
+    bs1 = np > 1 ? S[a.op.s_plane + pi] : 0.f;
+  }
+  if (tid < 32) sB0[tid] = 0.f;
+  __syncthreads();
+  if (bown) sB0[tid] = bw;
+
+  // X chunk of step i into sX buffer (i & 1): LDS-DMA, one 64-column row segment per
+  // wave instruction (rows past the valid batch repeat its first row: finite values
+  // whose dZ_0 rows are zero)
+  auto load_x = [&](int i) {
+    const int valid = st.valid(a, i);
+    const int* pr = a.perm + (long long)r * a.sPerm + (st.s0 + i) * a.B;
+    const float* Xr = a.X + (long long)r * a.sX + k0;
+    float* dst = sX + (i & 1) * 64 * XS;
+    const int myrow = pr[lane < valid ? lane : 0];   // lane b holds batch row b's data row
+    for (int v = 0; v < 16; ++v) {
+      const int b = w + 4 * v;
+      if (b >= BR) break;
+      const int row = __builtin_amdgcn_readlane(myrow, b);
+      const float* src = Xr + (long long)row * a.ldx;
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+        if (64 * h + lane < kreal) __builtin_amdgcn_global_load_lds(src + 64 * h + lane, dst + b * XS + 64 * h, 4, 0, 0);
+    }
+  };
+
+  // split-K partial of step i's layer-0 pre-activations for this tile -> workspace
+  const int part_base = (int)a.o_part + kc * 64 * H0 + n0;
+  auto fwd = [&](int i) {
+    const float* A = sX + (i & 1) * 64 * XS;
+    if (w * 16 < BR) {
+      f32x4 acc[2] = {zero4f(), zero4f()};
+      const float* arow = A + (w * 16 + i16) * XS;
+      for (int kb = 0; kb < KCP; kb += 64) {
+        float av[16], bv0[16], bv1[16];
+#pragma unroll
+        for (int ks = 0; ks < 16; ++ks) {
+          const int k = kb + 16 * g + ks;
+          av[ks] = arow[k];
+          bv0[ks] = sW[k * WS + i16];
+          bv1[ks] = nct > 1 ? sW[k * WS + 16 + i16] : 0.f;
+        }
+#pragma unroll
+        for (int ks = 0; ks < 16; ++ks) {
+          acc[0] = mma(av[ks], bv0[ks], acc[0]);
+          if (nct > 1) acc[1] = mma(av[ks], bv1[ks], acc[1]);
+        }
+      }
+      const int v = (w * 16 + 4 * g) * H0 + i16;
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) {
+        if (jj < nct) {
+          const float bv = has_b ? sB0[jj * 16 + i16] : 0.f;
+#pragma unroll
+          for (int qq = 0; qq < 4; ++qq) stw1(rs, v + qq * H0 + jj * 16, part_base, acc[jj][qq] + bv);
+        }
+      }
+    }
+    publish(flag_at(a, r, PMF_PART) + q, (unsigned)(i + 1));
+    pstamp(a, i, 1);
+  };
+
+  const int n = a.nsteps;
+  pstamp(a, 0, 0);
+  if (st.valid(a, 0) > 0) {
+    load_x(0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    fwd(0);
+  }
+  for (int i = 0; i < n; ++i) {
+    if (st.valid(a, i) == 0) break;
+    const bool nxt = i + 1 < n && st.valid(a, i + 1) > 0;
+    if (nxt) load_x(i + 1);
+    pstamp(a, i, 2);
+    if (!wait_all(a, flag_at(a, r, PMF_BWD), a.nch, (unsigned)(i + 1), 1u)) return;
+    pstamp(a, i, 3);
+    stage<2>(rs, (int)a.o_dz0 + n0, H0, BR, cw, sdZ, WS);   // dZ_0 columns of this tile
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");        // the X DMA and the dZ_0 loads
+    __syncthreads();
+    pstamp(a, i, 4);
+    // DW0 tile = X_i^T dZ_0 (reduction over the 64 batch rows), update in place
+    {
+      const float* Xi = sX + (i & 1) * 64 * XS;
+      f32x4 dw[TU];
+#pragma unroll
+      for (int u = 0; u < TU; ++u) dw[u] = zero4f();
+#pragma unroll
+      for (int half = 0; half < 2; ++half) {
+        float xa[TU][8], zb[2][8];
+#pragma unroll
+        for (int h8 = 0; h8 < 8; ++h8) {
+          const int b = 16 * g + 8 * half + h8;
+          zb[0][h8] = sdZ[b * WS + i16];
+          zb[1][h8] = nct > 1 ? sdZ[b * WS + 16 + i16] : 0.f;
+#pragma unroll
+          for (int u = 0; u < TU; ++u) xa[u][h8] = w + 4 * u < ntiles ? Xi[b * XS + rt[u] * 16 + i16] : 0.f;
+        }
+#pragma unroll
+        for (int h8 = 0; h8 < 8; ++h8) {
+#pragma unroll
+          for (int u = 0; u < TU; ++u)
+            if (w + 4 * u < ntiles) dw[u] = mma(xa[u][h8], ct[u] ? zb[1][h8] : zb[0][h8], dw[u]);
+        }
+      }
+      // bias gradient (first k-chunk): column sums of dZ_0 over the batch rows
+      const float gsum = has_b ? col_sums(sdZ, WS, cw, sRedL) : 0.f;
+      const long long it = iter_at(a.ctr, a.ntrain, a.B, r, st.s0, i);
+      float wv[TU * 4], gv[TU * 4];
+#pragma unroll
+      for (int u = 0; u < TU; ++u) {
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq) {
+          const int k = rt[u] * 16 + 4 * g + qq;
+          wv[4 * u + qq] = sW[k * WS + ct[u] * 16 + i16];
+          gv[4 * u + qq] = dw[u][qq] * a.op.grad_scale;
+        }
+      }
+      opt_update_v<TU * 4>(a.op, wv, gv, s0, s1, it);
+#pragma unroll
+      for (int u = 0; u < TU; ++u) {
+        if (w + 4 * u >= ntiles) continue;
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq) {
+          const int k = rt[u] * 16 + 4 * g + qq;
+          if (k < kreal) sW[k * WS + ct[u] * 16 + i16] = wv[4 * u + qq];
+        }
+      }
+      if (bown) {
+        float bv[1] = {bw}, bg[1] = {gsum * a.op.grad_scale}, t0[1] = {bs0}, t1[1] = {bs1};
+        opt_update_v<1>(a.op, bv, bg, t0, t1, it);
+        bw = bv[0];
+        bs0 = t0[0];
+        bs1 = t1[0];
+        sB0[tid] = bw;
+      }
+    }
+    __syncthreads();
+    pstamp(a, i, 5);
+    if (nxt) fwd(i + 1);
+    pstamp(a, i, 6);
+  }
+
+  // ---- epilogue: master tile, both weight-image parities, optimizer state
+  __syncthreads();
+  float* Wsh = a.Wsh + (long long)r * a.sWsh + a.wsh_off[0];
+  float* WTsh = a.WTsh + (long long)r * a.sWTsh + a.wtsh_off[0];
+  for (int e = tid; e < kreal * cw; e += 256) {
+    const int k = e / cw, nn = e - k * cw;
+    const float v = sW[k * WS + nn];
+    P[a.p_off0 + (long long)(k0 + k) * H0 + n0 + nn] = v;
+#pragma unroll
+    for (int par = 0; par < 2; ++par) {
+      Wsh[par * a.wsh_par + (long long)(k0 + k) * a.Np[0] + n0 + nn] = v;
+      WTsh[par * a.wtsh_par + (long long)(n0 + nn) * a.Kp[0] + k0 + k] = v;
+    }
+  }
+  if (np > 0) {
+#pragma unroll
+    for (int u = 0; u < TU; ++u) {
+      if (w + 4 * u >= ntiles) continue;
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq) {
+        const int k = rt[u] * 16 + 4 * g + qq, nn = ct[u] * 16 + i16;
+        if (k >= kreal) continue;
+        const long long pi = a.p_off0 + (long long)(k0 + k) * H0 + n0 + nn;
+        S[pi] = s0[4 * u + qq];
+        if (np > 1) S[a.op.s_plane + pi] = s1[4 * u + qq];
+      }
+    }
+  }
+  if (bown) {
+    const long long pi = a.p_off0 + (long long)a.K0 * H0 + n0 + tid;
+    P[pi] = bw;
+    if (np > 0) S[pi] = bs0;
+    if (np > 1) S[a.op.s_plane + pi] = bs1;
+  }
+}
+
+// ============================================================== chain (rows)
+// acc[jj] (jj < 2: column tiles ct0 + 4jj) += A[16][K] . B[K][16 cols], fragments from
+// LDS: A(i, k) = A[i * SAI + k], B(k, n) = B[k * SBK + n * SBN]; the 16 fragments of a
+// 64-deep block are read before its MFMAs
+template <int K, int SAI, int SBK, int SBN>
+__device__ __forceinline__ void rows_mm(const float* A, const float* B, int ct0, int nct, f32x4 (&acc)[2], int i16,
+                                        int g) {
+  acc[0] = zero4f();
+  acc[1] = zero4f();
+  if (ct0 >= nct) return;
+  const bool two = ct0 + 4 < nct;
+  const float* arow = A + i16 * SAI;
+  const float* b0 = B + (ct0 * 16 + i16) * SBN;
+  const float* b1 = B + ((ct0 + 4) * 16 + i16) * SBN;
+#pragma unroll
+  for (int kb = 0; kb < K; kb += 64) {
+    float av[16], bv0[16], bv1[16];
+#pragma unroll
+    for (int ks = 0; ks < 16; ++ks) {
+      const int k = kb + 16 * g + ks;
+      av[ks] = arow[k];
+      bv0[ks] = b0[k * SBK];
+      bv1[ks] = two ? b1[k * SBK] : 0.f;
+    }
+#pragma unroll
+    for (int ks = 0; ks < 16; ++ks) {
+      acc[0] = mma(av[ks], bv0[ks], acc[0]);
+      if (two) acc[1] = mma(av[ks], bv1[ks], acc[1]);
+    }
+  }
+}
+
+template <int H0, int H1, bool FAST>
+__device__ __forceinline__ void chain_role(const PersistArgs& a, float* smem, int r, int j) {
+  using Lo = ChainLds<H0, H1>;
+  constexpr int L0S = Lo::L0S, L1S = Lo::L1S;
+  constexpr int nt0 = H0 / 16, nt1 = H1 / 16;
+  const int tid = threadIdx.x, lane = tid & 63, i16 = lane & 15, g = lane >> 4;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int m0 = j * 16;
+  const int C = a.C;
+  const int BR = a.nch * 16;
+  const int nl0 = a.nk0 * a.nc0;
+  float* sW1 = smem;                 // [H0][L1S] W1 (k = layer-1 input, n = unit)
+  float* sW2 = smem + Lo::o_w2;      // [H1][17]
+  float* sA0 = smem + Lo::o_a0;      // [16][L0S] layer-0 activations (A of FWD1)
+  float* sG0 = smem + Lo::o_g0;      // [16][L0S] act'(z_0) * keep / (1 - rate)
+  float* sZ0 = smem + Lo::o_z0;      // [16][L0S] dZ_0 rows
+  float* sA1 = smem + Lo::o_a1;      // [16][L1S] layer-1 activations
+  float* sD1 = smem + Lo::o_d1;      // [16][L1S] dZ_1 (A of DX1)
+  float* sD2 = smem + Lo::o_d2;      // [16][17] dZ_2
+  float* sRed = smem + Lo::o_red;    // [4][256] split-K partials / column-sum partials
+  float* sLg = smem + Lo::o_lg;      // [16][36] logits -> dZ_2
+  float* sY = smem + Lo::o_y;        // [16][32] targets
+  float* sB1 = smem + Lo::o_b1;      // [H1]
+  float* sB2 = smem + Lo::o_b2;      // [16]
+  int* sRow = reinterpret_cast<int*>(smem + Lo::o_row);
+  // weight-gradient staging, over the W1 region (dead between DX1 and the W1 reload)
+  float* uA0 = sW1;                  // [64][L0S] layer-0 activations of every row
+  float* uD1 = uA0 + 64 * L0S;       // [64][33] dZ_1 of the owned layer-1 columns
+  float* uA1 = uD1 + 64 * 33;        // [64][33] layer-1 activations of the owned W2 rows
+  float* uD2 = uA1 + 64 * 33;        // [64][17] dZ_2
+
+  const rsrc_t rs = ws_rsrc(a.ws + (long long)r * a.ws_stride);
+  float* P = a.P + (long long)r * a.sP;
+  float* S = a.S ? a.S + (long long)r * a.sS : nullptr;
+  const int np = S ? opt_planes(a.op) : 0;
+  Steps st{ld_inv(a.ctr), ld_inv(a.ntrain + r)};
+
+  // owned tiles: layer-1 column tiles j + nch*c (c < nown) = layer-2 row tiles
+  const int nown = (nt1 - j + a.nch - 1) / a.nch;   // <= PM_NTU (host checks)
+  const int ndw1 = nt0 * nown;                      // DW1 tiles (row tile x owned col tile)
+
+  // ---- prologue: W1, W2, biases into LDS; owned masters / state into registers
+  for (int e = tid; e < Lo::TOTAL; e += 256) smem[e] = 0.f;
+  __syncthreads();
+  for (int e = tid; e < H0 * H1; e += 256) sW1[(e / H1) * L1S + (e % H1)] = P[a.p_off1 + e];
+  for (int e = tid; e < H1 * C; e += 256) {
+    const int k = e / C, nn = e - k * C;
+    sW2[k * S17 + nn] = P[a.p_off2 + e];
+  }
+  for (int e = tid; e < H1; e += 256) sB1[e] = a.bias1 ? P[a.p_off1 + (long long)H0 * H1 + e] : 0.f;
+  if (tid < C) sB2[tid] = a.bias2 ? P[a.p_off2 + (long long)H1 * C + tid] : 0.f;
+  // DW1 tiles of wave w: t = w + 4u -> (row tile t / nown, owned column c = t % nown);
+  // then (index 4*TU) the DW2 tile of wave w < nown: rows (j + nch*w)*16 + 4g + q, column i16
+  constexpr int NM = TU * 4 + 4;
+  float wm[NM], ws0[NM], ws1[NM];
+#pragma unroll
+  for (int u = 0; u < TU; ++u) {
+    const int t = w + 4 * u;
+    const int rt = t / nown, c = t - rt * nown;
+#pragma unroll
+    for (int qq = 0; qq < 4; ++qq) {
+      const int k = rt * 16 + 4 * g + qq, nn = (j + a.nch * c) * 16 + i16;
+      const bool in = t < ndw1;
+      const long long pi = a.p_off1 + (long long)k * H1 + nn;
+      wm[4 * u + qq] = in ? P[pi] : 0.f;
+      ws0[4 * u + qq] = (in && np > 0) ? S[pi] : 0.f;
+      ws1[4 * u + qq] = (in && np > 1) ? S[a.op.s_plane + pi] : 0.f;
+    }
+  }
+  const bool w2own = w < nown;
+#pragma unroll
+  for (int qq = 0; qq < 4; ++qq) {
+    const int k = (j + a.nch * w) * 16 + 4 * g + qq;
+    const bool in = w2own && i16 < C;
+    const long long pi = a.p_off2 + (long long)k * C + i16;
+    wm[4 * TU + qq] = in ? P[pi] : 0.f;
+    ws0[4 * TU + qq] = (in && np > 0) ? S[pi] : 0.f;
+    ws1[4 * TU + qq] = (in && np > 1) ? S[a.op.s_plane + pi] : 0.f;
+  }
+  // owned b1 entries: thread tid < 16 * nown -> unit (j + nch*(tid/16))*16 + tid%16; b2: chain 0, tid 64 + c
+  const bool b1own = a.bias1 && tid < 16 * nown;
+  const int b1n = (j + a.nch * (tid >> 4)) * 16 + (tid & 15);
+  const bool b2own = a.bias2 && j == 0 && tid >= 64 && tid < 64 + C;
+  float bm = 0.f, bst0 = 0.f, bst1 = 0.f;
+  if (b1own || b2own) {
+    const long long pi = b1own ? a.p_off1 + (long long)H0 * H1 + b1n : a.p_off2 + (long long)H1 * C + (tid - 64);
+    bm = P[pi];
+    bst0 = np > 0 ? S[pi] : 0.f;
+    bst1 = np > 1 ? S[a.op.s_plane + pi] : 0.f;
+  }
+  __syncthreads();
+
+  const int n = a.nsteps;
+  for (int i = 0; i < n; ++i) {
+    const int valid = st.valid(a, i);
+    if (valid == 0) break;
+    const long long it = iter_at(a.ctr, a.ntrain, a.B, r, st.s0, i);
+    const long long step = st.s0 + i;
+    // batch rows of this workgroup: targets requested before the wait
+    float yv[2];
+    {
+      const int* pr = a.perm + (long long)r * a.sPerm + step * a.B + m0;
+      const float* Yb = a.Y + (long long)r * a.sY;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int rr = (tid >> 5) + 8 * h, c = tid & 31;
+        const bool in = m0 + rr < valid && c < a.ldy;
+        const int prow = in ? pr[rr] : 0;
+        yv[h] = in ? Yb[(long long)prow * a.ldy + c] : 0.f;
+      }
+    }
+    pstamp(a, i, 0);
+    if (!wait_all(a, flag_at(a, r, PMF_PART), nl0, (unsigned)(i + 1), 2u)) return;
+    pstamp(a, i, 1);
+
+    // ---- phase 0: z_0 = sum of the split-K partials (b0 is in chunk 0's) -> act, dropout
+    {
+      const int rr = tid & 15, c0 = (tid >> 4) * 8;
+      const int m = m0 + rr;
+      const bool cin = c0 < H0;
+      const int v = rr * H0 + c0;
+      const int pbase = (int)a.o_part + m0 * H0;
+      float z[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) z[e] = 0.f;
+      f32x4 pv[2 * RC_MAXSPLIT];
+#pragma unroll
+      for (int u = 0; u < RC_MAXSPLIT; ++u) {
+        if (cin && u < a.nk0) {
+          pv[2 * u] = ldw4(rs, v, pbase + u * 64 * H0);
+          pv[2 * u + 1] = ldw4(rs, v + 4, pbase + u * 64 * H0);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < RC_MAXSPLIT; ++u) {
+        if (cin && u < a.nk0) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            z[e] += pv[2 * u][e];
+            z[4 + e] += pv[2 * u + 1][e];
+          }
+        }
+      }
+      float o[8], gg[8], dv[8];
+      act_fg_v<8>(a.act0, z, o, gg);
+      const float ks = a.rate0 > 0.f ? 1.f / (1.f - a.rate0) : 1.f;
+      const uint32_t db = dropout_base(a.seed, r, 0, it);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int c = c0 + e;
+        const bool live = cin && m < valid;
+        const float u = (live && a.rate0 > 0.f) ? dropout_u1(db, m, c) : 1.f;
+        const bool keep = live && u >= a.rate0;
+        dv[e] = keep ? o[e] * ks : 0.f;
+        if (cin) {
+          sA0[rr * L0S + c] = dv[e];
+          sG0[rr * L0S + c] = keep ? gg[e] * ks : 0.f;
+        }
+      }
+      if (cin) {
+        stw4(rs, v, (int)a.o_a0 + m0 * H0, f32x4{dv[0], dv[1], dv[2], dv[3]});
+        stw4(rs, v + 4, (int)a.o_a0 + m0 * H0, f32x4{dv[4], dv[5], dv[6], dv[7]});
+      }
+#pragma unroll
+      for (int h = 0; h < 2; ++h) sY[(tid >> 5) * 32 + 256 * h + (tid & 31)] = yv[h];
+      if (tid < 16) sRow[tid] = m0 + tid < valid ? 1 : -1;
+    }
+    __syncthreads();
+    pstamp(a, i, 2);
+
+    // ---- FWD1: column tiles w, w + 4 of the 16 x H1 output
+    float G1[8];
+    {
+      f32x4 acc[2];
+      rows_mm<H0, L0S, L1S, 1>(sA0, sW1, w, nt1, acc, i16, g);
+      const float ks = a.rate1 > 0.f ? 1.f / (1.f - a.rate1) : 1.f;
+      const uint32_t db = dropout_base(a.seed, r, 1, it);
+      float z[8], o[8], gg[8];
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) {
+        const int col = (w + 4 * jj) * 16 + i16;
+        const float b = w + 4 * jj < nt1 ? sB1[col] : 0.f;
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq) z[4 * jj + qq] = acc[jj][qq] + b;
+      }
+      act_fg_v<8>(a.act1, z, o, gg);
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) {
+        const int ct = w + 4 * jj;
+        if (ct >= nt1) continue;
+        const int col = ct * 16 + i16;
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq) {
+          const int rr = 4 * g + qq, m = m0 + rr;
+          const bool live = m < valid;
+          const float u = (live && a.rate1 > 0.f) ? dropout_u1(db, m, col) : 1.f;
+          const bool keep = live && u >= a.rate1;
+          G1[4 * jj + qq] = keep ? gg[4 * jj + qq] * ks : 0.f;
+          sA1[rr * L1S + col] = keep ? o[4 * jj + qq] * ks : 0.f;
+        }
+      }
+    }
+    __syncthreads();
+    pstamp(a, i, 3);
+    publish_rows16<H1>(rs, (int)a.o_a1 + m0 * H1, sA1, L1S);   // weight-gradient operand
+    // ---- FWD2: logits, the reduction split over the 4 waves (H1 / 16 k-steps each)
+    {
+      constexpr int PER = H1 / 16;
+      f32x4 acc = zero4f();
+      float av[PER], bv[PER];
+#pragma unroll
+      for (int s2 = 0; s2 < PER; ++s2) {
+        const int sx = w * PER + s2;
+        const int k = (sx >> 4) * 64 + 16 * g + (sx & 15);
+        av[s2] = sA1[i16 * L1S + k];
+        bv[s2] = sW2[k * S17 + i16];
+      }
+#pragma unroll
+      for (int s2 = 0; s2 < PER; ++s2) acc = mma(av[s2], bv[s2], acc);
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq) sRed[w * 256 + (4 * g + qq) * 16 + i16] = acc[qq];
+    }
+    __syncthreads();
+    {
+      const int rr = tid >> 4, c = tid & 15;
+      const float v = sRed[tid] + sRed[256 + tid] + sRed[512 + tid] + sRed[768 + tid];
+      sLg[rr * 36 + c] = c < C ? v + sB2[c] : 0.f;
+    }
+    __syncthreads();
+    // ---- loss / metrics -> dZ_2 = dL/dz (scaled by 1 / valid) in sLg
+    {
+      Prob pq;
+      pq.N = C;
+      pq.act = a.act2;
+      pq.loss = a.loss;
+      pq.nmet = a.nmet;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) pq.met[e] = a.met[e];
+      pq.Y = a.Y;
+      pq.pred = nullptr;
+      pq.sPred = 0;
+      pq.ldp = 0;
+      pq.chunk = 0;
+      pq.B = a.B;
+      const float inv_valid = 1.f / (float)valid;
+      float sums[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      if constexpr (FAST) {
+        if (w == 0) loss_tile_cce<4, 16, 36, 32>(pq, r, m0, sLg, sY, sRow, true, inv_valid, sums);
+      } else {
+        loss_tile_lds<16, 36, 32>(pq, r, m0, sLg, sY, sRow, true, inv_valid, sums);
+      }
+      if (a.acc && (!FAST || w == 0)) {
+#pragma unroll
+        for (int e = 0; e < 6; ++e) {
+          if (e < 2 + a.nmet) {
+            const float sv = row_sum<64>(sums[e]);
+            if (lane == 0 && sv != 0.f) atomicAdd(a.acc + (long long)r * a.acc_stride + e, (double)sv);
+          }
+        }
+      }
+    }
+    __syncthreads();
+    {
+      const int rr = tid >> 4, c = tid & 15;
+      sD2[rr * S17 + c] = c < C ? sLg[rr * 36 + c] : 0.f;
+    }
+    __syncthreads();
+    pstamp(a, i, 4);
+    publish_rows16<16>(rs, (int)a.o_dz2 + m0 * 16, sD2, S17);
+    // ---- DX2: dZ_1 = (dZ_2 . W2^T) * G_1 (reduction over the <= 16 logits)
+    {
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) {
+        const int ct = w + 4 * jj;
+        if (ct >= nt1) continue;
+        const int col = ct * 16 + i16;
+        float av[4], bv[4];
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+          const int c = 4 * ks + g;
+          av[ks] = sD2[i16 * S17 + c];
+          bv[ks] = sW2[col * S17 + c];
+        }
+        f32x4 acc = zero4f();
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) acc = mma(av[ks], bv[ks], acc);
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq) sD1[(4 * g + qq) * L1S + col] = acc[qq] * G1[4 * jj + qq];
+      }
+    }
+    __syncthreads();
+    publish_rows16<H1>(rs, (int)a.o_dz1 + m0 * H1, sD1, L1S);
+    // ---- DX1: dZ_0 = (dZ_1 . W1^T) * G_0 -> LDS, then published for the L0 tiles
+    {
+      f32x4 acc[2];
+      rows_mm<H1, L1S, 1, L1S>(sD1, sW1, w, nt0, acc, i16, g);
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) {
+        const int ct = w + 4 * jj;
+        if (ct >= nt0) continue;
+        const int col = ct * 16 + i16;
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq) {
+          const int rr = 4 * g + qq;
+          sZ0[rr * L0S + col] = acc[jj][qq] * sG0[rr * L0S + col];
+        }
+      }
+    }
+    __syncthreads();
+    publish_rows16<H0>(rs, (int)a.o_dz0 + m0 * H0, sZ0, L0S);
+    pstamp(a, i, 5);
+    publish(flag_at(a, r, PMF_BWD) + j, (unsigned)(i + 1));
+    pstamp(a, i, 6);
+
+    // ---- weight gradients of the owned layer-1 columns / layer-2 rows, update
+    if (!wait_all(a, flag_at(a, r, PMF_BWD), a.nch, (unsigned)(i + 1), 3u)) return;
+    pstamp(a, i, 7);
+    stage<H0 / 16>(rs, (int)a.o_a0, H0, BR, H0, uA0, L0S);
+#pragma unroll
+    for (int c = 0; c < PM_NTU; ++c) {
+      if (c < nown) {
+        const int col = (j + a.nch * c) * 16;
+        stage<1>(rs, (int)a.o_dz1 + col, H1, BR, 16, uD1 + c * 16, 33);
+        stage<1>(rs, (int)a.o_a1 + col, H1, BR, 16, uA1 + c * 16, 33);
+      }
+    }
+    stage<1>(rs, (int)a.o_dz2, 16, BR, 16, uD2, S17);
+    // rows BR..63 of the staging must be zero for the 64-deep reductions
+    for (int e = tid; e < (64 - BR) * L0S; e += 256) uA0[BR * L0S + e] = 0.f;
+    for (int e = tid; e < (64 - BR) * 33; e += 256) {
+      uD1[BR * 33 + e] = 0.f;
+      uA1[BR * 33 + e] = 0.f;
+    }
+    for (int e = tid; e < (64 - BR) * S17; e += 256) uD2[BR * S17 + e] = 0.f;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    pstamp(a, i, 8);
+    {
+      f32x4 dw[TU + 1];
+#pragma unroll
+      for (int u = 0; u <= TU; ++u) dw[u] = zero4f();
+#pragma unroll
+      for (int half = 0; half < 2; ++half) {
+        float xa[TU][8], zb[2][8], a1v[8], d2v[8];
+#pragma unroll
+        for (int h8 = 0; h8 < 8; ++h8) {
+          const int b = 16 * g + 8 * half + h8;
+          zb[0][h8] = uD1[b * 33 + i16];
+          zb[1][h8] = uD1[b * 33 + 16 + i16];
+#pragma unroll
+          for (int u = 0; u < TU; ++u) {
+            const int t = w + 4 * u;
+            xa[u][h8] = t < ndw1 ? uA0[b * L0S + (t / nown) * 16 + i16] : 0.f;
+          }
+          a1v[h8] = w2own ? uA1[b * 33 + w * 16 + i16] : 0.f;
+          d2v[h8] = uD2[b * S17 + i16];
+        }
+#pragma unroll
+        for (int h8 = 0; h8 < 8; ++h8) {
+#pragma unroll
+          for (int u = 0; u < TU; ++u) {
+            const int t = w + 4 * u;
+            if (t < ndw1) {
+              const int c = t - (t / nown) * nown;
+              dw[u] = mma(xa[u][h8], c ? zb[1][h8] : zb[0][h8], dw[u]);
+            }
+          }
+          if (w2own) dw[TU] = mma(a1v[h8], d2v[h8], dw[TU]);
+        }
+      }
+      // bias gradients: column sums of dZ_1 (owned columns) and dZ_2 over the batch rows
+      const float gb1 = col_sums(uD1, 33, nown * 16, sRed);   // in threads tid < 16 * nown
+      __syncthreads();
+      const float gb2 = col_sums(uD2, S17, C, sRed);
+      if (tid < C) sRed[512 + tid] = gb2;
+      __syncthreads();
+      float gb = 0.f;
+      if (b1own) gb = gb1;
+      else if (b2own) gb = sRed[512 + tid - 64];
+      const float gs = a.op.grad_scale;
+      float gv[NM];
+#pragma unroll
+      for (int u = 0; u <= TU; ++u)
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq) gv[4 * u + qq] = (u < TU || i16 < C) ? dw[u][qq] * gs : 0.f;
+      opt_update_v<NM>(a.op, wm, gv, ws0, ws1, it);
+      if (b1own || b2own) {
+        float bv[1] = {bm}, bg[1] = {gb * gs}, t0[1] = {bst0}, t1[1] = {bst1};
+        opt_update_v<1>(a.op, bv, bg, t0, t1, it);
+        bm = bv[0];
+        bst0 = t0[0];
+        bst1 = t1[0];
+      }
+    }
+    pstamp(a, i, 9);
+    const bool nxt = i + 1 < n && st.valid(a, i + 1) > 0;
+    if (!nxt) break;
+    // ---- publish the owned weights, gather everyone's into LDS for the next step
+#pragma unroll
+    for (int u = 0; u < TU; ++u) {
+      const int t = w + 4 * u;
+      if (t >= ndw1) continue;
+      const int rt = t / nown, c = t - rt * nown;
+      const int v = (rt * 16 + 4 * g) * H1 + i16;
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq) stw1(rs, v + qq * H1, (int)a.o_w1 + (j + a.nch * c) * 16, wm[4 * u + qq]);
+    }
+    if (w2own && i16 < C) {
+      const int v = (4 * g) * 16 + i16;
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq)
+        stw1(rs, v + qq * 16, (int)a.o_w2 + (j + a.nch * w) * 256, wm[4 * TU + qq]);
+    }
+    if (b1own) stw1(rs, b1n, (int)a.o_b1, bm);
+    if (b2own) stw1(rs, tid - 64, (int)a.o_b2, bm);
+    publish(flag_at(a, r, PMF_W) + j, (unsigned)(i + 1));
+    pstamp(a, i, 10);
+    if (!wait_all(a, flag_at(a, r, PMF_W), a.nch, (unsigned)(i + 1), 4u)) return;
+    pstamp(a, i, 11);
+    stage<H0 * H1 / 1024>(rs, (int)a.o_w1, H1, H0, H1, sW1, L1S);
+    stage<H1 / 64>(rs, (int)a.o_w2, 16, H1, 16, sW2, S17);
+    if (tid < H1 / 4) {
+      const f32x4 v = ldw4(rs, 4 * tid, (int)a.o_b1);
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq) sB1[4 * tid + qq] = a.bias1 ? v[qq] : 0.f;
+    } else if (tid >= 64 && tid < 68) {
+      const f32x4 v = ldw4(rs, 4 * (tid - 64), (int)a.o_b2);
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq) sB2[4 * (tid - 64) + qq] = (a.bias2 && 4 * (tid - 64) + qq < C) ? v[qq] : 0.f;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    pstamp(a, i, 12);
+  }
+
+  // ---- epilogue: owned masters, both weight-image parities, state
+  float* Wsh = a.Wsh + (long long)r * a.sWsh;
+  float* WTsh = a.WTsh + (long long)r * a.sWTsh;
+#pragma unroll
+  for (int u = 0; u < TU; ++u) {
+    const int t = w + 4 * u;
+    if (t >= ndw1) continue;
+    const int rt = t / nown, c = t - rt * nown;
+#pragma unroll
+    for (int qq = 0; qq < 4; ++qq) {
+      const int k = rt * 16 + 4 * g + qq, nn = (j + a.nch * c) * 16 + i16;
+      const long long pi = a.p_off1 + (long long)k * H1 + nn;
+      P[pi] = wm[4 * u + qq];
+      if (np > 0) S[pi] = ws0[4 * u + qq];
+      if (np > 1) S[a.op.s_plane + pi] = ws1[4 * u + qq];
+#pragma unroll
+      for (int par = 0; par < 2; ++par) {
+        Wsh[par * a.wsh_par + a.wsh_off[1] + (long long)k * a.Np[1] + nn] = wm[4 * u + qq];
+        WTsh[par * a.wtsh_par + a.wtsh_off[1] + (long long)nn * a.Kp[1] + k] = wm[4 * u + qq];
+      }
+    }
+  }
+  if (w2own && i16 < C) {
+#pragma unroll
+    for (int qq = 0; qq < 4; ++qq) {
+      const int k = (j + a.nch * w) * 16 + 4 * g + qq;
+      const long long pi = a.p_off2 + (long long)k * C + i16;
+      P[pi] = wm[4 * TU + qq];
+      if (np > 0) S[pi] = ws0[4 * TU + qq];
+      if (np > 1) S[a.op.s_plane + pi] = ws1[4 * TU + qq];
+#pragma unroll
+      for (int par = 0; par < 2; ++par) {
+        Wsh[par * a.wsh_par + a.wsh_off[2] + (long long)k * a.Np[2] + i16] = wm[4 * TU + qq];
+        WTsh[par * a.wtsh_par + a.wtsh_off[2] + (long long)i16 * a.Kp[2] + k] = wm[4 * TU + qq];
+      }
+    }
+  }
+  if (b1own || b2own) {
+    const long long pi = b1own ? a.p_off1 + (long long)H0 * H1 + b1n : a.p_off2 + (long long)H1 * C + (tid - 64);
+    P[pi] = bm;
+    if (np > 0) S[pi] = bst0;
+    if (np > 1) S[a.op.s_plane + pi] = bst1;
+  }
+}
+
+}  // namespace
+
+template <int H0, int H1, bool FAST>
+__global__ __launch_bounds__(256) void mlp_persist_kernel(PersistArgs a) {
+  __shared__ __attribute__((aligned(16))) float smem[LDS_FLOATS];
+  if (__hip_atomic_load((gu32*)(a.err), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) return;
+  const int b = blockIdx.x;
+  const int r = b % a.R, q = b / a.R;
+  const int nl0 = a.nk0 * a.nc0;
+  if (q < nl0) l0_role<H0>(a, smem, r, q / a.nc0, q - (q / a.nc0) * a.nc0, q);
+  else chain_role<H0, H1, FAST>(a, smem, r, q - nl0);
+}
+
+}  // namespace ea
+
+using namespace ea;
+
+extern "C" int ea_persist_lds_bytes() { return (int)(LDS_FLOATS * sizeof(float)); }
+
+// grid: R * wgs workgroups of 256 threads, every one resident (the host sizes the
+// grid to at most one workgroup per CU); hidden widths (64, 64) or (128, 128)
+extern "C" hipError_t ea_persist(const PersistArgs* a, hipStream_t s) {
+  if (a->nsteps <= 0) return hipSuccess;
+  bool fast = a->act2 == ACT_SOFTMAX && (a->loss == LOSS_CCE || a->loss == LOSS_SPARSE_CCE);
+  for (int i = 0; i < a->nmet; ++i)
+    fast = fast && (a->met[i] == MET_ACC_CAT || a->met[i] == MET_ACC_SPARSE || a->met[i] == LOSS_CCE ||
+                    a->met[i] == LOSS_SPARSE_CCE);
+  const dim3 grid(a->R * a->wgs);
+#define EA_PM(H0_, H1_)                                                                           \
+  if (fast) hipLaunchKernelGGL((mlp_persist_kernel<H0_, H1_, true>), grid, dim3(256), 0, s, *a);   \
+  else hipLaunchKernelGGL((mlp_persist_kernel<H0_, H1_, false>), grid, dim3(256), 0, s, *a);
+  if (a->H0 == 128 && a->H1 == 128) {
+    EA_PM(128, 128)
+  } else if (a->H0 == 64 && a->H1 == 64) {
+    EA_PM(64, 64)
+  } else {
+    return hipErrorInvalidValue;
+  }
+#undef EA_PM
+  return hipGetLastError();
+}

@@ -22,7 +22,7 @@ extern "C" int ea_gemm_tile_m(int cfg);
 extern "C" int ea_gemm_tile_n(int cfg);
 extern "C" void ea_gemm_init();
 extern "C" hipError_t ea_replica_average(float* P, long long sP, int R, long long n, float* out, int write_back,
-                                         hipStream_t s);
+                                         double scale, hipStream_t s);
 extern "C" hipError_t ea_axpby(const float* x, float* y, long long n, float alpha, float beta, hipStream_t s);
 extern "C" hipError_t ea_ps_sub(float* p, const float* d, long long n, float scale, int atomic, hipStream_t s);
 extern "C" hipError_t ea_poison_lds(unsigned pattern, hipStream_t s);
@@ -73,6 +73,8 @@ static ExecCfg parse_cfg(const py::dict& d) {
   c.thr_min_n = get<int>(d, "thr_min_n", 256);
   c.rowchain = get<int>(d, "rowchain", -1);
   c.rc_split = get<int>(d, "rc_split", 0);
+  c.persist = get<int>(d, "persist", -1);
+  c.persist_timeout_ms = get<long long>(d, "persist_timeout_ms", 2000);
   for (auto item : d["layers"].cast<py::list>()) {
     py::dict l = item.cast<py::dict>();
     LayerCfg lc;
@@ -179,6 +181,10 @@ PYBIND11_MODULE(_C, m) {
       .def("table_begins", &Executor::table_begins)
       .def("rowchain", &Executor::rowchain)
       .def("rowchain_split", &Executor::rowchain_split)
+      .def("persistent", &Executor::persistent)
+      .def("persist_geometry", &Executor::persist_geometry)
+      .def("persist_error", &Executor::persist_error)
+      .def("persist_clear_error", &Executor::persist_clear_error)
       .def("set_stamps", &Executor::set_stamps)
       .def("train_launch", [](Executor& e, int idx, uintptr_t s) { e.train_launch(idx, S(s)); })
       .def("grad_launches", &Executor::grad_launches)
@@ -225,10 +231,13 @@ PYBIND11_MODULE(_C, m) {
   m.def("tile_shape", [](int cfg) { return py::make_tuple(ea_gemm_tile_m(cfg), ea_gemm_tile_n(cfg)); });
 
   m.def("replica_average", [](uintptr_t P, long long sP, int R, long long n, uintptr_t out, int write_back,
-                              uintptr_t s) {
-    chk(ea_replica_average(reinterpret_cast<float*>(P), sP, R, n, reinterpret_cast<float*>(out), write_back, S(s)),
+                              uintptr_t s, double scale) {
+    // scale <= 0: the mean (1 / R); 1.0: the plain sum (the multi-rank averaging path)
+    chk(ea_replica_average(reinterpret_cast<float*>(P), sP, R, n, reinterpret_cast<float*>(out), write_back,
+                           scale > 0.0 ? scale : 1.0 / R, S(s)),
         "replica_average");
-  });
+  }, py::arg("P"), py::arg("sP"), py::arg("R"), py::arg("n"), py::arg("out"), py::arg("write_back"), py::arg("stream"),
+     py::arg("scale") = 0.0);
   m.def("axpby", [](uintptr_t x, uintptr_t y, long long n, float a, float b, uintptr_t s) {
     chk(ea_axpby(reinterpret_cast<const float*>(x), reinterpret_cast<float*>(y), n, a, b, S(s)), "axpby");
   });

@@ -16,6 +16,8 @@ extern "C" hipError_t ea_rowchain(const ea::RcArgs* a, int bf16, int nbw, hipStr
 extern "C" hipError_t ea_apply_update(ea::FlatArgs* a, int bf16, hipStream_t s);
 extern "C" hipError_t ea_refresh_shadows(ea::FlatArgs* a, int bf16, hipStream_t s);
 extern "C" hipError_t ea_advance(long long* ctr, const int* ntrain, int R, int B, int n, hipStream_t s);
+extern "C" hipError_t ea_persist(const ea::PersistArgs* a, hipStream_t s);
+extern "C" int ea_persist_lds_bytes();
 
 namespace ea {
 
@@ -35,6 +37,8 @@ Executor::Executor(const ExecCfg& cfg) : c_(cfg) {
   build();
   rc_.on = c_.rowchain != 0 && build_rowchain();
   if (c_.rowchain == 1 && !rc_) throw std::invalid_argument("row-chain plan requested but the model is not eligible");
+  pm_.on = c_.persist != 0 && build_persist();
+  if (c_.persist == 1 && !pm_.on) throw std::invalid_argument("persistent plan requested but the model is not eligible");
 }
 
 Executor::~Executor() {
@@ -42,6 +46,132 @@ Executor::~Executor() {
   if (d_probs_) (void)hipFree(d_probs_);
   if (d_zp_) (void)hipFree(d_zp_);
   if (d_zw_) (void)hipFree(d_zw_);
+  if (d_pws_) (void)hipFree(d_pws_);
+  if (d_pflags_) (void)hipFree(d_pflags_);
+  if (d_perr_) (void)hipFree(d_perr_);
+}
+
+// Persistent plan (persist.hip): 3 Dense layers, hidden widths 64 or 128, a last layer
+// of <= 16 units, fp32, B <= 64, and a grid of at most one workgroup per CU (every
+// workgroup must be resident: they wait for each other inside the launch).
+bool Executor::build_persist() {
+  const int L = (int)c_.layers.size();
+  if (c_.bf16 || L != 3) return false;
+  const LayerCfg &l0 = c_.layers[0], &l1 = c_.layers[1], &l2 = c_.layers[2];
+  // hidden widths (64, 64) or (128, 128): the kernel is compiled for those two shapes
+  if (!((l0.N == 64 && l1.N == 64) || (l0.N == 128 && l1.N == 128))) return false;
+  if (l1.K != l0.N || l2.K != l1.N || l2.N > PM_MAXC || c_.ldy > 32) return false;
+  if (c_.B > PM_ROWS || c_.B < 1) return false;
+  const int nch = cdiv(c_.B, 16);
+  if (cdiv(l1.N / 16, nch) > PM_NTU) return false;
+  int dev = 0, ncu = 0;
+  check(hipGetDevice(&dev), "hipGetDevice");
+  check(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev), "hipDeviceGetAttribute");
+  if (const char* e = std::getenv("ELEPHAS_AMD_PERSIST_CUS")) ncu = std::min(ncu, std::atoi(e));  // tests: a smaller grid
+  int lds_max = 0;
+  check(hipDeviceGetAttribute(&lds_max, hipDeviceAttributeMaxSharedMemoryPerBlock, dev), "hipDeviceGetAttribute");
+  if (ea_persist_lds_bytes() > lds_max) return false;
+  const int cap = std::min(ncu / c_.R - nch, PM_MAXWG);
+  if (cap < 1) return false;
+  // layer-0 tiles: the cheapest (kc0, cw) whose tile count fits; cost ~ the tile's
+  // MFMA work (FWD reduction padded to 64) + the partials every chain workgroup sums
+  int best_kc = 0, best_cw = 0;
+  long long best_cost = -1;
+  for (int cw : {16, 32}) {
+    if (l0.N % cw) continue;
+    const int nc0 = l0.N / cw;
+    for (int kc = 16; kc <= PM_MAXH; kc += 16) {
+      const int nk0 = cdiv(l0.K, kc);
+      if (nk0 * nc0 > cap || (kc / 16) * (cw / 16) > 16 || nk0 > RC_MAXSPLIT) continue;
+      const long long cost = (long long)(cdiv(std::min(kc, l0.K), 64) * 64 + kc) * cw + 512LL * nk0;
+      if (best_cost < 0 || cost < best_cost) { best_cost = cost; best_kc = kc; best_cw = cw; }
+    }
+  }
+  if (best_cost < 0) return false;
+  PersistArgs& a = pm_.args;
+  std::memset(&a, 0, sizeof(a));
+  a.R = c_.R; a.B = c_.B;
+  a.K0 = l0.K; a.H0 = l0.N; a.H1 = l1.N; a.C = l2.N;
+  a.kc0 = best_kc; a.cw = best_cw; a.nc0 = l0.N / best_cw; a.nk0 = cdiv(l0.K, best_kc);
+  a.nch = nch; a.wgs = a.nk0 * a.nc0 + nch;
+  a.act0 = l0.act; a.act1 = l1.act; a.act2 = l2.act;
+  a.rate0 = l0.rate; a.rate1 = l1.rate;
+  a.bias0 = l0.has_bias; a.bias1 = l1.has_bias; a.bias2 = l2.has_bias;
+  a.p_off0 = l0.p_off; a.p_off1 = l1.p_off; a.p_off2 = l2.p_off;
+  a.X = reinterpret_cast<const float*>(c_.X); a.sX = c_.sX; a.ldx = c_.ldx;
+  a.Y = reinterpret_cast<const float*>(c_.Y); a.sY = c_.sY; a.ldy = c_.ldy;
+  a.perm = reinterpret_cast<const int*>(c_.perm); a.sPerm = c_.sPerm;
+  a.ntrain = reinterpret_cast<const int*>(c_.ntrain);
+  a.P = reinterpret_cast<float*>(c_.P); a.sP = c_.sP;
+  a.S = reinterpret_cast<float*>(c_.S); a.sS = c_.sS;
+  a.op = c_.op;
+  a.Wsh = reinterpret_cast<float*>(c_.Wsh); a.sWsh = c_.sWsh; a.wsh_par = c_.wsh_par;
+  a.WTsh = reinterpret_cast<float*>(c_.WTsh); a.sWTsh = c_.sWTsh; a.wtsh_par = c_.wtsh_par;
+  for (int l = 0; l < 3; ++l) {
+    a.wsh_off[l] = c_.layers[l].wsh_off; a.wtsh_off[l] = c_.layers[l].wtsh_off;
+    a.Np[l] = c_.layers[l].Np; a.Kp[l] = c_.layers[l].Kp;
+  }
+  a.loss = c_.loss; a.nmet = c_.nmet;
+  for (int i = 0; i < 4; ++i) a.met[i] = c_.met[i];
+  a.acc = reinterpret_cast<double*>(c_.acc); a.acc_stride = c_.acc_stride;
+  a.ctr = reinterpret_cast<long long*>(c_.ctr);
+  a.seed = c_.seed;
+  // exchange workspace per replica (floats; every region 64-float aligned)
+  long long off = 0;
+  auto take = [&](long long n) { const long long o = off; off += (n + 63) / 64 * 64; return o; };
+  a.o_part = take((long long)a.nk0 * PM_ROWS * a.H0);
+  a.o_dz0 = take((long long)PM_ROWS * a.H0);
+  a.o_a0 = take((long long)PM_ROWS * a.H0);
+  a.o_a1 = take((long long)PM_ROWS * a.H1);
+  a.o_dz1 = take((long long)PM_ROWS * a.H1);
+  a.o_dz2 = take((long long)PM_ROWS * 16);
+  a.o_w1 = take((long long)a.H0 * a.H1);
+  a.o_w2 = take((long long)a.H1 * 16);
+  a.o_b1 = take(a.H1);
+  a.o_b2 = take(16);
+  a.ws_stride = off;
+  const size_t ws_bytes = sizeof(float) * (size_t)off * c_.R;
+  check(hipMalloc(&d_pws_, ws_bytes), "hipMalloc(persistent workspace)");
+  check(hipMemset(d_pws_, 0, ws_bytes), "hipMemset(persistent workspace)");
+  pm_.flag_bytes = sizeof(unsigned) * (size_t)c_.R * PMF_N * PM_MAXWG;
+  check(hipMalloc(&d_pflags_, pm_.flag_bytes), "hipMalloc(persistent flags)");
+  check(hipMemset(d_pflags_, 0, pm_.flag_bytes), "hipMemset(persistent flags)");
+  check(hipMalloc(&d_perr_, 256), "hipMalloc(persistent error word)");
+  check(hipMemset(d_perr_, 0, 256), "hipMemset(persistent error word)");
+  a.ws = d_pws_;
+  a.flags = d_pflags_;
+  a.err = d_perr_;
+  a.timeout = std::max<long long>(1, c_.persist_timeout_ms) * 100000LL;  // s_memrealtime: 100 MHz
+  return true;
+}
+
+std::vector<int> Executor::persist_geometry() const {
+  if (!pm_.on) return {};
+  const PersistArgs& a = pm_.args;
+  return {a.nk0, a.nc0, a.kc0, a.cw, a.nch, a.wgs, a.R * a.wgs};
+}
+
+unsigned Executor::persist_error() const {
+  if (!d_perr_) return 0;
+  unsigned v = 0;
+  check(hipMemcpy(&v, d_perr_, sizeof(v), hipMemcpyDeviceToHost), "hipMemcpy(persistent error word)");
+  return v;
+}
+
+void Executor::persist_clear_error() {
+  if (d_perr_) check(hipMemset(d_perr_, 0, 256), "hipMemset(persistent error word)");
+}
+
+void Executor::run_chunk(hipStream_t s, int nsteps) const {
+  if (pm_.on) {
+    // flags zeroed by a memset node ahead of every launch (tags restart at 1)
+    check(hipMemsetAsync(d_pflags_, 0, pm_.flag_bytes, s), "hipMemsetAsync(persistent flags)");
+    PersistArgs a = pm_.args;
+    a.nsteps = nsteps;
+    check(ea_persist(&a, s), "persistent step kernel");
+    return;
+  }
+  for (int i = 0; i < nsteps; ++i) run_step(s, i);
 }
 
 // Row-chain plan (rowchain.hip): 2 <= L <= RC_MAXL Dense layers, every layer but
@@ -586,6 +716,7 @@ void Executor::set_stamps(uintptr_t buf) {
     for (auto& L : *v) L.ga.stamps = p;
   rc_.ta_fwd.stamps = rc_.ta_dw.stamps = rc_.ta_grad.stamps = p;
   rc_.rc.stamps = p;
+  pm_.args.stamps = p;
 }
 
 std::vector<int> Executor::launch_blocks() const {
@@ -618,7 +749,7 @@ std::vector<int> Executor::launch_cfgs() const {
 }
 
 void Executor::train_step(hipStream_t s) {
-  run_step(s, 0);
+  run_chunk(s, 1);
   advance(1, s);
 }
 
@@ -716,7 +847,7 @@ int Executor::capture(int nsteps, int mode, hipStream_t s) {
   try {
     if (mode == 0) {
       // one chunk: steps at offsets 0..nsteps-1 from the counter base, then one advance
-      for (int i = 0; i < nsteps; ++i) run_step(s, i);
+      run_chunk(s, nsteps);
       advance(nsteps, s);
     } else {
       for (int i = 0; i < nsteps; ++i) {

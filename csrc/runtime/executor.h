@@ -9,6 +9,9 @@
 //   row-chain plan  (small MLPs, csrc/kernels/rowchain.hip; 3 launches):
 //                   [layer-0 split-K slabs + gather X^T] [row chain: layers 1..L-1
 //                   forward, loss, dZ_{L-1} .. dZ_0] [DW of every layer]
+//   persistent plan (3-layer MLPs with 64/128-wide hidden layers, fp32;
+//                   csrc/kernels/persist.hip): a whole chunk of steps in ONE launch
+//                   (+ a flag memset node and the counter advance)
 //
 // The step reads its batch index, dropout counter and optimizer iteration from
 // device counters, so one captured hipGraph of a step is replayed for every
@@ -64,6 +67,8 @@ struct ExecCfg {
   int rc_lean = 1;     // skip the update of layer 0's row-major weight image (no reader)
   int split_dwdx = 0;  // DW_l and DX_l in separate launches whenever their preferred tiles differ
   int rc_split = 0;    // layer-0 split-K slabs of the row-chain plan (0 = auto)
+  int persist = -1;    // persistent chunk kernel (persist.hip): -1 when eligible, 0 off, 1 required
+  long long persist_timeout_ms = 2000;  // spin limit of its in-launch waits
 };
 
 struct EvalSource {
@@ -100,6 +105,12 @@ class Executor {
   // launches per step (a captured chunk adds one 1-block counter advance)
   int launches_per_step() const { return rc_.on ? 3 : (int)fwd_.size() + (int)bwd_.size(); }
   bool rowchain() const { return rc_.on; }
+  bool persistent() const { return pm_.on; }
+  // persistent plan: {L0 k-chunks, L0 column blocks, k-chunk rows, block columns, chain
+  // workgroups, workgroups per replica, grid}
+  std::vector<int> persist_geometry() const;
+  unsigned persist_error() const;  // sticky error word (a timed-out in-launch wait), synchronous read
+  void persist_clear_error();
   int rowchain_split() const { return rc_.on ? rc_.nsplitk : 0; }
   std::vector<int> launch_cfgs() const;
   // diagnostics: bind a [blocks_max][16] int64 buffer for in-kernel stamps (0 = off)
@@ -136,6 +147,16 @@ class Executor {
   mutable float* d_zw_ = nullptr;  // (allocated by the const plan builder) wide last layer split-K logit slabs [R][ks][B][N_last]
   bool build_rowchain();
   void run_rowchain(hipStream_t s, int step_off, bool grad) const;
+  struct Persist {
+    bool on = false;
+    PersistArgs args{};
+    size_t flag_bytes = 0;
+  } pm_;
+  float* d_pws_ = nullptr;         // persistent plan: per-replica exchange workspace
+  unsigned* d_pflags_ = nullptr;   // [R][PMF_N][PM_MAXWG] flags (zeroed before every launch)
+  unsigned* d_perr_ = nullptr;     // sticky error word
+  bool build_persist();
+  void run_chunk(hipStream_t s, int nsteps) const;   // nsteps training steps (no counter advance)
   void run_step(hipStream_t s, int step_off) const;
   std::vector<std::pair<hipGraph_t, hipGraphExec_t>> graphs_;
 

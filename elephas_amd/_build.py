@@ -28,6 +28,7 @@ SOURCES = [
     "kernels/gemm_f32.hip",
     "kernels/flat.hip",
     "kernels/rowchain.hip",
+    "kernels/persist.hip",
     "kernels/peer.hip",
     "runtime/executor.cpp",
     "runtime/peer.cpp",

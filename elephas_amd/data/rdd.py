@@ -167,6 +167,15 @@ class ColumnarPartition:
         return f"ColumnarPartition({len(self)} rows)"
 
 
+def _owned_frozen(a):
+    """A read-only copy owned by the partition (the native trainer cache may then keep
+    its uploaded shard for as long as the partition lives: worker._DataKey)."""
+    import numpy as np
+    out = np.array(a, copy=True, order="C")
+    out.setflags(write=False)
+    return out
+
+
 def _columnar(parts) -> bool:
     return bool(parts) and all(isinstance(p, ColumnarPartition) for p in parts)
 
@@ -237,8 +246,8 @@ class RDD:
             import numpy as np
             x = np.concatenate([p.x for p in self._parts]) if len(self._parts) > 1 else self._parts[0].x
             y = np.concatenate([p.y for p in self._parts]) if len(self._parts) > 1 else self._parts[0].y
-            return RDD([ColumnarPartition(np.ascontiguousarray(x[i::n]), np.ascontiguousarray(y[i::n]))
-                        for i in range(n)], self.ctx)
+            return RDD([ColumnarPartition(_owned_frozen(x[i::n]), _owned_frozen(y[i::n])) for i in range(n)],
+                       self.ctx)
         parts = [[] for _ in range(n)]
         for i, x in enumerate(itertools.chain.from_iterable(self._parts)):
             parts[i % n].append(x)

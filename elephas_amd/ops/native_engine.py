@@ -34,6 +34,16 @@ from .plan import flatten_weights
 from .trainer import TrainerBase, prepare_features, prepare_targets, split_point
 
 
+def _gpu_shared() -> bool:
+    """More local ranks than visible GPUs (the single-GPU multi-rank rehearsals): ranks
+    share a device, so a persistent grid cannot count on owning every CU."""
+    try:
+        local = int(os.environ.get("LOCAL_WORLD_SIZE", "1"))
+        return local > max(1, torch.cuda.device_count())
+    except ValueError:
+        return False
+
+
 def pad8(n: int) -> int:
     return (int(n) + 7) // 8 * 8
 
@@ -44,12 +54,20 @@ class NativeTrainer(TrainerBase):
     GRAPH_CHUNK = 1 << (max(1, int(os.environ.get("ELEPHAS_AMD_GRAPH_CHUNK", "16"))).bit_length() - 1)
 
     def __init__(self, model, plan, R: int = 1, batch_size: int = 32, device=None, seed: Optional[int] = None,
-                 policy: Optional[str] = None, eval_batch: int = 2048, rowchain: Optional[int] = None):
+                 policy: Optional[str] = None, eval_batch: int = 2048, rowchain: Optional[int] = None,
+                 persist: Optional[int] = None):
         super().__init__(model, plan, R, batch_size)
         self.C = native.require()
         # row-chain step plan (3 launches, csrc/kernels/rowchain.hip): None ->
         # $ELEPHAS_AMD_ROWCHAIN (default -1: whenever the model is eligible), 0 off, 1 required
         self.rowchain_mode = int(os.environ.get("ELEPHAS_AMD_ROWCHAIN", "-1")) if rowchain is None else int(rowchain)
+        # persistent chunk kernel (csrc/kernels/persist.hip): None -> $ELEPHAS_AMD_PERSIST
+        # (default -1: whenever eligible), 0 off, 1 required.  It keeps a whole cluster of
+        # workgroups per replica resident and waiting on each other, so two processes
+        # sharing one GPU must turn it off (their grids could not both be resident)
+        self.persist_mode = int(os.environ.get("ELEPHAS_AMD_PERSIST", "-1")) if persist is None else int(persist)
+        if persist is None and self.persist_mode < 0 and _gpu_shared():
+            self.persist_mode = 0
         if not plan.native_ok:
             raise ValueError(f"model is not supported by the native engine: {plan.reason}")
         self.dev = torch.device(device) if device is not None else config.get_device()
@@ -153,6 +171,8 @@ class NativeTrainer(TrainerBase):
             thr_min_k=int(os.environ.get("ELEPHAS_AMD_THR_MIN_K", "64")),
             thr_min_n=int(os.environ.get("ELEPHAS_AMD_THR_MIN_N", "256")),
             rowchain=self.rowchain_mode if ws is self.ws else 0,
+            persist=self.persist_mode if ws is self.ws else 0,
+            persist_timeout_ms=int(os.environ.get("ELEPHAS_AMD_PERSIST_TIMEOUT_MS", "2000")),
             rc_split=int(os.environ.get("ELEPHAS_AMD_RC_SPLIT", "0")),
             layers=layers,
             X=self.X.data_ptr(), sX=self.nmax * self.Kp0, ldx=self.Kp0,
@@ -210,20 +230,31 @@ class NativeTrainer(TrainerBase):
     def get_weights_flat(self):
         return self._host(self.P)
 
-    def average_replicas(self, allreduce=None, world: int = 1):
-        """Reference synchronous averaging (spark_model.py:221-227) on the device: the mean
-        of the R replicas (one kernel, fp64 accumulation), optionally summed over ranks by
-        ``allreduce`` and divided by ``world``, then written back into every replica's
-        master and both weight-image parities (one kernel)."""
+    def average_replicas(self, allreduce=None, n_total: Optional[int] = None, include: bool = True):
+        """Reference synchronous averaging (spark_model.py:221-227) on the device, the one
+        implementation the bench and ``SparkModel`` share: theta <- (1/n_total) * sum of
+        every worker's theta_i.  This rank's R replicas are summed by one kernel (fp64
+        accumulation; ``include=False``: a rank without partitions contributes zeros),
+        summed over ranks by ``allreduce`` (issued on this trainer's stream, so every
+        read of the sum is stream-ordered after it), scaled, and written back into every
+        replica's master and both weight-image parities by one kernel.  No host sync.
+        Returns the mean as a device tensor valid in this trainer's stream order."""
+        n_total = int(n_total or self.R)
         with torch.cuda.stream(self.stream):
             avg = getattr(self, "_avg_buf", None)
             if avg is None or avg.numel() != self.n:
                 avg = self._avg_buf = torch.empty(self.n, dtype=torch.float32, device=self.dev)
-            self.C.replica_average(self.P.data_ptr(), self.P.stride(0), self.R, self.n, avg.data_ptr(), 0, self.s)
-            if allreduce is not None and world > 1:
+            if include:
+                scale = 1.0 if allreduce is not None else 1.0 / n_total
+                self.C.replica_average(self.P.data_ptr(), self.P.stride(0), self.R, self.n, avg.data_ptr(), 0,
+                                       self.s, scale)
+            else:
+                avg.zero_()
+            if allreduce is not None:
                 allreduce(avg)
-                avg.mul_(1.0 / world)
+                avg.mul_(1.0 / n_total)
             self.exe.refresh_from(avg.data_ptr(), 0, self.s)
+        return avg
 
     def reset_for_fit(self, flat, seed: Optional[int] = None):
         """Reuse this trainer (buffers, uploaded shards, eval executor) for a new fit the
@@ -545,7 +576,18 @@ class NativeTrainer(TrainerBase):
     def _host(self, t: torch.Tensor) -> np.ndarray:
         """Device -> host read ordered after everything queued on the executor stream."""
         self.stream.synchronize()
+        self.check()
         return t.detach().cpu().numpy().copy()
+
+    def check(self):
+        """Raise if a persistent-plan launch gave up waiting inside the kernel (its sticky
+        error word; every later launch of the executor then does nothing)."""
+        if self.exe is not None and self.exe.persistent():
+            e = self.exe.persist_error()
+            if e:
+                raise RuntimeError(f"persistent step kernel: an in-launch wait timed out (code {e}); "
+                                   "the GPU was shared or a workgroup was not resident -- set "
+                                   "ELEPHAS_AMD_PERSIST=0 to use the 3-launch row-chain plan")
 
     # ------------------------------------------------------------------- eval
     def _eval_src(self, x: np.ndarray, y: Optional[np.ndarray], want_pred: bool):
@@ -615,6 +657,20 @@ class NativeTrainer(TrainerBase):
 
     def launch_count(self) -> int:
         return self.exe.launches_per_step()
+
+    @property
+    def persistent(self) -> bool:
+        """True when training chunks run the persistent kernel (one launch per chunk)."""
+        return bool(self.exe.persistent())
+
+    def plan_name(self) -> str:
+        if self.exe.persistent():
+            nk0, nc0, kc0, cw, nch, wgs, grid = self.exe.persist_geometry()
+            return (f"persistent (1 launch per <= {self.GRAPH_CHUNK}-step chunk; per replica {nk0}x{nc0} "
+                    f"layer-0 tiles of {kc0}x{cw} + {nch} row-chain workgroups; grid {grid})")
+        if self.exe.rowchain():
+            return "row-chain (3 launches per step)"
+        return f"grouped ({self.exe.launches_per_step()} launches per step)"
 
     @property
     def rowchain(self) -> bool:

@@ -39,8 +39,8 @@ class PeerAllReduce:
     """
 
     def __init__(self, rank: Optional[int] = None, world: Optional[int] = None, device: Optional[int] = None,
-                 cap_elems: Optional[int] = None, allgather: Optional[Callable] = None, timeout_s: float = 20.0,
-                 verify: bool = True):
+                 cap_elems: Optional[int] = None, allgather: Optional[Callable] = None,
+                 timeout_s: Optional[float] = None, verify: bool = True):
         from ..ops import native
         self.C = native.require()
         self.rank = dist.rank() if rank is None else int(rank)
@@ -49,6 +49,9 @@ class PeerAllReduce:
         cap = cap_elems or int(os.environ.get("ELEPHAS_AMD_P2P_CAP_ELEMS", str(4 << 20)))
         self.max_bytes = int(os.environ.get("ELEPHAS_AMD_P2P_MAX_BYTES", str(64 << 20)))
         gather = allgather or dist.all_gather_object
+        # a peer wait gives up after timeout_s (error word + NaN-poisoned output, raised by
+        # check()); well above any expected rank skew (a checkpoint write, uneven shards)
+        timeout_s = float(os.environ.get("ELEPHAS_AMD_P2P_TIMEOUT_S", "60")) if timeout_s is None else timeout_s
         # every step is voted on by all ranks, so a rank whose allocation / IPC mapping
         # fails never leaves its peers waiting in a kernel for it
         self.impl, handle = None, b""
@@ -74,6 +77,16 @@ class PeerAllReduce:
                 self.ok = self._self_test(allgather)
         self._tmp = None
         self._bar = None
+        self._last_stream = None
+
+    def _order_after_last(self, s) -> None:
+        """Calls on one instance must reach the device in issue order on every rank (the
+        epoch / parity protocol of peer.hip and the shared alignment buffer assume it): a
+        call on another stream than the previous one waits for that stream first."""
+        last = self._last_stream
+        if last is not None and last != s:
+            s.wait_stream(last)
+        self._last_stream = s
 
     def _self_test(self, allgather) -> bool:
         """One-shot and two-shot all-reduce of known vectors on every rank, then a vote:
@@ -105,6 +118,7 @@ class PeerAllReduce:
         if not self.eligible(t):
             raise ValueError("PeerAllReduce: needs a contiguous fp32 CUDA tensor within max_bytes")
         s = stream or torch.cuda.current_stream(t.device)
+        self._order_after_last(s)
         n = t.numel()
         if t.data_ptr() % 16:   # the kernels move 16-byte vectors: go through an aligned copy
             with torch.cuda.stream(s):
@@ -125,6 +139,7 @@ class PeerAllReduce:
         if not (self.eligible(t) and t.data_ptr() % 16 == 0):
             raise ValueError("all_reduce_graph_: needs a 16-byte aligned contiguous fp32 CUDA tensor")
         s = stream or torch.cuda.current_stream(t.device)
+        self._order_after_last(s)
         self.impl.all_reduce_graph(t.data_ptr(), t.data_ptr(), t.numel(), s.cuda_stream, algo)
         return t
 
@@ -133,6 +148,7 @@ class PeerAllReduce:
         if self._bar is None:
             self._bar = torch.zeros(4, dtype=torch.float32, device=f"cuda:{self.device}")
         s = torch.cuda.current_stream(self.device)
+        self._order_after_last(s)
         self.impl.all_reduce(self._bar.data_ptr(), self._bar.data_ptr(), 4, s.cuda_stream, 0)
         s.synchronize()
         if self.impl.error():

@@ -300,17 +300,24 @@ class SparkModel:
         theta0 - sum(delta_i)/N), written back into every local replica."""
         fault.maybe_inject("allreduce", dist.rank())
         with self._timer.phase("allreduce"):
+            if hasattr(trainer, "average_replicas"):
+                # native engine: the bench's device path (NativeTrainer.average_replicas),
+                # all-reduce ordered on the trainer's stream
+                multi = dist.world_size() > 1
+                mean = trainer.average_replicas(dist.all_reduce_sum_ if multi else None, max(n_parts, 1),
+                                                include=bool(active_local))
+                if multi:
+                    trainer.stream.synchronize()
+                    from .parallel import p2p
+                    peer = p2p.current()
+                    if peer is not None:
+                        peer.check()   # a timed-out peer wait must not pass as a mean
+                return mean
             total = self._sum_replicas(trainer, n_params) if active_local else self._zeros(n_params)
             dist.all_reduce_sum_(total)
             mean = total / float(max(n_parts, 1))
         if active_local:
-            if hasattr(trainer, "P"):
-                import torch
-                with torch.cuda.stream(trainer.stream):
-                    trainer.P.copy_(mean.to(trainer.P.device).expand_as(trainer.P))
-                    trainer.sync_shadows()
-            else:
-                trainer.set_weights_flat(mean.cpu().numpy())
+            trainer.set_weights_flat(mean.cpu().numpy())
         return mean
 
     def _zeros(self, n):

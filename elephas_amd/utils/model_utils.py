@@ -5,12 +5,12 @@ Public contract of reference elephas/utils/model_utils.py:9-70 (``ModelType``,
 ``as_enum``); the ``{"__enum__": "ModelType.X"}`` JSON form is what saved
 ElephasTransformer files hold, so it is kept byte-compatible.
 
-The table is not hand-maintained: it is derived from the loss registry
-(models/losses.py, names and aliases): cross-entropy, hinge and KL-divergence
-losses are classification losses, every other registered loss a regression loss
-(the reference lists 11 names and answers None for the rest; for those it agrees
-with the reference's use of the answer, where None falls into the classification
-branch).  ``register_loss`` adds or overrides entries (custom losses).
+The default table holds exactly the reference's eleven loss names (regression: the
+squared / absolute / percentage / logarithmic errors, log-cosh and cosine proximity;
+classification: the three cross-entropies) and answers None for every other loss,
+as the reference does: callers treat None like a classification loss (the full
+output vector is kept), so a multi-output model trained with e.g. 'poisson' keeps
+all its prediction columns.  ``register_loss`` adds or overrides entries.
 """
 from __future__ import annotations
 
@@ -24,19 +24,14 @@ class ModelType(Enum):
     REGRESSION = 2
 
 
-# aliases the reference table lists that are not names in our loss registry
-_EXTRA_REGRESSION = ("cosine_proximity",)
+_REGRESSION_LOSSES = ("mean_squared_error", "mean_absolute_error", "mse", "mae", "cosine_proximity",
+                      "mean_absolute_percentage_error", "mean_squared_logarithmic_error", "logcosh")
+_CLASSIFICATION_LOSSES = ("binary_crossentropy", "categorical_crossentropy", "sparse_categorical_crossentropy")
 
 
 def _default_table() -> Dict[str, ModelType]:
-    from ..models import losses
-    table = {}
-    for name in losses.registered_names():
-        canon = losses.canonical(name).lower()
-        classify = any(k in canon for k in ("crossentropy", "hinge", "kullback"))
-        table[name] = ModelType.CLASSIFICATION if classify else ModelType.REGRESSION
-    for name in _EXTRA_REGRESSION:
-        table.setdefault(name, ModelType.REGRESSION)
+    table = dict.fromkeys(_REGRESSION_LOSSES, ModelType.REGRESSION)
+    table.update(dict.fromkeys(_CLASSIFICATION_LOSSES, ModelType.CLASSIFICATION))
     return table
 
 

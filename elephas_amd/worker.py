@@ -52,21 +52,42 @@ def _build_model(json_str, custom_objects, optimizer, loss, metrics, weights):
     return model
 
 
+def _frozen(a: np.ndarray) -> bool:
+    """True when no one can write a's bytes: a and every array it views are read-only."""
+    while isinstance(a, np.ndarray):
+        if a.flags.writeable:
+            return False
+        a = a.base
+    return True
+
+
+class _DataKey:
+    """Identity of a rank's partitions for the trainer cache.  Uploaded shards are
+    reused only for the very same array objects (held here, so their ids and buffers
+    cannot be recycled by the allocator) that are frozen -- read-only down the whole
+    view chain, as the columnar partitions ``RDD.repartition`` builds -- so no in-place
+    edit can go unseen.  Writable arrays never match: their shards are re-uploaded."""
+
+    __slots__ = ("arrays", "meta", "reusable")
+
+    def __init__(self, xs, ys, vs, active, shuffle):
+        self.arrays = tuple(np.asarray(a) for a in list(xs) + list(ys))
+        self.meta = (float(vs), tuple(bool(a) for a in active), bool(shuffle))
+        self.reusable = all(a.size == 0 or _frozen(a) for a in self.arrays)
+
+    def __eq__(self, other):
+        return (isinstance(other, _DataKey) and self.reusable and other.reusable and self.meta == other.meta
+                and len(self.arrays) == len(other.arrays)
+                and all(a is b for a, b in zip(self.arrays, other.arrays)))
+
+    def __ne__(self, other):
+        return not self.__eq__(other)
+
+    __hash__ = None
+
+
 def _data_key(xs, ys, vs, active, shuffle):
-    """Identity of a rank's partitions for the trainer cache: the arrays' objects, buffer
-    addresses and shapes plus a strided sample of their contents (cheap; catches the
-    common in-place edits of a dataset between fits, not every possible one)."""
-    key = [float(vs), tuple(bool(a) for a in active), bool(shuffle)]
-    for a in list(xs) + list(ys):
-        a = np.asarray(a)
-        if a.size == 0:
-            key.append((a.shape,))
-            continue
-        flat = a.reshape(-1)
-        step = max(1, flat.size // 4096)
-        key.append((id(a), a.__array_interface__["data"][0], a.shape, a.dtype.str,
-                    hash(np.ascontiguousarray(flat[::step]).tobytes()), hash(flat[-64:].tobytes())))
-    return tuple(key)
+    return _DataKey(xs, ys, vs, active, shuffle)
 
 
 class _TrainerCache:

@@ -129,3 +129,28 @@ def test_columnar_partitions_match_row_partitions():
     xs, ys = col.repartition(4).to_arrays()
     assert sorted(map(tuple, xs.tolist())) == sorted(map(tuple, x.tolist()))
     assert col.map(lambda r: r[1]).collect() == list(y)
+
+
+def test_trainer_cache_data_key_is_exact():
+    """Shards are reused only for the same frozen arrays (an in-place edit of
+    a writable array, or a new array at a recycled address, must never hit the cache)."""
+    from elephas_amd.worker import _data_key
+    from elephas_amd.data.rdd import RDD
+    x = np.arange(40, dtype=np.float32).reshape(20, 2)
+    y = np.arange(20, dtype=np.float32)
+    k1 = _data_key([x], [y], 0.1, [True], True)
+    assert k1 != _data_key([x], [y], 0.1, [True], True)      # writable: never reused
+    parts = RDD.from_arrays(x, y, 2).repartition(2).partitions()
+    xs, ys = [p.x for p in parts], [p.y for p in parts]
+    assert not xs[0].flags.writeable
+    with pytest.raises(ValueError):
+        xs[0][0, 0] = 1.0                                       # frozen partitions
+    a = _data_key(xs, ys, 0.1, [True, True], True)
+    assert a == _data_key(xs, ys, 0.1, [True, True], True)
+    assert a != _data_key(xs, ys, 0.2, [True, True], True)
+    copies = [np.array(v) for v in xs]
+    for c in copies:
+        c.setflags(write=False)
+    assert a != _data_key(copies, ys, 0.1, [True, True], True)  # equal bytes, other objects
+    x[0, 0] = 99.0                                              # the source edit does not reach
+    assert parts[0].x[0, 0] == 0.0                              # the owned partition copy

@@ -22,7 +22,8 @@ def _run(scenario, world=2, timeout=150, env_extra=None):
     procs = []
     for r in range(world):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
-                   MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
+                   MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0",
+                   ELEPHAS_AMD_PERSIST="0")   # ranks share the GPU: no persistent grids
         env.update(env_extra or {})
         cmd = [sys.executable, "-u", os.path.join(HERE, "_peer_worker.py"), scenario]
         prof = os.environ.get("ELEPHAS_AMD_PEER_PROF_DIR")   # tools: kernel trace of rank 0

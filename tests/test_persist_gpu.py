@@ -1,0 +1,184 @@
+"""Persistent chunk kernel (csrc/kernels/persist.hip) against the fp32 torch engine and
+against the 3-launch row-chain plan (GPU only).
+
+The kernel runs a whole chunk of training steps in one launch with each replica's
+workgroups handing activations, gradients and weights to each other inside the launch,
+so besides the math these tests pin the hand-offs: every step of every replica must
+see the previous step's updated weights (a stale read shows up as a weight gap far
+above fp32 rounding), partial batches and replicas that run out of data early must
+behave as in the other plans, and the chunking (graph chunks vs one-step launches)
+must not change a single bit.
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _mlp(in_dim, hidden, out, act="relu", out_act="softmax", dropout=0.0):
+    from elephas_amd.models import Sequential, Dense, Dropout, Activation
+    m = Sequential()
+    m.add(Dense(hidden[0], input_dim=in_dim))
+    m.add(Activation(act))
+    if dropout:
+        m.add(Dropout(dropout))
+    for h in hidden[1:]:
+        m.add(Dense(h, activation=act))
+        if dropout:
+            m.add(Dropout(dropout))
+    m.add(Dense(out, activation=out_act))
+    return m
+
+
+def _shards(sizes, d, k, seed=0, regression=False):
+    rng = np.random.default_rng(seed)
+    xs, ys = [], []
+    for n in sizes:
+        xs.append(rng.random((n, d), dtype=np.float32))
+        if regression:
+            ys.append(rng.normal(size=(n, k)).astype(np.float32))
+        else:
+            ys.append(np.eye(k, dtype=np.float32)[rng.integers(0, k, n)])
+    return xs, ys
+
+
+def _trainer(model, R, B, persist, seed=12345, rowchain=None):
+    from elephas_amd import config
+    from elephas_amd.ops.plan import build_plan
+    from elephas_amd.ops.native_engine import NativeTrainer
+    config.set_policy("float32")
+    return NativeTrainer(model, build_plan(model), R, B, torch.device("cuda"), seed=seed, persist=persist,
+                         rowchain=rowchain)
+
+
+@pytest.mark.parametrize("opt", ["sgd", "sgd_mom", "adam"])
+def test_persist_matches_fp32_reference_with_same_masks(opt):
+    """Persistent plan == fp32 torch autograd with the same dropout masks (2 replicas,
+    3 steps per epoch, 2 epochs: every hand-off of every step is exercised)."""
+    from elephas_amd.models import initializers, optimizers as O
+    from elephas_amd.ops.plan import build_plan
+    from elephas_amd.ops.torch_engine import TorchTrainer
+    initializers.set_seed(31)
+    model = _mlp(40, [64, 64], 6, dropout=0.3)
+    optim = {"sgd": O.SGD(0.2), "sgd_mom": O.SGD(0.05, momentum=0.9, nesterov=True),
+             "adam": O.Adam(0.003)}[opt]
+    model.compile(optim, "categorical_crossentropy", ["acc"])
+    xs, ys = _shards([96, 96], 40, 6, seed=3)
+    nat = _trainer(model, 2, 32, persist=1)
+    assert nat.persistent
+    ref = TorchTrainer(model, build_plan(model), 2, 32, torch.device("cuda"), hash_dropout_seed=12345)
+    w0 = nat.get_weights_flat()[0].copy()
+    for t in (nat, ref):
+        t.set_data(xs, ys, 0.0, shuffle=False)
+    hn = nat.fit(2)
+    hr = ref.fit(2)
+    wn, wr = nat.get_weights_flat(), ref.get_weights_flat()
+    step = np.abs(wr - w0).max()
+    if opt == "adam":   # adaptive rule: near-zero gradients amplify fp32 rounding
+        err = np.abs(wn - wr).mean() / np.abs(wr - w0).mean()
+        assert err < 1e-3, err
+    else:
+        err = np.abs(wn - wr).max() / step
+        assert err < 1e-4, err
+    for a, b in zip(hn, hr):
+        np.testing.assert_allclose(a["loss"], b["loss"], rtol=1e-4)
+        np.testing.assert_allclose(a["acc"], b["acc"], atol=1e-6)
+
+
+def test_persist_mnist_matches_rowchain_plan():
+    """The MNIST shape of the headline (784-128-128-10, dropout 0.2, B = 64) with a
+    validation split, shuffling, a partial last batch and a replica that runs out of
+    batches early: persistent plan == row-chain plan within fp32 summation order."""
+    from elephas_amd.models import initializers
+    from elephas_amd.models.optimizers import SGD
+    initializers.set_seed(2024)
+    model = _mlp(784, [128, 128], 10, dropout=0.2)
+    model.compile(SGD(learning_rate=0.1), "categorical_crossentropy", ["acc"])
+    xs, ys = _shards([300, 130, 40], 784, 10, seed=11)
+    out = []
+    for persist in (1, 0):
+        t = _trainer(model, 3, 64, persist=persist, seed=7, rowchain=1)
+        assert t.persistent == bool(persist)
+        t.set_data(xs, ys, 0.1, shuffle=True)
+        torch.manual_seed(5)   # epoch shuffles draw from the global CUDA generator
+        h = t.fit(2)
+        out.append((t.get_weights_flat(), h, t.evaluate(xs[0], ys[0])))
+    (wp, hp, ep), (wr, hr, er) = out
+    scale = np.abs(wr).max()
+    assert np.abs(wp - wr).max() <= 1e-4 * scale, (np.abs(wp - wr).max(), scale)
+    for a, b in zip(hp, hr):
+        for key in a:
+            np.testing.assert_allclose(a[key], b[key], rtol=5e-4, atol=5e-4)
+    # the weight images written back at the end of the launch serve evaluation
+    np.testing.assert_allclose(ep, er, rtol=1e-4, atol=1e-5)
+
+
+def test_persist_regression_generic_loss_matches_reference():
+    """Generic loss epilogue (mse, linear output, mae metric), one output unit, SGD
+    with momentum (a state plane), 64-wide hidden layers, 4 replicas of B = 32."""
+    from elephas_amd.models import initializers
+    from elephas_amd.models.optimizers import SGD
+    from elephas_amd.ops.plan import build_plan
+    from elephas_amd.ops.torch_engine import TorchTrainer
+    initializers.set_seed(5)
+    model = _mlp(13, [64, 64], 1, out_act="linear")
+    model.compile(SGD(0.01, momentum=0.9), "mse", ["mae"])
+    xs, ys = _shards([100, 77, 64, 33], 13, 1, seed=4, regression=True)
+    nat = _trainer(model, 4, 32, persist=1)
+    assert nat.persistent
+    ref = TorchTrainer(model, build_plan(model), 4, 32, torch.device("cuda"))
+    w0 = nat.get_weights_flat()[0].copy()
+    for t in (nat, ref):
+        t.set_data(xs, ys, 0.0, shuffle=False)
+    hn, hr = nat.fit(3), ref.fit(3)
+    wn, wr = nat.get_weights_flat(), ref.get_weights_flat()
+    err = np.abs(wn - wr).max() / np.abs(wr - w0).max()
+    assert err < 1e-4, err
+    for a, b in zip(hn, hr):
+        np.testing.assert_allclose(a["loss"], b["loss"], rtol=1e-4, atol=1e-6)
+        np.testing.assert_allclose(a["mae"], b["mae"], rtol=1e-4, atol=1e-6)
+
+
+def test_persist_chunking_is_bit_exact():
+    """37 steps as 16 + 16 + 4 + 1 graph-replayed chunks == 37 one-step launches,
+    bit for bit (every launch re-reads the masters it wrote back)."""
+    from elephas_amd.models import initializers
+    from elephas_amd.models.optimizers import SGD
+    initializers.set_seed(9)
+    model = _mlp(784, [128, 128], 10, dropout=0.2)
+    model.compile(SGD(0.05, momentum=0.5), "categorical_crossentropy", ["acc"])
+    xs, ys = _shards([64 * 40] * 2, 784, 10, seed=2)
+    ws = []
+    for graph in (True, False):
+        t = _trainer(model, 2, 64, persist=1, seed=99)
+        t.set_data(xs, ys, 0.0, shuffle=False)
+        t.begin_epoch()
+        t.run_steps(37, use_graph=graph)
+        ws.append((t.get_weights_flat(), t.get_state_flat()[0]))
+    assert np.array_equal(ws[0][0], ws[1][0])
+    assert np.array_equal(ws[0][1], ws[1][1])
+
+
+def test_persist_headline_shape_plan_and_progress():
+    """The bench's shape (8 replicas x B 64, MNIST MLP) runs on the persistent plan with
+    one workgroup per CU at most, and a short fit lowers the loss on separable data."""
+    from elephas_amd.models import initializers
+    from elephas_amd.models.optimizers import SGD
+    from elephas_amd.models.datasets import synthetic_classification
+    initializers.set_seed(1)
+    model = _mlp(784, [128, 128], 10, dropout=0.2)
+    model.compile(SGD(0.1), "categorical_crossentropy", ["acc"])
+    t = _trainer(model, 8, 64, persist=-1)
+    assert t.persistent, t.plan_name()
+    nk0, nc0, kc0, cw, nch, wgs, grid = t.exe.persist_geometry()
+    assert grid <= torch.cuda.get_device_properties(0).multi_processor_count
+    assert nk0 * kc0 >= 784 and nc0 * cw == 128 and nch == 4
+    xx, yy = synthetic_classification(8 * 1024, 784, 10, seed=5)
+    xs = [xx[i::8] / 10 for i in range(8)]
+    ys = [np.eye(10, dtype=np.float32)[yy[i::8]] for i in range(8)]
+    t.set_data(xs, ys, 0.1)
+    h = t.fit(3)
+    for hr in h:
+        assert hr["loss"][-1] < hr["loss"][0]
+    t.check()

@@ -94,6 +94,12 @@ def test_model_type_mapper(loss, model_type):
     assert LossModelTypeMapper().get_model_type(loss) == model_type
 
 
+@pytest.mark.parametrize("loss", ["poisson", "cosine_similarity", "log_cosh", "MeanSquaredError", "hinge"])
+def test_model_type_mapper_unlisted_is_none(loss):
+    # the reference table has 11 names and answers None for every other loss
+    assert LossModelTypeMapper().get_model_type(loss) is None
+
+
 def test_model_type_mapper_custom():
     LossModelTypeMapper().register_loss("test", ModelType.REGRESSION)
     assert LossModelTypeMapper().get_model_type("test") == ModelType.REGRESSION
