@@ -202,7 +202,7 @@ struct PersistArgs {
   unsigned* flags;                  // [R][PMF_N][PM_MAXWG], zeroed before every launch
   unsigned* err;                    // sticky error word (a timed-out wait), read by the host
   long long timeout;                // spin limit in s_memrealtime ticks (100 MHz)
-  long long* stamps;                // diagnostics: [block][PM_STAMP_STEPS][16] s_memrealtime (null = off)
+  long long* stamps;                // diagnostics: [block][PM_STAMP_STEPS][32] s_memrealtime (null = off)
 };
 constexpr int PM_STAMP_STEPS = 8;
 

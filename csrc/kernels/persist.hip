@@ -138,6 +138,34 @@ __device__ __forceinline__ bool wait_all(const PersistArgs& a, const unsigned* f
   return ok != 0;
 }
 
+// the same for two producer sets at once (lanes [0, n) watch set A, [n, n + m) set B)
+__device__ __forceinline__ bool wait_two(const PersistArgs& a, const unsigned* fa, int n, unsigned ta,
+                                         const unsigned* fb, int m, unsigned tb, unsigned code) {
+  int ok = 1;
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    const bool inA = lane < n, inB = lane >= n && lane < n + m;
+    const unsigned* f = inA ? fa + lane : fb + (inB ? lane - n : 0);
+    const unsigned want = inA ? ta : tb;
+    const unsigned long long t0 = wall_clock64();
+    for (;;) {
+      const unsigned v = (inA || inB) ? __hip_atomic_load((gu32*)(const_cast<unsigned*>(f)), __ATOMIC_RELAXED,
+                                                          __HIP_MEMORY_SCOPE_AGENT)
+                                      : want;
+      if (__all(v >= want)) break;
+      if ((long long)(wall_clock64() - t0) > a.timeout) {
+        ok = 0;
+        if (lane == 0) __hip_atomic_store((gu32*)(a.err), code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  ok = __syncthreads_and(ok);
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  return ok != 0;
+}
+
 __device__ __forceinline__ float dropout_u1(uint32_t base, int row, int c) {
   // the per-column-pair hash of dropout_u8 (common.h): the row-chain / grouped masks
   const uint32_t h = fmix32(base ^ (((uint32_t)row << 16) | (uint32_t)(c >> 1)));
@@ -147,7 +175,11 @@ __device__ __forceinline__ float dropout_u1(uint32_t base, int row, int c) {
 // diagnostics (tools/persist_stamps.py): s_memrealtime of phase k of step i (i < PM_STAMP_STEPS)
 __device__ __forceinline__ void pstamp(const PersistArgs& a, int i, int k) {
   if (a.stamps && threadIdx.x == 0 && i >= 0 && i < PM_STAMP_STEPS)
-    a.stamps[((long long)blockIdx.x * PM_STAMP_STEPS + i) * 16 + k] = (long long)__builtin_amdgcn_s_memrealtime();
+    a.stamps[((long long)blockIdx.x * PM_STAMP_STEPS + i) * 32 + k] = (long long)__builtin_amdgcn_s_memrealtime();
+}
+__device__ __forceinline__ void pcycle(const PersistArgs& a, int i, int k) {   // shader-clock stamp
+  if (a.stamps && threadIdx.x == 0 && i >= 0 && i < PM_STAMP_STEPS)
+    a.stamps[((long long)blockIdx.x * PM_STAMP_STEPS + i) * 32 + k] = (long long)__builtin_amdgcn_s_memtime();
 }
 
 // global (sc1) rows [0, nrows) x columns [0, ncols) of a row-major block (row stride ld,
@@ -159,15 +191,45 @@ __device__ __forceinline__ void stage(rsrc_t rs, int base, int ld, int nrows, in
   const int row0 = threadIdx.x / c4n, c4 = threadIdx.x - row0 * c4n;
   const int v = row0 * ld + 4 * c4;
   f32x4 x[NMAX];
+  // branch-free loads (a row past nrows re-reads row 0; its value is not written): a
+  // guarded load per element would split the issue into one basic block (and one
+  // wait) per load
 #pragma unroll
-  for (int u = 0; u < NMAX; ++u)
-    if (row0 + u * rpp < nrows) x[u] = ldw4(rs, v, base + u * rpp * ld);
+  for (int u = 0; u < NMAX; ++u) x[u] = ldw4(rs, row0 + u * rpp < nrows ? v : 4 * c4, base + u * rpp * ld);
 #pragma unroll
   for (int u = 0; u < NMAX; ++u) {
     if (row0 + u * rpp < nrows) {
       float* d = dst + (row0 + u * rpp) * lds + 4 * c4;
 #pragma unroll
       for (int q = 0; q < 4; ++q) d[q] = x[u][q];
+    }
+  }
+}
+
+// stage() in two halves: issue the loads (registers), later commit them to LDS
+template <int NMAX>
+struct Staged {
+  f32x4 x[NMAX];
+  int row0, c4, rpp;
+};
+template <int NMAX>
+__device__ __forceinline__ void stage_issue(Staged<NMAX>& st, rsrc_t rs, int base, int ld, int nrows, int ncols) {
+  const int c4n = ncols >> 2;
+  st.rpp = 256 / c4n;
+  st.row0 = threadIdx.x / c4n;
+  st.c4 = threadIdx.x - st.row0 * c4n;
+  const int v = st.row0 * ld + 4 * st.c4;
+#pragma unroll
+  for (int u = 0; u < NMAX; ++u) st.x[u] = ldw4(rs, st.row0 + u * st.rpp < nrows ? v : 4 * st.c4, base + u * st.rpp * ld);
+}
+template <int NMAX>
+__device__ __forceinline__ void stage_commit(const Staged<NMAX>& st, int nrows, float* dst, int lds) {
+#pragma unroll
+  for (int u = 0; u < NMAX; ++u) {
+    if (st.row0 + u * st.rpp < nrows) {
+      float* d = dst + (st.row0 + u * st.rpp) * lds + 4 * st.c4;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) d[q] = st.x[u][q];
     }
   }
 }
@@ -207,6 +269,34 @@ __device__ __forceinline__ float col_sums(const float* tile, int ld, int ncols, 
   return t;
 }
 
+// optimizer update of NV masters: NPT == 0 is plain SGD (no state planes, no rule
+// dispatch); NPT < 0 dispatches on the rule at run time (common.h opt_update_v)
+template <int NPT, int NV>
+__device__ __forceinline__ void pm_update(const OptParams& op, float (&w)[NV], const float (&g)[NV], float (&s0)[NV],
+                                          float (&s1)[NV], long long it) {
+  if constexpr (NPT == 0) {
+    const float lr = op.lr / (1.f + op.decay * (float)it);
+#pragma unroll
+    for (int q = 0; q < NV; ++q) w[q] -= lr * g[q];
+  } else {
+    opt_update_v<NV>(op, w, g, s0, s1, it);
+  }
+}
+
+// hidden activation and its derivative: RELU compiles relu alone, else the run-time table
+template <bool RELU, int NV>
+__device__ __forceinline__ void pm_act(int act, const float (&z)[NV], float (&o)[NV], float (&g)[NV]) {
+  if constexpr (RELU) {
+#pragma unroll
+    for (int q = 0; q < NV; ++q) {
+      o[q] = fmaxf(z[q], 0.f);
+      g[q] = z[q] > 0.f ? 1.f : 0.f;
+    }
+  } else {
+    act_fg_v<NV>(act, z, o, g);
+  }
+}
+
 struct Steps {
   long long s0;
   int ntr;
@@ -217,11 +307,11 @@ struct Steps {
 };
 
 // ============================================================== layer-0 tiles
-template <int H0>
+template <int H0, int NPT>
 __device__ __forceinline__ void l0_role(const PersistArgs& a, float* smem, int r, int kc, int cb, int q) {
   constexpr int XS = 129;                       // X chunk rows (<= 128 columns)
   const int tid = threadIdx.x, lane = tid & 63, i16 = lane & 15, g = lane >> 4;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6) & 3;
   const int k0 = kc * a.kc0;
   const int kreal = a.K0 - k0 < a.kc0 ? a.K0 - k0 : a.kc0;
   const int KCP = (kreal + 63) & ~63;           // FWD reduction, zero padded to 64
@@ -237,7 +327,7 @@ __device__ __forceinline__ void l0_role(const PersistArgs& a, float* smem, int r
   const rsrc_t rs = ws_rsrc(a.ws + (long long)r * a.ws_stride);
   float* P = a.P + (long long)r * a.sP;
   float* S = a.S ? a.S + (long long)r * a.sS : nullptr;
-  const int np = S ? opt_planes(a.op) : 0;
+  const int np = NPT >= 0 ? NPT : (S ? opt_planes(a.op) : 0);
   const bool has_b = kc == 0 && a.bias0;
   Steps st{ld_inv(a.ctr), ld_inv(a.ntrain + r)};
 
@@ -303,6 +393,7 @@ __device__ __forceinline__ void l0_role(const PersistArgs& a, float* smem, int r
     if (w * 16 < BR) {
       f32x4 acc[2] = {zero4f(), zero4f()};
       const float* arow = A + (w * 16 + i16) * XS;
+#pragma unroll 1
       for (int kb = 0; kb < KCP; kb += 64) {
         float av[16], bv0[16], bv1[16];
 #pragma unroll
@@ -310,14 +401,15 @@ __device__ __forceinline__ void l0_role(const PersistArgs& a, float* smem, int r
           const int k = kb + 16 * g + ks;
           av[ks] = arow[k];
           bv0[ks] = sW[k * WS + i16];
-          bv1[ks] = nct > 1 ? sW[k * WS + 16 + i16] : 0.f;
+          bv1[ks] = sW[k * WS + 16 + i16];   // cw = 16: garbage, never stored
         }
 #pragma unroll
         for (int ks = 0; ks < 16; ++ks) {
           acc[0] = mma(av[ks], bv0[ks], acc[0]);
-          if (nct > 1) acc[1] = mma(av[ks], bv1[ks], acc[1]);
+          acc[1] = mma(av[ks], bv1[ks], acc[1]);
         }
       }
+      pstamp(a, i, 10);
       const int v = (w * 16 + 4 * g) * H0 + i16;
 #pragma unroll
       for (int jj = 0; jj < 2; ++jj) {
@@ -364,19 +456,21 @@ __device__ __forceinline__ void l0_role(const PersistArgs& a, float* smem, int r
         for (int h8 = 0; h8 < 8; ++h8) {
           const int b = 16 * g + 8 * half + h8;
           zb[0][h8] = sdZ[b * WS + i16];
-          zb[1][h8] = nct > 1 ? sdZ[b * WS + 16 + i16] : 0.f;
+          zb[1][h8] = sdZ[b * WS + 16 + i16];   // cw = 16: garbage, never used
 #pragma unroll
-          for (int u = 0; u < TU; ++u) xa[u][h8] = w + 4 * u < ntiles ? Xi[b * XS + rt[u] * 16 + i16] : 0.f;
+          for (int u = 0; u < TU; ++u) xa[u][h8] = Xi[b * XS + rt[u] * 16 + i16];   // rt = 0 past the tiles
         }
+        // branch-free: tiles past ntiles compute garbage that is never stored
 #pragma unroll
         for (int h8 = 0; h8 < 8; ++h8) {
 #pragma unroll
-          for (int u = 0; u < TU; ++u)
-            if (w + 4 * u < ntiles) dw[u] = mma(xa[u][h8], ct[u] ? zb[1][h8] : zb[0][h8], dw[u]);
+          for (int u = 0; u < TU; ++u) dw[u] = mma(xa[u][h8], ct[u] ? zb[1][h8] : zb[0][h8], dw[u]);
         }
       }
+      pstamp(a, i, 7);
       // bias gradient (first k-chunk): column sums of dZ_0 over the batch rows
       const float gsum = has_b ? col_sums(sdZ, WS, cw, sRedL) : 0.f;
+      pstamp(a, i, 8);
       const long long it = iter_at(a.ctr, a.ntrain, a.B, r, st.s0, i);
       float wv[TU * 4], gv[TU * 4];
 #pragma unroll
@@ -388,7 +482,8 @@ __device__ __forceinline__ void l0_role(const PersistArgs& a, float* smem, int r
           gv[4 * u + qq] = dw[u][qq] * a.op.grad_scale;
         }
       }
-      opt_update_v<TU * 4>(a.op, wv, gv, s0, s1, it);
+      pm_update<NPT, TU * 4>(a.op, wv, gv, s0, s1, it);
+      pstamp(a, i, 9);
 #pragma unroll
       for (int u = 0; u < TU; ++u) {
         if (w + 4 * u >= ntiles) continue;
@@ -400,7 +495,7 @@ __device__ __forceinline__ void l0_role(const PersistArgs& a, float* smem, int r
       }
       if (bown) {
         float bv[1] = {bw}, bg[1] = {gsum * a.op.grad_scale}, t0[1] = {bs0}, t1[1] = {bs1};
-        opt_update_v<1>(a.op, bv, bg, t0, t1, it);
+        pm_update<NPT, 1>(a.op, bv, bg, t0, t1, it);
         bw = bv[0];
         bs0 = t0[0];
         bs1 = t1[0];
@@ -462,7 +557,7 @@ __device__ __forceinline__ void rows_mm(const float* A, const float* B, int ct0,
   const bool two = ct0 + 4 < nct;
   const float* arow = A + i16 * SAI;
   const float* b0 = B + (ct0 * 16 + i16) * SBN;
-  const float* b1 = B + ((ct0 + 4) * 16 + i16) * SBN;
+  const float* b1 = two ? B + ((ct0 + 4) * 16 + i16) * SBN : b0;   // branch-free: acc[1] then unused
 #pragma unroll
   for (int kb = 0; kb < K; kb += 64) {
     float av[16], bv0[16], bv1[16];
@@ -471,23 +566,23 @@ __device__ __forceinline__ void rows_mm(const float* A, const float* B, int ct0,
       const int k = kb + 16 * g + ks;
       av[ks] = arow[k];
       bv0[ks] = b0[k * SBK];
-      bv1[ks] = two ? b1[k * SBK] : 0.f;
+      bv1[ks] = b1[k * SBK];
     }
 #pragma unroll
     for (int ks = 0; ks < 16; ++ks) {
       acc[0] = mma(av[ks], bv0[ks], acc[0]);
-      if (two) acc[1] = mma(av[ks], bv1[ks], acc[1]);
+      acc[1] = mma(av[ks], bv1[ks], acc[1]);
     }
   }
 }
 
-template <int H0, int H1, bool FAST>
+template <int H0, int H1, bool FAST, int NPT, bool RELU>
 __device__ __forceinline__ void chain_role(const PersistArgs& a, float* smem, int r, int j) {
   using Lo = ChainLds<H0, H1>;
   constexpr int L0S = Lo::L0S, L1S = Lo::L1S;
   constexpr int nt0 = H0 / 16, nt1 = H1 / 16;
   const int tid = threadIdx.x, lane = tid & 63, i16 = lane & 15, g = lane >> 4;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6) & 3;
   const int m0 = j * 16;
   const int C = a.C;
   const int BR = a.nch * 16;
@@ -515,12 +610,19 @@ __device__ __forceinline__ void chain_role(const PersistArgs& a, float* smem, in
   const rsrc_t rs = ws_rsrc(a.ws + (long long)r * a.ws_stride);
   float* P = a.P + (long long)r * a.sP;
   float* S = a.S ? a.S + (long long)r * a.sS : nullptr;
-  const int np = S ? opt_planes(a.op) : 0;
+  const int np = NPT >= 0 ? NPT : (S ? opt_planes(a.op) : 0);
   Steps st{ld_inv(a.ctr), ld_inv(a.ntrain + r)};
 
   // owned tiles: layer-1 column tiles j + nch*c (c < nown) = layer-2 row tiles
   const int nown = (nt1 - j + a.nch - 1) / a.nch;   // <= PM_NTU (host checks)
   const int ndw1 = nt0 * nown;                      // DW1 tiles (row tile x owned col tile)
+  int urt[TU], uct[TU];                             // wave w's DW1 tiles t = w + 4u (row 0 past ndw1)
+#pragma unroll
+  for (int u = 0; u < TU; ++u) {
+    const int t = w + 4 * u;
+    urt[u] = t < ndw1 ? t / nown : 0;
+    uct[u] = t < ndw1 ? t - (t / nown) * nown : 0;
+  }
 
   // ---- prologue: W1, W2, biases into LDS; owned masters / state into registers
   for (int e = tid; e < Lo::TOTAL; e += 256) smem[e] = 0.f;
@@ -593,8 +695,22 @@ __device__ __forceinline__ void chain_role(const PersistArgs& a, float* smem, in
       }
     }
     pstamp(a, i, 0);
-    if (!wait_all(a, flag_at(a, r, PMF_PART), nl0, (unsigned)(i + 1), 2u)) return;
+    // this step's partials and (after step 0) every chain workgroup's updated W1 / W2
+    // columns of the previous step, watched by one wave
+    if (!wait_two(a, flag_at(a, r, PMF_PART), nl0, (unsigned)(i + 1), flag_at(a, r, PMF_W), i > 0 ? a.nch : 0,
+                  (unsigned)i, 2u))
+      return;
     pstamp(a, i, 1);
+    // the weight loads go first: their latency overlaps the partial sums below
+    Staged<H0 * H1 / 1024> w1s;
+    Staged<H1 / 64> w2s;
+    f32x4 bvec = zero4f();
+    if (i > 0) {
+      stage_issue(w1s, rs, (int)a.o_w1, H1, H0, H1);
+      stage_issue(w2s, rs, (int)a.o_w2, 16, H1, 16);
+      if (tid < H1 / 4) bvec = ldw4(rs, 4 * tid, (int)a.o_b1);
+      else if (tid >= 64 && tid < 68) bvec = ldw4(rs, 4 * (tid - 64), (int)a.o_b2);
+    }
 
     // ---- phase 0: z_0 = sum of the split-K partials (b0 is in chunk 0's) -> act, dropout
     {
@@ -607,12 +723,12 @@ __device__ __forceinline__ void chain_role(const PersistArgs& a, float* smem, in
 #pragma unroll
       for (int e = 0; e < 8; ++e) z[e] = 0.f;
       f32x4 pv[2 * RC_MAXSPLIT];
+      const int vv = cin ? v : 0;
 #pragma unroll
-      for (int u = 0; u < RC_MAXSPLIT; ++u) {
-        if (cin && u < a.nk0) {
-          pv[2 * u] = ldw4(rs, v, pbase + u * 64 * H0);
-          pv[2 * u + 1] = ldw4(rs, v + 4, pbase + u * 64 * H0);
-        }
+      for (int u = 0; u < RC_MAXSPLIT; ++u) {   // branch-free: chunks past nk0 re-read the last one
+        const int uc = u < a.nk0 ? u : a.nk0 - 1;
+        pv[2 * u] = ldw4(rs, vv, pbase + uc * 64 * H0);
+        pv[2 * u + 1] = ldw4(rs, vv + 4, pbase + uc * 64 * H0);
       }
 #pragma unroll
       for (int u = 0; u < RC_MAXSPLIT; ++u) {
@@ -624,8 +740,21 @@ __device__ __forceinline__ void chain_role(const PersistArgs& a, float* smem, in
           }
         }
       }
+      pstamp(a, i, 13);
+      pcycle(a, i, 28);
+      if (i > 0) {   // the previous step's weights -> LDS (read after the barrier below)
+        stage_commit(w1s, H0, sW1, L1S);
+        stage_commit(w2s, H1, sW2, S17);
+        if (tid < H1 / 4) {
+#pragma unroll
+          for (int qq = 0; qq < 4; ++qq) sB1[4 * tid + qq] = a.bias1 ? bvec[qq] : 0.f;
+        } else if (tid >= 64 && tid < 68) {
+#pragma unroll
+          for (int qq = 0; qq < 4; ++qq) sB2[4 * (tid - 64) + qq] = (a.bias2 && 4 * (tid - 64) + qq < C) ? bvec[qq] : 0.f;
+        }
+      }
       float o[8], gg[8], dv[8];
-      act_fg_v<8>(a.act0, z, o, gg);
+      pm_act<RELU, 8>(a.act0, z, o, gg);
       const float ks = a.rate0 > 0.f ? 1.f / (1.f - a.rate0) : 1.f;
       const uint32_t db = dropout_base(a.seed, r, 0, it);
 #pragma unroll
@@ -640,6 +769,7 @@ __device__ __forceinline__ void chain_role(const PersistArgs& a, float* smem, in
           sG0[rr * L0S + c] = keep ? gg[e] * ks : 0.f;
         }
       }
+      pstamp(a, i, 14);
       if (cin) {
         stw4(rs, v, (int)a.o_a0 + m0 * H0, f32x4{dv[0], dv[1], dv[2], dv[3]});
         stw4(rs, v + 4, (int)a.o_a0 + m0 * H0, f32x4{dv[4], dv[5], dv[6], dv[7]});
@@ -647,6 +777,7 @@ __device__ __forceinline__ void chain_role(const PersistArgs& a, float* smem, in
 #pragma unroll
       for (int h = 0; h < 2; ++h) sY[(tid >> 5) * 32 + 256 * h + (tid & 31)] = yv[h];
       if (tid < 16) sRow[tid] = m0 + tid < valid ? 1 : -1;
+      pstamp(a, i, 15);
     }
     __syncthreads();
     pstamp(a, i, 2);
@@ -656,6 +787,7 @@ __device__ __forceinline__ void chain_role(const PersistArgs& a, float* smem, in
     {
       f32x4 acc[2];
       rows_mm<H0, L0S, L1S, 1>(sA0, sW1, w, nt1, acc, i16, g);
+      pstamp(a, i, 16);
       const float ks = a.rate1 > 0.f ? 1.f / (1.f - a.rate1) : 1.f;
       const uint32_t db = dropout_base(a.seed, r, 1, it);
       float z[8], o[8], gg[8];
@@ -666,7 +798,7 @@ __device__ __forceinline__ void chain_role(const PersistArgs& a, float* smem, in
 #pragma unroll
         for (int qq = 0; qq < 4; ++qq) z[4 * jj + qq] = acc[jj][qq] + b;
       }
-      act_fg_v<8>(a.act1, z, o, gg);
+      pm_act<RELU, 8>(a.act1, z, o, gg);
 #pragma unroll
       for (int jj = 0; jj < 2; ++jj) {
         const int ct = w + 4 * jj;
@@ -682,6 +814,7 @@ __device__ __forceinline__ void chain_role(const PersistArgs& a, float* smem, in
           sA1[rr * L1S + col] = keep ? o[4 * jj + qq] * ks : 0.f;
         }
       }
+      pstamp(a, i, 17);
     }
     __syncthreads();
     pstamp(a, i, 3);
@@ -704,12 +837,14 @@ __device__ __forceinline__ void chain_role(const PersistArgs& a, float* smem, in
       for (int qq = 0; qq < 4; ++qq) sRed[w * 256 + (4 * g + qq) * 16 + i16] = acc[qq];
     }
     __syncthreads();
+    pstamp(a, i, 18);
     {
       const int rr = tid >> 4, c = tid & 15;
       const float v = sRed[tid] + sRed[256 + tid] + sRed[512 + tid] + sRed[768 + tid];
       sLg[rr * 36 + c] = c < C ? v + sB2[c] : 0.f;
     }
     __syncthreads();
+    pstamp(a, i, 19);
     // ---- loss / metrics -> dZ_2 = dL/dz (scaled by 1 / valid) in sLg
     {
       Prob pq;
@@ -732,15 +867,23 @@ __device__ __forceinline__ void chain_role(const PersistArgs& a, float* smem, in
       } else {
         loss_tile_lds<16, 36, 32>(pq, r, m0, sLg, sY, sRow, true, inv_valid, sums);
       }
-      if (a.acc && (!FAST || w == 0)) {
+      // per-row sums sit in the row leaders (a quad per row / 16 lanes per row): through
+      // LDS to 6 threads, one fp64 atomic per value (no 64-lane shuffle chains)
+      float* sAcc = sRed;   // [16][8]; the FWD2 partials are consumed (barrier above)
+      const bool leader = FAST ? (tid < 64 && (tid & 3) == 0) : ((tid & 15) == 0);
+      const int lrow = FAST ? (tid >> 2) : (tid >> 4);
+      if (leader) {
 #pragma unroll
-        for (int e = 0; e < 6; ++e) {
-          if (e < 2 + a.nmet) {
-            const float sv = row_sum<64>(sums[e]);
-            if (lane == 0 && sv != 0.f) atomicAdd(a.acc + (long long)r * a.acc_stride + e, (double)sv);
-          }
-        }
+        for (int e = 0; e < 6; ++e) sAcc[lrow * 8 + e] = sums[e];
       }
+      __syncthreads();
+      if (a.acc && tid < 2 + a.nmet) {
+        float sv = 0.f;
+#pragma unroll
+        for (int rr = 0; rr < 16; ++rr) sv += sAcc[rr * 8 + tid];
+        if (sv != 0.f) atomicAdd(a.acc + (long long)r * a.acc_stride + tid, (double)sv);
+      }
+      pstamp(a, i, 20);
     }
     __syncthreads();
     {
@@ -770,13 +913,16 @@ __device__ __forceinline__ void chain_role(const PersistArgs& a, float* smem, in
 #pragma unroll
         for (int qq = 0; qq < 4; ++qq) sD1[(4 * g + qq) * L1S + col] = acc[qq] * G1[4 * jj + qq];
       }
+      pstamp(a, i, 21);
     }
     __syncthreads();
     publish_rows16<H1>(rs, (int)a.o_dz1 + m0 * H1, sD1, L1S);
+    pstamp(a, i, 22);
     // ---- DX1: dZ_0 = (dZ_1 . W1^T) * G_0 -> LDS, then published for the L0 tiles
     {
       f32x4 acc[2];
       rows_mm<H1, L1S, 1, L1S>(sD1, sW1, w, nt0, acc, i16, g);
+      pstamp(a, i, 23);
 #pragma unroll
       for (int jj = 0; jj < 2; ++jj) {
         const int ct = w + 4 * jj;
@@ -831,32 +977,26 @@ __device__ __forceinline__ void chain_role(const PersistArgs& a, float* smem, in
           zb[0][h8] = uD1[b * 33 + i16];
           zb[1][h8] = uD1[b * 33 + 16 + i16];
 #pragma unroll
-          for (int u = 0; u < TU; ++u) {
-            const int t = w + 4 * u;
-            xa[u][h8] = t < ndw1 ? uA0[b * L0S + (t / nown) * 16 + i16] : 0.f;
-          }
-          a1v[h8] = w2own ? uA1[b * 33 + w * 16 + i16] : 0.f;
+          for (int u = 0; u < TU; ++u) xa[u][h8] = uA0[b * L0S + urt[u] * 16 + i16];
+          a1v[h8] = uA1[b * 33 + (w2own ? w : 0) * 16 + i16];
           d2v[h8] = uD2[b * S17 + i16];
         }
+        // branch-free: tiles a wave does not own compute garbage that is never stored
 #pragma unroll
         for (int h8 = 0; h8 < 8; ++h8) {
 #pragma unroll
-          for (int u = 0; u < TU; ++u) {
-            const int t = w + 4 * u;
-            if (t < ndw1) {
-              const int c = t - (t / nown) * nown;
-              dw[u] = mma(xa[u][h8], c ? zb[1][h8] : zb[0][h8], dw[u]);
-            }
-          }
-          if (w2own) dw[TU] = mma(a1v[h8], d2v[h8], dw[TU]);
+          for (int u = 0; u < TU; ++u) dw[u] = mma(xa[u][h8], uct[u] ? zb[1][h8] : zb[0][h8], dw[u]);
+          dw[TU] = mma(a1v[h8], d2v[h8], dw[TU]);
         }
       }
+      pstamp(a, i, 24);
       // bias gradients: column sums of dZ_1 (owned columns) and dZ_2 over the batch rows
       const float gb1 = col_sums(uD1, 33, nown * 16, sRed);   // in threads tid < 16 * nown
       __syncthreads();
       const float gb2 = col_sums(uD2, S17, C, sRed);
       if (tid < C) sRed[512 + tid] = gb2;
       __syncthreads();
+      pstamp(a, i, 25);
       float gb = 0.f;
       if (b1own) gb = gb1;
       else if (b2own) gb = sRed[512 + tid - 64];
@@ -866,10 +1006,11 @@ __device__ __forceinline__ void chain_role(const PersistArgs& a, float* smem, in
       for (int u = 0; u <= TU; ++u)
 #pragma unroll
         for (int qq = 0; qq < 4; ++qq) gv[4 * u + qq] = (u < TU || i16 < C) ? dw[u][qq] * gs : 0.f;
-      opt_update_v<NM>(a.op, wm, gv, ws0, ws1, it);
+      pm_update<NPT, NM>(a.op, wm, gv, ws0, ws1, it);
+      pstamp(a, i, 26);
       if (b1own || b2own) {
         float bv[1] = {bm}, bg[1] = {gb * gs}, t0[1] = {bst0}, t1[1] = {bst1};
-        opt_update_v<1>(a.op, bv, bg, t0, t1, it);
+        pm_update<NPT, 1>(a.op, bv, bg, t0, t1, it);
         bm = bv[0];
         bst0 = t0[0];
         bst1 = t1[0];
@@ -898,22 +1039,7 @@ __device__ __forceinline__ void chain_role(const PersistArgs& a, float* smem, in
     if (b2own) stw1(rs, tid - 64, (int)a.o_b2, bm);
     publish(flag_at(a, r, PMF_W) + j, (unsigned)(i + 1));
     pstamp(a, i, 10);
-    if (!wait_all(a, flag_at(a, r, PMF_W), a.nch, (unsigned)(i + 1), 4u)) return;
-    pstamp(a, i, 11);
-    stage<H0 * H1 / 1024>(rs, (int)a.o_w1, H1, H0, H1, sW1, L1S);
-    stage<H1 / 64>(rs, (int)a.o_w2, 16, H1, 16, sW2, S17);
-    if (tid < H1 / 4) {
-      const f32x4 v = ldw4(rs, 4 * tid, (int)a.o_b1);
-#pragma unroll
-      for (int qq = 0; qq < 4; ++qq) sB1[4 * tid + qq] = a.bias1 ? v[qq] : 0.f;
-    } else if (tid >= 64 && tid < 68) {
-      const f32x4 v = ldw4(rs, 4 * (tid - 64), (int)a.o_b2);
-#pragma unroll
-      for (int qq = 0; qq < 4; ++qq) sB2[4 * (tid - 64) + qq] = (a.bias2 && 4 * (tid - 64) + qq < C) ? v[qq] : 0.f;
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    pstamp(a, i, 12);
+    pcycle(a, i, 29);
   }
 
   // ---- epilogue: owned masters, both weight-image parities, state
@@ -963,15 +1089,32 @@ __device__ __forceinline__ void chain_role(const PersistArgs& a, float* smem, in
 
 }  // namespace
 
-template <int H0, int H1, bool FAST>
+template <int H0, int H1, bool FAST, int NPT, bool RELU>
 __global__ __launch_bounds__(256) void mlp_persist_kernel(PersistArgs a) {
   __shared__ __attribute__((aligned(16))) float smem[LDS_FLOATS];
   if (__hip_atomic_load((gu32*)(a.err), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) return;
   const int b = blockIdx.x;
   const int r = b % a.R, q = b / a.R;
   const int nl0 = a.nk0 * a.nc0;
-  if (q < nl0) l0_role<H0>(a, smem, r, q / a.nc0, q - (q / a.nc0) * a.nc0, q);
-  else chain_role<H0, H1, FAST>(a, smem, r, q - nl0);
+  if (q < nl0) l0_role<H0, NPT>(a, smem, r, q / a.nc0, q - (q / a.nc0) * a.nc0, q);
+  else chain_role<H0, H1, FAST, NPT, RELU>(a, smem, r, q - nl0);
+}
+
+// the instances of one hidden width: the specialised MNIST-style one (relu, softmax +
+// cross-entropy, plain SGD) and the general ones
+template <int H>
+hipError_t persist_launch(const PersistArgs* a, hipStream_t s) {
+  bool fast = a->act2 == ACT_SOFTMAX && (a->loss == LOSS_CCE || a->loss == LOSS_SPARSE_CCE);
+  for (int i = 0; i < a->nmet; ++i)
+    fast = fast && (a->met[i] == MET_ACC_CAT || a->met[i] == MET_ACC_SPARSE || a->met[i] == LOSS_CCE ||
+                    a->met[i] == LOSS_SPARSE_CCE);
+  const bool relu = a->act0 == ACT_RELU && a->act1 == ACT_RELU;
+  const bool sgd = !a->S || (a->op.opt == OPT_SGD && a->op.mom == 0.f);
+  const dim3 grid(a->R * a->wgs);
+  if (fast && relu && sgd) hipLaunchKernelGGL((mlp_persist_kernel<H, H, true, 0, true>), grid, dim3(256), 0, s, *a);
+  else if (fast) hipLaunchKernelGGL((mlp_persist_kernel<H, H, true, -1, false>), grid, dim3(256), 0, s, *a);
+  else hipLaunchKernelGGL((mlp_persist_kernel<H, H, false, -1, false>), grid, dim3(256), 0, s, *a);
+  return hipGetLastError();
 }
 
 }  // namespace ea
@@ -984,21 +1127,7 @@ extern "C" int ea_persist_lds_bytes() { return (int)(LDS_FLOATS * sizeof(float))
 // grid to at most one workgroup per CU); hidden widths (64, 64) or (128, 128)
 extern "C" hipError_t ea_persist(const PersistArgs* a, hipStream_t s) {
   if (a->nsteps <= 0) return hipSuccess;
-  bool fast = a->act2 == ACT_SOFTMAX && (a->loss == LOSS_CCE || a->loss == LOSS_SPARSE_CCE);
-  for (int i = 0; i < a->nmet; ++i)
-    fast = fast && (a->met[i] == MET_ACC_CAT || a->met[i] == MET_ACC_SPARSE || a->met[i] == LOSS_CCE ||
-                    a->met[i] == LOSS_SPARSE_CCE);
-  const dim3 grid(a->R * a->wgs);
-#define EA_PM(H0_, H1_)                                                                           \
-  if (fast) hipLaunchKernelGGL((mlp_persist_kernel<H0_, H1_, true>), grid, dim3(256), 0, s, *a);   \
-  else hipLaunchKernelGGL((mlp_persist_kernel<H0_, H1_, false>), grid, dim3(256), 0, s, *a);
-  if (a->H0 == 128 && a->H1 == 128) {
-    EA_PM(128, 128)
-  } else if (a->H0 == 64 && a->H1 == 64) {
-    EA_PM(64, 64)
-  } else {
-    return hipErrorInvalidValue;
-  }
-#undef EA_PM
-  return hipGetLastError();
+  if (a->H0 == 128 && a->H1 == 128) return persist_launch<128>(a, s);
+  if (a->H0 == 64 && a->H1 == 64) return persist_launch<64>(a, s);
+  return hipErrorInvalidValue;
 }

@@ -52,6 +52,9 @@ class NativeTrainer(TrainerBase):
     # steps per captured graph: a power of two (run_steps splits a remainder into the
     # binary fractions of it), ELEPHAS_AMD_GRAPH_CHUNK rounded down to one
     GRAPH_CHUNK = 1 << (max(1, int(os.environ.get("ELEPHAS_AMD_GRAPH_CHUNK", "16"))).bit_length() - 1)
+    # the persistent plan runs a whole chunk in one launch (its fill / drain and the
+    # launch's P / S / weight-image round trip are paid once per chunk): longer chunks
+    PERSIST_CHUNK = 1 << (max(1, int(os.environ.get("ELEPHAS_AMD_PERSIST_CHUNK", "64"))).bit_length() - 1)
 
     def __init__(self, model, plan, R: int = 1, batch_size: int = 32, device=None, seed: Optional[int] = None,
                  policy: Optional[str] = None, eval_batch: int = 2048, rowchain: Optional[int] = None,
@@ -193,6 +196,7 @@ class NativeTrainer(TrainerBase):
             self.exe.destroy_graphs()
         self._graphs = {}
         self.exe = self.C.Executor(self._cfg(self.ws))
+        self.GRAPH_CHUNK = self.PERSIST_CHUNK if self.exe.persistent() else type(self).GRAPH_CHUNK
 
     def _eval_exe(self):
         if self.exe_eval is None:

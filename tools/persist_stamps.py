@@ -37,7 +37,7 @@ def main():
     t.set_data(xs, ys, 0.1)
     nk0, nc0, kc0, cw, nch, wgs, grid = t.exe.persist_geometry()
     print("geometry", dict(nk0=nk0, nc0=nc0, kc0=kc0, cw=cw, nch=nch, wgs=wgs, grid=grid))
-    st = torch.zeros(grid * 8 * 16, dtype=torch.int64, device="cuda")
+    st = torch.zeros(grid * 8 * 32, dtype=torch.int64, device="cuda")
     t.begin_epoch()
     t.run_steps(32, use_graph=False)   # warm
     torch.cuda.synchronize()
@@ -51,24 +51,30 @@ def main():
         t.exe.replay(g, t.s)
         torch.cuda.synchronize()
     t.check()
-    s = st.view(grid, 8, 16).cpu().numpy().astype(np.int64)
+    s = st.view(grid, 8, 32).cpu().numpy().astype(np.int64)
     nl0 = nk0 * nc0
     q = np.arange(grid) // R
     chain = q >= nl0
     l0 = ~chain
     base_all = s[chain, :, 1]   # chain: partials seen
     print("ticks of 10 ns; per step (median over workgroups) relative to the chain's partial-wait end")
-    names_c = ["part_wait0", "part_seen", "phase0", "fwd1", "fwd2+loss", "dx2+dx1", "bwd_pub", "bwd_seen",
-               "stage_ld", "dw_upd", "w_pub", "w_seen", "w_loaded"]
-    names_l = ["start", "part_pub", "bwd_wait0", "bwd_seen", "dz_ld", "dw_upd", "fwd_done"]
+    names_c = {0: "part_wait0", 1: "part_seen", 13: "p0_loads", 14: "p0_act", 15: "p0_st", 2: "phase0",
+               16: "fwd1_mm", 17: "fwd1_epi", 3: "fwd1", 18: "fwd2", 19: "logits", 20: "loss", 4: "dz2",
+               21: "dx2", 22: "dz1_pub", 23: "dx1_mm", 5: "dx1", 6: "bwd_pub", 7: "bwd_seen",
+               8: "stage_ld", 24: "dw_mm", 25: "colsum", 26: "opt", 9: "upd", 10: "w_pub"}
+    names_l = {0: "start", 1: "part_pub", 2: "bwd_wait0", 3: "bwd_seen", 4: "dz_ld", 7: "dw_mm", 8: "colsum",
+               9: "opt", 5: "dw_upd", 10: "fwd_mm", 6: "fwd_done"}
     for i in range(min(8, nst)):
         b0 = np.median(base_all[:, i])
         if b0 == 0:
             continue
-        c = {n: (np.median(s[chain, i, k]) - b0) / 100.0 for k, n in enumerate(names_c) if (s[chain, i, k] > 0).all()}
-        l = {n: (np.median(s[l0, i, k]) - b0) / 100.0 for k, n in enumerate(names_l) if (s[l0, i, k] > 0).all()}
+        c = {n: (np.median(s[chain, i, k]) - b0) / 100.0 for k, n in names_c.items() if (s[chain, i, k] > 0).all()}
+        l = {n: (np.median(s[l0, i, k]) - b0) / 100.0 for k, n in names_l.items() if (s[l0, i, k] > 0).all()}
         print(f"step {i}: chain " + " ".join(f"{k}={v:.2f}" for k, v in c.items()))
         print(f"        l0    " + " ".join(f"{k}={v:.2f}" for k, v in l.items()))
+    cyc = (s[chain, 1:7, 29] - s[chain, 1:7, 28]).astype(np.float64)
+    rt = (s[chain, 1:7, 10] - s[chain, 1:7, 13]).astype(np.float64) / 100.0
+    print("chain shader clock (MHz, median):", np.median(cyc / np.maximum(rt, 1e-9)))
     steps = [np.median(base_all[:, i]) for i in range(min(8, nst))]
     d = np.diff([x for x in steps if x > 0]) / 100.0
     print("step period (us):", np.round(d, 2))
