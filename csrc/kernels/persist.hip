@@ -185,10 +185,21 @@ __device__ __forceinline__ void pcycle(const PersistArgs& a, int i, int k) {   /
 // global (sc1) rows [0, nrows) x columns [0, ncols) of a row-major block (row stride ld,
 // first element at uniform offset base) -> LDS tile (row stride lds).  ncols / 4 must
 // divide 256.  Every load of the thread is issued before the first LDS write.
+// Thread -> (row, float4 column) map of a 256-thread pass over rows of c4n float4s
+__device__ __forceinline__ void pass_map(int c4n, int& row0, int& c4, int& rpp) {
+  // row-major (a half-wave reads whole 512-byte rows): measured faster than a
+  // bank-conflict-free quad-per-row map whose global reads span 4 rows per half-wave
+  // (23.0 vs 20.9 us per step, profiles/persist_stamps_r3_*)
+  const int t = threadIdx.x;
+  row0 = t / c4n;
+  c4 = t - row0 * c4n;
+  rpp = 256 / c4n;
+}
+
 template <int NMAX>
 __device__ __forceinline__ void stage(rsrc_t rs, int base, int ld, int nrows, int ncols, float* dst, int lds) {
-  const int c4n = ncols >> 2, rpp = 256 / c4n;
-  const int row0 = threadIdx.x / c4n, c4 = threadIdx.x - row0 * c4n;
+  int row0, c4, rpp;
+  pass_map(ncols >> 2, row0, c4, rpp);
   const int v = row0 * ld + 4 * c4;
   f32x4 x[NMAX];
   // branch-free loads (a row past nrows re-reads row 0; its value is not written): a
@@ -214,10 +225,7 @@ struct Staged {
 };
 template <int NMAX>
 __device__ __forceinline__ void stage_issue(Staged<NMAX>& st, rsrc_t rs, int base, int ld, int nrows, int ncols) {
-  const int c4n = ncols >> 2;
-  st.rpp = 256 / c4n;
-  st.row0 = threadIdx.x / c4n;
-  st.c4 = threadIdx.x - st.row0 * c4n;
+  pass_map(ncols >> 2, st.row0, st.c4, st.rpp);
   const int v = st.row0 * ld + 4 * st.c4;
 #pragma unroll
   for (int u = 0; u < NMAX; ++u) st.x[u] = ldw4(rs, st.row0 + u * st.rpp < nrows ? v : 4 * st.c4, base + u * st.rpp * ld);
@@ -238,13 +246,14 @@ __device__ __forceinline__ void stage_commit(const Staged<NMAX>& st, int nrows, 
 // stride W), as 16-byte write-through stores
 template <int W>
 __device__ __forceinline__ void publish_rows16(rsrc_t rs, int base, const float* src, int lds) {
-  constexpr int C4 = W / 4, TOT = 16 * C4, RPP = 256 / C4;
-  const int row0 = threadIdx.x / C4, c4 = threadIdx.x - row0 * C4;
+  constexpr int C4 = W / 4, TOT = 16 * C4;
+  int row0, c4, rpp;
+  pass_map(C4, row0, c4, rpp);
 #pragma unroll
   for (int u = 0; u < (TOT + 255) / 256; ++u) {
-    if (threadIdx.x + 256 * u < TOT) {
-      const float* s = src + (row0 + u * RPP) * lds + 4 * c4;
-      stw4(rs, row0 * W + 4 * c4, base + u * RPP * W, f32x4{s[0], s[1], s[2], s[3]});
+    if (row0 + u * rpp < 16) {
+      const float* s = src + (row0 + u * rpp) * lds + 4 * c4;
+      stw4(rs, row0 * W + 4 * c4, base + u * rpp * W, f32x4{s[0], s[1], s[2], s[3]});
     }
   }
 }
@@ -297,6 +306,26 @@ __device__ __forceinline__ void pm_act(int act, const float (&z)[NV], float (&o)
   }
 }
 
+// prologue copy of n consecutive floats of P into LDS (element e -> dst[map(e)]): 16
+// loads per thread in flight per batch (a loop of dependent load -> store pairs took
+// one memory latency per element group and dominated the launch's fill)
+template <typename Map>
+__device__ __forceinline__ void p_to_lds(const float* src, int n, float* dst, Map map) {
+  for (int base = 0; base < n; base += 16 * 256) {
+    float v[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int e = base + threadIdx.x + 256 * u;
+      v[u] = src[e < n ? e : 0];
+    }
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int e = base + threadIdx.x + 256 * u;
+      if (e < n) dst[map(e)] = v[u];
+    }
+  }
+}
+
 struct Steps {
   long long s0;
   int ntr;
@@ -334,9 +363,20 @@ __device__ __forceinline__ void l0_role(const PersistArgs& a, float* smem, int r
   // ---- prologue: zero LDS (padding rows / columns stay zero), W0 tile and state
   for (int e = tid; e < L0_LDS; e += 256) smem[e] = 0.f;
   __syncthreads();
-  for (int e = tid; e < kreal * cw; e += 256) {
-    const int k = e / cw, n = e - k * cw;
-    sW[k * WS + n] = P[a.p_off0 + (long long)(k0 + k) * H0 + n0 + n];
+  // the W0 tile: kreal rows of cw floats (row stride H0 in P)
+  for (int base = 0; base < kreal * cw; base += 16 * 256) {
+    float v[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int e = base + tid + 256 * u, el = e < kreal * cw ? e : 0;
+      const int k = el / cw, n = el - k * cw;
+      v[u] = P[a.p_off0 + (long long)(k0 + k) * H0 + n0 + n];
+    }
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int e = base + tid + 256 * u;
+      if (e < kreal * cw) sW[(e / cw) * WS + (e % cw)] = v[u];
+    }
   }
   int rt[TU], ct[TU];
   float s0[TU * 4], s1[TU * 4];
@@ -662,13 +702,15 @@ __device__ __forceinline__ void chain_role(const PersistArgs& a, float* smem, in
     ws0[4 * TU + qq] = (in && np > 0) ? S[pi] : 0.f;
     ws1[4 * TU + qq] = (in && np > 1) ? S[a.op.s_plane + pi] : 0.f;
   }
-  // owned b1 entries: thread tid < 16 * nown -> unit (j + nch*(tid/16))*16 + tid%16; b2: chain 0, tid 64 + c
-  const bool b1own = a.bias1 && tid < 16 * nown;
-  const int b1n = (j + a.nch * (tid >> 4)) * 16 + (tid & 15);
-  const bool b2own = a.bias2 && j == 0 && tid >= 64 && tid < 64 + C;
+  // owned biases, where their gradients come out of the bias MFMAs (all-ones A rows):
+  // b1 of the owned column tiles in wave 2 (lane -> unit (j + nch*(lane/16))*16 + lane%16),
+  // b2 (chain workgroup 0) in wave 3, lanes < C -- the waves without a layer-2 tile
+  const bool b1own = a.bias1 && w == 2 && lane < 16 * nown;
+  const int b1n = (j + a.nch * (lane >> 4)) * 16 + (lane & 15);
+  const bool b2own = a.bias2 && j == 0 && w == 3 && lane < C;
   float bm = 0.f, bst0 = 0.f, bst1 = 0.f;
   if (b1own || b2own) {
-    const long long pi = b1own ? a.p_off1 + (long long)H0 * H1 + b1n : a.p_off2 + (long long)H1 * C + (tid - 64);
+    const long long pi = b1own ? a.p_off1 + (long long)H0 * H1 + b1n : a.p_off2 + (long long)H1 * C + lane;
     bm = P[pi];
     bst0 = np > 0 ? S[pi] : 0.f;
     bst1 = np > 1 ? S[a.op.s_plane + pi] : 0.f;
@@ -965,7 +1007,7 @@ __device__ __forceinline__ void chain_role(const PersistArgs& a, float* smem, in
     __syncthreads();
     pstamp(a, i, 8);
     {
-      f32x4 dw[TU + 1];
+      f32x4 dw[TU + 1], db[2] = {zero4f(), zero4f()};
 #pragma unroll
       for (int u = 0; u <= TU; ++u) dw[u] = zero4f();
 #pragma unroll
@@ -988,18 +1030,19 @@ __device__ __forceinline__ void chain_role(const PersistArgs& a, float* smem, in
           for (int u = 0; u < TU; ++u) dw[u] = mma(xa[u][h8], uct[u] ? zb[1][h8] : zb[0][h8], dw[u]);
           dw[TU] = mma(a1v[h8], d2v[h8], dw[TU]);
         }
+        // bias gradients = column sums over the batch rows: an all-ones A operand (every
+        // output row holds the sums), in the waves that own the biases
+        if (w >= 2) {
+#pragma unroll
+          for (int h8 = 0; h8 < 8; ++h8) {
+            db[0] = mma(1.f, w == 2 ? zb[0][h8] : d2v[h8], db[0]);
+            db[1] = mma(1.f, zb[1][h8], db[1]);
+          }
+        }
       }
       pstamp(a, i, 24);
-      // bias gradients: column sums of dZ_1 (owned columns) and dZ_2 over the batch rows
-      const float gb1 = col_sums(uD1, 33, nown * 16, sRed);   // in threads tid < 16 * nown
-      __syncthreads();
-      const float gb2 = col_sums(uD2, S17, C, sRed);
-      if (tid < C) sRed[512 + tid] = gb2;
-      __syncthreads();
       pstamp(a, i, 25);
-      float gb = 0.f;
-      if (b1own) gb = gb1;
-      else if (b2own) gb = sRed[512 + tid - 64];
+      const float gb = (b1own && lane >= 16) ? db[1][0] : db[0][0];
       const float gs = a.op.grad_scale;
       float gv[NM];
 #pragma unroll
@@ -1036,7 +1079,7 @@ __device__ __forceinline__ void chain_role(const PersistArgs& a, float* smem, in
         stw1(rs, v + qq * 16, (int)a.o_w2 + (j + a.nch * w) * 256, wm[4 * TU + qq]);
     }
     if (b1own) stw1(rs, b1n, (int)a.o_b1, bm);
-    if (b2own) stw1(rs, tid - 64, (int)a.o_b2, bm);
+    if (b2own) stw1(rs, lane, (int)a.o_b2, bm);
     publish(flag_at(a, r, PMF_W) + j, (unsigned)(i + 1));
     pstamp(a, i, 10);
     pcycle(a, i, 29);
@@ -1080,7 +1123,7 @@ __device__ __forceinline__ void chain_role(const PersistArgs& a, float* smem, in
     }
   }
   if (b1own || b2own) {
-    const long long pi = b1own ? a.p_off1 + (long long)H0 * H1 + b1n : a.p_off2 + (long long)H1 * C + (tid - 64);
+    const long long pi = b1own ? a.p_off1 + (long long)H0 * H1 + b1n : a.p_off2 + (long long)H1 * C + lane;
     P[pi] = bm;
     if (np > 0) S[pi] = bst0;
     if (np > 1) S[a.op.s_plane + pi] = bst1;
