@@ -32,6 +32,7 @@ Prints ONE JSON line on rank 0.
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import math
 import os
@@ -268,6 +269,29 @@ def main():
     dts = dist.all_gather_object(dt)
     dt_max = max(dts)
     samples = rows_done * (R if not batch_mode else 1) * world
+    # evidence for the multi-GPU record, gathered after the timed region: every rank's
+    # HIP device, the all-reduce path actually taken, and a bit-exact digest of the
+    # averaged theta (equal on every rank iff the all-reduce gave all ranks one result)
+    if gpu:
+        props = torch.cuda.get_device_properties(dev)
+        where = (torch.cuda.current_device(), "%x:%x" % (getattr(props, "pci_bus_id", -1),
+                                                        getattr(props, "pci_device_id", -1)))
+        theta = t.get_weights_flat()[0]
+    else:
+        where, theta = None, t.get_weights_flat()[0]
+    digest = hashlib.sha1(np.ascontiguousarray(theta, np.float32).tobytes()).hexdigest()[:16]
+    devices = dist.all_gather_object(where)
+    digests = dist.all_gather_object(digest)
+    from elephas_amd.parallel import p2p
+    nbytes = (t.G.numel() if batch_mode and gpu else theta.size) * 4
+    if channel is not None:
+        path = "peer-memory kernel captured in the step's hipGraph (dedicated channel)"
+    elif gpu and world > 1 and not batch_mode:
+        path = p2p.describe(nbytes)
+    elif world > 1:
+        path = f"torch.distributed {dist.backend()}" if not gpu else p2p.describe(nbytes)
+    else:
+        path = None
     if rank == 0:
         value = samples / dt_max
         launches = t.launch_count() if gpu else None
@@ -300,10 +324,14 @@ def main():
                 "batch_per_worker": B,
                 "rows_per_worker": rows,
                 "sync": "reference (one-shot averaging per fit)" if not batch_mode else "per-step gradient all-reduce",
-                "allreduce": ("peer-memory kernel in the step's hipGraph" if channel is not None
-                              else ("torch.distributed" if world > 1 else None)),
+                "allreduce": path,
+                "allreduce_bytes": nbytes if world > 1 else None,
+                "comm_world_size": dist.world_size(),
+                "rank_devices": devices,
+                "theta_sha1_16": digests[0],
+                "theta_equal_on_all_ranks": all(d == digests[0] for d in digests),
                 "optimizer": "SGD(lr=%g)" % MODELS[args.model][4],
-                "engine": "native HIP executor + hipGraph" if gpu else "torch CPU reference",
+                "engine": ("native HIP executor + hipGraph: " + t.plan_name()) if gpu else "torch CPU reference",
                 "launches_per_step": launches,
                 "policy": args.policy,
                 "validation_passes_timed": state["val_passes"],

@@ -659,7 +659,10 @@ class NativeTrainer(TrainerBase):
         cnt = max(s[1], 1.0)
         return [float(s[0] / cnt)] + [float(s[2 + i] / cnt) for i in range(len(self.metrics))]
 
-    def launch_count(self) -> int:
+    def launch_count(self):
+        """Kernel launches per training step (the persistent plan: one per chunk)."""
+        if self.exe.persistent():
+            return 1.0 / self.GRAPH_CHUNK
         return self.exe.launches_per_step()
 
     @property

@@ -190,6 +190,21 @@ def get() -> Optional[PeerAllReduce]:
     return _peer
 
 
+def describe(nbytes: int) -> Optional[str]:
+    """Which path ``dist.all_reduce_sum_`` takes for an fp32 CUDA tensor of ``nbytes``
+    (collective on first use: it may create the job-wide instance and run its
+    self-test).  None on a single-rank job."""
+    if not dist.is_initialized() or dist.world_size() < 2:
+        return None
+    peer = get()
+    if peer is not None and nbytes <= peer.max_bytes:
+        shot = "two-shot" if nbytes >= peer.impl.twoshot_min_bytes else "one-shot"
+        return f"peer-memory {shot} kernel (self-test passed on all {peer.world} ranks)"
+    why = "self-test failed" if isinstance(_peer, _Disabled) else (
+        "over max_bytes" if peer is not None else "peer path off")
+    return f"torch.distributed {dist.backend()} ({why})"
+
+
 def graph_channel(n: int) -> Optional[PeerAllReduce]:
     """A dedicated peer all-reduce of exactly n floats for graph-captured per-step
     gradient exchange (collective; None when the peer path is unavailable).  The

@@ -224,13 +224,16 @@ def test_graph_replay_equals_eager():
     assert not np.array_equal(ws[0][0], ws[0][1])  # replicas draw different dropout masks
 
 
-def _fit_weights(model, policy, B, xs, ys, rowchain, epochs=1, val=0.0, R=None, seed=7):
+def _fit_weights(model, policy, B, xs, ys, rowchain, epochs=1, val=0.0, R=None, seed=7, persist=0):
     from elephas_amd import config
     from elephas_amd.ops.plan import build_plan
     from elephas_amd.ops.native_engine import NativeTrainer
     config.set_policy(policy)
     R = R or len(xs)
-    t = NativeTrainer(model, build_plan(model), R, B, torch.device("cuda"), seed=seed, rowchain=rowchain)
+    # persist=0: these cases pin the row-chain and grouped plans (the persistent plan has
+    # its own file, tests/test_persist_gpu.py)
+    t = NativeTrainer(model, build_plan(model), R, B, torch.device("cuda"), seed=seed, rowchain=rowchain,
+                      persist=persist)
     t.set_data(xs, ys, val, shuffle=True)
     np.random.seed(3)
     torch.manual_seed(5)   # epoch shuffles draw from the global CUDA generator
