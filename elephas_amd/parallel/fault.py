@@ -10,7 +10,8 @@ visible instead of silent:
 * worker threads (async / hogwild) re-raise their first exception in the driver;
 * ``$ELEPHAS_AMD_FAULT_INJECT`` (``rank=R,phase=P[,after=N]``) raises
   ``InjectedFault`` on rank R the (N+1)-th time phase P is reached -- the hook the
-  failure tests use. Phases: ``train``, ``allreduce``, ``push``, ``pull``.
+  failure tests use. Phases: ``train``, ``allreduce``, ``push``, ``pull``, ``ps_selftest`` (the
+  rank pushes a wrong delta in the device PS self-test, which must then fail).
 """
 from __future__ import annotations
 

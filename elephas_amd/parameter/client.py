@@ -9,6 +9,7 @@ which is what the MI355X workers use on the hot path.
 from __future__ import annotations
 
 import abc
+import os
 import socket
 import urllib.request as urllib2
 from typing import List
@@ -106,10 +107,76 @@ class DeviceClient(BaseParameterClient):
         self.ps = native.require().ShardedParameterServer(rank, world, int(n), consistent, device, chunk)
         self.ps.open(exchange_handles(self.ps.handle(), allgather))
         self.n = int(n)
+        self.chunk = int(chunk)
+        if world > 1 and os.environ.get("ELEPHAS_AMD_PS_SELFTEST", "1") != "0":
+            self.self_test(rank, world, bool(consistent), allgather or dist.all_gather_object)
         if server is not None:
             server.native = self.ps
             self.like = server._like
         return self
+
+    def self_test(self, rank: int, world: int, consistent: bool, allgather, K: int = 6) -> dict:
+        """Collective check of the sharded PS on the actual interconnect before any worker
+        uses it (remote fp32 atomics into peer-mapped uncached memory, flag ordering
+        across devices): every rank pushes K integer-valued deltas at once while pulling
+        snapshots; the final theta must be the exact sum of every push, no wait may time
+        out, and (asynchronous mode) no snapshot may hold a torn chunk -- a chunk is
+        constant in the pattern, so a consistent pull sees every element of it from
+        the same set of pushes.  Voted: every rank raises if any rank failed.
+        theta is left at zero; the caller sets the initial weights afterwards."""
+        import torch
+        from ..parallel import fault
+        n, ch = self.n, self.chunk
+        dev = torch.device("cuda", torch.cuda.current_device())
+        s = torch.cuda.current_stream(dev)
+        zero = torch.zeros(n, dtype=torch.float32, device=dev)
+        if rank == 0:
+            torch.cuda.synchronize(dev)
+            self.ps.set(zero.data_ptr(), s.cuda_stream)
+        torch.cuda.synchronize(dev)
+        allgather(None)   # theta = 0 before any push
+        pat = (torch.arange(n, device=dev) // ch % 5 + 1).to(torch.float32)
+        delta = pat * -float(rank + 1)   # push does theta -= delta
+        try:
+            fault.maybe_inject("ps_selftest", rank)
+        except fault.InjectedFault:
+            delta = delta * 2.0           # a wrong contribution the vote must catch
+        nsnap = K if n <= (4 << 20) else 2
+        # rows padded to 16 bytes: pull writes 16-byte vectors
+        snaps = torch.empty(nsnap, (n + 3) // 4 * 4, dtype=torch.float32, device=dev)[:, :n]
+        sp, sq = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+        sp.wait_stream(s)
+        sq.wait_stream(s)
+        for k in range(K):
+            self.ps.push_delta(delta.data_ptr(), sp.cuda_stream)
+            if k < nsnap:
+                self.ps.pull(snaps[k].data_ptr(), sq.cuda_stream)
+        torch.cuda.synchronize(dev)
+        allgather(None)   # every rank's pushes have landed
+        fin = torch.empty(n, dtype=torch.float32, device=dev)
+        self.ps.pull(fin.data_ptr(), s.cuda_stream)
+        torch.cuda.synchronize(dev)
+        want = pat * float(K * world * (world + 1) // 2)
+        res = {"exact": bool(torch.equal(fin, want)), "error": int(self.ps.error()), "torn_chunks": 0}
+        if consistent:
+            pad = (-n) % ch
+            blk = torch.nn.functional.pad(snaps, (0, pad)).reshape(nsnap, -1, ch)
+            edge = blk[:, :, :1].expand_as(blk).clone()
+            if pad:   # the padded tail of the last chunk compares against itself
+                blk[:, -1, ch - pad:] = edge[:, -1, ch - pad:]
+            res["torn_chunks"] = int((blk != edge).any(2).sum())
+        if rank == 0:
+            self.ps.set(zero.data_ptr(), s.cuda_stream)
+            torch.cuda.synchronize(dev)
+        votes = allgather(res)
+        self.self_test_result = votes
+        bad = [(r, v) for r, v in enumerate(votes) if not v["exact"] or v["error"] or v["torn_chunks"]]
+        if bad:
+            raise RuntimeError(
+                "device parameter server self-test failed on the peer interconnect "
+                f"(rank, result): {bad}; the sharded HBM parameter server cannot be trusted on this "
+                "node -- use parameter_server_mode='http' or 'socket', or mode='synchronous'")
+        return res
 
     def close(self, release: bool = False):
         """Drop this rank's endpoint.  ``release``: the caller guarantees every rank has

@@ -14,7 +14,9 @@ device-to-device with the DeviceClient (no host round trip).
 """
 from __future__ import annotations
 
+import logging
 import math
+import os
 from typing import List, Optional, Sequence
 
 import numpy as np
@@ -24,6 +26,8 @@ from .models import model_from_json
 from .ops.plan import flatten_weights, unflatten_weights
 from .parameter.client import BaseParameterClient, DeviceClient
 from .utils.functional_utils import subtract_params
+
+_log = logging.getLogger(__name__)
 
 
 def _value(parameters):
@@ -444,14 +448,14 @@ class _Group:
         self.hist = t.new_history()
         self.before = torch.empty(t.P.shape[1], dtype=torch.float32, device=t.P.device)
         self.graphs = {}
+        self.capture_error = None   # repr of the exception if hipGraph capture failed
 
     @property
     def graph(self):
         return bool(self.graphs)
 
     def capture(self, worker):
-        """Capture the CHUNK-round and 1-round graphs; eager launches if capture fails."""
-        import os
+        """Capture the CHUNK-round and 1-round graphs; eager launches (logged) if capture fails."""
         import torch
         from .parallel import fault
         if os.environ.get("ELEPHAS_AMD_ASYNC_GRAPH", "1") == "0" or fault.injection_active():
@@ -466,8 +470,16 @@ class _Group:
                         self.t.exe.train_step(self.t.s)
                         worker._push(self)
                 self.graphs[k] = g
-        except Exception:  # noqa: BLE001 - eager launches are equivalent, just slower
+        except Exception as e:  # noqa: BLE001 - eager launches are equivalent, just slower
+            # a capture failure is the first thing a new box / driver shows: say so (once
+            # per group, with the cause) instead of silently running every step eagerly;
+            # ELEPHAS_AMD_ASYNC_GRAPH=require turns it into an error
             self.graphs = {}
+            if os.environ.get("ELEPHAS_AMD_ASYNC_GRAPH") == "require":
+                raise RuntimeError(f"async group: hipGraph capture failed: {e!r}") from e
+            _log.warning("async worker group: hipGraph capture failed (%r); running its pull/step/push "
+                         "rounds as eager launches", e)
+            self.capture_error = repr(e)
 
     def steps(self, worker, n):
         """Enqueue n pull/step/push rounds (no host synchronisation)."""

@@ -177,6 +177,69 @@ def spark_async(dist, rank, world, mode):
                 same_on_all_ranks=len(set(digests)) == 1)
 
 
+def ps_selftest(dist, rank, world):
+    """DeviceClient.connect's collective self-test of the sharded PS, both consistency
+    modes; with ELEPHAS_AMD_FAULT_INJECT=rank=1,phase=ps_selftest one rank pushes a
+    wrong delta and every rank must raise."""
+    from elephas_amd.parameter.client import DeviceClient
+    out = {}
+    for mode in ("asynchronous", "hogwild"):
+        c = DeviceClient()
+        try:
+            c.connect(70_001, mode, allgather=_allgather(dist), chunk=4096)
+            out[mode] = dict(raised=False, votes=c.self_test_result)
+        except RuntimeError as e:
+            out[mode] = dict(raised=True, msg=str(e)[:300])
+        dist.barrier()   # nobody frees its shard while a peer may still read it
+    return out
+
+
+def spark_sync(dist, rank, world, gran):
+    """SparkModel(mode='synchronous') at one sync granularity on the native engine with
+    the peer all-reduce, then distributed predict / evaluate and ElephasTransformer
+    .transform; everything is saved for the test to compare against a single-process
+    run of the same scenario (no dropout, no shuffling: every partition's trajectory is
+    deterministic, so the only difference is the fp32 summation order of averaging)."""
+    import torch
+    from elephas_amd import config
+    from elephas_amd.data import SparkContext
+    from elephas_amd.ml.adapter import to_data_frame
+    from elephas_amd.ml_model import ElephasTransformer
+    from elephas_amd.models import Sequential, Dense, initializers
+    from elephas_amd.models.optimizers import SGD
+    from elephas_amd.spark_model import SparkModel
+    from elephas_amd.utils.model_utils import ModelType
+    from elephas_amd.utils.rdd_utils import to_simple_rdd
+    from elephas_amd.parallel import p2p
+    config.set_policy("float32")
+    rng = np.random.default_rng(21)
+    centers = rng.normal(0, 1, size=(5, 30)).astype(np.float32)
+    y = rng.integers(0, 5, 1600)
+    x = (centers[y] + rng.normal(0, 1.0, size=(1600, 30))).astype(np.float32)
+    yo = np.eye(5, dtype=np.float32)[y]
+    initializers.set_seed(8)
+    m = Sequential([Dense(48, activation="relu", input_dim=30), Dense(5, activation="softmax")])
+    m.compile(SGD(learning_rate=0.05, momentum=0.5), "categorical_crossentropy", ["acc"])
+    sm = SparkModel(m, mode="synchronous", sync_granularity=gran, num_workers=4)
+    sm.fit(to_simple_rdd(SparkContext(master="local[4]"), x, yo), epochs=2, batch_size=32, verbose=0,
+           validation_split=0.0, shuffle=False)
+    preds = np.stack(sm.predict(x[:333]))
+    ev = np.asarray(sm.evaluate(x, yo, batch_size=64))
+    tr = ElephasTransformer(weights=sm.master_network.get_weights(), model_type=ModelType.CLASSIFICATION)
+    tr.set_keras_model_config(sm.master_network.to_json())
+    tr.set_inference_batch_size(64)
+    df = to_data_frame(SparkContext(master="local[4]"), x[:257], yo[:257], categorical=True)
+    trans = np.asarray([r[tr.getOutputCol()] for r in tr.transform(df).collect()])
+    w = [np.asarray(a) for a in sm.master_network.get_weights()]
+    out_dir = os.environ["ELEPHAS_AMD_TEST_OUT"]
+    np.savez(os.path.join(out_dir, f"{gran}_w{world}_r{rank}.npz"), *w, preds=preds, ev=ev, trans=trans)
+    peer = p2p.current()
+    digests = _allgather(dist)(float(np.float64(np.concatenate([a.ravel() for a in w])).sum()))
+    return dict(peer_path=peer is not None, same_on_all_ranks=len(set(digests)) == 1,
+                histories=len(sm.training_histories), native=bool(sm._native_ok()),
+                gpu=bool(torch.cuda.is_available()))
+
+
 def step_graph(dist, rank, world):
     """Per-step gradient all-reduce captured in the training step's hipGraph (peer
     kernels, device-side epochs) vs the eager path with a gloo all-reduce of the same
@@ -239,6 +302,10 @@ def main():
         res = step_graph(dist, rank, world)
     elif scenario == "ps":
         res = ps(dist, rank, world)
+    elif scenario == "ps_selftest":
+        res = ps_selftest(dist, rank, world)
+    elif scenario.startswith("spark_sync_"):
+        res = spark_sync(dist, rank, world, scenario.rsplit("_", 1)[1])
     elif scenario in ("spark_asynchronous", "spark_hogwild"):
         res = spark_async(dist, rank, world, scenario.split("_", 1)[1])
     else:

@@ -8,6 +8,7 @@ import socket
 import subprocess
 import sys
 
+import numpy as np
 import pytest
 
 pytestmark = pytest.mark.gpu
@@ -86,3 +87,37 @@ def test_spark_model_async_two_ranks_learns(mode):
     for r in _run(f"spark_{mode}"):
         assert r["finite"] and r["same_on_all_ranks"], r
         assert r["acc"] > max(0.6, r["acc0"] + 0.3), r
+
+
+def test_ps_self_test_passes_and_catches_a_bad_rank():
+    """DeviceClient.connect runs a voted self-test of the sharded PS (concurrent exact
+    integer pushes, torn-chunk check in asynchronous mode); a rank that contributes a
+    wrong delta makes every rank raise instead of training on a broken server."""
+    for r in _run("ps_selftest"):
+        for mode in ("asynchronous", "hogwild"):
+            v = r[mode]
+            assert not v["raised"], v
+            assert all(x["exact"] and x["error"] == 0 and x["torn_chunks"] == 0 for x in v["votes"]), v
+    for r in _run("ps_selftest", env_extra={"ELEPHAS_AMD_FAULT_INJECT": "rank=1,phase=ps_selftest"}):
+        assert r["asynchronous"]["raised"] and "self-test failed" in r["asynchronous"]["msg"], r
+
+
+@pytest.mark.parametrize("gran", ["fit", "epoch", "batch"])
+def test_spark_model_synchronous_two_ranks_equals_single_process(tmp_path, gran):
+    """SparkModel(mode='synchronous') with two ranks on the native engine, averaging /
+    gradient exchange through the peer all-reduce (reference integration matrix,
+    tests/integration/test_end_to_end.py:18-67 with num_workers=2), then distributed
+    predict, evaluate and ElephasTransformer.transform: both ranks agree bit for bit and
+    match a single-process run over the same 4 partitions."""
+    env = {"ELEPHAS_AMD_TEST_OUT": str(tmp_path), "ELEPHAS_AMD_P2P_ANY_BACKEND": "1"}
+    two = _run(f"spark_sync_{gran}", env_extra=env)
+    one = _run(f"spark_sync_{gran}", world=1, env_extra=env)
+    for r in two:
+        assert r["peer_path"] and r["same_on_all_ranks"] and r["native"] and r["histories"] == 4, r
+    a, b = (np.load(tmp_path / f"{gran}_w2_r{r}.npz") for r in (0, 1))
+    ref = np.load(tmp_path / f"{gran}_w1_r0.npz")
+    for k in a.files:
+        assert np.array_equal(a[k], b[k]), k
+    for k in a.files:
+        scale = max(1.0, float(np.abs(ref[k]).max()))
+        np.testing.assert_allclose(a[k], ref[k], rtol=0, atol=2e-6 * scale, err_msg=k)
