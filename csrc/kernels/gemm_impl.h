@@ -1116,14 +1116,7 @@ static void set_attr() {
 // Kind-specialised variants (the latency-bound small-MLP path): every launch of a
 // training step holds one of three kind sets, and the variant that compiles only
 // those epilogues is a fraction of the all-kinds kernel's code (MNIST step
-// 65.9 -> 60.6 us). ELEPHAS_AMD_KSPEC=0 falls back to the all-kinds kernel.
-inline bool kspec_enabled() {
-  static const int on = [] {
-    const char* e = getenv("ELEPHAS_AMD_KSPEC");
-    return (e && e[0] == '0') ? 0 : 1;
-  }();
-  return on != 0;
-}
+// 65.9 -> 60.6 us); launches with other kind sets take the all-kinds kernel.
 
 template <typename T, int WM, int WN, int WAVES_M, int WAVES_N, int KSPLIT, unsigned KM0, unsigned KM1>
 static bool launch_if(const GroupArgs& ga, size_t lds, hipStream_t s, hipError_t& err) {
@@ -1143,7 +1136,7 @@ static hipError_t launch_cfg(const GroupArgs& ga, hipStream_t s) {
   for (int i = 0; i < ga.nprob; ++i) loss |= ga.p[i].kind == PK_FWD_LOSS;
   const size_t lds = lds_bytes<T, WM, WN, WAVES_M, WAVES_N, KSPLIT>(loss);
   if constexpr (SPEC) {
-    if (kspec_enabled() && ga.nprob <= 2) {
+    if (ga.nprob <= 2) {
       hipError_t e = hipSuccess;
       if (launch_if<T, WM, WN, WAVES_M, WAVES_N, KSPLIT, KM_FWD, KM_GATHER>(ga, lds, s, e) ||
           launch_if<T, WM, WN, WAVES_M, WAVES_N, KSPLIT, KM_LOSS, KM_NONE>(ga, lds, s, e) ||

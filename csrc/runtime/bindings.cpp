@@ -67,7 +67,6 @@ static ExecCfg parse_cfg(const py::dict& d) {
   c.seed = get<unsigned long long>(d, "seed", 0);
   c.force_cfg = get<int>(d, "force_cfg", -1);
   c.big = get<int>(d, "big", 0);
-  c.split_dwdx = get<int>(d, "split_dwdx", 0);
   c.rc_lean = get<int>(d, "rc_lean", 1);
   c.thr_min_k = get<int>(d, "thr_min_k", 64);
   c.thr_min_n = get<int>(d, "thr_min_n", 256);

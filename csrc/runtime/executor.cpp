@@ -642,10 +642,9 @@ void Executor::build() {
       x.lddt = c_.Bp;
       x.sDT = (long long)pv.N * c_.Bp;
       const int cw = pick_cfg(w.M, w.N, w.K), cx = pick_cfg(x.M, x.N, x.K);
-      if ((cw == 4) != (cx == 4) || (c_.split_dwdx && cw != cx)) {
+      if ((cw == 4) != (cx == 4)) {
         // one of the two products fills the chip with 256x256 tiles, the other
-        // would leave most CUs idle on them (or, with split_dwdx, any two different
-        // preferred tiles): two launches, each on its own tile
+        // would leave most CUs idle on them: two launches, each on its own tile
         La.cfg = cw;
         finalize(La);
         bwd_.push_back(La);

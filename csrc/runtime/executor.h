@@ -65,7 +65,6 @@ struct ExecCfg {
   int thr_min_k = 64;  // smallest reduction depth for the 128-row THR tiles (Otto DW, K = batch 128: 135 -> 127 us/step)
   int rowchain = -1;   // row-chain step plan: -1 when eligible, 0 off, 1 required
   int rc_lean = 1;     // skip the update of layer 0's row-major weight image (no reader)
-  int split_dwdx = 0;  // DW_l and DX_l in separate launches whenever their preferred tiles differ
   int rc_split = 0;    // layer-0 split-K slabs of the row-chain plan (0 = auto)
   int persist = -1;    // persistent chunk kernel (persist.hip): -1 when eligible, 0 off, 1 required
   long long persist_timeout_ms = 2000;  // spin limit of its in-launch waits

@@ -1,62 +1,65 @@
-"""Reader/writer lock with writer priority (reference elephas/utils/rwlock.py:10-67).
+"""Writer-preferring shared/exclusive lock for the host-side (http / socket)
+parameter servers -- the role of reference elephas/utils/rwlock.py:10-67.
 
-Several readers may hold the lock, or exactly one writer; a waiting writer
-blocks new readers.  Used by the host-side (http/socket) parameter servers;
-the device parameter server uses the native std::shared_mutex / POSIX shm
-rwlock equivalent (csrc/runtime/param_server.cpp)."""
+Design: one condition variable guards a small state record (number of shared
+holders, whether an exclusive holder exists, how many exclusive requests are
+queued).  Shared requests back off while any exclusive request is queued, so a
+stream of pulls cannot starve a push; every state change wakes all waiters and
+each re-checks its own admission predicate (simpler to reason about than
+targeted wake-ups, and the waiter count here is the number of worker threads).
+The device parameter server does not use it: its pulls and pushes are
+lock-free kernels with per-chunk counters (csrc/kernels/peer.hip).
+"""
 import threading
+from contextlib import contextmanager
 
 
 class RWLock:
     def __init__(self):
-        self.rwlock = 0          # >0: readers holding, -1: writer holding
-        self.writers_waiting = 0
-        self.monitor = threading.Lock()
-        self.readers_ok = threading.Condition(self.monitor)
-        self.writers_ok = threading.Condition(self.monitor)
+        self._cv = threading.Condition(threading.Lock())
+        self._shared = 0          # threads holding the lock shared
+        self._exclusive = False   # a thread holds it exclusively
+        self._queued = 0          # exclusive requests waiting for admission
 
-    def acquire_read(self):
-        with self.monitor:
-            while self.rwlock < 0 or self.writers_waiting:
-                self.readers_ok.wait()
-            self.rwlock += 1
+    # ----------------------------------------------------------- admission
+    def acquire_read(self) -> None:
+        with self._cv:
+            self._cv.wait_for(lambda: not self._exclusive and self._queued == 0)
+            self._shared += 1
 
-    def acquire_write(self):
-        with self.monitor:
-            while self.rwlock != 0:
-                self.writers_waiting += 1
-                self.writers_ok.wait()
-                self.writers_waiting -= 1
-            self.rwlock = -1
+    def acquire_write(self) -> None:
+        with self._cv:
+            self._queued += 1
+            try:
+                self._cv.wait_for(lambda: not self._exclusive and self._shared == 0)
+            finally:
+                self._queued -= 1
+            self._exclusive = True
 
-    def release(self):
-        with self.monitor:
-            if self.rwlock < 0:
-                self.rwlock = 0
-            elif self.rwlock > 0:
-                self.rwlock -= 1
+    def release(self) -> None:
+        """Release one hold, shared or exclusive (whichever this lock is in)."""
+        with self._cv:
+            if self._exclusive:
+                self._exclusive = False
+            elif self._shared:
+                self._shared -= 1
             else:
                 raise RuntimeError("release of an unlocked RWLock")
-            wake_writers = self.writers_waiting and self.rwlock == 0
-            wake_readers = self.writers_waiting == 0
-            if wake_writers:
-                self.writers_ok.notify()
-            elif wake_readers:
-                self.readers_ok.notify_all()
+            self._cv.notify_all()
 
-    # context-manager helpers
-    class _Ctx:
-        def __init__(self, acq, rel):
-            self.acq, self.rel = acq, rel
-
-        def __enter__(self):
-            self.acq()
-
-        def __exit__(self, *a):
-            self.rel()
-
+    # ------------------------------------------------------------ helpers
+    @contextmanager
     def read_locked(self):
-        return RWLock._Ctx(self.acquire_read, self.release)
+        self.acquire_read()
+        try:
+            yield self
+        finally:
+            self.release()
 
+    @contextmanager
     def write_locked(self):
-        return RWLock._Ctx(self.acquire_write, self.release)
+        self.acquire_write()
+        try:
+            yield self
+        finally:
+            self.release()

@@ -757,3 +757,39 @@ def test_spark_model_refit_reuses_trainer_exactly():
     ref.fit(rdd2, **kw)
     for a, b in zip(w3, ref.master_network.get_weights()):
         np.testing.assert_array_equal(a, b)
+
+
+def test_sparkmodel_averaging_is_the_bench_kernel_bit_for_bit():
+    """SparkModel._average_into and the bench's NativeTrainer.average_replicas are one
+    implementation: both give fp32(fp64 replica sum * 1/n) bit for bit (3 replicas, so
+    1/n is inexact), written back into every replica, with no host synchronisation in
+    between (the result is read after the trainer's stream)."""
+    from elephas_amd import config
+    from elephas_amd.models import Sequential, Dense, initializers
+    from elephas_amd.models.optimizers import SGD
+    from elephas_amd.ops.native_engine import NativeTrainer
+    from elephas_amd.ops.plan import build_plan
+    from elephas_amd.spark_model import SparkModel
+    from elephas_amd.profiling import PhaseTimer
+    config.set_policy("float32")
+    initializers.set_seed(4)
+    m = Sequential([Dense(40, activation="relu", input_dim=24), Dense(7, activation="softmax")])
+    m.compile(SGD(0.1), "categorical_crossentropy", ["acc"])
+    n = sum(w.size for w in m.get_weights())
+    P = np.random.default_rng(6).normal(size=(3, n)).astype(np.float32)
+    want = (P.astype(np.float64).sum(0) * (1.0 / 3)).astype(np.float32)
+    outs = []
+    for path in ("bench", "spark"):
+        t = NativeTrainer(m, build_plan(m), 3, 32, torch.device("cuda"), seed=1)
+        t.set_weights_flat(P)
+        if path == "bench":
+            mean = t.average_replicas(None, 3)
+        else:
+            sm = SparkModel(m, mode="synchronous")
+            sm._timer = PhaseTimer()
+            mean = sm._average_into(t, n, 3, True)
+        t.stream.synchronize()
+        outs.append((mean.cpu().numpy(), t.get_weights_flat()))
+    for mean, reps in outs:
+        assert np.array_equal(mean, want)
+        assert all(np.array_equal(r, want) for r in reps)
