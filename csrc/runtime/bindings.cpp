@@ -27,6 +27,8 @@ extern "C" hipError_t ea_axpby(const float* x, float* y, long long n, float alph
 extern "C" hipError_t ea_ps_sub(float* p, const float* d, long long n, float scale, int atomic, hipStream_t s);
 extern "C" hipError_t ea_poison_lds(unsigned pattern, hipStream_t s);
 extern "C" hipError_t ea_sub(const float* a, const float* b, float* out, long long n, hipStream_t s);
+extern "C" hipError_t ea_shuffle_perm(int* perm, long long sPerm, const int* ntrain, int R, int nmax, uint32_t key,
+                                      int shuffle, hipStream_t s);
 
 static void chk(hipError_t e, const char* w) {
   if (e != hipSuccess) throw std::runtime_error(std::string("HIP error in ") + w + ": " + hipGetErrorString(e));
@@ -237,6 +239,14 @@ PYBIND11_MODULE(_C, m) {
         "replica_average");
   }, py::arg("P"), py::arg("sP"), py::arg("R"), py::arg("n"), py::arg("out"), py::arg("write_back"), py::arg("stream"),
      py::arg("scale") = 0.0);
+  m.def("shuffle_perm", [](uintptr_t perm, long long sPerm, uintptr_t ntrain, int R, int nmax, uint32_t key,
+                           int shuffle, uintptr_t s) {
+    // per-replica keyed Feistel permutation of rows [0, ntrain[r]) (csrc/kernels/shuffle.hip)
+    chk(ea_shuffle_perm(reinterpret_cast<int*>(perm), sPerm, reinterpret_cast<const int*>(ntrain), R, nmax, key,
+                        shuffle, S(s)),
+        "shuffle_perm");
+  }, py::arg("perm"), py::arg("sPerm"), py::arg("ntrain"), py::arg("R"), py::arg("nmax"), py::arg("key"),
+     py::arg("shuffle"), py::arg("stream"));
   m.def("axpby", [](uintptr_t x, uintptr_t y, long long n, float a, float b, uintptr_t s) {
     chk(ea_axpby(reinterpret_cast<const float*>(x), reinterpret_cast<float*>(y), n, a, b, S(s)), "axpby");
   });
@@ -317,6 +327,12 @@ PYBIND11_MODULE(_C, m) {
         py::gil_scoped_release rel;
         L.upload_rows(reinterpret_cast<const char*>(host), host_ld, reinterpret_cast<char*>(dev), dev_ld, nrows,
                       row_bytes, S(s));
+      })
+      .def("upload_rows_bf16", [](HostLoader& L, uintptr_t host, long long host_ld, uintptr_t dev, long long dev_ld,
+                                  long long nrows, long long ncols, uintptr_t s) {
+        py::gil_scoped_release rel;
+        L.upload_rows_bf16(reinterpret_cast<const float*>(host), host_ld, reinterpret_cast<char*>(dev), dev_ld,
+                           nrows, ncols, S(s));
       })
       .def_property_readonly("bytes_uploaded", &HostLoader::bytes_uploaded)
       .def_property_readonly("threads", &HostLoader::threads)

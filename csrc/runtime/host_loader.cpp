@@ -1,6 +1,7 @@
 #include "host_loader.h"
 
 #include <algorithm>
+#include <cstdint>
 #include <cstdlib>
 #include <cstring>
 #include <thread>
@@ -67,9 +68,26 @@ void HostLoader::upload(const void* host, void* dev, long long nbytes, hipStream
   }
 }
 
-void HostLoader::pack(char* buf, const char* host, long long host_ld, long long row_bytes, long long nr) const {
+// branch-free so the packing loop vectorises
+static inline uint16_t bf16_rne(float f) {
+  uint32_t u;
+  std::memcpy(&u, &f, 4);
+  const uint32_t rne = (u + 0x7FFFu + ((u >> 16) & 1u)) >> 16;
+  const uint32_t qnan = (u >> 16) | 0x40u;
+  return (uint16_t)((u & 0x7FFFFFFFu) > 0x7F800000u ? qnan : rne);
+}
+
+void HostLoader::pack(char* buf, const char* host, long long host_ld, long long row_bytes, long long nr,
+                      bool cvt) const {
   auto part = [&](long long r0, long long r1) {
-    if (host_ld == row_bytes) {
+    if (cvt) {
+      const long long nc = row_bytes / 2;
+      for (long long r = r0; r < r1; ++r) {
+        const float* src = reinterpret_cast<const float*>(host + r * host_ld);
+        uint16_t* dst = reinterpret_cast<uint16_t*>(buf + r * row_bytes);
+        for (long long c = 0; c < nc; ++c) dst[c] = bf16_rne(src[c]);
+      }
+    } else if (host_ld == row_bytes) {
       std::memcpy(buf + r0 * row_bytes, host + r0 * host_ld, (size_t)((r1 - r0) * row_bytes));
     } else {
       for (long long r = r0; r < r1; ++r) std::memcpy(buf + r * row_bytes, host + r * host_ld, (size_t)row_bytes);
@@ -92,12 +110,22 @@ void HostLoader::pack(char* buf, const char* host, long long host_ld, long long 
 
 void HostLoader::upload_rows(const char* host, long long host_ld, char* dev, long long dev_ld, long long nrows,
                              long long row_bytes, hipStream_t s) {
+  rows_(host, host_ld, dev, dev_ld, nrows, row_bytes, false, s);
+}
+
+void HostLoader::upload_rows_bf16(const float* host, long long host_ld, char* dev, long long dev_ld, long long nrows,
+                                  long long ncols, hipStream_t s) {
+  rows_(reinterpret_cast<const char*>(host), host_ld, dev, dev_ld, nrows, 2 * ncols, true, s);
+}
+
+void HostLoader::rows_(const char* host, long long host_ld, char* dev, long long dev_ld, long long nrows,
+                       long long row_bytes, bool cvt, hipStream_t s) {
   if (row_bytes > chunk_) throw std::invalid_argument("row larger than loader chunk");
   const long long rows_per_chunk = std::max<long long>(1, chunk_ / row_bytes);
   for (long long r0 = 0; r0 < nrows; r0 += rows_per_chunk) {
     const long long nr = std::min(rows_per_chunk, nrows - r0);
     char* buf = acquire(s);
-    pack(buf, host + r0 * host_ld, host_ld, row_bytes, nr);
+    pack(buf, host + r0 * host_ld, host_ld, row_bytes, nr, cvt);
     chk(hipMemcpy2DAsync(dev + r0 * dev_ld, (size_t)dev_ld, buf, (size_t)row_bytes, (size_t)row_bytes, (size_t)nr,
                          hipMemcpyHostToDevice, s),
         "loader H2D 2D");

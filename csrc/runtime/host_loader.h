@@ -24,6 +24,10 @@ class HostLoader {
   // row-strided copy (e.g. pad rows to a 16-byte multiple on the device)
   void upload_rows(const char* host, long long host_ld, char* dev, long long dev_ld, long long nrows,
                    long long row_bytes, hipStream_t s);
+  // fp32 rows -> bf16 rows (round to nearest even, NaN kept quiet), converted by the
+  // packing threads: half the PCIe bytes of staging fp32 and converting on the device
+  void upload_rows_bf16(const float* host, long long host_ld, char* dev, long long dev_ld, long long nrows,
+                        long long ncols, hipStream_t s);
   long long bytes_uploaded() const { return bytes_; }
   int threads() const { return threads_; }
   // threads the most recent chunk was packed with (diagnostics / tests)
@@ -34,7 +38,10 @@ class HostLoader {
   int threads_ = 1;
   mutable int last_nt_ = 0;
   // rows [0, nr) of `host` (stride host_ld) -> dense rows in `buf`, split over threads_
-  void pack(char* buf, const char* host, long long host_ld, long long row_bytes, long long nr) const;
+  // cvt: host rows are fp32 and buf rows bf16 (row_bytes = 2 * columns)
+  void pack(char* buf, const char* host, long long host_ld, long long row_bytes, long long nr, bool cvt = false) const;
+  void rows_(const char* host, long long host_ld, char* dev, long long dev_ld, long long nrows, long long row_bytes,
+             bool cvt, hipStream_t s);
   std::vector<char*> bufs_;
   std::vector<hipEvent_t> evs_;
   std::vector<bool> busy_;

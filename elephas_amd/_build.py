@@ -30,6 +30,7 @@ SOURCES = [
     "kernels/rowchain.hip",
     "kernels/persist.hip",
     "kernels/peer.hip",
+    "kernels/shuffle.hip",
     "runtime/executor.cpp",
     "runtime/peer.cpp",
     "runtime/rwlock.cpp",

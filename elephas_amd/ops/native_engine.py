@@ -294,20 +294,29 @@ class NativeTrainer(TrainerBase):
         self._exit()
 
     # ------------------------------------------------------------------- data
-    def _upload_rows(self, dst: torch.Tensor, x: np.ndarray):
-        """Stream host rows into a device tensor through the native pinned loader."""
-        x = np.ascontiguousarray(x, dtype=np.float32)
+    def _upload_rows(self, dst: torch.Tensor, x: np.ndarray, stream: Optional[torch.cuda.Stream] = None):
+        """Stream host rows into the rows of a device tensor (fp32 or bf16, row stride
+        >= the row) through the native pinned double-buffered loader, on ``stream``
+        (default: the trainer's). Asynchronous: the loader packs (and, for a bf16
+        destination, converts) each chunk into pinned staging on the host before its
+        DMA is queued, so ``x`` may be released as soon as this returns."""
+        x = np.asarray(x, dtype=np.float32)
+        if x.ndim == 1:
+            x = x.reshape(-1, 1)
+        if x.strides[1] != 4:
+            x = np.ascontiguousarray(x)
         n, k = x.shape
         if n == 0:
             return
-        if dst.dtype == torch.float32 and dst.shape[-1] >= k:
-            self.loader.upload_rows(x.ctypes.data, k * 4, dst.data_ptr(), dst.stride(0) * 4, n, k * 4, self.s)
-            torch.cuda.current_stream(self.dev)  # keep ordering explicit: loader ran on self.stream
+        s = int((stream or self.stream).cuda_stream)
+        if dst.shape[-1] < k or dst.stride(-1) != 1:
+            raise ValueError("destination rows too narrow")
+        if dst.dtype == torch.float32:
+            self.loader.upload_rows(x.ctypes.data, x.strides[0], dst.data_ptr(), dst.stride(0) * 4, n, k * 4, s)
+        elif dst.dtype == torch.bfloat16:
+            self.loader.upload_rows_bf16(x.ctypes.data, x.strides[0], dst.data_ptr(), dst.stride(0) * 2, n, k, s)
         else:
-            stage = torch.empty(n, k, dtype=torch.float32, device=self.dev)
-            self.loader.upload_rows(x.ctypes.data, k * 4, stage.data_ptr(), k * 4, n, k * 4, self.s)
-            dst[:n, :k].copy_(stage)
-        self.stream.synchronize()  # host buffer must stay alive until the DMA is done
+            raise TypeError(f"upload into {dst.dtype}")
 
     def set_data(self, xs, ys, validation_split=0.0, active=None, shuffle=True):
         assert len(xs) == self.R and len(ys) == self.R
@@ -351,16 +360,17 @@ class NativeTrainer(TrainerBase):
         self._exit()
 
     def _new_perm(self, gen: Optional[torch.Generator] = None):
-        R, nmax = self.R, self.nmax
-        with torch.cuda.stream(self.stream):
-            if self.shuffle:
-                keys = torch.rand(R, nmax, device=self.dev, generator=gen)
-                nt = self.ntrain.to(torch.int64).view(R, 1)
-                ar = torch.arange(nmax, device=self.dev).view(1, nmax)
-                keys = torch.where(ar < nt, keys, torch.full_like(keys, 2.0))
-                self.perm.copy_(torch.argsort(keys, dim=1).to(torch.int32))
-            else:
-                self.perm.copy_(torch.arange(nmax, device=self.dev, dtype=torch.int32).expand(R, nmax))
+        """This epoch's row order of every replica: one launch of the keyed Feistel
+        permutation kernel (csrc/kernels/shuffle.hip). The key is a pure function of the
+        trainer seed and an epoch counter (or drawn from ``gen``), so a run is
+        reproducible from its seed."""
+        if gen is not None:
+            key = int(torch.randint(0, 2**31 - 1, (1,), generator=gen, device=gen.device).item())
+        else:
+            self._perm_epoch = getattr(self, "_perm_epoch", 0) + 1
+            key = (self.seed * 0x9E3779B97F4A7C15 + self._perm_epoch * 0xBF58476D1CE4E5B9) >> 17
+        self.C.shuffle_perm(self.perm.data_ptr(), self.nmax, self.ntrain.data_ptr(), self.R, self.nmax,
+                            key & 0xFFFFFFFF, int(bool(self.shuffle)), self.s)
 
     # ------------------------------------------------------------------ train
     def steps_per_epoch(self) -> int:
@@ -593,38 +603,89 @@ class NativeTrainer(TrainerBase):
                                    "ELEPHAS_AMD_PERSIST=0 to use the 3-launch row-chain plan")
 
     # ------------------------------------------------------------------- eval
-    def _eval_src(self, x: np.ndarray, y: Optional[np.ndarray], want_pred: bool):
+    def _eval_buffers(self, n: int, with_y: bool, want_pred: bool):
+        """Device input / target / prediction buffers for ``n`` rows and a pinned host
+        buffer for the predictions, grown on demand and kept (HBM is plentiful; a
+        pinned allocation per call would cost more than the transfer)."""
+        cap = getattr(self, "_ebuf", None)
+        need = max(int(n), 1)
+        if cap is None or cap["n"] < need:
+            n2 = max(need, 2 * cap["n"] if cap else 0)
+            with torch.cuda.device(self.dev):
+                cap = self._ebuf = dict(n=n2, X=None, Y=None, pred=None, host=None)
+        with torch.cuda.device(self.dev):
+            if cap["X"] is None:
+                cap["X"] = torch.zeros(cap["n"], self.Kp0, dtype=self.T, device=self.dev)
+            if with_y and cap["Y"] is None:
+                cap["Y"] = torch.zeros(cap["n"], self.ldy, dtype=torch.float32, device=self.dev)
+            if want_pred and cap["pred"] is None:
+                cap["pred"] = torch.empty(cap["n"], self.n_out, dtype=torch.float32, device=self.dev)
+                cap["host"] = torch.empty(cap["n"], self.n_out, dtype=torch.float32, pin_memory=True)
+        return cap
+
+    def _copy_streams(self):
+        if getattr(self, "_h2d", None) is None:
+            self._h2d = torch.cuda.Stream(device=self.dev)
+            self._d2h = torch.cuda.Stream(device=self.dev)
+        return self._h2d, self._d2h
+
+    def _eval_pipeline(self, x: np.ndarray, y: Optional[np.ndarray], want_pred: bool, r: int):
+        """Inference over host rows as a three-stream pipeline: chunk c+1 is packed on
+        the host and DMA'd to HBM (copy stream) while the eval kernels run chunk c (the
+        trainer's stream) and chunk c-1's predictions stream back into pinned host
+        memory (a second copy stream); events order each chunk's kernels after its
+        upload and its download after its kernels. Only replica ``r`` computes (the
+        others see zero rows). Returns the pinned prediction view (or None)."""
         n = len(x)
+        B = self.eval_B
+        nch = int(math.ceil(n / B))
+        exe = self._eval_exe()
+        buf = self._eval_buffers(n, y is not None, want_pred)
+        h2d, d2h = self._copy_streams()
+        cur = torch.cuda.current_stream(self.dev)
+        h2d.wait_stream(cur)
+        self.stream.wait_stream(cur)
         with torch.cuda.stream(self.stream):
-            Xe = torch.zeros(1, max(n, 1), self.Kp0, dtype=self.T, device=self.dev)
-            self._upload_rows(Xe[0], x)
-            src = dict(X=Xe.data_ptr(), sX=0, ldx=self.Kp0,
-                       vstart=torch.zeros(self.R, dtype=torch.int32, device=self.dev),
-                       vcount=torch.full((self.R,), n, dtype=torch.int32, device=self.dev))
-            keep = [Xe, src["vstart"], src["vcount"]]
-            src["vstart"], src["vcount"] = src["vstart"].data_ptr(), src["vcount"].data_ptr()
+            vstart = torch.zeros(self.R, dtype=torch.int32, device=self.dev)
+            vcount = torch.zeros(self.R, dtype=torch.int32, device=self.dev)
+            vcount[r] = n
+        src = dict(X=buf["X"].data_ptr(), sX=0, ldx=self.Kp0, vstart=vstart.data_ptr(), vcount=vcount.data_ptr(),
+                   acc=self.acc_val.data_ptr())
+        if y is not None:
+            src.update(Y=buf["Y"].data_ptr(), sY=0, ldy=self.ldy)
+        if want_pred:
+            src.update(pred=buf["pred"].data_ptr(), sPred=0, ldp=self.n_out)
+            d2h.wait_stream(cur)
+        for c in range(nch):
+            lo, hi = c * B, min(n, (c + 1) * B)
+            self._upload_rows(buf["X"][lo:hi], x[lo:hi], h2d)
             if y is not None:
-                Ye = torch.zeros(1, max(n, 1), self.ldy, dtype=torch.float32, device=self.dev)
-                self._upload_rows(Ye[0], y)
-                keep.append(Ye)
-                src.update(Y=Ye.data_ptr(), sY=0, ldy=self.ldy)
+                self._upload_rows(buf["Y"][lo:hi], y[lo:hi], h2d)
+            up = torch.cuda.Event()
+            up.record(h2d)
+            self.stream.wait_event(up)
+            exe.eval_chunk(c, src, self.s)
             if want_pred:
-                pred = torch.zeros(self.R, max(n, 1), self.n_out, dtype=torch.float32, device=self.dev)
-                keep.append(pred)
-                src.update(pred=pred.data_ptr(), sPred=max(n, 1) * self.n_out, ldp=self.n_out)
-        return src, keep
+                done = torch.cuda.Event()
+                done.record(self.stream)
+                d2h.wait_event(done)
+                with torch.cuda.stream(d2h):
+                    buf["host"][lo:hi].copy_(buf["pred"][lo:hi], non_blocking=True)
+        for t in (vstart, vcount):
+            t.record_stream(self.stream)
+        if want_pred:
+            d2h.synchronize()
+            self.stream.wait_stream(d2h)
+            return buf["host"][:n]
+        return None
 
     def evaluate_sums(self, x, y, batch_size=None, r: int = 0) -> np.ndarray:
         x = prepare_features(x, self.in_dim)
         y = prepare_targets(y, self.n_out, self.loss)
         self._enter()
-        exe = self._eval_exe()
-        src, keep = self._eval_src(x, y, False)
         with torch.cuda.stream(self.stream):
             self.acc_val.zero_()
-            src["acc"] = self.acc_val.data_ptr()
-            for c in range(int(math.ceil(len(x) / self.eval_B))):
-                exe.eval_chunk(c, src, self.s)
+        self._eval_pipeline(x, y, False, r)
         out = self._host(self.acc_val[r])
         self._exit()
         return out
@@ -639,12 +700,9 @@ class NativeTrainer(TrainerBase):
         if len(x) == 0:
             return np.zeros((0, self.n_out), np.float32)
         self._enter()
-        exe = self._eval_exe()
-        src, keep = self._eval_src(x, None, True)
-        with torch.cuda.stream(self.stream):
-            for c in range(int(math.ceil(len(x) / self.eval_B))):
-                exe.eval_chunk(c, src, self.s)
-        out = self._host(keep[-1][r, :len(x)])
+        host = self._eval_pipeline(x, None, True, r)
+        self.check()
+        out = host.numpy().copy()
         self._exit()
         return out
 

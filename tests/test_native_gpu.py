@@ -793,3 +793,43 @@ def test_sparkmodel_averaging_is_the_bench_kernel_bit_for_bit():
     for mean, reps in outs:
         assert np.array_equal(mean, want)
         assert all(np.array_equal(r, want) for r in reps)
+
+
+@pytest.mark.parametrize("policy", ["float32", "mixed_bfloat16"])
+def test_pipelined_inference_multi_chunk(policy):
+    """predict / evaluate stream the rows through the three-stream pipeline (chunked
+    uploads on a copy stream, eval kernels per chunk, chunked downloads): the result of
+    one call over many chunks equals the single-chunk calls, only replica r computes,
+    and the bf16 host conversion matches torch's fp32 -> bf16 rounding bit for bit."""
+    from elephas_amd import config
+    from elephas_amd.ops.plan import build_plan
+    from elephas_amd.ops.native_engine import NativeTrainer
+    model = _mlp(50, [64], 7)
+    model.compile("sgd", "categorical_crossentropy", ["acc"])
+    config.set_policy(policy)
+    try:
+        t = NativeTrainer(model, build_plan(model), 3, 32, torch.device("cuda"), eval_batch=256)
+        x, y = _data(1000, 50, 7, seed=5)
+        x[3, 4] = np.nan                     # a quiet NaN stays NaN through the converting pack
+        x[5, :] = np.float32(1.0 + 2.0 ** -8)   # a tie: rounds to even
+        t.set_weights_flat(np.stack([t.get_weights_flat()[0] * s for s in (1.0, 0.5, 2.0)]))
+        full = t.predict(x, r=2)
+        parts = np.concatenate([t.predict(x[i:i + 200], r=2) for i in range(0, 1000, 200)])
+        assert np.array_equal(np.isnan(full), np.isnan(parts))
+        ok = ~np.isnan(full).any(1)
+        np.testing.assert_array_equal(full[ok], parts[ok])
+        assert not np.allclose(full[ok], t.predict(x, r=0)[ok])   # replica 2 != replica 0
+        ev = t.evaluate(x[ok], y[ok], r=1)
+        ev_parts = [t.evaluate_sums(x[ok][i:i + 300], y[ok][i:i + 300], r=1) for i in range(0, ok.sum(), 300)]
+        s = np.sum(ev_parts, 0)
+        assert np.allclose(ev, [s[0] / s[1], s[2] / s[1]], rtol=1e-6)
+        if policy == "mixed_bfloat16":
+            dev = torch.zeros(4, t.Kp0, dtype=torch.bfloat16, device="cuda")
+            t._upload_rows(dev, x[:4])
+            t.stream.synchronize()
+            want = torch.from_numpy(x[:4]).to(torch.bfloat16)
+            got = dev[:, :50].cpu()
+            assert torch.equal(got.view(torch.int16)[~torch.isnan(want)], want.view(torch.int16)[~torch.isnan(want)])
+            assert torch.isnan(got[3, 4])
+    finally:
+        config.set_policy("float32")
