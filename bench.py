@@ -98,7 +98,9 @@ def main():
                          "strong: the reference job itself -- 8 partitions in total (examples/"
                          "mnist_mlp_spark_synchronous.py local[8]), 8/N workers per GPU")
     ap.add_argument("--workers-per-gpu", type=int, default=8)
-    ap.add_argument("--batch", type=int, default=64)
+    ap.add_argument("--batch", type=int, default=None,
+                    help="rows per worker per step (default: 64 MNIST, 128 Otto -- the reference examples' sizes, "
+                         "1024 Wide)")
     ap.add_argument("--policy", default="float32", choices=["mixed_bfloat16", "float32"],
                     help="float32 = the reference's Keras precision (default); mixed_bfloat16 = bf16 MFMA "
                          "operands with fp32 master weights")
@@ -126,6 +128,8 @@ def main():
     ap.add_argument("--infer-rows", type=int, default=None, help="rows per GPU for --task predict/evaluate")
     args = ap.parse_args()
 
+    if args.batch is None:
+        args.batch = {"mnist": 64, "otto": 128, "wide": 1024}[args.model]
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(_spawn_ranks(sys.argv[1:], args.gpus))
 
@@ -311,7 +315,8 @@ def main():
             "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": "bf16" if args.policy == "mixed_bfloat16" else "fp32",
-            "data": "synthetic MNIST-shaped (784 features, 10 classes), random-init weights",
+            "data": (f"synthetic {args.model.upper()}-shaped ({MODELS[args.model][0][0]} features, "
+                     f"{MODELS[args.model][2]} classes), random-init weights"),
             "config": {
                 "model": names[args.model],
                 "global_batch": B * W * world,
@@ -351,28 +356,42 @@ def main():
 
 
 def bench_fit(args, model, dist, rank, world, dev):
-    """End-to-end SparkModel.fit wall time -- the reference's measured unit
-    (examples/mnist_mlp_spark_synchronous.py:47-57: 60,000 rows in local[8]
-    partitions, 1 epoch, batch 64, validation_split 0.1, mode='synchronous'), through
-    the public API: RDD partitions -> workers -> native executor -> averaging.
-    A "step" = one whole fit call; warmup fits absorb executor construction.
-    strong: the reference job (60k rows, 8 partitions) split over the GPUs;
-    weak: that job on every GPU."""
+    """End-to-end fit wall time through the public API -- the reference's measured unit.
+    MNIST (default): SparkModel.fit as in examples/mnist_mlp_spark_synchronous.py:47-57
+      (60,000 rows in local[8] partitions, 1 epoch, batch 64, validation_split 0.1).
+    Otto (--model otto, BASELINE config #4): SparkMLlibModel.fit on an RDD of
+      LabeledPoints (reference spark_model.py:311-341; model of examples/ml_pipeline_otto.py
+      :57-68: 93-512-512-512-9, Dropout 0.5, batch 128, validation_split 0.15,
+      categorical labels, 61,878 rows), 8 partitions, mode='synchronous'.
+    RDD partitions -> workers -> native executor -> averaging. A "step" = one whole fit
+    call; warmup fits absorb executor construction.
+    strong: the reference job split over the GPUs; weak: that job on every GPU."""
     import torch
     from elephas_amd.data import SparkContext
-    from elephas_amd.spark_model import SparkModel
-    from elephas_amd.utils.rdd_utils import to_simple_rdd
+    from elephas_amd.spark_model import SparkMLlibModel, SparkModel
+    from elephas_amd.utils.rdd_utils import to_labeled_point, to_simple_rdd
     dims, _, classes, _, _ = MODELS[args.model]
+    otto = args.model == "otto"
+    base_rows = 61878 if otto else 60000
     parts = 8 if args.scaling == "strong" else 8 * world
-    rows = 60000 if args.scaling == "strong" else 60000 * world
+    rows = base_rows if args.scaling == "strong" else base_rows * world
     rng = np.random.default_rng(2024)
     centers = rng.normal(0, 1, size=(classes, dims[0])).astype(np.float32)
     y = rng.integers(0, classes, rows)
     x = np.clip(centers[y] * 0.25 + 0.5 + rng.normal(0, 0.25, size=(rows, dims[0])), 0, 1).astype(np.float32)
     yo = np.eye(classes, dtype=np.float32)[y]
-    rdd = to_simple_rdd(SparkContext(master=f"local[{parts}]"), x, yo)
-    sm = SparkModel(model, mode="synchronous")
-    kw = dict(epochs=1, batch_size=args.batch, verbose=0, validation_split=args.validation_split)
+    sc = SparkContext(master=f"local[{parts}]")
+    if otto:
+        x = (x - x.mean(0)) / x.std(0)              # the pipeline's StandardScaler(withMean, withStd)
+        data = to_labeled_point(sc, x, y.astype(np.float64))
+        sm = SparkMLlibModel(model, mode="synchronous", num_workers=parts)
+        vs = 0.15 if args.validation_split == 0.1 else args.validation_split
+        kw = dict(epochs=1, batch_size=args.batch, verbose=0, validation_split=vs, categorical=True,
+                  nb_classes=classes)
+    else:
+        data = to_simple_rdd(sc, x, yo)
+        sm = SparkModel(model, mode="synchronous")
+        kw = dict(epochs=1, batch_size=args.batch, verbose=0, validation_split=args.validation_split)
 
     def sync():
         if torch.cuda.is_available():
@@ -380,11 +399,11 @@ def bench_fit(args, model, dist, rank, world, dev):
         dist.barrier()
 
     for _ in range(max(args.warmup, 0)):
-        sm.fit(rdd, **kw)
+        sm.fit(data, **kw)
     sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        sm.fit(rdd, **kw)
+        sm.fit(data, **kw)
     sync()
     dt = time.perf_counter() - t0
     dt_max = max(dist.all_gather_object(dt))
@@ -392,14 +411,18 @@ def bench_fit(args, model, dist, rank, world, dev):
     if rank == 0:
         acc = sm.master_network.evaluate(x[:10000], yo[:10000])[1]
         line = {
-            "metric": "samples/sec (whole node) MNIST-MLP 784-128-128-10 SparkModel.fit wall (end to end)",
+            "metric": ("samples/sec (whole node) Otto-MLP 93-512-512-512-9 SparkMLlibModel.fit wall (end to end)"
+                       if otto else "samples/sec (whole node) MNIST-MLP 784-128-128-10 SparkModel.fit wall (end to end)"),
             "value": round(samples / dt_max, 1), "unit": "samples/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(dt_max / args.steps * 1e3, 4), "higher_is_better": True,
             "scaling": args.scaling, "vs_baseline": None,
             "dtype": "bf16" if args.policy == "mixed_bfloat16" else "fp32",
-            "data": "synthetic MNIST-shaped, learnable (class centers + noise), random-init weights",
-            "config": {"model": "MNIST-MLP 784-128-128-10", "rows": rows, "partitions": parts, "epochs": 1,
-                       "batch": args.batch, "validation_split": args.validation_split, "mode": "synchronous",
+            "data": (f"synthetic {args.model.upper()}-shaped, learnable (class centers + noise)"
+                     f"{', standardised, LabeledPoint RDD' if otto else ''}, random-init weights"),
+            "config": {"model": "Otto-MLP 93-512-512-512-9" if otto else "MNIST-MLP 784-128-128-10",
+                       "api": "SparkMLlibModel" if otto else "SparkModel", "rows": rows, "partitions": parts,
+                       "epochs": 1, "batch": args.batch, "validation_split": kw["validation_split"],
+                       "mode": "synchronous",
                        "seq_len": None, "global_batch": args.batch * parts, "parallelism": f"dp{world}",
                        "phases_ms_last_fit": {k: round(v * 1e3, 3) for k, v in sm.metrics["phases"].items()},
                        "train_accuracy_after": round(float(acc), 4)},
@@ -521,7 +544,7 @@ def bench_async(args, model, dist, rank, world, dev):
     groups = []
     for g in range(G):
         lo, hi = bounds[g], bounds[g + 1]
-        t = NativeTrainer(model, plan, hi - lo, B, dev, seed=4321 + 97 * rank + g)
+        t = NativeTrainer(model, plan, hi - lo, B, dev, seed=4321 + 97 * rank + g, persist=0 if G > 1 else None)
         t.set_data(dx[lo:hi], dy[lo:hi], args.validation_split, shuffle=True)
         t.begin_epoch()
         grp = _Group(t, [True] * (hi - lo))
@@ -593,6 +616,9 @@ def bench_async(args, model, dist, rank, world, dev):
                                     else "eager launches")},
         }
         print(json.dumps(line), flush=True)
+        if args.out:
+            with open(args.out, "a") as f:
+                f.write(json.dumps(line) + "\n")
     dist.barrier()
     client.close()
     if dist.is_initialized():

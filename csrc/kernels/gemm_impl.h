@@ -862,7 +862,10 @@ __device__ __forceinline__ void run_prob(const GA& ga, const Prob& p, const int 
       }
     }
 
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    // wave index as a scalar: the k-step loop bounds below depend on it, and with a
+    // VGPR wave index their branches became exec-masked and the waitcnt pass fell
+    // back to vmcnt(0) at every join
+    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int wk = wave % KSPLIT;
     const int wsp = wave / KSPLIT;
     const int wm = wsp / WAVES_N, wn = wsp % WAVES_N;
@@ -956,20 +959,17 @@ __device__ __forceinline__ void run_prob(const GA& ga, const Prob& p, const int 
       auto sel = [](bool c, const uint4& a, const uint4& b) {
         return make_uint4(c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z, c ? a.w : b.w);
       };
-      auto load_frags = [&](int kc, uint4 (&a)[WM], uint4 (&b)[WN]) {
+      // The ring holds RAW loaded fragments; masks are applied when a slot is consumed.
+      // (Selecting on the value right after its load made the compiler wait for every
+      // load as soon as it was issued -- vmcnt(0) per k-step -- so the PF-deep ring
+      // never had more than one step in flight.)
+      auto issue_frags = [&](int kc, uint4 (&a)[WM], uint4 (&b)[WN]) {
         const int kk = kc + g * EPL;
-        const bool kin = kk < Keff;
-        const int kq = kin ? kk : 0;
+        const int kq = kk < Keff ? kk : 0;
 #pragma unroll
-        for (int i = 0; i < WM; ++i) {
-          const uint4 v = *reinterpret_cast<const uint4*>(arow[i] + kq);
-          a[i] = sel(kin && ((amask >> i) & 1u), v, sel(kin && ((aones_m >> i) & 1u), one, zero));
-        }
+        for (int i = 0; i < WM; ++i) a[i] = *reinterpret_cast<const uint4*>(arow[i] + kq);
 #pragma unroll
-        for (int j = 0; j < WN; ++j) {
-          const uint4 v = *reinterpret_cast<const uint4*>(bcol[j] + kq);
-          b[j] = sel(kin && ((bmask >> j) & 1u), v, zero);
-        }
+        for (int j = 0; j < WN; ++j) b[j] = *reinterpret_cast<const uint4*>(bcol[j] + kq);
       };
       // PF-deep register ring: PF k-steps of fragments in flight per wave, so a
       // K = 784 layer waits on ~2 load round trips instead of one per step.
@@ -979,19 +979,22 @@ __device__ __forceinline__ void run_prob(const GA& ga, const Prob& p, const int 
       const int nsteps = kbeg < Keff ? (Keff - kbeg + KSTEP - 1) / KSTEP : 0;
       uint4 ra[PF][WM], rb[PF][WN];
 #pragma unroll
-      for (int u = 0; u < PF; ++u)
-        if (u < nsteps) load_frags(kbeg + u * KSTEP, ra[u], rb[u]);
+      for (int u = 0; u < PF; ++u) issue_frags(kbeg + u * KSTEP, ra[u], rb[u]);
       for (int s0 = 0; s0 < nsteps; s0 += PF) {
 #pragma unroll
         for (int u = 0; u < PF; ++u) {
           const int st_ = s0 + u;
           if (st_ < nsteps) {
+            const bool kin = kbeg + st_ * KSTEP + g * EPL < Keff;
             uint4 a[WM], b[WN];
 #pragma unroll
-            for (int i = 0; i < WM; ++i) a[i] = ra[u][i];
+            for (int i = 0; i < WM; ++i)
+              a[i] = sel(kin && ((amask >> i) & 1u), ra[u][i], sel(kin && ((aones_m >> i) & 1u), one, zero));
 #pragma unroll
-            for (int j = 0; j < WN; ++j) b[j] = rb[u][j];
-            if (st_ + PF < nsteps) load_frags(kbeg + (st_ + PF) * KSTEP, ra[u], rb[u]);
+            for (int j = 0; j < WN; ++j) b[j] = sel(kin && ((bmask >> j) & 1u), rb[u][j], zero);
+            // unconditional: past the end the addresses clamp to k = 0 and the values
+            // are masked at consumption (no branch around the loads)
+            issue_frags(kbeg + (st_ + PF) * KSTEP, ra[u], rb[u]);
 #pragma unroll
             for (int i = 0; i < WM; ++i)
 #pragma unroll

@@ -60,12 +60,12 @@ __device__ __forceinline__ void ring_load(Ring<T, NBW, PF>& R, int slot, int ks,
   constexpr int EPL = KT<T>::EPL, KC = KT<T>::KC;
   const int kk = ks * KC + (lane >> 4) * EPL;
   const bool kin = kk < R.Kd;
+  // raw values: the k-range mask is applied when the slot is consumed (ring_run), so
+  // no wait is forced on a load right after it is issued
 #pragma unroll
   for (int j = 0; j < NBW; ++j) {
-    if (w + 4 * j < R.nb) {  // wave-uniform
-      const uint4 v = *reinterpret_cast<const uint4*>(R.bp[j] + (kin ? kk : 0));
-      R.b[slot][j] = kin ? v : zero4();
-    }
+    if (w + 4 * j < R.nb)  // wave-uniform
+      R.b[slot][j] = *reinterpret_cast<const uint4*>(R.bp[j] + (kin ? kk : 0));
   }
 }
 
@@ -104,11 +104,11 @@ __device__ __forceinline__ void ring_run(Ring<T, NBW, PF>& R, const T* A, int ld
   for (int ks = 0; ks < NKMAX; ++ks) {
     if (ks < R.nks) {
       const int slot = ks % PF;
+      const bool kin = ks * KC + kg < R.Kd;
       uint4 b[NBW];
 #pragma unroll
-      for (int j = 0; j < NBW; ++j) b[j] = R.b[slot][j];
+      for (int j = 0; j < NBW; ++j) b[j] = kin ? R.b[slot][j] : zero4();
       if (NKMAX > PF && ks + PF < R.nks) ring_load(R, slot, ks + PF, w, lane);
-      const bool kin = ks * KC + kg < R.Kd;
       const uint4 av = *reinterpret_cast<const uint4*>(arow + (kin ? ks * KC : 0));
       const uint4 a = kin ? av : zero4();
 #pragma unroll

@@ -317,7 +317,7 @@ PYBIND11_MODULE(_C, m) {
 
   // ---- host loader (pinned, double-buffered H2D)
   py::class_<HostLoader>(m, "HostLoader")
-      .def(py::init<long long, int, int>(), py::arg("chunk_bytes"), py::arg("nbuf") = 2, py::arg("threads") = 0)
+      .def(py::init<long long, int, int>(), py::arg("chunk_bytes"), py::arg("nbuf") = 3, py::arg("threads") = 0)
       .def("upload", [](HostLoader& L, uintptr_t host, uintptr_t dev, long long nbytes, uintptr_t s) {
         py::gil_scoped_release rel;
         L.upload(reinterpret_cast<const void*>(host), reinterpret_cast<void*>(dev), nbytes, S(s));
@@ -334,7 +334,36 @@ PYBIND11_MODULE(_C, m) {
         L.upload_rows_bf16(reinterpret_cast<const float*>(host), host_ld, reinterpret_cast<char*>(dev), dev_ld,
                            nrows, ncols, S(s));
       })
+      .def_property_readonly("chunk_bytes", &HostLoader::chunk_bytes)
       .def_property_readonly("bytes_uploaded", &HostLoader::bytes_uploaded)
       .def_property_readonly("threads", &HostLoader::threads)
       .def_property_readonly("last_pack_threads", &HostLoader::last_pack_threads);
+
+  m.def("infer_pipeline", [](Executor& exe, HostLoader& L, py::dict a, py::dict src, uintptr_t s_up, uintptr_t s_comp,
+                             uintptr_t s_down) {
+    // inference over host rows: staged uploads / eval chunks / prediction downloads on
+    // three streams (csrc/runtime/host_loader.h)
+    InferPipeArgs p;
+    p.x = reinterpret_cast<const float*>(get<uintptr_t>(a, "x", 0));
+    p.x_ld = get<long long>(a, "x_ld", 0);
+    p.n = get<long long>(a, "n", 0);
+    p.k = get<long long>(a, "k", 0);
+    p.dX = reinterpret_cast<char*>(get<uintptr_t>(a, "dX", 0));
+    p.dX_ld = get<long long>(a, "dX_ld", 0);
+    p.x_bf16 = get<int>(a, "x_bf16", 0);
+    p.y = reinterpret_cast<const float*>(get<uintptr_t>(a, "y", 0));
+    p.y_ld = get<long long>(a, "y_ld", 0);
+    p.ky = get<long long>(a, "ky", 0);
+    p.dY = reinterpret_cast<float*>(get<uintptr_t>(a, "dY", 0));
+    p.dY_ld = get<long long>(a, "dY_ld", 0);
+    p.dPred = reinterpret_cast<float*>(get<uintptr_t>(a, "dPred", 0));
+    p.ldp = get<long long>(a, "ldp", 0);
+    p.hPred = reinterpret_cast<float*>(get<uintptr_t>(a, "hPred", 0));
+    p.out = reinterpret_cast<float*>(get<uintptr_t>(a, "out", 0));
+    p.stage_rows = get<long long>(a, "stage_rows", 0);
+    p.B = get<int>(a, "B", 0);
+    const EvalSource es = parse_src(src);
+    py::gil_scoped_release rel;
+    infer_pipeline(exe, L, p, es, S(s_up), S(s_comp), S(s_down));
+  });
 }

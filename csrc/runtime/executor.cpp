@@ -642,7 +642,18 @@ void Executor::build() {
       x.lddt = c_.Bp;
       x.sDT = (long long)pv.N * c_.Bp;
       const int cw = pick_cfg(w.M, w.N, w.K), cx = pick_cfg(x.M, x.N, x.K);
-      if ((cw == 4) != (cx == 4)) {
+      // the shared launch's tile is the larger product's; when that tile leaves the
+      // launch short of two workgroups per CU while the two products prefer different
+      // tiles, each gets its own launch (Otto 512x512 layers: DW 513x512x128 on 128x64
+      // tiles = 320 workgroups but DX 128x512x512 on them only 64, each reducing K = 512
+      // alone -- 58 us; on its own 64x32 split-K tile DX is 256 workgroups)
+      const long long wwork = (long long)w.M * w.N * w.K, xwork = (long long)x.M * x.N * x.K;
+      const int cs = pick_cfg(xwork > wwork ? x.M : w.M, xwork > wwork ? x.N : w.N, xwork > wwork ? x.K : w.K);
+      auto tiles = [&](const Prob& p, int c) {
+        return (long long)c_.R * cdiv(p.M, ea_gemm_tile_m(c)) * cdiv(p.N, ea_gemm_tile_n(c));
+      };
+      const bool underfilled = cw != cx && tiles(w, cs) + tiles(x, cs) < 512;
+      if ((cw == 4) != (cx == 4) || underfilled) {
         // one of the two products fills the chip with 256x256 tiles, the other
         // would leave most CUs idle on them: two launches, each on its own tile
         La.cfg = cw;

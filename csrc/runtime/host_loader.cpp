@@ -4,9 +4,10 @@
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
-#include <thread>
 #include <stdexcept>
 #include <string>
+
+#include "executor.h"
 
 namespace ea {
 
@@ -30,9 +31,16 @@ HostLoader::HostLoader(long long chunk_bytes, int nbuf, int threads) : chunk_(ch
     evs_.push_back(e);
     busy_.push_back(false);
   }
+  for (int i = 1; i < threads_; ++i) pool_.emplace_back(&HostLoader::worker, this, i);
 }
 
 HostLoader::~HostLoader() {
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    stop_ = true;
+  }
+  cv_.notify_all();
+  for (auto& t : pool_) t.join();
   for (size_t i = 0; i < bufs_.size(); ++i) {
     if (busy_[i]) (void)hipEventSynchronize(evs_[i]);
     (void)hipEventDestroy(evs_[i]);
@@ -40,7 +48,47 @@ HostLoader::~HostLoader() {
   }
 }
 
-char* HostLoader::acquire(hipStream_t) {
+// Pool thread `id` runs part `id` of every job that has more than `id` parts.
+void HostLoader::worker(int id) {
+  long long seen = 0;
+  for (;;) {
+    const std::function<void(int)>* job;
+    {
+      std::unique_lock<std::mutex> lk(mu_);
+      cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+      if (stop_) return;
+      seen = gen_;
+      if (id >= job_parts_) continue;
+      job = job_;
+    }
+    (*job)(id);
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      if (--pending_ == 0) done_cv_.notify_one();
+    }
+  }
+}
+
+void HostLoader::run_parts(const std::function<void(int)>& f, int n) {
+  if (n <= 1) {
+    f(0);
+    return;
+  }
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    job_ = &f;
+    job_parts_ = n;
+    pending_ = n - 1;
+    ++gen_;
+  }
+  cv_.notify_all();
+  f(0);
+  std::unique_lock<std::mutex> lk(mu_);
+  done_cv_.wait(lk, [&] { return pending_ == 0; });
+  job_ = nullptr;
+}
+
+char* HostLoader::acquire() {
   const int i = next_;
   if (busy_[i]) chk(hipEventSynchronize(evs_[i]), "loader wait");  // DMA of this buffer finished
   busy_[i] = false;
@@ -54,17 +102,15 @@ void HostLoader::release(hipStream_t s) {
 }
 
 void HostLoader::upload(const void* host, void* dev, long long nbytes, hipStream_t s) {
-  const char* h = reinterpret_cast<const char*>(host);
-  char* d = reinterpret_cast<char*>(dev);
-  for (long long off = 0; off < nbytes; off += chunk_) {
-    const long long n = std::min(chunk_, nbytes - off);
-    char* buf = acquire(s);
-    const long long pg = 4096, full = n / pg * pg;  // split contiguous bytes into 4 KB rows
-    pack(buf, h + off, pg, pg, full / pg);
-    if (n > full) std::memcpy(buf + full, h + off + full, (size_t)(n - full));
-    chk(hipMemcpyAsync(d + off, buf, (size_t)n, hipMemcpyHostToDevice, s), "loader H2D");
+  const long long pg = 4096, full = nbytes / pg * pg;  // contiguous bytes as 4 KB rows + a tail
+  if (full) rows_(reinterpret_cast<const char*>(host), pg, reinterpret_cast<char*>(dev), pg, full / pg, pg, false, s);
+  if (nbytes > full) {
+    char* buf = acquire();
+    std::memcpy(buf, reinterpret_cast<const char*>(host) + full, (size_t)(nbytes - full));
+    chk(hipMemcpyAsync(reinterpret_cast<char*>(dev) + full, buf, (size_t)(nbytes - full), hipMemcpyHostToDevice, s),
+        "loader H2D");
     release(s);
-    bytes_ += n;
+    bytes_ += nbytes - full;
   }
 }
 
@@ -77,8 +123,7 @@ static inline uint16_t bf16_rne(float f) {
   return (uint16_t)((u & 0x7FFFFFFFu) > 0x7F800000u ? qnan : rne);
 }
 
-void HostLoader::pack(char* buf, const char* host, long long host_ld, long long row_bytes, long long nr,
-                      bool cvt) const {
+void HostLoader::pack(char* buf, const char* host, long long host_ld, long long row_bytes, long long nr, bool cvt) {
   auto part = [&](long long r0, long long r1) {
     if (cvt) {
       const long long nc = row_bytes / 2;
@@ -93,19 +138,21 @@ void HostLoader::pack(char* buf, const char* host, long long host_ld, long long 
       for (long long r = r0; r < r1; ++r) std::memcpy(buf + r * row_bytes, host + r * host_ld, (size_t)row_bytes);
     }
   };
-  // one thread per 256 KB of the chunk (a 1 MB chunk uses up to 4): below that a
-  // thread costs more to start than its share of the copy
+  // one part per 256 KB of the chunk (a 1 MB chunk uses up to 4): below that the
+  // hand-off costs more than the part's share of the copy
   const int nt = (int)std::min<long long>(threads_, std::max<long long>(1, (nr * row_bytes) >> 18));
   last_nt_ = nt;
-  if (nt <= 1) {
-    part(0, nr);
-    return;
-  }
-  std::vector<std::thread> ts;
-  ts.reserve(nt - 1);
-  for (int i = 1; i < nt; ++i) ts.emplace_back(part, nr * i / nt, nr * (i + 1) / nt);
-  part(0, nr / nt);
-  for (auto& t : ts) t.join();
+  const std::function<void(int)> f = [&](int i) { part(nr * i / nt, nr * (i + 1) / nt); };
+  run_parts(f, nt);
+}
+
+void HostLoader::copy_out(void* dst, const void* src, long long nbytes) {
+  const int nt = (int)std::min<long long>(threads_, std::max<long long>(1, nbytes >> 18));
+  const std::function<void(int)> f = [&](int i) {
+    const long long a = nbytes * i / nt / 64 * 64, b = i + 1 == nt ? nbytes : nbytes * (i + 1) / nt / 64 * 64;
+    std::memcpy(reinterpret_cast<char*>(dst) + a, reinterpret_cast<const char*>(src) + a, (size_t)(b - a));
+  };
+  run_parts(f, nt);
 }
 
 void HostLoader::upload_rows(const char* host, long long host_ld, char* dev, long long dev_ld, long long nrows,
@@ -124,14 +171,76 @@ void HostLoader::rows_(const char* host, long long host_ld, char* dev, long long
   const long long rows_per_chunk = std::max<long long>(1, chunk_ / row_bytes);
   for (long long r0 = 0; r0 < nrows; r0 += rows_per_chunk) {
     const long long nr = std::min(rows_per_chunk, nrows - r0);
-    char* buf = acquire(s);
+    char* buf = acquire();
     pack(buf, host + r0 * host_ld, host_ld, row_bytes, nr, cvt);
-    chk(hipMemcpy2DAsync(dev + r0 * dev_ld, (size_t)dev_ld, buf, (size_t)row_bytes, (size_t)row_bytes, (size_t)nr,
-                         hipMemcpyHostToDevice, s),
-        "loader H2D 2D");
+    if (dev_ld == row_bytes)  // dense destination rows: one linear DMA
+      chk(hipMemcpyAsync(dev + r0 * dev_ld, buf, (size_t)(nr * row_bytes), hipMemcpyHostToDevice, s), "loader H2D");
+    else
+      chk(hipMemcpy2DAsync(dev + r0 * dev_ld, (size_t)dev_ld, buf, (size_t)row_bytes, (size_t)row_bytes, (size_t)nr,
+                           hipMemcpyHostToDevice, s),
+          "loader H2D 2D");
     release(s);
     bytes_ += nr * row_bytes;
   }
+}
+
+void infer_pipeline(Executor& exe, HostLoader& L, const InferPipeArgs& a, const EvalSource& src, hipStream_t s_up,
+                    hipStream_t s_comp, hipStream_t s_down) {
+  if (a.n <= 0) return;
+  if (a.B <= 0 || a.stage_rows <= 0 || a.stage_rows % a.B) throw std::invalid_argument("infer_pipeline: bad stage");
+  const long long nst = (a.n + a.stage_rows - 1) / a.stage_rows;
+  std::vector<hipEvent_t> evs;  // [up, done] + one download event per stage
+  auto mk = [&]() {
+    hipEvent_t e;
+    chk(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
+    evs.push_back(e);
+    return e;
+  };
+  long long copied = 0;  // stages whose predictions are in `out`
+  auto copy_stage = [&](long long st) {
+    const long long lo = st * a.stage_rows, nr = std::min(a.stage_rows, a.n - lo);
+    L.copy_out(a.out + lo * a.ldp, a.hPred + lo * a.ldp, nr * a.ldp * 4);
+  };
+  try {
+    hipEvent_t up = mk(), done = mk();
+    std::vector<hipEvent_t> dn;
+    for (long long st = 0; st < nst; ++st) {
+      const long long lo = st * a.stage_rows, nr = std::min(a.stage_rows, a.n - lo);
+      const char* xh = reinterpret_cast<const char*>(a.x) + lo * a.x_ld * 4;
+      if (a.x_bf16)
+        L.upload_rows_bf16(reinterpret_cast<const float*>(xh), a.x_ld * 4, a.dX + lo * a.dX_ld, a.dX_ld, nr, a.k, s_up);
+      else
+        L.upload_rows(xh, a.x_ld * 4, a.dX + lo * a.dX_ld, a.dX_ld, nr, a.k * 4, s_up);
+      if (a.y)
+        L.upload_rows(reinterpret_cast<const char*>(a.y + lo * a.y_ld), a.y_ld * 4,
+                      reinterpret_cast<char*>(a.dY + lo * a.dY_ld), a.dY_ld * 4, nr, a.ky * 4, s_up);
+      chk(hipEventRecord(up, s_up), "hipEventRecord");
+      chk(hipStreamWaitEvent(s_comp, up, 0), "hipStreamWaitEvent");
+      for (long long c = lo / a.B; c * a.B < lo + nr; ++c) exe.eval_chunk(c, src, s_comp);
+      if (a.hPred) {
+        chk(hipEventRecord(done, s_comp), "hipEventRecord");
+        chk(hipStreamWaitEvent(s_down, done, 0), "hipStreamWaitEvent");
+        chk(hipMemcpyAsync(a.hPred + lo * a.ldp, a.dPred + lo * a.ldp, (size_t)(nr * a.ldp * 4),
+                           hipMemcpyDeviceToHost, s_down),
+            "infer D2H");
+        dn.push_back(mk());
+        chk(hipEventRecord(dn.back(), s_down), "hipEventRecord");
+        // finished stages' results -> `out` while later stages are in flight
+        while (a.out && copied < st && hipEventQuery(dn[copied]) == hipSuccess) copy_stage(copied++);
+      }
+    }
+    if (a.out) {
+      for (; copied < nst; ++copied) {
+        chk(hipEventSynchronize(dn[copied]), "hipEventSynchronize");
+        copy_stage(copied);
+      }
+    }
+  } catch (...) {
+    for (auto e : evs) (void)hipEventDestroy(e);
+    throw;
+  }
+  // destroying a recorded event is legal: its pending waits stay valid
+  for (auto e : evs) (void)hipEventDestroy(e);
 }
 
 }  // namespace ea

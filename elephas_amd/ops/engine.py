@@ -34,7 +34,9 @@ def native_supported(model, plan=None) -> (bool, str):
 
 
 def make_trainer(model, replicas: int = 1, batch_size: int = 32, device=None, engine: Optional[str] = None,
-                 seed: Optional[int] = None):
+                 seed: Optional[int] = None, **native_kw):
+    """Native executor on a GPU when the model is supported (``native_kw`` go to
+    NativeTrainer, e.g. persist=0), else the torch reference engine."""
     device = device if device is not None else config.get_device()
     engine = engine or config.get_engine()
     plan = build_plan(model)
@@ -45,7 +47,7 @@ def make_trainer(model, replicas: int = 1, batch_size: int = 32, device=None, en
         if ok:
             native.require()
             from .native_engine import NativeTrainer
-            return NativeTrainer(model, plan, replicas, batch_size, dev, seed=seed)
+            return NativeTrainer(model, plan, replicas, batch_size, dev, seed=seed, **native_kw)
         if engine == "native":
             raise ValueError(f"native engine cannot run this model: {why}")
         log.info("elephas_amd: torch engine on %s (%s)", dev, why)

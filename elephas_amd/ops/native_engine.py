@@ -44,6 +44,14 @@ def _gpu_shared() -> bool:
         return False
 
 
+# The persistent chunk kernel needs every workgroup of its grid resident at once (they
+# wait for each other inside the launch), so two of them in flight on different streams
+# of one device can each hold part of the GPU and wait forever. Persistent launches of
+# all trainers of a device are therefore serialised: each waits for the device's most
+# recent one (an event) unless that one was issued on its own stream.
+_PERSIST_LAST: Dict[int, tuple] = {}
+
+
 def pad8(n: int) -> int:
     return (int(n) + 7) // 8 * 8
 
@@ -82,7 +90,7 @@ class NativeTrainer(TrainerBase):
         self.seed = int(seed) if seed is not None else int(np.random.randint(1, 2**62))
         self.eval_B = max(int(eval_batch), self.B)
         self.stream = torch.cuda.Stream(device=self.dev)
-        self.loader = self.C.HostLoader(8 << 20, 2)
+        self.loader = self.C.HostLoader(8 << 20, 3)
         # optimizer
         opt = model.optimizer
         nat = opt.native() if opt is not None else None
@@ -382,10 +390,33 @@ class NativeTrainer(TrainerBase):
             self._graphs[key] = self.exe.capture(nsteps, mode, self.s)
         return self._graphs[key]
 
+    def _persist_fence(self) -> bool:
+        """Order this trainer's next persistent launch after the device's previous one
+        (see _PERSIST_LAST); returns whether the plan is persistent."""
+        if not self.exe.persistent():
+            return False
+        last = _PERSIST_LAST.get(self.dev.index)
+        if last is not None and last[0] != self.s:
+            self.stream.wait_event(last[1])
+        return True
+
+    def _persist_mark(self):
+        ev = torch.cuda.Event()
+        ev.record(self.stream)
+        _PERSIST_LAST[self.dev.index] = (self.s, ev)
+
     def run_steps(self, nsteps: int, use_graph: bool = True):
         """Launch nsteps fused training steps on self.stream (asynchronous)."""
         if nsteps <= 0:
             return
+        persistent = self._persist_fence()
+        try:
+            self._run_steps(nsteps, use_graph)
+        finally:
+            if persistent:
+                self._persist_mark()
+
+    def _run_steps(self, nsteps: int, use_graph: bool):
         if not use_graph:
             for _ in range(nsteps):
                 self.exe.train_step(self.s)
@@ -629,55 +660,58 @@ class NativeTrainer(TrainerBase):
             self._d2h = torch.cuda.Stream(device=self.dev)
         return self._h2d, self._d2h
 
-    def _eval_pipeline(self, x: np.ndarray, y: Optional[np.ndarray], want_pred: bool, r: int):
-        """Inference over host rows as a three-stream pipeline: chunk c+1 is packed on
-        the host and DMA'd to HBM (copy stream) while the eval kernels run chunk c (the
-        trainer's stream) and chunk c-1's predictions stream back into pinned host
-        memory (a second copy stream); events order each chunk's kernels after its
-        upload and its download after its kernels. Only replica ``r`` computes (the
-        others see zero rows). Returns the pinned prediction view (or None)."""
+    def _eval_pipeline(self, x: np.ndarray, y: Optional[np.ndarray], want_pred: bool, r: int,
+                       out: Optional[np.ndarray] = None):
+        """Inference over host rows as a three-stream pipeline run natively
+        (csrc/runtime/host_loader.cpp infer_pipeline): the loader's packing threads fill
+        pinned staging for stage s+1 and its DMA runs on a copy stream while the eval
+        kernels compute stage s on the trainer's stream and stage s-1's predictions
+        stream back into pinned host memory on a second copy stream; events order each
+        stage's kernels after its upload and its download after its kernels. Only
+        replica ``r`` computes (the others see zero rows). With ``want_pred`` the
+        predictions land in ``out`` (a C-contiguous fp32 [n, n_out] array): the packing
+        threads copy each finished stage out of pinned memory while later stages are
+        still in flight."""
         n = len(x)
-        B = self.eval_B
-        nch = int(math.ceil(n / B))
+        if x.strides[1] != 4 or x.strides[0] % 4:
+            x = np.ascontiguousarray(x)
         exe = self._eval_exe()
         buf = self._eval_buffers(n, y is not None, want_pred)
         h2d, d2h = self._copy_streams()
         cur = torch.cuda.current_stream(self.dev)
         h2d.wait_stream(cur)
         self.stream.wait_stream(cur)
+        d2h.wait_stream(cur)
         with torch.cuda.stream(self.stream):
-            vstart = torch.zeros(self.R, dtype=torch.int32, device=self.dev)
             vcount = torch.zeros(self.R, dtype=torch.int32, device=self.dev)
             vcount[r] = n
+            vstart = torch.zeros(self.R, dtype=torch.int32, device=self.dev)
         src = dict(X=buf["X"].data_ptr(), sX=0, ldx=self.Kp0, vstart=vstart.data_ptr(), vcount=vcount.data_ptr(),
                    acc=self.acc_val.data_ptr())
+        esz = buf["X"].element_size()
+        # ~32 MB of staged input per stage (whole eval chunks): big DMAs, few events
+        row_bytes = self.in_dim * esz
+        stage = max(1, (4 * self.loader.chunk_bytes // max(row_bytes, 1)) // self.eval_B) * self.eval_B
+        a = dict(x=x.ctypes.data, x_ld=x.strides[0] // 4, n=n, k=self.in_dim, dX=buf["X"].data_ptr(),
+                 dX_ld=self.Kp0 * esz, x_bf16=int(buf["X"].dtype == torch.bfloat16), stage_rows=stage,
+                 B=self.eval_B)
         if y is not None:
+            y2 = np.asarray(y, dtype=np.float32).reshape(len(y), -1)
+            if y2.strides[1] != 4 or y2.strides[0] % 4:
+                y2 = np.ascontiguousarray(y2)
             src.update(Y=buf["Y"].data_ptr(), sY=0, ldy=self.ldy)
+            a.update(y=y2.ctypes.data, y_ld=y2.strides[0] // 4, ky=y2.shape[1], dY=buf["Y"].data_ptr(),
+                     dY_ld=self.ldy)
         if want_pred:
             src.update(pred=buf["pred"].data_ptr(), sPred=0, ldp=self.n_out)
-            d2h.wait_stream(cur)
-        for c in range(nch):
-            lo, hi = c * B, min(n, (c + 1) * B)
-            self._upload_rows(buf["X"][lo:hi], x[lo:hi], h2d)
-            if y is not None:
-                self._upload_rows(buf["Y"][lo:hi], y[lo:hi], h2d)
-            up = torch.cuda.Event()
-            up.record(h2d)
-            self.stream.wait_event(up)
-            exe.eval_chunk(c, src, self.s)
-            if want_pred:
-                done = torch.cuda.Event()
-                done.record(self.stream)
-                d2h.wait_event(done)
-                with torch.cuda.stream(d2h):
-                    buf["host"][lo:hi].copy_(buf["pred"][lo:hi], non_blocking=True)
+            assert out is not None and out.flags.c_contiguous and out.dtype == np.float32 and out.shape == (n, self.n_out)
+            a.update(dPred=buf["pred"].data_ptr(), ldp=self.n_out, hPred=buf["host"].data_ptr(), out=out.ctypes.data)
+        self.C.infer_pipeline(exe, self.loader, a, src, int(h2d.cuda_stream), self.s, int(d2h.cuda_stream))
         for t in (vstart, vcount):
             t.record_stream(self.stream)
+        self.stream.wait_stream(h2d)
         if want_pred:
-            d2h.synchronize()
-            self.stream.wait_stream(d2h)
-            return buf["host"][:n]
-        return None
+            self.stream.wait_stream(d2h)   # the next call's kernels overwrite pred after these copies
 
     def evaluate_sums(self, x, y, batch_size=None, r: int = 0) -> np.ndarray:
         x = prepare_features(x, self.in_dim)
@@ -700,9 +734,9 @@ class NativeTrainer(TrainerBase):
         if len(x) == 0:
             return np.zeros((0, self.n_out), np.float32)
         self._enter()
-        host = self._eval_pipeline(x, None, True, r)
+        out = np.empty((len(x), self.n_out), np.float32)
+        self._eval_pipeline(x, None, True, r, out)
         self.check()
-        out = host.numpy().copy()
         self._exit()
         return out
 

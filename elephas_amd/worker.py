@@ -369,7 +369,9 @@ class BatchedAsynchronousWorker:
         groups = []
         for g in range(G):
             xs, ys = zip(*data[bounds[g]:bounds[g + 1]])
-            t = make_trainer(self.model, len(xs), bs, engine="native")
+            # several groups run concurrently on their own streams: no persistent chunk
+            # kernel (it needs the whole GPU resident, and the group graphs hold it)
+            t = make_trainer(self.model, len(xs), bs, engine="native", **({"persist": 0} if G > 1 else {}))
             active = [len(x) > bs for x in xs]   # inactive replicas push a zero delta
             if self.frequency == "epoch":
                 t.set_data(list(xs), list(ys), vs, active=active, shuffle=True)

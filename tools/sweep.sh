@@ -14,5 +14,7 @@ run --mode asynchronous --frequency epoch --steps 500 --warmup 50
 run --mode asynchronous --frequency batch --steps 300 --warmup 30
 run --task predict --steps 10 --warmup 2
 run --model otto --workers-per-gpu 8 --batch 128 --steps 200 --warmup 20
+run --task fit --model otto --steps 3 --warmup 1
+run --task predict --model wide --policy mixed_bfloat16 --steps 10 --warmup 2
 run --model wide --policy mixed_bfloat16 --workers-per-gpu 1 --batch 1024 --steps 32 --warmup 8
 echo sweep ok
