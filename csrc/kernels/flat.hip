@@ -302,6 +302,26 @@ extern "C" hipError_t ea_sub(const float* a, const float* b, float* out, long lo
   return hipGetLastError();
 }
 
+// fp32 rows -> bf16 rows on the device (inference uploads of bf16 executors:
+// the rows are DMA'd as fp32 straight from pinned host memory and converted here)
+__global__ __launch_bounds__(256) void cvt_rows_bf16_kernel(const float* __restrict__ src, long long src_ld,
+                                                            __bf16* __restrict__ dst, long long dst_ld, long long nr,
+                                                            long long k) {
+  const long long total = nr * k;
+  for (long long e = (long long)blockIdx.x * 256 + threadIdx.x; e < total; e += (long long)gridDim.x * 256) {
+    const long long r = e / k, c = e % k;
+    dst[r * dst_ld + c] = from_f<__bf16>(src[r * src_ld + c]);
+  }
+}
+
+extern "C" hipError_t ea_cvt_rows_bf16(const float* src, long long src_ld, void* dst, long long dst_ld, long long nr,
+                                       long long k, hipStream_t s) {
+  if (nr <= 0 || k <= 0) return hipSuccess;
+  hipLaunchKernelGGL(cvt_rows_bf16_kernel, dim3(grid_for(nr * k)), dim3(256), 0, s, src, src_ld,
+                     reinterpret_cast<__bf16*>(dst), dst_ld, nr, k);
+  return hipGetLastError();
+}
+
 // Diagnostics: fill every CU's LDS with a pattern (e.g. NaN) so a kernel that
 // reads LDS it never wrote shows it deterministically instead of inheriting
 // whatever the previous workgroup on that CU left there.

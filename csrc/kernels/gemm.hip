@@ -8,6 +8,7 @@ hipError_t ea_gemm_launch_lat_bf16(const ea::GroupArgs* ga, hipStream_t s);
 hipError_t ea_gemm_launch_thr_bf16(const ea::GroupArgs* ga, hipStream_t s);
 hipError_t ea_gemm_launch_thr64_bf16(const ea::GroupArgs* ga, hipStream_t s);
 hipError_t ea_gemm_launch_big_bf16(const ea::GroupArgs* ga, hipStream_t s);
+hipError_t ea_gemm_launch_big_var_bf16(const ea::GroupArgs* ga, int v, hipStream_t s);
 hipError_t ea_gemm_launch_f32(const ea::GroupArgs* ga, int cfg, hipStream_t s);
 hipError_t ea_gemm_table_lat_bf16(const ea::TableArgs* ta, int dw, hipStream_t s);
 hipError_t ea_gemm_table_f32(const ea::TableArgs* ta, int dw, hipStream_t s);
@@ -33,8 +34,9 @@ extern "C" hipError_t ea_gemm_grouped(const ea::GroupArgs* ga, int bf16, int cfg
       hipLaunchKernelGGL(loss_rows_kernel<float>, dim3(ga->R, ga->total_blocks), dim3(256), lds, s, *ga);
     return hipGetLastError();
   }
-  if (!bf16) return ea_gemm_launch_f32(ga, cfg == 4 ? 1 : cfg, s);
+  if (!bf16) return ea_gemm_launch_f32(ga, cfg >= 4 ? 1 : cfg, s);
   if (cfg == 4) return ea_gemm_launch_big_bf16(ga, s);
+  if (cfg >= 5) return ea_gemm_launch_big_var_bf16(ga, cfg - 4, s);
   if (cfg == 0) return ea_gemm_launch_lat_bf16(ga, s);
   if (cfg == 2) return ea_gemm_launch_thr64_bf16(ga, s);
   return ea_gemm_launch_thr_bf16(ga, s);
@@ -59,8 +61,8 @@ extern "C" void ea_gemm_init() {
 
 // cfg 3: the 64x64 tile of the row-chain weight-gradient table launch (not a
 // grouped-launch config)
-extern "C" int ea_gemm_tile_m(int cfg) { return cfg == 4 ? 256 : ((cfg == 0 || cfg == 3) ? 64 : 128); }
+extern "C" int ea_gemm_tile_m(int cfg) { return cfg >= 4 ? 256 : ((cfg == 0 || cfg == 3) ? 64 : 128); }
 extern "C" int ea_gemm_tile_n(int cfg) {
-  return cfg == 4 ? 256 : (cfg == 0 ? 32 : ((cfg == 2 || cfg == 3) ? 64 : 128));
+  return cfg >= 4 ? 256 : (cfg == 0 ? 32 : ((cfg == 2 || cfg == 3) ? 64 : 128));
 }
 extern "C" int ea_gather_tile() { return 64; }

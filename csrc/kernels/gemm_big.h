@@ -1,33 +1,35 @@
-// 256x256 bf16 GEMM tile for the wide layers: 8 waves in two ping-pong groups.
+// 256x256 bf16 GEMM tile for the wide layers: 8 waves, 8-phase ping-pong schedule.
 //
 //   C[m][n] = sum_k A[m][k] * BT[n][k]   (the NT form of gemm_impl.h, same Prob kinds)
 //
 // Why a second tile: the 128x128 THR tile (gemm_impl.h) runs one barrier-separated
 // "wait, stage, read, MFMA" step per 64-deep k-tile with one wave per SIMD per
-// workgroup, and stalls every wave on the same LDS read burst after each barrier
-// (~840 TF at 4096^3 vs ~1450 for hipBLASLt, profiles/README.md). Here:
+// workgroup: every k-step drains its global->LDS copies before the barrier (~840 TF
+// at 4096^3 vs ~1450 for hipBLASLt, profiles/README.md). This tile follows the
+// 8-phase structure of the CDNA4 guide (cdna_hip_programming.md §5, T1-T5):
 //
 //   * 512 threads = 8 waves; wave w owns output rows (w >> 2) * 128 .. +128 and
-//     columns (w & 3) * 64 .. +64 (8 x 4 fragments of 16x16, 128 accumulator VGPRs).
-//   * Waves w and w + 4 share a SIMD; they are in different GROUPS (g = w >> 2).
-//     Group 1 starts one barrier late, so on every SIMD one wave runs its 32 MFMAs
-//     while its partner reads its next fragments from LDS and issues its share of
-//     the global->LDS copies (a "tick" = the interval between two workgroup
-//     barriers; group 0 reads sub-tile t in tick 2t and multiplies in 2t+1, group
-//     1 reads in 2t+1 and multiplies in 2t+2). The matrix pipe of a SIMD is never
-//     waiting for an LDS burst of its own wave.
-//   * The k dimension advances in 32-deep sub-tiles (A 256x32 + B^T 256x32 bf16 =
-//     32 KB) through a ring of NSLOT LDS slots (4 -> 128 KB, 5 -> 160 KB), filled
-//     with 16-byte global_load_lds (no VGPR round trip). Group 0 copies the A half,
-//     group 1 the B^T half (4 copies per lane per sub-tile each). Sub-tile t + NSLOT
-//     - 1 is issued in the read tick of t (its slot held t - 1, whose last reader
-//     retired its reads -- lgkmcnt(0) -- before the previous barrier), and each
-//     group retires its copies of t + 1 with a COUNTED vmcnt before the barrier that
-//     precedes the first read of t + 1, leaving the younger sub-tiles in flight.
-//   * LDS image of a sub-tile row (64 bytes = 4 chunks of 8 k): chunk c of row r
-//     lives in slot c ^ ((r >> 2) & 3). A fragment read (16 rows x one chunk per
-//     16-lane group) then covers all 64 banks once: conflict-free. glds writes
-//     lane-linear, so the swizzle is applied to each lane's SOURCE address.
+//     columns (w & 3) * 64 .. +64 (8 x 4 fragments of 16x16, 128 accumulators).
+//     Waves w and w + 4 share a SIMD and sit in different GROUPS (g = w >> 2);
+//     group 1 runs one barrier behind group 0, so on every SIMD one wave issues its
+//     16 MFMAs while its partner reads LDS fragments and issues its global->LDS
+//     copies (a "tick" = the interval between two workgroup barriers).
+//   * A 64-deep k-tile is 4 half-tiles of 128 rows x 128 B (A top / bottom, B^T
+//     left / right); LDS holds two k-tiles (8 half-tile slots, 128 KB). A k-tile
+//     is consumed in 4 phases, one output quadrant (64 rows x 32 columns x K 64 =
+//     16 MFMAs) per phase in snake order (m0,n0) (m0,n1) (m1,n1) (m1,n0): fragment
+//     reads 12 / 4 / 8 / 0 ds_read_b128 (the n0 B fragments stay in registers).
+//   * Every phase stages ONE half-tile with 2 16-byte global_load_lds per thread:
+//     phases 0 / 1 of k-tile t copy A top / bottom of t + 1 (their slots were last
+//     read in phase 2 of t - 1), phases 2 / 3 copy B^T left / right of t + 2 (slots
+//     last read in phase 1 of t). ONE counted wait per k-tile, in phase 3:
+//     vmcnt(4) retires everything k-tile t + 1 needs and leaves the two B^T
+//     half-tiles of t + 2 in flight (never vmcnt(0) in steady state); t + 1 is read
+//     from the next phase on, after a barrier.
+//   * LDS image rows are 128 B; chunk c of image row R holds source chunk
+//     c ^ ((R >> 1) & 7) (the swizzle is applied to each lane's global SOURCE
+//     address -- glds writes lane-linear): every ds_read_b128 lane group covers the
+//     16 slots of a bank row once (conflict-free for the 16x16x32 fragment reads).
 //
 // The epilogue stages the finished tile through LDS in two 128-row halves (one
 // group's rows each, 128 x 260 fp32 = 133 KB) and runs the shared fused Dense
@@ -38,24 +40,12 @@
 
 namespace ea {
 
-constexpr int BIG_BM = 256, BIG_BN = 256, BIG_BK = 32, BIG_NT = 512;
-constexpr int BIG_HALF = BIG_BM * BIG_BK * 2;   // bytes of one operand's sub-tile (16 KB)
-constexpr int BIG_SLOT = 2 * BIG_HALF;          // A + B^T sub-tile (32 KB)
-#ifndef EA_BIG_NSLOT
-#define EA_BIG_NSLOT 5
-#endif
-constexpr int BIG_NSLOT = EA_BIG_NSLOT;
+constexpr int BIG_BM = 256, BIG_BN = 256, BIG_BK = 64, BIG_NT = 512;
+constexpr int BIG_HT = 128 * BIG_BK * 2;        // one half-tile: 128 rows x 128 B (16 KB)
+constexpr int BIG_SET = 4 * BIG_HT;             // one k-tile: A top, A bottom, B^T left, B^T right
 constexpr int BIG_EPI_LDS = 128 * (BIG_BN + 4) * 4;  // one 128-row half of the fp32 tile
-constexpr int BIG_LDS = (BIG_NSLOT * BIG_SLOT > BIG_EPI_LDS) ? BIG_NSLOT * BIG_SLOT : BIG_EPI_LDS;
+constexpr int BIG_LDS = (2 * BIG_SET > BIG_EPI_LDS) ? 2 * BIG_SET : BIG_EPI_LDS;
 static_assert(BIG_LDS <= 160 * 1024, "LDS per workgroup");
-
-// s_waitcnt vmcnt(4 * n): this wave's copies of the n youngest sub-tiles may stay in flight
-__device__ __forceinline__ void big_wait_vm(int n) {
-  if (n <= 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  else if (n == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  else if (n == 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-}
 
 __device__ __forceinline__ void big_barrier() {
   __builtin_amdgcn_sched_barrier(0);
@@ -63,91 +53,177 @@ __device__ __forceinline__ void big_barrier() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
-// srow[t]: source row of this lane's t-th staged row (nullptr = zero row) in the
-// operand its group copies (group 0: A, group 1: B^T); ones: bit t = bias ones row.
-// acc[i][j]: output rows grp*128 + i*16 + .., columns (wave & 3)*64 + j*16 + ..
-__device__ __forceinline__ void big_mainloop(const __bf16* const (&srow)[4], unsigned ones, int K, f32x4 (&acc)[8][4],
-                                             char* sbase) {
+// src[h][i]: source row of this thread's i-th staged row of half-tile h (0 A top,
+// 1 A bottom, 2 B^T left, 3 B^T right; image row i * 64 + wave * 8 + lane / 8), as
+// a byte address (the zero row / the bias ones row for rows without data);
+// mov bit 2h + i: that row advances with k. acc[i][j]: output rows grp*128 + i*16
+// + .., columns (wave & 3)*64 + j*16 + ..
+// V (diagnostics / schedule variants, tools/big_variants.py): 0 the schedule above;
+// 1 A half-tiles staged one phase earlier (A bottom of t + 1 in phase 0, A top of
+// t + 2 in phase 3: 3 phases between the last copy k-tile t + 1 needs and its wait,
+// vmcnt(6)); 2 = 1 without any copy after the prologue (timing only: stale data);
+// 3 = 1 without fragment reads (timing only)
+template <int V = 0>
+__device__ __forceinline__ void big_mainloop(const unsigned long long (&src)[4][2], unsigned mov, int K,
+                                             f32x4 (&acc)[8][4], char* sbase) {
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int grp = wave >> 2, wig = wave & 3;
-  const int i16 = lane & 15, g = lane >> 4;
-  const int ns = (K + BIG_BK - 1) / BIG_BK;
+  const int grp = wave >> 2, wc = wave & 3;
+  const int nk = (K + BIG_BK - 1) / BIG_BK;
   const unsigned lds_base = (unsigned)(size_t)((__attribute__((address_space(3))) char*)sbase);
   typedef unsigned long long u64;
-  const u64 zp = (u64)(const void*)g_thr_zero, op = (u64)(const void*)g_thr_ones;
-  // staged chunk of this lane: LDS slot (lane & 3) of row lane >> 2 holds chunk
-  // (lane & 3) ^ ((row >> 2) & 3) of that row
-  const int c8 = ((lane & 3) ^ ((lane >> 4) & 3)) * 8;
-  u64 base[4];
-  unsigned mov = 0;
-#pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    const bool o = (ones >> t) & 1u, real = srow[t] != nullptr && !o;
-    base[t] = o ? op : (srow[t] ? (u64)srow[t] : zp);
-    mov |= real ? 1u << t : 0u;
-  }
-  // copy sub-tile s into its ring slot: instruction t of wave wig covers rows
-  // t*64 + wig*16 .. +16 of this group's operand (1 KB, lane-linear)
-  auto stage = [&](int s) {
-    const int kk = s * BIG_BK + c8;
+  const u64 zp = (u64)(const void*)g_thr_zero;
+  // staged 16-byte piece of this lane: image row i*64 + wave*8 + lane/8, image chunk
+  // lane & 7 <- source chunk (lane & 7) ^ ((row >> 1) & 7) (row bits 1..3 = lane bits 4..5, wave bit 0)
+  const int sc8 = ((lane & 7) ^ ((((wave & 1) << 2) | (lane >> 4)) & 7)) * 8;
+  auto stage = [&](int h, int kt, int set) {
+    const int kk = kt * BIG_BK + sc8;
     const bool kin = kk < K;
     const u64 koff = (u64)kk * 2u;
-    char* d = sbase + (s % BIG_NSLOT) * BIG_SLOT + grp * BIG_HALF + wig * 1024;
+    char* d = sbase + set * BIG_SET + h * BIG_HT + wave * 1024;
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const u64 a = base[t] + (((mov >> t) & 1u) ? koff : 0u);
-      glds16((const void*)(kin ? a : zp), d + t * 4096);
+    for (int i = 0; i < 2; ++i) {
+      const u64 a = src[h][i] + (((mov >> (2 * h + i)) & 1u) ? koff : 0u);
+      glds16((const void*)(kin ? a : zp), d + i * 8192);
     }
   };
-  const unsigned swz = (unsigned)((g ^ ((i16 >> 2) & 3)) * 16);
-  const unsigned a_off = (unsigned)((grp * 128 + i16) * 64) + swz;
-  const unsigned b_off = (unsigned)(BIG_HALF + (wig * 64 + i16) * 64) + swz;
-  uint4 fa[8], fb[4];
-  auto read = [&](int s) {
-    const unsigned sb = lds_base + (unsigned)((s % BIG_NSLOT) * BIG_SLOT);
+  // fragment reads: image row = base + (lane & 15), source chunk 4 ks + lane / 16
+  const int x = (lane & 15) >> 1;
+  const unsigned ck0 = (unsigned)((((lane >> 4)) ^ x) * 16), ck1 = (unsigned)(((4 + (lane >> 4)) ^ x) * 16);
+  const unsigned a_row = (unsigned)(grp * BIG_HT + (lane & 15) * 128);
+  const unsigned b_row = (unsigned)((2 + (wc >> 1)) * BIG_HT + ((wc & 1) * 64 + (lane & 15)) * 128);
+  uint4 fa[4][2], fb0[2][2], fb1[2][2];
+  auto read_a = [&](int set, int mh) {
+    const unsigned b = lds_base + (unsigned)(set * BIG_SET) + a_row + (unsigned)(mh * 64 * 128);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) ds_read16(fb[j], sb + b_off + (unsigned)(j * 16 * 64));
-#pragma unroll
-    for (int i = 0; i < 8; ++i) ds_read16(fa[i], sb + a_off + (unsigned)(i * 16 * 64));
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    for (int i = 0; i < 4; ++i) {
+      ds_read16(fa[i][0], b + (unsigned)(i * 16 * 128) + ck0);
+      ds_read16(fa[i][1], b + (unsigned)(i * 16 * 128) + ck1);
+    }
   };
-  auto mfma = [&]() {
+  auto read_b = [&](int set, int nh, uint4 (&fb)[2][2]) {
+    const unsigned b = lds_base + (unsigned)(set * BIG_SET) + b_row + (unsigned)(nh * 32 * 128);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      ds_read16(fb[j][0], b + (unsigned)(j * 16 * 128) + ck0);
+      ds_read16(fb[j][1], b + (unsigned)(j * 16 * 128) + ck1);
+    }
+  };
+  auto mfma = [&](int mh, int nh, const uint4 (&fb)[2][2]) {
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
+    for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) mma16<__bf16>(acc[i][j], fa[i], fb[j]);
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) mma16<__bf16>(acc[mh * 4 + i][nh * 2 + j], fa[i][ks], fb[j][ks]);
     __builtin_amdgcn_s_setprio(0);
   };
-  // copies of the youngest sub-tiles this wave may leave in flight once sub-tile t
-  // must have landed (it has issued 0 .. min(t + NSLOT - 2, ns - 1) or, after the
-  // read tick of t - 1, up to min(t + NSLOT - 2, ns - 1) as well)
-  auto ahead = [&](int t) { return (t + BIG_NSLOT - 2 < ns - 1 ? t + BIG_NSLOT - 2 : ns - 1) - t; };
+  auto lgkm0 = [] { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); };
 
+  if constexpr (V == 0) {
+  // prologue: k-tile 0 whole, B^T halves of k-tile 1; retire k-tile 0
 #pragma unroll
-  for (int s = 0; s < BIG_NSLOT - 1; ++s)
-    if (s < ns) stage(s);
-  big_wait_vm(ahead(0));
+  for (int h = 0; h < 4; ++h) stage(h, 0, 0);
+  if (nk > 1) {
+    stage(2, 1, 1);
+    stage(3, 1, 1);
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
   big_barrier();
   if (grp == 1) big_barrier();  // the ping-pong offset
-  for (int t = 0; t < ns; ++t) {
-    // read tick: refill the slot of t - 1, fetch this wave's fragments of t
-    if (t + BIG_NSLOT - 1 < ns) stage(t + BIG_NSLOT - 1);
-    read(t);
-    if (grp == 1 && t + 1 < ns) big_wait_vm(ahead(t + 1));  // B^T of t + 1 landed
+  for (int t = 0; t < nk; ++t) {
+    const int set = t & 1;
+    // phase 0: quadrant (m0, n0); stage A top of t + 1
+    read_b(set, 0, fb0);
+    read_a(set, 0);
+    if (t + 1 < nk) stage(0, t + 1, set ^ 1);
+    lgkm0();
     big_barrier();
-    // MFMA tick
-    mfma();
-    if (grp == 0 && t + 1 < ns) big_wait_vm(ahead(t + 1));  // A of t + 1 landed
+    mfma(0, 0, fb0);
     big_barrier();
+    // phase 1: (m0, n1); stage A bottom of t + 1
+    read_b(set, 1, fb1);
+    if (t + 1 < nk) stage(1, t + 1, set ^ 1);
+    lgkm0();
+    big_barrier();
+    mfma(0, 1, fb1);
+    big_barrier();
+    // phase 2: (m1, n1); stage B^T left of t + 2 (this set's B^T slots were last read in phase 1)
+    read_a(set, 1);
+    if (t + 2 < nk) stage(2, t + 2, set);
+    lgkm0();
+    big_barrier();
+    mfma(1, 1, fb1);
+    big_barrier();
+    // phase 3: (m1, n0) from registers; stage B^T right of t + 2; retire k-tile t + 1
+    if (t + 2 < nk) {
+      stage(3, t + 2, set);
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    } else if (t + 1 < nk) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    big_barrier();
+    mfma(1, 0, fb0);
+    big_barrier();
+  }
+  } else {
+  // V >= 1: per k-tile t, phase 0 copies A bottom of t + 1, phase 2 B^T left of t + 2,
+  // phase 3 B^T right and A top of t + 2 (this set's A slots were last read in phase 2,
+  // its B^T slots in phase 1); the wait in phase 3 leaves those three in flight
+  constexpr bool CP = V != 2, RD = V != 3;
+#pragma unroll
+  for (int h = 0; h < 4; ++h) stage(h, 0, 0);
+  if (nk > 1) {
+    stage(2, 1, 1);
+    stage(3, 1, 1);
+    stage(0, 1, 1);
+    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  big_barrier();
+  if (grp == 1) big_barrier();  // the ping-pong offset
+  for (int t = 0; t < nk; ++t) {
+    const int set = t & 1;
+    if (RD) { read_b(set, 0, fb0); read_a(set, 0); }
+    if (CP && t + 1 < nk) stage(1, t + 1, set ^ 1);
+    lgkm0();
+    big_barrier();
+    mfma(0, 0, fb0);
+    big_barrier();
+    if (RD) read_b(set, 1, fb1);
+    lgkm0();
+    big_barrier();
+    mfma(0, 1, fb1);
+    big_barrier();
+    if (RD) read_a(set, 1);
+    if (CP && t + 2 < nk) stage(2, t + 2, set);
+    lgkm0();
+    big_barrier();
+    mfma(1, 1, fb1);
+    big_barrier();
+    if (CP && t + 2 < nk) {
+      stage(3, t + 2, set);
+      stage(0, t + 2, set);
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    } else if (CP && t + 1 < nk) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    big_barrier();
+    mfma(1, 0, fb0);
+    big_barrier();
+  }
+  if (!CP) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   if (grp == 0) big_barrier();  // group 1's last MFMA tick
 }
 
 // One problem tile of the big config: block setup as run_prob, the ping-pong main
 // loop, then the fused epilogue over two 128-row halves.
-template <unsigned KM, typename GA>
+template <unsigned KM, int V = 0, typename GA>
 __device__ __forceinline__ void run_prob_big(const GA& ga, const Prob& p, const int r, const int lb, float* smem) {
   using T = __bf16;
   const int tm = lb / p.tiles_n, tn = lb % p.tiles_n;
@@ -167,29 +243,39 @@ __device__ __forceinline__ void run_prob_big(const GA& ga, const Prob& p, const 
     const __bf16* A = reinterpret_cast<const __bf16*>(p.A) + (long long)r * p.sA;
     const __bf16* BTp = reinterpret_cast<const __bf16*>(p.BT) + (long long)r * p.sB +
                         (p.bt_shadow ? (iter & 1) * p.bt_par : 0);
-    const __bf16* srow[4];
-    unsigned ones = 0;
+    typedef unsigned long long u64;
+    const u64 zp = (u64)(const void*)g_thr_zero, op = (u64)(const void*)g_thr_ones;
+    u64 src[4][2];
+    unsigned mov = 0;
+    const int wv = threadIdx.x >> 6;
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const int rr = t * 64 + wig * 16 + (lane >> 2);
-      srow[t] = nullptr;
-      if (grp == 0) {
-        const int m = m0 + rr;
-        if (m == p.ones_row) {
-          ones |= 1u << t;
-        } else if (m < p.M) {
-          if (p.a_gather) {
-            if (m < valid) srow[t] = A + batch_row(p, r, step, m) * p.lda;
-          } else {
-            srow[t] = A + (long long)m * p.lda;
+    for (int h = 0; h < 4; ++h) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int rr = (h & 1) * 128 + i * 64 + wv * 8 + (lane >> 3);  // row of the 256-row operand tile
+        u64 v = zp;
+        bool real = false;
+        if (h < 2) {
+          const int m = m0 + rr;
+          if (m == p.ones_row) {
+            v = op;
+          } else if (m < p.M) {
+            if (p.a_gather) {
+              if (m < valid) { v = (u64)(A + batch_row(p, r, step, m) * p.lda); real = true; }
+            } else {
+              v = (u64)(A + (long long)m * p.lda);
+              real = true;
+            }
           }
+        } else {
+          const int n = n0 + rr;
+          if (n < p.N) { v = (u64)(BTp + (long long)n * p.ldb); real = true; }
         }
-      } else {
-        const int n = n0 + rr;
-        if (n < p.N) srow[t] = BTp + (long long)n * p.ldb;
+        src[h][i] = v;
+        mov |= real ? 1u << (2 * h + i) : 0u;
       }
     }
-    big_mainloop(srow, ones, p.K, acc, reinterpret_cast<char*>(smem));
+    big_mainloop<V>(src, mov, p.K, acc, reinterpret_cast<char*>(smem));
   }
   stamp(ga, 2);
   __syncthreads();  // every wave is done with the staging ring
@@ -231,7 +317,7 @@ __device__ __forceinline__ int big_tile_of(int b, int ntiles, int tiles_m, int t
 
 // grid (R, total_blocks): problem by block range as gemm_grouped; the tile order
 // inside a problem is XCD-aware when the launch has one replica
-template <unsigned KM0, unsigned KM1>
+template <unsigned KM0, unsigned KM1, int V = 0>
 __global__ __launch_bounds__(BIG_NT) void gemm_big(GroupArgs ga) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   stamp(ga, 0);
@@ -241,8 +327,8 @@ __global__ __launch_bounds__(BIG_NT) void gemm_big(GroupArgs ga) {
   int lb = bid - p.block_begin;
   const int nt = p.tiles_m * p.tiles_n;
   if (ga.R == 1 && ga.nprob == 1) lb = big_tile_of(lb, nt, p.tiles_m, p.tiles_n);
-  if (pi) run_prob_big<KM1>(ga, ga.p[1], r, lb, smem);
-  else run_prob_big<KM0>(ga, ga.p[0], r, lb, smem);
+  if (pi) run_prob_big<KM1, V>(ga, ga.p[1], r, lb, smem);
+  else run_prob_big<KM0, V>(ga, ga.p[0], r, lb, smem);
   stamp(ga, 4);
 }
 

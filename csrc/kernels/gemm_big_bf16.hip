@@ -11,8 +11,8 @@ static bool big_if(const GroupArgs& ga, hipStream_t s, hipError_t& e) {
   e = hipGetLastError();
   return true;
 }
-template <unsigned KM0, unsigned KM1> static void big_attr() {
-  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_big<KM0, KM1>),
+template <unsigned KM0, unsigned KM1, int V = 0> static void big_attr() {
+  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_big<KM0, KM1, V>),
                             hipFuncAttributeMaxDynamicSharedMemorySize, BIG_LDS);
 }
 constexpr unsigned KM_PLAIN_ = KB(PK_PLAIN);
@@ -28,8 +28,22 @@ extern "C" hipError_t ea_gemm_launch_big_bf16(const ea::GroupArgs* ga, hipStream
   return hipErrorInvalidValue;  // a kind the big tile has no epilogue for (loss, gather, split-K)
 }
 
+// schedule variants of the plain GEMM for tools/big_variants.py (cfg 5 + V - 1)
+extern "C" hipError_t ea_gemm_launch_big_var_bf16(const ea::GroupArgs* ga, int v, hipStream_t s) {
+  using namespace ea;
+  if (ga->total_blocks <= 0) return hipSuccess;
+  if (ga->nprob != 1 || ga->p[0].kind != PK_PLAIN) return hipErrorInvalidValue;
+  if (v == 1) hipLaunchKernelGGL((gemm_big<KM_PLAIN_, KM_NONE, 1>), dim3(ga->R, ga->total_blocks), dim3(BIG_NT), BIG_LDS, s, *ga);
+  else if (v == 2) hipLaunchKernelGGL((gemm_big<KM_PLAIN_, KM_NONE, 2>), dim3(ga->R, ga->total_blocks), dim3(BIG_NT), BIG_LDS, s, *ga);
+  else hipLaunchKernelGGL((gemm_big<KM_PLAIN_, KM_NONE, 3>), dim3(ga->R, ga->total_blocks), dim3(BIG_NT), BIG_LDS, s, *ga);
+  return hipGetLastError();
+}
+
 extern "C" void ea_gemm_init_big_bf16() {
   using namespace ea;
+  big_attr<KM_PLAIN_, KM_NONE, 1>();
+  big_attr<KM_PLAIN_, KM_NONE, 2>();
+  big_attr<KM_PLAIN_, KM_NONE, 3>();
   big_attr<KM_PLAIN_, KM_NONE>();
   big_attr<KM_FWD, KM_NONE>();
   big_attr<KM_DW, KM_DX>();

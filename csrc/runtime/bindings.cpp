@@ -199,10 +199,10 @@ PYBIND11_MODULE(_C, m) {
     // 16-byte aligned and K padded to whole chunks, or it reads out of bounds
     const int epl = bf16 ? 8 : 4;
     if (M <= 0 || N <= 0 || K <= 0 || (K % epl) || (lda % epl) || (ldb % epl) || lda < K || ldb < K || ldc < N ||
-        (A % 16) || (BT % 16) || (C % 4) || cfg < 0 || cfg > 4 || cfg == 3)
+        (A % 16) || (BT % 16) || (C % 4) || cfg < 0 || cfg > 7 || cfg == 3)
       throw std::invalid_argument("gemm_nt: K, lda, ldb must be multiples of 16 bytes, pointers 16-byte aligned");
     ea_gemm_init();
-    if (cfg == 4 && !bf16) cfg = 1;  // the 256x256 tile is bf16-only; fp32 runs the THR tile
+    if (cfg >= 4 && !bf16) cfg = 1;  // the 256x256 tiles are bf16-only; fp32 runs the THR tile
     GroupArgs ga;
     std::memset(&ga, 0, sizeof(ga));
     Prob& p = ga.p[0];
@@ -360,6 +360,7 @@ PYBIND11_MODULE(_C, m) {
     p.ldp = get<long long>(a, "ldp", 0);
     p.hPred = reinterpret_cast<float*>(get<uintptr_t>(a, "hPred", 0));
     p.out = reinterpret_cast<float*>(get<uintptr_t>(a, "out", 0));
+    p.dStage = reinterpret_cast<float*>(get<uintptr_t>(a, "dStage", 0));
     p.stage_rows = get<long long>(a, "stage_rows", 0);
     p.B = get<int>(a, "B", 0);
     const EvalSource es = parse_src(src);

@@ -184,19 +184,50 @@ void HostLoader::rows_(const char* host, long long host_ld, char* dev, long long
   }
 }
 
+namespace {
+// a host range pinned for the duration of one call (owned: this call registered it)
+struct HostPin {
+  void* p = nullptr;
+  bool owned = false;
+  HostPin(const void* ptr, size_t bytes) {
+    if (!ptr || !bytes) return;
+    const hipError_t e = hipHostRegister(const_cast<void*>(ptr), bytes, hipHostRegisterDefault);
+    if (e == hipSuccess) {
+      p = const_cast<void*>(ptr);
+      owned = true;
+    } else {
+      (void)hipGetLastError();
+      if (e == hipErrorHostMemoryAlreadyRegistered) p = const_cast<void*>(ptr);
+    }
+  }
+  ~HostPin() {
+    if (owned) (void)hipHostUnregister(p);
+  }
+  explicit operator bool() const { return p != nullptr; }
+};
+}  // namespace
+
+extern "C" hipError_t ea_cvt_rows_bf16(const float* src, long long src_ld, void* dst, long long dst_ld, long long nr,
+                                       long long k, hipStream_t s);
+
 void infer_pipeline(Executor& exe, HostLoader& L, const InferPipeArgs& a, const EvalSource& src, hipStream_t s_up,
                     hipStream_t s_comp, hipStream_t s_down) {
   if (a.n <= 0) return;
   if (a.B <= 0 || a.stage_rows <= 0 || a.stage_rows % a.B) throw std::invalid_argument("infer_pipeline: bad stage");
+  if (a.x_bf16 && !a.dStage) throw std::invalid_argument("infer_pipeline: bf16 rows need a device staging buffer");
   const long long nst = (a.n + a.stage_rows - 1) / a.stage_rows;
-  std::vector<hipEvent_t> evs;  // [up, done] + one download event per stage
+  const HostPin xpin(a.x, (size_t)(((a.n - 1) * a.x_ld + a.k) * 4));
+  const HostPin ypin(a.y, a.y ? (size_t)(((a.n - 1) * a.y_ld + a.ky) * 4) : 0);
+  const HostPin opin(a.out, a.out ? (size_t)(a.n * a.ldp * 4) : 0);
+  std::vector<hipEvent_t> evs;  // [up, done] + one download event per stage (staged copy-out)
   auto mk = [&]() {
     hipEvent_t e;
     chk(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
     evs.push_back(e);
     return e;
   };
-  long long copied = 0;  // stages whose predictions are in `out`
+  const bool out_direct = a.out && opin;
+  long long copied = 0;  // stages whose predictions are in `out` (staged copy-out)
   auto copy_stage = [&](long long st) {
     const long long lo = st * a.stage_rows, nr = std::min(a.stage_rows, a.n - lo);
     L.copy_out(a.out + lo * a.ldp, a.hPred + lo * a.ldp, nr * a.ldp * 4);
@@ -206,36 +237,62 @@ void infer_pipeline(Executor& exe, HostLoader& L, const InferPipeArgs& a, const 
     std::vector<hipEvent_t> dn;
     for (long long st = 0; st < nst; ++st) {
       const long long lo = st * a.stage_rows, nr = std::min(a.stage_rows, a.n - lo);
-      const char* xh = reinterpret_cast<const char*>(a.x) + lo * a.x_ld * 4;
-      if (a.x_bf16)
-        L.upload_rows_bf16(reinterpret_cast<const float*>(xh), a.x_ld * 4, a.dX + lo * a.dX_ld, a.dX_ld, nr, a.k, s_up);
-      else
-        L.upload_rows(xh, a.x_ld * 4, a.dX + lo * a.dX_ld, a.dX_ld, nr, a.k * 4, s_up);
-      if (a.y)
-        L.upload_rows(reinterpret_cast<const char*>(a.y + lo * a.y_ld), a.y_ld * 4,
-                      reinterpret_cast<char*>(a.dY + lo * a.dY_ld), a.dY_ld * 4, nr, a.ky * 4, s_up);
+      const float* xh = a.x + lo * a.x_ld;
+      if (xpin && a.x_bf16) {
+        chk(hipMemcpy2DAsync(a.dStage, (size_t)(a.k * 4), xh, (size_t)(a.x_ld * 4), (size_t)(a.k * 4), (size_t)nr,
+                             hipMemcpyHostToDevice, s_up),
+            "infer H2D");
+        chk(ea_cvt_rows_bf16(a.dStage, a.k, a.dX + lo * a.dX_ld, a.dX_ld / 2, nr, a.k, s_up), "infer cvt");
+      } else if (xpin) {
+        chk(hipMemcpy2DAsync(a.dX + lo * a.dX_ld, (size_t)a.dX_ld, xh, (size_t)(a.x_ld * 4), (size_t)(a.k * 4),
+                             (size_t)nr, hipMemcpyHostToDevice, s_up),
+            "infer H2D");
+      } else if (a.x_bf16) {
+        L.upload_rows_bf16(xh, a.x_ld * 4, a.dX + lo * a.dX_ld, a.dX_ld, nr, a.k, s_up);
+      } else {
+        L.upload_rows(reinterpret_cast<const char*>(xh), a.x_ld * 4, a.dX + lo * a.dX_ld, a.dX_ld, nr, a.k * 4, s_up);
+      }
+      if (a.y) {
+        const float* yh = a.y + lo * a.y_ld;
+        if (ypin)
+          chk(hipMemcpy2DAsync(a.dY + lo * a.dY_ld, (size_t)(a.dY_ld * 4), yh, (size_t)(a.y_ld * 4), (size_t)(a.ky * 4),
+                               (size_t)nr, hipMemcpyHostToDevice, s_up),
+              "infer H2D y");
+        else
+          L.upload_rows(reinterpret_cast<const char*>(yh), a.y_ld * 4, reinterpret_cast<char*>(a.dY + lo * a.dY_ld),
+                        a.dY_ld * 4, nr, a.ky * 4, s_up);
+      }
       chk(hipEventRecord(up, s_up), "hipEventRecord");
       chk(hipStreamWaitEvent(s_comp, up, 0), "hipStreamWaitEvent");
       for (long long c = lo / a.B; c * a.B < lo + nr; ++c) exe.eval_chunk(c, src, s_comp);
-      if (a.hPred) {
+      if (a.hPred || out_direct) {
         chk(hipEventRecord(done, s_comp), "hipEventRecord");
         chk(hipStreamWaitEvent(s_down, done, 0), "hipStreamWaitEvent");
-        chk(hipMemcpyAsync(a.hPred + lo * a.ldp, a.dPred + lo * a.ldp, (size_t)(nr * a.ldp * 4),
-                           hipMemcpyDeviceToHost, s_down),
+        float* dst = out_direct ? a.out : a.hPred;
+        chk(hipMemcpyAsync(dst + lo * a.ldp, a.dPred + lo * a.ldp, (size_t)(nr * a.ldp * 4), hipMemcpyDeviceToHost,
+                           s_down),
             "infer D2H");
         dn.push_back(mk());
         chk(hipEventRecord(dn.back(), s_down), "hipEventRecord");
-        // finished stages' results -> `out` while later stages are in flight
-        while (a.out && copied < st && hipEventQuery(dn[copied]) == hipSuccess) copy_stage(copied++);
+        // staged results: finished stages -> `out` while later stages are in flight
+        while (a.out && !out_direct && copied < st && hipEventQuery(dn[copied]) == hipSuccess) copy_stage(copied++);
       }
     }
-    if (a.out) {
-      for (; copied < nst; ++copied) {
-        chk(hipEventSynchronize(dn[copied]), "hipEventSynchronize");
-        copy_stage(copied);
+    // the host arrays are unpinned on return: every transfer touching them must be done
+    if (a.out && !dn.empty()) {
+      if (out_direct) {
+        chk(hipEventSynchronize(dn.back()), "hipEventSynchronize");
+      } else {
+        for (; copied < nst; ++copied) {
+          chk(hipEventSynchronize(dn[copied]), "hipEventSynchronize");
+          copy_stage(copied);
+        }
       }
     }
+    if (xpin.owned || ypin.owned) chk(hipEventSynchronize(up), "hipEventSynchronize");
   } catch (...) {
+    (void)hipStreamSynchronize(s_up);
+    (void)hipStreamSynchronize(s_down);
     for (auto e : evs) (void)hipEventDestroy(e);
     throw;
   }

@@ -84,10 +84,15 @@ struct InferPipeArgs {
   float* dY = nullptr; long long dY_ld = 0;                      // device targets (floats stride)
   float* dPred = nullptr; long long ldp = 0; float* hPred = nullptr;  // optional predictions (pinned)
   float* out = nullptr;                                          // optional: predictions copied here too
+  float* dStage = nullptr;                                       // bf16 x: fp32 device staging, stage_rows x k
   long long stage_rows = 0;                                      // rows per stage (multiple of B)
   int B = 0;                                                     // the eval executor's chunk rows
 };
 
+// The host arrays x, y and out are pinned in place for the call (hipHostRegister,
+// ~0.8 ms for 200 MB) so every transfer is a direct DMA from / to them (bf16 x: fp32
+// rows DMA'd into dStage and converted on the device); where pinning is refused the
+// loader's packing threads stage through pinned buffers instead.
 // Stage s: upload its rows (+ targets) on s_up -> event -> the eval chunks of those
 // rows on s_comp -> event -> download their predictions into pinned host memory on
 // s_down. The host packs stage s+1 while the GPU computes stage s, and copies the

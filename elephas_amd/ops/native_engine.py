@@ -66,7 +66,7 @@ class NativeTrainer(TrainerBase):
 
     def __init__(self, model, plan, R: int = 1, batch_size: int = 32, device=None, seed: Optional[int] = None,
                  policy: Optional[str] = None, eval_batch: int = 2048, rowchain: Optional[int] = None,
-                 persist: Optional[int] = None):
+                 persist: Optional[int] = None, stream: Optional[torch.cuda.Stream] = None):
         super().__init__(model, plan, R, batch_size)
         self.C = native.require()
         # row-chain step plan (3 launches, csrc/kernels/rowchain.hip): None ->
@@ -89,7 +89,9 @@ class NativeTrainer(TrainerBase):
         self.T = torch.bfloat16 if self.bf16 else torch.float32
         self.seed = int(seed) if seed is not None else int(np.random.randint(1, 2**62))
         self.eval_B = max(int(eval_batch), self.B)
-        self.stream = torch.cuda.Stream(device=self.dev)
+        # every launch of this trainer goes to one HIP stream (shared by several trainers
+        # when a caller wants their work serialised on one hardware queue)
+        self.stream = stream if stream is not None else torch.cuda.Stream(device=self.dev)
         self.loader = self.C.HostLoader(8 << 20, 3)
         # optimizer
         opt = model.optimizer
@@ -695,6 +697,11 @@ class NativeTrainer(TrainerBase):
         a = dict(x=x.ctypes.data, x_ld=x.strides[0] // 4, n=n, k=self.in_dim, dX=buf["X"].data_ptr(),
                  dX_ld=self.Kp0 * esz, x_bf16=int(buf["X"].dtype == torch.bfloat16), stage_rows=stage,
                  B=self.eval_B)
+        if a["x_bf16"]:
+            st = getattr(self, "_stage32", None)
+            if st is None or st.numel() < stage * self.in_dim:
+                st = self._stage32 = torch.empty(stage * self.in_dim, dtype=torch.float32, device=self.dev)
+            a["dStage"] = st.data_ptr()
         if y is not None:
             y2 = np.asarray(y, dtype=np.float32).reshape(len(y), -1)
             if y2.strides[1] != 4 or y2.strides[0] % 4:

@@ -316,6 +316,18 @@ class AsynchronousSparkWorker:
             self.client.update_parameters(unflatten_weights(delta, self.model.get_weights()))
 
 
+def async_streams(groups: int):
+    """HIP streams for ``groups`` independently progressing worker groups: at most
+    $ELEPHAS_AMD_ASYNC_STREAMS (default 4 = GPU_MAX_HW_QUEUES, the hardware queues HIP
+    gives a process). Streams beyond the queue count share queues and serialise behind
+    each other's kernels (profiles/README.md, stream probe: 8 row-chain groups on 8
+    streams 92 us per 8-worker step vs 49 us on 4); groups past the stream count are
+    dealt round-robin onto them and still pull / train / push independently."""
+    import torch
+    n = max(1, min(groups, int(os.environ.get("ELEPHAS_AMD_ASYNC_STREAMS", "4") or 4)))
+    return [torch.cuda.Stream() for _ in range(n)]
+
+
 class BatchedAsynchronousWorker:
     """GPU path of the asynchronous / hogwild workers for all of a rank's partitions.
 
@@ -367,11 +379,13 @@ class BatchedAsynchronousWorker:
         G = self._n_groups(len(parts))
         bounds = [len(parts) * g // G for g in range(G + 1)]
         groups = []
+        streams = async_streams(G)
         for g in range(G):
             xs, ys = zip(*data[bounds[g]:bounds[g + 1]])
             # several groups run concurrently on their own streams: no persistent chunk
             # kernel (it needs the whole GPU resident, and the group graphs hold it)
-            t = make_trainer(self.model, len(xs), bs, engine="native", **({"persist": 0} if G > 1 else {}))
+            t = make_trainer(self.model, len(xs), bs, engine="native",
+                             **({"persist": 0, "stream": streams[g % len(streams)]} if G > 1 else {}))
             active = [len(x) > bs for x in xs]   # inactive replicas push a zero delta
             if self.frequency == "epoch":
                 t.set_data(list(xs), list(ys), vs, active=active, shuffle=True)
