@@ -518,7 +518,7 @@ def bench_async(args, model, dist, rank, world, dev):
     from elephas_amd.ops.native_engine import NativeTrainer
     from elephas_amd.ops.plan import build_plan, flatten_weights
     from elephas_amd.parameter.client import DeviceClient
-    from elephas_amd.worker import BatchedAsynchronousWorker, _Group, async_streams
+    from elephas_amd.worker import BatchedAsynchronousWorker, _Group, group_persist_cus
     dims, drop, classes, rows, _ = MODELS[args.model]
     W, B = args.workers_per_gpu, args.batch
     G = max(1, min(W, args.async_groups or W))
@@ -542,11 +542,10 @@ def bench_async(args, model, dist, rank, world, dev):
     freq = args.frequency
     worker = BatchedAsynchronousWorker(None, None, client, {}, freq, None, None, None, None)
     groups = []
-    streams = async_streams(G)
     for g in range(G):
         lo, hi = bounds[g], bounds[g + 1]
-        t = NativeTrainer(model, plan, hi - lo, B, dev, seed=4321 + 97 * rank + g, persist=0 if G > 1 else None,
-                          stream=streams[g % len(streams)] if G > 1 else None)
+        t = NativeTrainer(model, plan, hi - lo, B, dev, seed=4321 + 97 * rank + g,
+                          persist_cus=group_persist_cus(G, dev) if G > 1 else None)
         t.set_data(dx[lo:hi], dy[lo:hi], args.validation_split, shuffle=True)
         t.begin_epoch()
         grp = _Group(t, [True] * (hi - lo))
@@ -611,7 +610,8 @@ def bench_async(args, model, dist, rank, world, dev):
             "data": "synthetic, random-init weights",
             "config": {"model": args.model, "global_batch": B * W * world, "seq_len": None,
                        "parallelism": f"{args.mode}-dp{world}", "workers_per_gpu": W, "batch_per_worker": B,
-                       "frequency": freq, "groups_per_gpu": G, "streams_per_gpu": len(streams),
+                       "frequency": freq, "groups_per_gpu": G,
+                       "plan": groups[0].t.plan_name() if hasattr(groups[0].t, "plan_name") else None,
                        "ps": f"sharded over {world} GPU(s), 4096-parameter chunks, IPC-mapped",
                        "exchange": ("pull / push per epoch around hipGraph training chunks" if freq == "epoch"
                                     else "hipGraph per group-step (pull, refresh, train, push)" if groups[0].graph

@@ -61,8 +61,8 @@ __device__ __forceinline__ void big_barrier() {
 // V (diagnostics / schedule variants, tools/big_variants.py): 0 the schedule above;
 // 1 A half-tiles staged one phase earlier (A bottom of t + 1 in phase 0, A top of
 // t + 2 in phase 3: 3 phases between the last copy k-tile t + 1 needs and its wait,
-// vmcnt(6)); 2 = 1 without any copy after the prologue (timing only: stale data);
-// 3 = 1 without fragment reads (timing only)
+// vmcnt(6)); 5 and 6 below. (Measured with copies removed: 1042 / 1434 TF at 4096^3 /
+// 8192^3; with fragment reads removed: 1129 / 1507 -- profiles/big_variants_r3.txt.)
 template <int V = 0>
 __device__ __forceinline__ void big_mainloop(const unsigned long long (&src)[4][2], unsigned mov, int K,
                                              f32x4 (&acc)[8][4], char* sbase) {
@@ -172,8 +172,16 @@ __device__ __forceinline__ void big_mainloop(const unsigned long long (&src)[4][
   } else {
   // V >= 1: per k-tile t, phase 0 copies A bottom of t + 1, phase 2 B^T left of t + 2,
   // phase 3 B^T right and A top of t + 2 (this set's A slots were last read in phase 2,
-  // its B^T slots in phase 1); the wait in phase 3 leaves those three in flight
-  constexpr bool CP = V != 2, RD = V != 3;
+  // its B^T slots in phase 1); the wait in phase 3 leaves those three in flight.
+  // V 6: the copies are issued in the MFMA tick (between MFMAs an LDS-DMA issue costs
+  // less than beside a burst of reads); each group then retires k-tile t + 1 in its
+  // read tick of phase 3 (vmcnt(2): B^T left of t + 2 in flight), before the barrier
+  // that precedes the other group's first read of it. V 5: V 6 with the fragment-read
+  // wait behind the barrier (the read tick ends once the reads are issued; the MFMA
+  // tick absorbs what is left of their latency). Copies must stay in MFMA ticks then:
+  // a read is only retired after the barrier that ends its tick, so a copy issued in
+  // the next read tick of the other group could overwrite a slot still being read.
+  constexpr bool LATE = V == 5, MCP = V >= 5;
 #pragma unroll
   for (int h = 0; h < 4; ++h) stage(h, 0, 0);
   if (nk > 1) {
@@ -186,37 +194,52 @@ __device__ __forceinline__ void big_mainloop(const unsigned long long (&src)[4][
   }
   big_barrier();
   if (grp == 1) big_barrier();  // the ping-pong offset
+  auto tick_end = [&] {
+    if (!LATE) lgkm0();
+    big_barrier();
+    if (LATE) lgkm0();
+  };
   for (int t = 0; t < nk; ++t) {
     const int set = t & 1;
-    if (RD) { read_b(set, 0, fb0); read_a(set, 0); }
-    if (CP && t + 1 < nk) stage(1, t + 1, set ^ 1);
-    lgkm0();
-    big_barrier();
+    read_b(set, 0, fb0);
+    read_a(set, 0);
+    if (!MCP && t + 1 < nk) stage(1, t + 1, set ^ 1);
+    tick_end();
+    if (MCP && t + 1 < nk) stage(1, t + 1, set ^ 1);
     mfma(0, 0, fb0);
     big_barrier();
-    if (RD) read_b(set, 1, fb1);
-    lgkm0();
-    big_barrier();
+    read_b(set, 1, fb1);
+    tick_end();
     mfma(0, 1, fb1);
     big_barrier();
-    if (RD) read_a(set, 1);
-    if (CP && t + 2 < nk) stage(2, t + 2, set);
-    lgkm0();
-    big_barrier();
+    read_a(set, 1);
+    if (!MCP && t + 2 < nk) stage(2, t + 2, set);
+    tick_end();
+    if (MCP && t + 2 < nk) stage(2, t + 2, set);
     mfma(1, 1, fb1);
     big_barrier();
-    if (CP && t + 2 < nk) {
-      stage(3, t + 2, set);
-      stage(0, t + 2, set);
-      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-    } else if (CP && t + 1 < nk) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (MCP) {
+      if (t + 2 < nk) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      else if (t + 1 < nk) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      big_barrier();
+      if (t + 2 < nk) {
+        stage(3, t + 2, set);
+        stage(0, t + 2, set);
+      }
+    } else {
+      if (t + 2 < nk) {
+        stage(3, t + 2, set);
+        stage(0, t + 2, set);
+        asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      } else if (t + 1 < nk) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      big_barrier();
     }
-    big_barrier();
     mfma(1, 0, fb0);
     big_barrier();
   }
-  if (!CP) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   if (grp == 0) big_barrier();  // group 1's last MFMA tick
 }

@@ -34,16 +34,16 @@ extern "C" hipError_t ea_gemm_launch_big_var_bf16(const ea::GroupArgs* ga, int v
   if (ga->total_blocks <= 0) return hipSuccess;
   if (ga->nprob != 1 || ga->p[0].kind != PK_PLAIN) return hipErrorInvalidValue;
   if (v == 1) hipLaunchKernelGGL((gemm_big<KM_PLAIN_, KM_NONE, 1>), dim3(ga->R, ga->total_blocks), dim3(BIG_NT), BIG_LDS, s, *ga);
-  else if (v == 2) hipLaunchKernelGGL((gemm_big<KM_PLAIN_, KM_NONE, 2>), dim3(ga->R, ga->total_blocks), dim3(BIG_NT), BIG_LDS, s, *ga);
-  else hipLaunchKernelGGL((gemm_big<KM_PLAIN_, KM_NONE, 3>), dim3(ga->R, ga->total_blocks), dim3(BIG_NT), BIG_LDS, s, *ga);
+  else if (v == 2) hipLaunchKernelGGL((gemm_big<KM_PLAIN_, KM_NONE, 6>), dim3(ga->R, ga->total_blocks), dim3(BIG_NT), BIG_LDS, s, *ga);
+  else hipLaunchKernelGGL((gemm_big<KM_PLAIN_, KM_NONE, 5>), dim3(ga->R, ga->total_blocks), dim3(BIG_NT), BIG_LDS, s, *ga);
   return hipGetLastError();
 }
 
 extern "C" void ea_gemm_init_big_bf16() {
   using namespace ea;
   big_attr<KM_PLAIN_, KM_NONE, 1>();
-  big_attr<KM_PLAIN_, KM_NONE, 2>();
-  big_attr<KM_PLAIN_, KM_NONE, 3>();
+  big_attr<KM_PLAIN_, KM_NONE, 6>();
+  big_attr<KM_PLAIN_, KM_NONE, 5>();
   big_attr<KM_PLAIN_, KM_NONE>();
   big_attr<KM_FWD, KM_NONE>();
   big_attr<KM_DW, KM_DX>();

@@ -68,6 +68,7 @@ bool Executor::build_persist() {
   check(hipGetDevice(&dev), "hipGetDevice");
   check(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev), "hipDeviceGetAttribute");
   if (const char* e = std::getenv("ELEPHAS_AMD_PERSIST_CUS")) ncu = std::min(ncu, std::atoi(e));  // tests: a smaller grid
+  if (c_.persist_cus > 0) ncu = std::min(ncu, c_.persist_cus);  // a share of the GPU (concurrent executors)
   int lds_max = 0;
   check(hipDeviceGetAttribute(&lds_max, hipDeviceAttributeMaxSharedMemoryPerBlock, dev), "hipDeviceGetAttribute");
   if (ea_persist_lds_bytes() > lds_max) return false;

@@ -68,6 +68,7 @@ struct ExecCfg {
   int rc_split = 0;    // layer-0 split-K slabs of the row-chain plan (0 = auto)
   int persist = -1;    // persistent chunk kernel (persist.hip): -1 when eligible, 0 off, 1 required
   long long persist_timeout_ms = 2000;  // spin limit of its in-launch waits
+  int persist_cus = 0;  // > 0: CUs the persistent grid may occupy (several executors side by side)
 };
 
 struct EvalSource {

@@ -66,7 +66,8 @@ class NativeTrainer(TrainerBase):
 
     def __init__(self, model, plan, R: int = 1, batch_size: int = 32, device=None, seed: Optional[int] = None,
                  policy: Optional[str] = None, eval_batch: int = 2048, rowchain: Optional[int] = None,
-                 persist: Optional[int] = None, stream: Optional[torch.cuda.Stream] = None):
+                 persist: Optional[int] = None, stream: Optional[torch.cuda.Stream] = None,
+                 persist_cus: Optional[int] = None):
         super().__init__(model, plan, R, batch_size)
         self.C = native.require()
         # row-chain step plan (3 launches, csrc/kernels/rowchain.hip): None ->
@@ -79,6 +80,11 @@ class NativeTrainer(TrainerBase):
         self.persist_mode = int(os.environ.get("ELEPHAS_AMD_PERSIST", "-1")) if persist is None else int(persist)
         if persist is None and self.persist_mode < 0 and _gpu_shared():
             self.persist_mode = 0
+        # persist_cus: the persistent grid is sized to this share of the GPU's CUs, so
+        # several trainers whose shares sum to at most the CU count run their persistent
+        # kernels side by side (async worker groups); without it a trainer assumes the
+        # whole GPU and its persistent launches are serialised with every other trainer's
+        self.persist_cus = int(persist_cus) if persist_cus else 0
         if not plan.native_ok:
             raise ValueError(f"model is not supported by the native engine: {plan.reason}")
         self.dev = torch.device(device) if device is not None else config.get_device()
@@ -185,6 +191,7 @@ class NativeTrainer(TrainerBase):
             rowchain=self.rowchain_mode if ws is self.ws else 0,
             persist=self.persist_mode if ws is self.ws else 0,
             persist_timeout_ms=int(os.environ.get("ELEPHAS_AMD_PERSIST_TIMEOUT_MS", "2000")),
+            persist_cus=self.persist_cus,
             rc_split=int(os.environ.get("ELEPHAS_AMD_RC_SPLIT", "0")),
             layers=layers,
             X=self.X.data_ptr(), sX=self.nmax * self.Kp0, ldx=self.Kp0,
@@ -397,6 +404,8 @@ class NativeTrainer(TrainerBase):
         (see _PERSIST_LAST); returns whether the plan is persistent."""
         if not self.exe.persistent():
             return False
+        if self.persist_cus:
+            return False   # a partitioned grid: co-resident with the other shares by construction
         last = _PERSIST_LAST.get(self.dev.index)
         if last is not None and last[0] != self.s:
             self.stream.wait_event(last[1])

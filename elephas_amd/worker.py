@@ -316,16 +316,16 @@ class AsynchronousSparkWorker:
             self.client.update_parameters(unflatten_weights(delta, self.model.get_weights()))
 
 
-def async_streams(groups: int):
-    """HIP streams for ``groups`` independently progressing worker groups: at most
-    $ELEPHAS_AMD_ASYNC_STREAMS (default 4 = GPU_MAX_HW_QUEUES, the hardware queues HIP
-    gives a process). Streams beyond the queue count share queues and serialise behind
-    each other's kernels (profiles/README.md, stream probe: 8 row-chain groups on 8
-    streams 92 us per 8-worker step vs 49 us on 4); groups past the stream count are
-    dealt round-robin onto them and still pull / train / push independently."""
+def group_persist_cus(groups: int, device=None) -> int:
+    """CU share of each of ``groups`` concurrently running worker groups: their persistent
+    chunk kernels (csrc/kernels/persist.hip) need every workgroup resident, so the grids
+    are sized to split the GPU between them -- their total never exceeds the CU count,
+    so each can always become resident once the transient kernels (parameter-server
+    pulls / pushes) beside it finish. (MNIST: 8 groups x 32 CUs = one replica's grid each.)"""
     import torch
-    n = max(1, min(groups, int(os.environ.get("ELEPHAS_AMD_ASYNC_STREAMS", "4") or 4)))
-    return [torch.cuda.Stream() for _ in range(n)]
+    ncu = torch.cuda.get_device_properties(device if device is not None else torch.cuda.current_device()
+                                           ).multi_processor_count
+    return max(1, ncu // max(1, groups))
 
 
 class BatchedAsynchronousWorker:
@@ -379,13 +379,12 @@ class BatchedAsynchronousWorker:
         G = self._n_groups(len(parts))
         bounds = [len(parts) * g // G for g in range(G + 1)]
         groups = []
-        streams = async_streams(G)
         for g in range(G):
             xs, ys = zip(*data[bounds[g]:bounds[g + 1]])
-            # several groups run concurrently on their own streams: no persistent chunk
-            # kernel (it needs the whole GPU resident, and the group graphs hold it)
+            # several groups run concurrently on their own streams: each persistent grid
+            # gets its share of the CUs so all of them are resident at once
             t = make_trainer(self.model, len(xs), bs, engine="native",
-                             **({"persist": 0, "stream": streams[g % len(streams)]} if G > 1 else {}))
+                             **({"persist_cus": group_persist_cus(G)} if G > 1 else {}))
             active = [len(x) > bs for x in xs]   # inactive replicas push a zero delta
             if self.frequency == "epoch":
                 t.set_data(list(xs), list(ys), vs, active=active, shuffle=True)

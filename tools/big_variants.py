@@ -1,6 +1,6 @@
 """Schedule variants of the 8-phase 256x256 tile (gemm_big.h V): cfg 4 = V0, 5 = V1
-(A copies one phase earlier), 6 = V1 without copies, 7 = V1 without fragment reads
-(6 and 7 are timing-only diagnostics). Checks cfg 4/5 against torch and times all."""
+(A copies one phase earlier), 6 = V6 (copies in the MFMA ticks), 7 = V5 (V6 with the
+fragment-read wait behind the barrier). Checks them against torch and times all."""
 import os
 import sys
 import time
@@ -19,7 +19,7 @@ for (M, N, K) in [(1024, 1024, 1024), (513, 770, 264), (4097, 4096, 1024)]:
     A = torch.randn(M, K, device=dev).to(torch.bfloat16)
     BT = torch.randn(N, K, device=dev).to(torch.bfloat16)
     ref = A.float() @ BT.float().t()
-    for cfg in (4, 5):
+    for cfg in (4, 5, 6, 7):
         Cm = torch.zeros(M, N, device=dev)
         C.gemm_nt(A.data_ptr(), BT.data_ptr(), Cm.data_ptr(), M, N, K, K, K, N, 1, cfg, s)
         torch.cuda.synchronize()
