@@ -31,11 +31,20 @@ Prints ONE JSON line on rank 0.
 """
 from __future__ import annotations
 
+import os
+
+# at least 16 HIP hardware queues per process (ELEPHAS_AMD_HW_QUEUES, 0 = leave the
+# runtime's setting; the environment may pin HIP's default of 4): the HIP runtime
+# reads this when its library loads (on `import torch`), so it is set before any import
+# that could load it (elephas_amd/__init__.py explains the measurements)
+_hwq = int(os.environ.get("ELEPHAS_AMD_HW_QUEUES", "16") or 0)
+if _hwq > 0 and int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < _hwq:
+    os.environ["GPU_MAX_HW_QUEUES"] = str(min(32, _hwq))
+
 import argparse
 import hashlib
 import json
 import math
-import os
 import sys
 import time
 

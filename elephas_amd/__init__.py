@@ -8,5 +8,17 @@ torch.distributed (RCCL over xGMI) plus a device-resident parameter server.
 """
 __version__ = "0.1.0"
 
+import os as _os
+
+# Hardware queues per process (read by the HIP runtime once, when its library loads --
+# so this only takes effect when elephas_amd is imported before torch). HIP's default
+# of 4 maps the streams beyond the fourth onto shared queues, where they run one after
+# another: the asynchronous / hogwild worker groups (one stream each) measured 7.5 M
+# samples/s with 4 queues, 9.7 M with 8 and 15.8 M with 16 (8 groups, MNIST,
+# profiles/README.md). Raised to ELEPHAS_AMD_HW_QUEUES (default 16) when lower; 0 leaves it.
+_hwq = int(_os.environ.get("ELEPHAS_AMD_HW_QUEUES", "16") or 0)
+if _hwq > 0 and int(_os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < _hwq:
+    _os.environ["GPU_MAX_HW_QUEUES"] = str(min(32, _hwq))
+
 from . import config  # noqa: F401
 from .config import get_device, get_policy, set_device, set_engine, set_policy  # noqa: F401
