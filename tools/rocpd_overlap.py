@@ -2,7 +2,8 @@
 """Concurrency of the kernels in a rocprofv3 --kernel-trace database: per queue and
 stream the kernel count and busy time, and over the whole trace the sum of kernel
 durations vs the length of their union (sum / union > 1 means kernels overlapped).
-Usage: python tools/rocpd_overlap.py run_results.db [name-substring]"""
+Usage: python tools/rocpd_overlap.py run_results.db [name-substring]
+       python tools/rocpd_overlap.py run_results.db --copies   (copy / kernel overlap)"""
 import sqlite3
 import sys
 
@@ -49,5 +50,37 @@ def main():
           ", ".join(f"{d}: {v / 1e6:.3f}" for d, v in sorted(hist.items()) if v > 0))
 
 
-if __name__ == "__main__":
+if __name__ == "__main__" and "--copies" not in sys.argv:
     main()
+
+
+def copy_kernel_overlap(db):
+    """Memory copies vs kernels (a --memory-copy-trace run): bytes, copy time, and how much
+    of the copy time ran while at least one kernel was running."""
+    c = sqlite3.connect(db)
+    ks = c.execute("select start, end from kernels order by start").fetchall()
+    cs = c.execute("select start, end, size from memory_copies order by start").fetchall()
+    # merge kernel intervals
+    merged = []
+    for s, e in ks:
+        if merged and s <= merged[-1][1]:
+            merged[-1][1] = max(merged[-1][1], e)
+        else:
+            merged.append([s, e])
+    import bisect
+    starts = [m[0] for m in merged]
+    tot = ov = nbytes = 0
+    for s, e, n in cs:
+        tot += e - s
+        nbytes += n
+        i = max(0, bisect.bisect_right(starts, s) - 1)
+        while i < len(merged) and merged[i][0] < e:
+            ov += max(0, min(e, merged[i][1]) - max(s, merged[i][0]))
+            i += 1
+    print(f"copies {len(cs)}: {nbytes / 1e9:.3f} GB in {tot / 1e6:.3f} ms ({nbytes / max(tot, 1):.1f} GB/s while "
+          f"copying); {100.0 * ov / max(tot, 1):.1f} % of copy time overlapped kernels; kernels busy "
+          f"{sum(e - s for s, e in merged) / 1e6:.3f} ms")
+
+
+if __name__ == "__main__" and "--copies" in sys.argv:
+    copy_kernel_overlap(sys.argv[1])
