@@ -133,6 +133,7 @@ struct TableArgs {
 constexpr int RC_MAXL = 4;
 constexpr int RC_ROWS = 16;
 constexpr int RC_MAXW = 256;
+constexpr int RC_TAILW = 512;    // the tail chain (L = 2: the last two layers of a deeper stack)
 constexpr int RC_MAXSPLIT = 8;   // layer-0 split-K slabs
 constexpr int LOSS_RPB = 4;        // rows per workgroup of the wide-output loss rows kernel (one per wave)
 constexpr int LOSS_MAX_SPLIT = 4;  // split-K slabs of a wide last layer summed by the loss rows kernel
@@ -159,6 +160,13 @@ struct RcArgs {
   long long* ctr; int step_off;
   unsigned long long seed;
   long long* stamps;
+  // tail chain: the chain's layer 0 is model layer l0 (dropout streams are keyed by
+  // model layer) whose pre-activations Zsrc [R][B][ldzs] (fp32, bias included) a grouped
+  // FWD launch wrote -- read instead of split-K slabs (null: slabs); dZ_0 also goes out
+  // row-major (the A operand of the grouped DX launch below the chain; null = not written)
+  int l0;
+  const float* Zsrc; long long ldzs;
+  void* dZ0; long long ldz0;
 };
 
 // ------------------------------------------------- persistent replica-cluster step

@@ -150,7 +150,9 @@ __device__ __forceinline__ void rstamp(const RcArgs& a, int k) {
 }  // namespace
 
 // T: compute dtype; L: Dense layers (2..4); NBW: 16-column blocks per wave of the
-// widest hidden layer (2: widths <= 128, 4: <= 256); GEN: the generic loss path
+// widest hidden layer (2: widths <= 128, 4: <= 256, 8: <= 512 -- the tail chain of a
+// deeper stack, L = 2 only: its layer 0 is the stack's second-to-last layer, whose
+// pre-activations the grouped FWD launch before it wrote); GEN: the generic loss path
 // (every Keras loss / activation / metric pairing, ~20k instructions) instead of
 // the softmax + (sparse) categorical cross-entropy one -- picked on the host
 template <typename T, int L, int NBW, bool GEN>
@@ -164,8 +166,13 @@ __global__ __launch_bounds__(256) void rowchain_kernel(RcArgs a) {
   constexpr int NKF = (NKMAX + 3) / 4;                      // last-layer forward chunks per wave (K split 4 ways)
   constexpr int NKL = (32 + KC - 1) / KC;                   // last-layer input-gradient chunks (Np_last <= 32)
   constexpr int CPT = NBW * 4;                              // phase 0: columns per thread (16 threads per row)
+  constexpr bool ZONLY = NBW >= 8;                          // the 512-wide tail reads z_0, never slabs
+  constexpr int CPP = (CPT > 16 && !ZONLY) ? 16 : CPT;      // ... in passes of CPP columns
+  constexpr int NPS = CPT / CPP;
+  constexpr int MSPLIT = ZONLY ? 1 : RC_MAXSPLIT;           // slabs in flight
+  static_assert(NBW < 8 || L == 2, "the 512-wide chain is the two-layer tail only");
   __shared__ __attribute__((aligned(16))) T sD[NH][RB * LD];
-  __shared__ __attribute__((aligned(16))) T sdZ[2][RB * LD];
+  __shared__ __attribute__((aligned(16))) T sdZ[L > 2 ? 2 : 1][RB * LD];
   __shared__ __attribute__((aligned(16))) float sG0[RB * LDG];
   __shared__ __attribute__((aligned(16))) float sRed[4][RB * 32];
   __shared__ __attribute__((aligned(16))) float sLg[RB * 36];
@@ -186,29 +193,51 @@ __global__ __launch_bounds__(256) void rowchain_kernel(RcArgs a) {
   // following it (phase 0 waits only for these; the wait counter drains in issue order)
   const int row = tid >> 4, c0 = (tid & 15) * CPT;
   const int m = m0 + row;
-  float4 sv[RC_MAXSPLIT][CPT / 4];
-  float z[CPT];
-  {
+  float4 sv[MSPLIT][CPP / 4];
+  float z[CPP];
+  // pass ps of phase 0: this thread's columns c0 + ps * CPP + [0, CPP) of every slab + bias
+  auto load_pass = [&](int ps) {
     const RcLayer l0 = a.ly[0];
     const float* Zr = a.Zp + (long long)r * a.sZp + (long long)(m < a.B ? m : 0) * l0.Np;
     const float* bias = Pr + l0.p_off + (long long)l0.K * l0.N;
+    const int cb = c0 + ps * CPP;
+    if (ZONLY || a.Zsrc) {  // tail chain: z_0 (bias included) as the grouped FWD launch stored it
+      const float* zr = a.Zsrc + (long long)r * a.B * a.ldzs + (long long)(m < a.B ? m : 0) * a.ldzs;
+      const bool vec = (a.ldzs & 3) == 0;  // 16-byte rows: cb is a multiple of 4
 #pragma unroll
-    for (int kc = 0; kc < RC_MAXSPLIT; ++kc) {
+      for (int v = 0; v < CPP / 4; ++v) {
+        const int c = cb + 4 * v;
+        if (vec && c + 4 <= l0.N) {
+          const float4 q = *reinterpret_cast<const float4*>(zr + c);
+          z[4 * v] = q.x; z[4 * v + 1] = q.y; z[4 * v + 2] = q.z; z[4 * v + 3] = q.w;
+        } else {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const float e = zr[c + k < l0.N ? c + k : 0];
+            z[4 * v + k] = c + k < l0.N ? e : 0.f;
+          }
+        }
+      }
+      return;
+    }
+#pragma unroll
+    for (int kc = 0; kc < MSPLIT; ++kc) {
       const float* slab = Zr + (long long)(kc < a.nsplitk ? kc : 0) * a.sZpk;
 #pragma unroll
-      for (int v = 0; v < CPT / 4; ++v) {
-        const int c = c0 + 4 * v;
+      for (int v = 0; v < CPP / 4; ++v) {
+        const int c = cb + 4 * v;
         sv[kc][v] = *reinterpret_cast<const float4*>(slab + (c < l0.Np ? c : 0));
       }
     }
 #pragma unroll
-    for (int i = 0; i < CPT; ++i) {
-      const int c = c0 + i;
+    for (int i = 0; i < CPP; ++i) {
+      const int c = cb + i;
       const bool cv = c < l0.N && l0.has_bias;
       const float bv = bias[cv ? c : 0];
       z[i] = cv ? bv : 0.f;
     }
-  }
+  };
+  load_pass(0);
   const long long s0 = ld_inv(a.ctr);
   const long long step = s0 + a.step_off;
   const long long cnt = (long long)ld_inv(a.ntrain + r) - step * a.B;
@@ -313,37 +342,42 @@ __global__ __launch_bounds__(256) void rowchain_kernel(RcArgs a) {
       }
       if (tid < RB) sRow[tid] = m0 + tid < valid ? 1 : -1;
     }
-#pragma unroll
-    for (int kc = 0; kc < RC_MAXSPLIT; ++kc) {
-      if (kc >= a.nsplitk) break;  // uniform; every load above is already in flight
-#pragma unroll
-      for (int v = 0; v < CPT / 4; ++v) {
-        z[4 * v + 0] += sv[kc][v].x;
-        z[4 * v + 1] += sv[kc][v].y;
-        z[4 * v + 2] += sv[kc][v].z;
-        z[4 * v + 3] += sv[kc][v].w;
-      }
-    }
-    rstamp(a, 12);  // slabs summed
-    float o[CPT], gg[CPT], dv[CPT], gv[CPT];
-    act_fg_v<CPT>(l0.act, z, o, gg);
     const float keep_scale = l0.rate > 0.f ? 1.f / (1.f - l0.rate) : 1.f;
-    const uint32_t dbase = dropout_base(a.seed, r, 0, iter);
+    const uint32_t dbase = dropout_base(a.seed, r, a.l0, iter);
 #pragma unroll
-    for (int i = 0; i < CPT; ++i) {
-      const int c = c0 + i;
-      const bool live = c < l0.N && rv;
-      const float u = (live && l0.rate > 0.f) ? dropout_u1(dbase, m, c) : 1.f;
-      const bool keep = live && u >= l0.rate;
-      dv[i] = keep ? o[i] * keep_scale : 0.f;
-      gv[i] = keep ? gg[i] * keep_scale : 0.f;
-    }
+    for (int ps = 0; ps < NPS; ++ps) {
+      if (ps > 0) load_pass(ps);
+      const int cb = c0 + ps * CPP;
 #pragma unroll
-    for (int i = 0; i < CPT; i += 4) {
-      if (c0 + i < NBW * 64) {
-        *reinterpret_cast<float4*>(sG0 + row * LDG + c0 + i) = make_float4(gv[i], gv[i + 1], gv[i + 2], gv[i + 3]);
+      for (int kc = 0; kc < MSPLIT; ++kc) {
+        if (kc >= a.nsplitk) break;  // uniform; every load above is already in flight
 #pragma unroll
-        for (int k = 0; k < 4; ++k) sD[0][row * LD + c0 + i + k] = from_f<T>(dv[i + k]);
+        for (int v = 0; v < CPP / 4; ++v) {
+          z[4 * v + 0] += sv[kc][v].x;
+          z[4 * v + 1] += sv[kc][v].y;
+          z[4 * v + 2] += sv[kc][v].z;
+          z[4 * v + 3] += sv[kc][v].w;
+        }
+      }
+      if (ps == 0) rstamp(a, 12);  // slabs summed
+      float o[CPP], gg[CPP], dv[CPP], gv[CPP];
+      act_fg_v<CPP>(l0.act, z, o, gg);
+#pragma unroll
+      for (int i = 0; i < CPP; ++i) {
+        const int c = cb + i;
+        const bool live = c < l0.N && rv;
+        const float u = (live && l0.rate > 0.f) ? dropout_u1(dbase, m, c) : 1.f;
+        const bool keep = live && u >= l0.rate;
+        dv[i] = keep ? o[i] * keep_scale : 0.f;
+        gv[i] = keep ? gg[i] * keep_scale : 0.f;
+      }
+#pragma unroll
+      for (int i = 0; i < CPP; i += 4) {
+        if (cb + i < NBW * 64) {
+          *reinterpret_cast<float4*>(sG0 + row * LDG + cb + i) = make_float4(gv[i], gv[i + 1], gv[i + 2], gv[i + 3]);
+#pragma unroll
+          for (int k = 0; k < 4; ++k) sD[0][row * LD + cb + i + k] = from_f<T>(dv[i + k]);
+        }
       }
     }
   }
@@ -351,7 +385,8 @@ __global__ __launch_bounds__(256) void rowchain_kernel(RcArgs a) {
   lds_barrier();
   rstamp(a, 14);
   // D_0^T (layer 1's weight-gradient operand) from the LDS tile: 4 rows per store
-  {
+  // (the tail chain's grouped FWD launch already stored it)
+  if (!a.Zsrc) {
     const RcLayer l0 = a.ly[0];
     T* DT0 = reinterpret_cast<T*>(l0.DT) + (long long)r * l0.N * a.Bp;
     for (int e = tid; e < l0.N * (RB / 4); e += 256) {
@@ -386,7 +421,7 @@ __global__ __launch_bounds__(256) void rowchain_kernel(RcArgs a) {
       for (int q = 0; q < 4; ++q) z[j * 4 + q] = acc[j][q] + hb[l][j];
     act_fg_v<NBW * 4>(ly.act, z, o, gg);
     const float keep_scale = ly.rate > 0.f ? 1.f / (1.f - ly.rate) : 1.f;
-    const uint32_t dbase = dropout_base(a.seed, r, l, iter);
+    const uint32_t dbase = dropout_base(a.seed, r, a.l0 + l, iter);
     T* DTl = reinterpret_cast<T*>(ly.DT) + (long long)r * ly.N * a.Bp;
 #pragma unroll
     for (int j = 0; j < NBW; ++j) {
@@ -537,6 +572,12 @@ __global__ __launch_bounds__(256) void rowchain_kernel(RcArgs a) {
         if (l > 1) sdZ[cur ^ 1][(4 * g + q) * LD + col] = from_f<T>(v[q]);
       }
       if (col < pv.N && m0 + 4 * g < a.Bp) st4t<T>(dZT + (long long)col * a.Bp + m0 + 4 * g, v);
+      if (l == 1 && a.dZ0 && col < pv.Np) {  // tail chain: row-major dZ_0 (zero past N)
+        T* d = reinterpret_cast<T*>(a.dZ0) + (long long)r * a.B * a.ldz0 + col;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          if (m0 + 4 * g + q < a.B) d[(long long)(m0 + 4 * g + q) * a.ldz0] = from_f<T>(v[q]);
+      }
     }
     cur ^= 1;
     if (l > 1) lds_barrier();
@@ -548,9 +589,32 @@ __global__ __launch_bounds__(256) void rowchain_kernel(RcArgs a) {
 
 using namespace ea;
 
+namespace {
+// one instantiation per (dtype, width class, loss path); the 512-wide class exists for
+// the two-layer tail only
+template <typename TT, int NB, bool GN>
+void launch_rc(const RcArgs* a, dim3 grid, hipStream_t s) {
+  if constexpr (NB == 8) {
+    hipLaunchKernelGGL((rowchain_kernel<TT, 2, NB, GN>), grid, dim3(256), 0, s, *a);
+  } else {
+    switch (a->L) {
+      case 2: hipLaunchKernelGGL((rowchain_kernel<TT, 2, NB, GN>), grid, dim3(256), 0, s, *a); break;
+      case 3: hipLaunchKernelGGL((rowchain_kernel<TT, 3, NB, GN>), grid, dim3(256), 0, s, *a); break;
+      default: hipLaunchKernelGGL((rowchain_kernel<TT, 4, NB, GN>), grid, dim3(256), 0, s, *a); break;
+    }
+  }
+}
+template <typename TT, int NB>
+void launch_rc_g(const RcArgs* a, bool fast, dim3 grid, hipStream_t s) {
+  if (fast) launch_rc<TT, NB, false>(a, grid, s);
+  else launch_rc<TT, NB, true>(a, grid, s);
+}
+}  // namespace
+
 // grid: (R, ceil(B / 16)) workgroups of 256 threads
 extern "C" hipError_t ea_rowchain(const RcArgs* a, int bf16, int nbw, hipStream_t s) {
-  if (a->L < 2 || a->L > RC_MAXL || (nbw != 2 && nbw != 4)) return hipErrorInvalidValue;
+  if (a->L < 2 || a->L > RC_MAXL || (nbw != 2 && nbw != 4 && nbw != 8)) return hipErrorInvalidValue;
+  if (nbw == 8 && (a->L != 2 || !a->Zsrc || a->nsplitk != 0)) return hipErrorInvalidValue;
   const dim3 grid(a->R, (a->B + RC_ROWS - 1) / RC_ROWS);
   // the loss_tile_cce path: softmax + (sparse) CCE with accuracy / CCE metrics
   bool fast = a->ly[a->L - 1].act == ACT_SOFTMAX && (a->loss == LOSS_CCE || a->loss == LOSS_SPARSE_CCE) &&
@@ -558,22 +622,14 @@ extern "C" hipError_t ea_rowchain(const RcArgs* a, int bf16, int nbw, hipStream_
   for (int i = 0; i < a->nmet; ++i)
     fast = fast && (a->met[i] == MET_ACC_CAT || a->met[i] == MET_ACC_SPARSE || a->met[i] == LOSS_CCE ||
                     a->met[i] == LOSS_SPARSE_CCE);
-#define EA_RC(TT, LL, NB, GN) hipLaunchKernelGGL((rowchain_kernel<TT, LL, NB, GN>), grid, dim3(256), 0, s, *a)
-#define EA_RC_L(TT, NB, GN)           \
-  switch (a->L) {                     \
-    case 2: EA_RC(TT, 2, NB, GN); break; \
-    case 3: EA_RC(TT, 3, NB, GN); break; \
-    default: EA_RC(TT, 4, NB, GN); break; \
-  }
-#define EA_RC_G(TT, NB) \
-  if (fast) { EA_RC_L(TT, NB, false) } else { EA_RC_L(TT, NB, true) }
   if (bf16) {
-    if (nbw == 2) { EA_RC_G(__bf16, 2) } else { EA_RC_G(__bf16, 4) }
+    if (nbw == 2) launch_rc_g<__bf16, 2>(a, fast, grid, s);
+    else if (nbw == 4) launch_rc_g<__bf16, 4>(a, fast, grid, s);
+    else launch_rc_g<__bf16, 8>(a, fast, grid, s);
   } else {
-    if (nbw == 2) { EA_RC_G(float, 2) } else { EA_RC_G(float, 4) }
+    if (nbw == 2) launch_rc_g<float, 2>(a, fast, grid, s);
+    else if (nbw == 4) launch_rc_g<float, 4>(a, fast, grid, s);
+    else launch_rc_g<float, 8>(a, fast, grid, s);
   }
-#undef EA_RC_G
-#undef EA_RC_L
-#undef EA_RC
   return hipGetLastError();
 }

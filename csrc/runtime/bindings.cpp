@@ -74,6 +74,7 @@ static ExecCfg parse_cfg(const py::dict& d) {
   c.thr_min_n = get<int>(d, "thr_min_n", 256);
   c.rowchain = get<int>(d, "rowchain", -1);
   c.rc_split = get<int>(d, "rc_split", 0);
+  c.tail = get<int>(d, "tail", -1);
   c.persist = get<int>(d, "persist", -1);
   c.persist_timeout_ms = get<long long>(d, "persist_timeout_ms", 2000);
   c.persist_cus = get<int>(d, "persist_cus", 0);
@@ -157,6 +158,7 @@ PYBIND11_MODULE(_C, m) {
   py::class_<Executor>(m, "Executor")
       .def(py::init([](py::dict cfg) { return new Executor(parse_cfg(cfg)); }))
       .def("train_step", [](Executor& e, uintptr_t s) { e.train_step(S(s)); })
+      .def("train_chunk", [](Executor& e, int n, uintptr_t s) { e.train_chunk(n, S(s)); })
       .def("forward_backward", [](Executor& e, uintptr_t s) { e.forward_backward(S(s)); })
       .def("apply", [](Executor& e, uintptr_t s) { e.apply(S(s)); })
       .def("eval_chunk", [](Executor& e, long long chunk, py::dict src, uintptr_t s) {
@@ -183,6 +185,7 @@ PYBIND11_MODULE(_C, m) {
       .def("table_begins", &Executor::table_begins)
       .def("rowchain", &Executor::rowchain)
       .def("rowchain_split", &Executor::rowchain_split)
+      .def("tailchain", &Executor::tailchain)
       .def("persistent", &Executor::persistent)
       .def("persist_geometry", &Executor::persist_geometry)
       .def("persist_error", &Executor::persist_error)

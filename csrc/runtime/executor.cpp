@@ -37,6 +37,7 @@ Executor::Executor(const ExecCfg& cfg) : c_(cfg) {
   build();
   rc_.on = c_.rowchain != 0 && build_rowchain();
   if (c_.rowchain == 1 && !rc_) throw std::invalid_argument("row-chain plan requested but the model is not eligible");
+  tl_.on = !rc_ && c_.rowchain != 0 && c_.tail != 0 && build_tail();
   pm_.on = c_.persist != 0 && build_persist();
   if (c_.persist == 1 && !pm_.on) throw std::invalid_argument("persistent plan requested but the model is not eligible");
 }
@@ -199,37 +200,7 @@ bool Executor::build_rowchain() {
   check(hipMalloc(&d_zp_, sizeof(float) * (size_t)c_.R * ns * slab), "hipMalloc(row-chain slabs)");
   check(hipMemset(d_zp_, 0, sizeof(float) * (size_t)c_.R * ns * slab), "hipMemset(row-chain slabs)");
 
-  // tile geometry of the table launches: 64x32 (layer 0), 64x64 (weight gradients)
-  auto blocks = [&](const Prob& p) {  // tiles per replica (grid (R, tiles))
-    if (p.kind == PK_GATHER_T) return cdiv(p.B, 64) * cdiv(p.K, 64);
-    return p.tiles_m * p.tiles_n * std::max(1, p.tiles_k);
-  };
-  auto table = [&](TableArgs& ta, Prob* host, int n, Prob* dev, int cfg) {
-    const int bm = ea_gemm_tile_m(cfg), bn = ea_gemm_tile_n(cfg);
-    std::memset(&ta, 0, sizeof(ta));
-    int begin = 0;
-    for (int i = 0; i < n; ++i) {
-      Prob& p = host[i];
-      if (p.kind == PK_GATHER_T) {
-        p.tiles_m = cdiv(p.B, 64);
-        p.tiles_n = cdiv(p.K, 64);
-      } else {
-        p.tiles_m = cdiv(p.M, bm);
-        p.tiles_n = cdiv(p.N, bn);
-      }
-      if (p.kind != PK_PARTIAL) p.tiles_k = 1;
-      p.block_begin = 0;
-      ta.begin[i] = begin;
-      begin += blocks(p);
-    }
-    ta.probs = dev;
-    ta.nprob = n;
-    ta.R = c_.R;
-    ta.total_blocks = begin;
-    ta.ctr = reinterpret_cast<long long*>(c_.ctr);
-    ta.seed = c_.seed;
-    check(hipMemcpy(dev, host, sizeof(Prob) * n, hipMemcpyHostToDevice), "hipMemcpy(problem table)");
-  };
+  auto table = [&](TableArgs& ta, Prob* host, int n, Prob* dev, int cfg) { make_table(ta, host, n, dev, cfg); };
   check(hipMalloc(&d_probs_, sizeof(Prob) * 3 * TABLE_MAX), "hipMalloc(problem tables)");
 
   // A: layer-0 product as split-K slabs + the X^T gather (from the grouped FWD_0 launch)
@@ -289,6 +260,121 @@ bool Executor::build_rowchain() {
   return true;
 }
 
+// tile geometry of the table launches: 64x32 (cfg 0: layer-0 / tail slabs), 64x64
+// (cfg 3: weight gradients); problem i owns tiles [begin[i], begin[i+1]) per replica
+void Executor::make_table(TableArgs& ta, Prob* host, int n, Prob* dev, int cfg) const {
+  const int bm = ea_gemm_tile_m(cfg), bn = ea_gemm_tile_n(cfg);
+  std::memset(&ta, 0, sizeof(ta));
+  int begin = 0;
+  for (int i = 0; i < n; ++i) {
+    Prob& p = host[i];
+    if (p.kind == PK_GATHER_T) {
+      p.tiles_m = cdiv(p.B, 64);
+      p.tiles_n = cdiv(p.K, 64);
+    } else {
+      p.tiles_m = cdiv(p.M, bm);
+      p.tiles_n = cdiv(p.N, bn);
+    }
+    if (p.kind != PK_PARTIAL) p.tiles_k = 1;
+    p.block_begin = 0;
+    ta.begin[i] = begin;
+    begin += p.tiles_m * p.tiles_n * std::max(1, p.tiles_k);
+  }
+  ta.probs = dev;
+  ta.nprob = n;
+  ta.R = c_.R;
+  ta.total_blocks = begin;
+  ta.ctr = reinterpret_cast<long long*>(c_.ctr);
+  ta.seed = c_.seed;
+  check(hipMemcpy(dev, host, sizeof(Prob) * n, hipMemcpyHostToDevice), "hipMemcpy(problem table)");
+}
+
+// Tail-chain plan: the row chain (rowchain.hip, L = 2) over the last two layers of a
+// deeper stack whose layer L-2 is at most RC_TAILW wide and whose last layer has at
+// most 32 units (Otto: 512 -> 9). The chain starts from the pre-activations z_{L-2}
+// the grouped FWD_{L-2} launch stored (activation and dropout recomputed in-row), and
+// replaces the loss launch (FWD_{L-1}: 2 workgroups per replica at B = 128) and the
+// last layer's input-gradient launch; DW_{L-1} joins a backward launch with a free slot.
+bool Executor::build_tail() {
+  const int L = (int)c_.layers.size();
+  if (L < 3 || (int)fwd_.size() != L || (int)bwd_.size() < L) return false;
+  const LayerCfg& la = c_.layers[L - 2];
+  const LayerCfg& lb = c_.layers[L - 1];
+  if (la.N > RC_TAILW || lb.N > 32 || c_.ldy > 32) return false;
+  if (fwd_[L - 2].ga.p[0].kind != PK_FWD || !fwd_[L - 2].ga.p[0].Z) return false;
+  if (fwd_[L - 1].ga.nprob != 1 || fwd_[L - 1].ga.p[0].kind != PK_FWD_LOSS) return false;
+  // bwd_: [DW_{L-1} (+ DX_{L-1})] or [DW_{L-1}] [DX_{L-1}], then layer L-2's launch(es)
+  const Prob dw_last = bwd_[0].ga.p[0];
+  if (dw_last.kind != PK_DW_UPDATE) return false;
+  const int i = (bwd_[0].ga.nprob == 2) ? 1 : 2;  // skip them (DX_{L-1} runs in the chain)
+  if (i == 2 && (bwd_[1].ga.nprob != 1 || bwd_[1].ga.p[0].kind != PK_DX)) return false;
+  if (i >= (int)bwd_.size() || bwd_[i].ga.p[0].kind != PK_DW_UPDATE) return false;
+  tl_.nbw = la.N <= 128 ? 2 : la.N <= 256 ? 4 : 8;
+  tl_.pre.assign(fwd_.begin(), fwd_.begin() + (L - 1));
+
+  // DW_{L-1} needs only the chain's outputs: it rides in the first backward launch
+  // with a free problem slot (Otto: DW_{L-2}'s), else it gets its own launch
+  tl_.post.assign(bwd_.begin() + i, bwd_.end());
+  bool placed = false;
+  for (auto& La : tl_.post) {
+    if (La.ga.nprob == 1) {
+      La.ga.p[1] = dw_last;
+      La.ga.nprob = 2;
+      finalize(La);
+      placed = true;
+      break;
+    }
+  }
+  if (!placed) {
+    Launch La;
+    std::memset(&La, 0, sizeof(La));
+    La.ga.p[0] = dw_last;
+    La.ga.nprob = 1;
+    La.cfg = bwd_[0].cfg;
+    finalize(La);
+    tl_.post.insert(tl_.post.begin(), La);
+  }
+
+  RcArgs& a = tl_.rc;
+  std::memset(&a, 0, sizeof(a));
+  a.L = 2; a.R = c_.R; a.B = c_.B; a.Bp = c_.Bp;
+  a.nsplitk = 0;
+  for (int l = 0; l < 2; ++l) {
+    const LayerCfg& ly = c_.layers[L - 2 + l];
+    RcLayer& q = a.ly[l];
+    q.K = ly.K; q.N = ly.N; q.Kp = ly.Kp; q.Np = ly.Np;
+    q.act = ly.act; q.has_bias = ly.has_bias; q.rate = ly.rate;
+    q.p_off = ly.p_off; q.wsh_off = ly.wsh_off; q.wtsh_off = ly.wtsh_off;
+    q.DT = reinterpret_cast<void*>(ly.DT);
+    q.dZT = reinterpret_cast<void*>(ly.dZT);
+  }
+  a.Y = reinterpret_cast<const float*>(c_.Y); a.sY = c_.sY; a.ldy = c_.ldy;
+  a.perm = reinterpret_cast<const int*>(c_.perm); a.sPerm = c_.sPerm;
+  a.ntrain = reinterpret_cast<const int*>(c_.ntrain);
+  a.P = reinterpret_cast<const float*>(c_.P); a.sP = c_.sP;
+  a.Wsh = reinterpret_cast<const void*>(c_.Wsh); a.sWsh = c_.sWsh; a.wsh_par = c_.wsh_par;
+  a.WTsh = reinterpret_cast<const void*>(c_.WTsh); a.sWTsh = c_.sWTsh; a.wtsh_par = c_.wtsh_par;
+  a.loss = c_.loss; a.nmet = c_.nmet;
+  for (int k = 0; k < 4; ++k) a.met[k] = c_.met[k];
+  a.acc = reinterpret_cast<double*>(c_.acc); a.acc_stride = c_.acc_stride;
+  a.ctr = reinterpret_cast<long long*>(c_.ctr);
+  a.seed = c_.seed;
+  a.l0 = L - 2;
+  a.Zsrc = reinterpret_cast<const float*>(la.Z);
+  a.ldzs = la.N;
+  a.dZ0 = reinterpret_cast<void*>(la.dZ);
+  a.ldz0 = la.Np;
+  return true;
+}
+
+void Executor::run_tail(hipStream_t s, int step_off) const {
+  run(tl_.pre, s, step_off);
+  RcArgs a = tl_.rc;
+  a.step_off = step_off;
+  check(ea_rowchain(&a, c_.bf16, tl_.nbw, s), "tail chain");
+  run(tl_.post, s, step_off);
+}
+
 void Executor::run_rowchain(hipStream_t s, int step_off, bool grad) const {
   TableArgs ta = rc_.ta_fwd;
   ta.step_off = step_off;
@@ -304,6 +390,8 @@ void Executor::run_rowchain(hipStream_t s, int step_off, bool grad) const {
 void Executor::run_step(hipStream_t s, int step_off) const {
   if (rc_) {
     run_rowchain(s, step_off, false);
+  } else if (tl_.on) {
+    run_tail(s, step_off);
   } else {
     run(fwd_, s, step_off);
     run(bwd_, s, step_off);
@@ -700,6 +788,18 @@ void Executor::train_launch(int idx, hipStream_t s) {
     else check(ea_gemm_table(&rc_.ta_dw, c_.bf16, 1, s), "train_launch");
     return;
   }
+  if (tl_.on) {
+    const int np = (int)tl_.pre.size();
+    if (idx < np) {
+      check(ea_gemm_grouped(&tl_.pre[idx].ga, c_.bf16, tl_.pre[idx].cfg, s), "train_launch");
+    } else if (idx == np) {
+      check(ea_rowchain(&tl_.rc, c_.bf16, tl_.nbw, s), "train_launch");
+    } else {
+      const Launch& L = tl_.post[idx - np - 1];
+      check(ea_gemm_grouped(&L.ga, c_.bf16, L.cfg, s), "train_launch");
+    }
+    return;
+  }
   const int nf = (int)fwd_.size();
   const Launch& L = idx < nf ? fwd_[idx] : bwd_[idx - nf];
   check(ea_gemm_grouped(&L.ga, c_.bf16, L.cfg, s), "train_launch");
@@ -728,6 +828,9 @@ void Executor::set_stamps(uintptr_t buf) {
   rc_.ta_fwd.stamps = rc_.ta_dw.stamps = rc_.ta_grad.stamps = p;
   rc_.rc.stamps = p;
   pm_.args.stamps = p;
+  for (auto* v : {&tl_.pre, &tl_.post})
+    for (auto& L : *v) L.ga.stamps = p;
+  tl_.rc.stamps = p;
 }
 
 std::vector<int> Executor::launch_blocks() const {
@@ -736,6 +839,12 @@ std::vector<int> Executor::launch_blocks() const {
     v.push_back(c_.R * rc_.ta_fwd.total_blocks);
     v.push_back(c_.R * cdiv(c_.B, RC_ROWS));
     v.push_back(c_.R * rc_.ta_dw.total_blocks);
+    return v;
+  }
+  if (tl_.on) {
+    for (auto& L : tl_.pre) v.push_back(c_.R * L.ga.total_blocks);
+    v.push_back(c_.R * cdiv(c_.B, RC_ROWS));
+    for (auto& L : tl_.post) v.push_back(c_.R * L.ga.total_blocks);
     return v;
   }
   for (auto& L : fwd_) v.push_back(c_.R * L.ga.total_blocks);
@@ -754,6 +863,12 @@ std::vector<int> Executor::table_begins(int launch) const {
 std::vector<int> Executor::launch_cfgs() const {
   std::vector<int> v;
   if (rc_) return {0, -1, 3};  // table launches (64x32 / 64x64 tiles), the row chain (-1)
+  if (tl_.on) {
+    for (auto& L : tl_.pre) v.push_back(L.cfg);
+    v.push_back(-1);  // the tail chain
+    for (auto& L : tl_.post) v.push_back(L.cfg);
+    return v;
+  }
   for (auto& L : fwd_) v.push_back(L.cfg);
   for (auto& L : bwd_) v.push_back(L.cfg);
   return v;
@@ -762,6 +877,12 @@ std::vector<int> Executor::launch_cfgs() const {
 void Executor::train_step(hipStream_t s) {
   run_chunk(s, 1);
   advance(1, s);
+}
+
+void Executor::train_chunk(int nsteps, hipStream_t s) {
+  if (nsteps <= 0) return;
+  run_chunk(s, nsteps);
+  advance(nsteps, s);
 }
 
 void Executor::forward_backward(hipStream_t s) {

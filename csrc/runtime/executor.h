@@ -9,6 +9,11 @@
 //   row-chain plan  (small MLPs, csrc/kernels/rowchain.hip; 3 launches):
 //                   [layer-0 split-K slabs + gather X^T] [row chain: layers 1..L-1
 //                   forward, loss, dZ_{L-1} .. dZ_0] [DW of every layer]
+//   tail-chain plan (deeper stacks whose last two layers fit a 512-wide row chain,
+//                   e.g. Otto 93-512-512-512-9): [FWD_0 + gather X^T] .. [FWD_{L-2}]
+//                   [chain: layer L-1 forward, loss, dZ_{L-1}, dZ_{L-2}]
+//                   [DW_{L-2} + DW_{L-1}] [DX_{L-2}] .. [DW_0] -- the loss launch and
+//                   the last layer's backward launch of the grouped plan disappear
 //   persistent plan (3-layer MLPs with 64/128-wide hidden layers, fp32;
 //                   csrc/kernels/persist.hip): a whole chunk of steps in ONE launch
 //                   (+ a flag memset node and the counter advance)
@@ -66,6 +71,7 @@ struct ExecCfg {
   int rowchain = -1;   // row-chain step plan: -1 when eligible, 0 off, 1 required
   int rc_lean = 1;     // skip the update of layer 0's row-major weight image (no reader)
   int rc_split = 0;    // layer-0 split-K slabs of the row-chain plan (0 = auto)
+  int tail = -1;       // tail-chain plan when the row chain is not eligible: -1 when eligible, 0 off
   int persist = -1;    // persistent chunk kernel (persist.hip): -1 when eligible, 0 off, 1 required
   long long persist_timeout_ms = 2000;  // spin limit of its in-launch waits
   int persist_cus = 0;  // > 0: CUs the persistent grid may occupy (several executors side by side)
@@ -86,6 +92,9 @@ class Executor {
 
   // eager launches on `stream`
   void train_step(hipStream_t s);          // fused-update path (+ counter advance)
+  // nsteps fused-update steps (+ one counter advance): ONE launch on the persistent
+  // plan whatever nsteps is (no graph needed: memset + kernel + advance)
+  void train_chunk(int nsteps, hipStream_t s);
   void forward_backward(hipStream_t s);    // gradient path: writes G (no update)
   void apply(hipStream_t s);               // gradient path: optimizer apply + advance
   void eval_chunk(long long chunk, const EvalSource& src, hipStream_t s);
@@ -103,8 +112,13 @@ class Executor {
   void destroy_graphs();
 
   // launches per step (a captured chunk adds one 1-block counter advance)
-  int launches_per_step() const { return rc_.on ? 3 : (int)fwd_.size() + (int)bwd_.size(); }
+  int launches_per_step() const {
+    if (rc_.on) return 3;
+    if (tl_.on) return (int)tl_.pre.size() + 1 + (int)tl_.post.size();
+    return (int)fwd_.size() + (int)bwd_.size();
+  }
   bool rowchain() const { return rc_.on; }
+  bool tailchain() const { return tl_.on; }
   bool persistent() const { return pm_.on; }
   // persistent plan: {L0 k-chunks, L0 column blocks, k-chunk rows, block columns, chain
   // workgroups, workgroups per replica, grid}
@@ -147,6 +161,17 @@ class Executor {
   mutable float* d_zw_ = nullptr;  // (allocated by the const plan builder) wide last layer split-K logit slabs [R][ks][B][N_last]
   bool build_rowchain();
   void run_rowchain(hipStream_t s, int step_off, bool grad) const;
+  void make_table(TableArgs& ta, Prob* host, int n, Prob* dev, int cfg) const;
+  // tail-chain plan: grouped launches before the chain, the chain, grouped launches
+  // after it
+  struct Tail {
+    bool on = false;
+    int nbw = 8;
+    std::vector<Launch> pre, post;
+    RcArgs rc{};
+  } tl_;
+  bool build_tail();
+  void run_tail(hipStream_t s, int step_off) const;
   struct Persist {
     bool on = false;
     PersistArgs args{};

@@ -9,6 +9,7 @@ header is newer.
 from __future__ import annotations
 
 import os
+import re
 import subprocess
 import sys
 import sysconfig
@@ -48,13 +49,25 @@ def _hipcc() -> str:
     return os.path.join(rocm, "bin", "hipcc")
 
 
-def _headers():
-    out = []
-    for d in ("kernels", "runtime"):
-        for f in os.listdir(os.path.join(CSRC, d)):
-            if f.endswith(".h"):
-                out.append(os.path.join(CSRC, d, f))
-    return out
+_INCLUDE = re.compile(r'^\s*#\s*include\s+"([^"]+)"', re.M)
+
+
+def _deps(path, seen=None):
+    """path plus every local header it includes, transitively (quoted includes
+    resolved against the including file's directory, then csrc/)."""
+    seen = set() if seen is None else seen
+    if path in seen or not os.path.exists(path):
+        return seen
+    seen.add(path)
+    with open(path) as f:
+        text = f.read()
+    for inc in _INCLUDE.findall(text):
+        for base in (os.path.dirname(path), CSRC):
+            cand = os.path.normpath(os.path.join(base, inc))
+            if os.path.exists(cand):
+                _deps(cand, seen)
+                break
+    return seen
 
 
 def _newest(paths):
@@ -68,13 +81,12 @@ def build(verbose: bool = False, force: bool = False, jobs: int = 6) -> str:
     inc = ["-I" + pybind11.get_include(), "-I" + sysconfig.get_paths()["include"], "-I" + CSRC]
     flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-fvisibility=hidden",
              "-Wno-unused-result"]
-    hdr_time = _newest(_headers())
     objs, cmds = [], []
     for src in SOURCES:
         s = os.path.join(CSRC, src)
         o = os.path.join(BUILD, src.replace("/", "_") + ".o")
         objs.append(o)
-        if force or not os.path.exists(o) or os.path.getmtime(o) < max(os.path.getmtime(s), hdr_time):
+        if force or not os.path.exists(o) or os.path.getmtime(o) < _newest(_deps(s)):
             lang = [] if src.endswith(".hip") else ["-x", "hip"]
             cmds.append([_hipcc()] + flags + inc + lang + ["-c", s, "-o", o])
 

@@ -62,7 +62,7 @@ class NativeTrainer(TrainerBase):
     GRAPH_CHUNK = 1 << (max(1, int(os.environ.get("ELEPHAS_AMD_GRAPH_CHUNK", "16"))).bit_length() - 1)
     # the persistent plan runs a whole chunk in one launch (its fill / drain and the
     # launch's P / S / weight-image round trip are paid once per chunk): longer chunks
-    PERSIST_CHUNK = 1 << (max(1, int(os.environ.get("ELEPHAS_AMD_PERSIST_CHUNK", "64"))).bit_length() - 1)
+    PERSIST_CHUNK = max(1, int(os.environ.get("ELEPHAS_AMD_PERSIST_CHUNK", "128")))
 
     def __init__(self, model, plan, R: int = 1, batch_size: int = 32, device=None, seed: Optional[int] = None,
                  policy: Optional[str] = None, eval_batch: int = 2048, rowchain: Optional[int] = None,
@@ -151,6 +151,10 @@ class NativeTrainer(TrainerBase):
         self.shuffle = True
         self.exe = None
         self.exe_eval = None
+        # the weight images (Wsh / WTsh) lag P: set by an averaging that only rewrote the
+        # masters (the persistent kernel reads P alone); every other reader of the images
+        # refreshes them first (_ensure_images)
+        self._images_stale = False
         self._graphs: Dict[tuple, int] = {}
         self._build_executor()
         self.set_weights_flat(flatten_weights(model.get_weights()))
@@ -193,6 +197,7 @@ class NativeTrainer(TrainerBase):
             persist_timeout_ms=int(os.environ.get("ELEPHAS_AMD_PERSIST_TIMEOUT_MS", "2000")),
             persist_cus=self.persist_cus,
             rc_split=int(os.environ.get("ELEPHAS_AMD_RC_SPLIT", "0")),
+            tail=int(os.environ.get("ELEPHAS_AMD_TAIL", "-1")) if ws is self.ws else 0,
             layers=layers,
             X=self.X.data_ptr(), sX=self.nmax * self.Kp0, ldx=self.Kp0,
             Y=self.Y.data_ptr(), sY=self.nmax * self.ldy, ldy=self.ldy,
@@ -241,11 +246,19 @@ class NativeTrainer(TrainerBase):
             self.P.copy_(torch.from_numpy(np.array(flat, dtype=np.float32, copy=True)).to(self.dev))
             self.exe.refresh_shadows(True, self.s)
         self._exit()
+        self._images_stale = False
 
     def sync_shadows(self):
         """Rebuild the weight images after P was modified on device (all-reduce, PS pull)."""
         with torch.cuda.stream(self.stream):
             self.exe.refresh_shadows(True, self.s)
+        self._images_stale = False
+
+    def _ensure_images(self):
+        """Before a launch that reads the weight images: rebuild them if an averaging left
+        only the masters current (stream-ordered, no host sync)."""
+        if self._images_stale:
+            self.sync_shadows()
 
     def get_weights_flat(self):
         return self._host(self.P)
@@ -264,6 +277,21 @@ class NativeTrainer(TrainerBase):
             avg = getattr(self, "_avg_buf", None)
             if avg is None or avg.numel() != self.n:
                 avg = self._avg_buf = torch.empty(self.n, dtype=torch.float32, device=self.dev)
+            if self.exe.persistent() and include:
+                # the next training chunk reads only the masters: write the mean into
+                # every replica's P (one kernel; after the all-reduce, one broadcast copy)
+                # and leave the weight images to whichever reader comes first
+                if allreduce is None:
+                    self.C.replica_average(self.P.data_ptr(), self.P.stride(0), self.R, self.n, avg.data_ptr(), 1,
+                                           self.s, 1.0 / n_total)
+                else:
+                    self.C.replica_average(self.P.data_ptr(), self.P.stride(0), self.R, self.n, avg.data_ptr(), 0,
+                                           self.s, 1.0)
+                    allreduce(avg)
+                    avg.mul_(1.0 / n_total)
+                    self.P.copy_(avg.expand_as(self.P))
+                self._images_stale = True
+                return avg
             if include:
                 scale = 1.0 if allreduce is not None else 1.0 / n_total
                 self.C.replica_average(self.P.data_ptr(), self.P.stride(0), self.R, self.n, avg.data_ptr(), 0,
@@ -274,6 +302,7 @@ class NativeTrainer(TrainerBase):
                 allreduce(avg)
                 avg.mul_(1.0 / n_total)
             self.exe.refresh_from(avg.data_ptr(), 0, self.s)
+        self._images_stale = False
         return avg
 
     def reset_for_fit(self, flat, seed: Optional[int] = None):
@@ -428,6 +457,18 @@ class NativeTrainer(TrainerBase):
                 self._persist_mark()
 
     def _run_steps(self, nsteps: int, use_graph: bool):
+        if self.exe.persistent():
+            # one persistent launch per chunk of up to PERSIST_CHUNK steps, a remainder
+            # included (the kernel takes its step count at launch): a chunk is three
+            # stream operations (flag memset, kernel, counter advance), so there is
+            # nothing for a graph to save, and every extra launch would pay the
+            # kernel's fill / drain (weights, optimizer state, first forward) again
+            while nsteps > 0:
+                n = min(nsteps, self.GRAPH_CHUNK)
+                self.exe.train_chunk(n, self.s)
+                nsteps -= n
+            return
+        self._ensure_images()
         if not use_graph:
             for _ in range(nsteps):
                 self.exe.train_step(self.s)
@@ -448,6 +489,8 @@ class NativeTrainer(TrainerBase):
 
     def prepare_graphs(self, allreduce_path: bool = False):
         """Capture (without running) every graph run_steps / run_steps_allreduce use."""
+        if self.exe.persistent() and not allreduce_path:
+            return   # persistent chunks launch without graphs (_run_steps)
         chunks = []
         b = self.GRAPH_CHUNK
         while b >= 1:
@@ -459,6 +502,7 @@ class NativeTrainer(TrainerBase):
 
     def run_steps_allreduce(self, nsteps: int, allreduce, use_graph: bool = True):
         """Per-step gradient all-reduce path: [fwd+bwd -> G] -> allreduce(G) -> [apply]."""
+        self._ensure_images()
         for _ in range(nsteps):
             if use_graph:
                 self.exe.replay(self._graph(1, 1), self.s)
@@ -476,6 +520,7 @@ class NativeTrainer(TrainerBase):
         all-reduce of G over IPC-mapped buffers (parallel/p2p.py graph channel), the
         optimizer apply -- captured as ONE hipGraph of GRAPH_CHUNK steps (and one of 1
         step), so the host launches one graph per 16 steps.  R == 1 (one replica per rank)."""
+        self._ensure_images()
         if self.R != 1:
             raise ValueError("run_steps_allreduce_graph: one replica per rank")
         graphs = self._graphs.setdefault(("peer_ar", id(channel)), {})
@@ -502,6 +547,7 @@ class NativeTrainer(TrainerBase):
         dW / db has run, ``allreduce_bucket(G[:, lo:hi])`` is issued on ``comm_stream``
         (RCCL runs it beside the next backward launch); the optimizer apply waits for
         every bucket. Eager launches (the buckets' host calls sit between them)."""
+        self._ensure_images()
         comm = comm_stream or getattr(self, "_comm_stream", None)
         if comm is None:
             comm = self._comm_stream = torch.cuda.Stream(device=self.dev)
@@ -611,6 +657,7 @@ class NativeTrainer(TrainerBase):
         replica, dropout off) into acc_val, and a copy of it into ``dst`` (a [R, 6]
         fp64 device tensor) if given; no host synchronisation."""
         exe = self._eval_exe()
+        self._ensure_images()
         with torch.cuda.stream(self.stream):
             self.acc_val.zero_()
             nch = int(math.ceil(max(self.vcount_h) / self.eval_B))
@@ -687,6 +734,7 @@ class NativeTrainer(TrainerBase):
         if x.strides[1] != 4 or x.strides[0] % 4:
             x = np.ascontiguousarray(x)
         exe = self._eval_exe()
+        self._ensure_images()
         buf = self._eval_buffers(n, y is not None, want_pred)
         h2d, d2h = self._copy_streams()
         cur = torch.cuda.current_stream(self.dev)
@@ -784,6 +832,8 @@ class NativeTrainer(TrainerBase):
                     f"layer-0 tiles of {kc0}x{cw} + {nch} row-chain workgroups; grid {grid})")
         if self.exe.rowchain():
             return "row-chain (3 launches per step)"
+        if self.exe.tailchain():
+            return f"tail-chain ({self.exe.launches_per_step()} launches per step)"
         return f"grouped ({self.exe.launches_per_step()} launches per step)"
 
     @property

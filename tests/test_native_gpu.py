@@ -833,3 +833,67 @@ def test_pipelined_inference_multi_chunk(policy):
             assert torch.isnan(got[3, 4])
     finally:
         config.set_policy("float32")
+
+
+@pytest.mark.parametrize("hidden,B,policy", [([96, 320, 272], 64, "float32"),   # 512-wide class (NBW 8)
+                                             ([300, 120], 48, "float32"),        # 128-wide tail (NBW 2)
+                                             ([64, 512], 40, "float32"),         # Otto's widths, partial batch
+                                             ([96, 320, 272], 64, "mixed_bfloat16")])
+def test_tail_chain_matches_fp32_reference_with_same_masks(hidden, B, policy):
+    """Tail-chain plan (rowchain.hip at L = 2 over the last two layers of a deeper stack:
+    after the grouped FWD of layer L-2, one row-local kernel recomputes its activation /
+    dropout from the stored pre-activations and runs the last layer's forward, the loss
+    and both input gradients) == the fp32 torch engine
+    drawing the same dropout masks, over several steps of 2 replicas with a partial last
+    batch; the plan really is the tail chain (one launch fewer than FWD + BWD per layer)."""
+    from elephas_amd import config
+    from elephas_amd.models.optimizers import SGD
+    from elephas_amd.ops.plan import build_plan
+    from elephas_amd.ops.native_engine import NativeTrainer
+    from elephas_amd.ops.torch_engine import TorchTrainer
+    config.set_policy(policy)
+    model = _mlp(40, hidden, 9, dropout=0.3)
+    model.compile(SGD(0.1), "categorical_crossentropy", ["acc"])
+    plan = build_plan(model)
+    xs, ys = [], []
+    for r in range(2):
+        x, y = _data(3 * B - 7, 40, 9, seed=40 + r)
+        xs.append(x)
+        ys.append(y)
+    nat = NativeTrainer(model, plan, 2, B, torch.device("cuda"), seed=777)
+    assert nat.exe.tailchain() and not nat.exe.rowchain() and not nat.persistent
+    config.set_policy("float32")
+    ref = TorchTrainer(model, plan, 2, B, torch.device("cuda"), hash_dropout_seed=777)
+    w0 = nat.get_weights_flat()[0].copy()
+    for t in (nat, ref):
+        t.set_data(xs, ys, 0.1, shuffle=False)
+    hn = nat.fit(2)
+    hr = ref.fit(2)
+    wn, wr = nat.get_weights_flat(), ref.get_weights_flat()
+    if policy == "float32":
+        err = np.abs(wn - wr).max() / np.abs(wr - w0).max()
+        assert err < 1e-4, err
+        for a, b in zip(hn, hr):
+            np.testing.assert_allclose(a["loss"], b["loss"], rtol=1e-4)
+    else:
+        err = np.abs(wn - wr).mean() / np.abs(wr - w0).mean()
+        assert err < 0.05, err
+    # the grouped plan (tail off) computes the same step
+    import os
+    os.environ["ELEPHAS_AMD_TAIL"] = "0"
+    try:
+        config.set_policy(policy)
+        grp = NativeTrainer(model, plan, 2, B, torch.device("cuda"), seed=777)
+    finally:
+        del os.environ["ELEPHAS_AMD_TAIL"]
+    assert not grp.exe.tailchain()
+    assert nat.exe.launches_per_step() < grp.exe.launches_per_step(), (nat.plan_name(), grp.plan_name())
+    grp.set_weights_flat(w0)
+    grp.set_data(xs, ys, 0.1, shuffle=False)
+    hg = grp.fit(2)
+    tol = 1e-5 if policy == "float32" else 2e-2
+    for a, b in zip(hn, hg):
+        np.testing.assert_allclose(a["val_loss"], b["val_loss"], rtol=10 * tol)
+    d = np.abs(grp.get_weights_flat() - wn).max() / np.abs(wn - w0).max()
+    assert d < tol, d
+    config.set_policy("float32")
