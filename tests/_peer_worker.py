@@ -211,14 +211,21 @@ def spark_sync(dist, rank, world, gran):
     from elephas_amd.utils.model_utils import ModelType
     from elephas_amd.utils.rdd_utils import to_simple_rdd
     from elephas_amd.parallel import p2p
+    from elephas_amd import worker as worker_mod
     config.set_policy("float32")
+    persist = gran.endswith("p")   # 'fitp' / 'epochp': a model the persistent plan takes
+    gran = gran.rstrip("p")
     rng = np.random.default_rng(21)
     centers = rng.normal(0, 1, size=(5, 30)).astype(np.float32)
     y = rng.integers(0, 5, 1600)
     x = (centers[y] + rng.normal(0, 1.0, size=(1600, 30))).astype(np.float32)
     yo = np.eye(5, dtype=np.float32)[y]
     initializers.set_seed(8)
-    m = Sequential([Dense(48, activation="relu", input_dim=30), Dense(5, activation="softmax")])
+    if persist:
+        m = Sequential([Dense(64, activation="relu", input_dim=30), Dense(64, activation="relu"),
+                        Dense(5, activation="softmax")])
+    else:
+        m = Sequential([Dense(48, activation="relu", input_dim=30), Dense(5, activation="softmax")])
     m.compile(SGD(learning_rate=0.05, momentum=0.5), "categorical_crossentropy", ["acc"])
     sm = SparkModel(m, mode="synchronous", sync_granularity=gran, num_workers=4)
     sm.fit(to_simple_rdd(SparkContext(master="local[4]"), x, yo), epochs=2, batch_size=32, verbose=0,
@@ -232,11 +239,14 @@ def spark_sync(dist, rank, world, gran):
     trans = np.asarray([r[tr.getOutputCol()] for r in tr.transform(df).collect()])
     w = [np.asarray(a) for a in sm.master_network.get_weights()]
     out_dir = os.environ["ELEPHAS_AMD_TEST_OUT"]
-    np.savez(os.path.join(out_dir, f"{gran}_w{world}_r{rank}.npz"), *w, preds=preds, ev=ev, trans=trans)
+    tag = gran + ("p" if persist else "")
+    np.savez(os.path.join(out_dir, f"{tag}_w{world}_r{rank}.npz"), *w, preds=preds, ev=ev, trans=trans)
+    entry = worker_mod._trainer_cache._entry
+    persistent = bool(entry is not None and getattr(entry[0], "persistent", False))
     peer = p2p.current()
     digests = _allgather(dist)(float(np.float64(np.concatenate([a.ravel() for a in w])).sum()))
     return dict(peer_path=peer is not None, same_on_all_ranks=len(set(digests)) == 1,
-                histories=len(sm.training_histories), native=bool(sm._native_ok()),
+                histories=len(sm.training_histories), native=bool(sm._native_ok()), persistent=persistent,
                 gpu=bool(torch.cuda.is_available()))
 
 
@@ -304,7 +314,7 @@ def main():
         res = ps(dist, rank, world)
     elif scenario == "ps_selftest":
         res = ps_selftest(dist, rank, world)
-    elif scenario.startswith("spark_sync_"):
+    elif scenario.startswith("spark_sync_"):  # spark_sync_<fit|epoch|batch>[p]
         res = spark_sync(dist, rank, world, scenario.rsplit("_", 1)[1])
     elif scenario in ("spark_asynchronous", "spark_hogwild"):
         res = spark_async(dist, rank, world, scenario.split("_", 1)[1])

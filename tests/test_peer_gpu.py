@@ -121,3 +121,27 @@ def test_spark_model_synchronous_two_ranks_equals_single_process(tmp_path, gran)
     for k in a.files:
         scale = max(1.0, float(np.abs(ref[k]).max()))
         np.testing.assert_allclose(a[k], ref[k], rtol=0, atol=2e-6 * scale, err_msg=k)
+
+
+@pytest.mark.parametrize("gran", ["fit", "epoch"])
+def test_spark_model_sync_persistent_plan_two_ranks_match_one(gran, tmp_path):
+    """The persistent plan under SparkModel(mode='synchronous') across 2 ranks (each rank's
+    persistent grid limited to half the CUs, so both stay resident on the shared GPU):
+    the averaging writes the mean into the masters and leaves the weight images to the
+    next reader (NativeTrainer._ensure_images) -- both ranks agree bit for bit and match a
+    single-process run; predict / evaluate / transform read refreshed images."""
+    env = {"ELEPHAS_AMD_TEST_OUT": str(tmp_path), "ELEPHAS_AMD_P2P_ANY_BACKEND": "1",
+           "ELEPHAS_AMD_PERSIST": "1", "ELEPHAS_AMD_PERSIST_CUS": "128"}
+    two = _run(f"spark_sync_{gran}p", env_extra=env)
+    one = _run(f"spark_sync_{gran}p", world=1, env_extra=env)
+    for r in two + one:
+        assert r["persistent"] and r["same_on_all_ranks"] and r["native"] and r["histories"] == 4, r
+    for r in two:
+        assert r["peer_path"], r
+    a, b = (np.load(tmp_path / f"{gran}p_w2_r{r}.npz") for r in (0, 1))
+    ref = np.load(tmp_path / f"{gran}p_w1_r0.npz")
+    for k in a.files:
+        assert np.array_equal(a[k], b[k]), k
+    for k in a.files:
+        scale = max(1.0, float(np.abs(ref[k]).max()))
+        np.testing.assert_allclose(a[k], ref[k], rtol=0, atol=2e-6 * scale, err_msg=k)
