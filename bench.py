@@ -527,7 +527,7 @@ def bench_async(args, model, dist, rank, world, dev):
     from elephas_amd.ops.native_engine import NativeTrainer
     from elephas_amd.ops.plan import build_plan, flatten_weights
     from elephas_amd.parameter.client import DeviceClient
-    from elephas_amd.worker import BatchedAsynchronousWorker, _Group, group_persist_cus
+    from elephas_amd.worker import BatchedAsynchronousWorker, _Group, group_persist_cus, run_group_rounds
     dims, drop, classes, rows, _ = MODELS[args.model]
     W, B = args.workers_per_gpu, args.batch
     G = max(1, min(W, args.async_groups or W))
@@ -583,11 +583,11 @@ def bench_async(args, model, dist, rank, world, dev):
                     grp.t.begin_epoch()
                 state["pos"] = 0
             n = min(k, spe - state["pos"])
-            for grp in groups:            # every group enqueues n rounds on its own stream
-                if freq == "epoch":
+            if freq == "epoch":
+                for grp in groups:        # every group enqueues n steps on its own stream
                     grp.t.run_steps(n, use_graph=not args.no_graph)
-                else:
-                    grp.steps(worker, n)
+            else:
+                run_group_rounds(groups, worker, n)
             state["pos"] += n
             k -= n
         if freq == "epoch":

@@ -222,13 +222,27 @@ __device__ __forceinline__ bool ps_timed_out(const PsArgs& a, unsigned long long
 }
 
 // dst = theta, one chunk per workgroup
-__global__ __launch_bounds__(256) void ps_gather_kernel(PsArgs a, float* __restrict__ dst, int consistent) {
+// dst = theta; with P != null also every replica row P[r] (stride sP) = theta: a pull
+// straight into the masters of a trainer whose step kernel reads only those
+__global__ __launch_bounds__(256) void ps_gather_kernel(PsArgs a, float* __restrict__ dst, int consistent,
+                                                        float* __restrict__ P, long long sP, int R) {
   const long long c = blockIdx.x;
   const long long lo = c * a.chunk, hi = lo + a.chunk < a.n ? lo + a.chunk : a.n;
   const int owner = ps_owner(a, c);
   const float* th = ps_theta(a, owner);
-  if (!consistent) {
+  auto copy_all = [&]() {
     copy_span(th, dst, lo, hi);
+    for (int r = 0; P && r < R; ++r) {
+      float* row = P + (long long)r * sP;
+      if ((reinterpret_cast<uintptr_t>(row) & 15) == 0) {
+        copy_span(th, row, lo, hi);
+      } else {  // replica rows of an odd-sized vector are only 8-byte aligned
+        for (long long i = lo + threadIdx.x; i < hi; i += blockDim.x) row[i] = th[i];
+      }
+    }
+  };
+  if (!consistent) {
+    copy_all();
     return;
   }
   unsigned* began = ps_ctr(a, owner, c, 0);
@@ -248,7 +262,7 @@ __global__ __launch_bounds__(256) void ps_gather_kernel(PsArgs a, float* __restr
     }
     __syncthreads();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-    copy_span(th, dst, lo, hi);
+    copy_all();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // the copy's loads complete before the re-check
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -299,8 +313,9 @@ extern "C" hipError_t ea_allreduce_peer(const PeerArgs* a, int twoshot, int nblo
   return hipGetLastError();
 }
 
-extern "C" hipError_t ea_ps_gather(const PsArgs* a, float* dst, int consistent, hipStream_t s) {
-  hipLaunchKernelGGL(ps_gather_kernel, dim3((unsigned)a->nchunks), dim3(256), 0, s, *a, dst, consistent);
+extern "C" hipError_t ea_ps_gather(const PsArgs* a, float* dst, int consistent, float* P, long long sP, int R,
+                                   hipStream_t s) {
+  hipLaunchKernelGGL(ps_gather_kernel, dim3((unsigned)a->nchunks), dim3(256), 0, s, *a, dst, consistent, P, sP, R);
   return hipGetLastError();
 }
 

@@ -302,6 +302,9 @@ PYBIND11_MODULE(_C, m) {
       .def("pull", [](ShardedParameterServer& p, uintptr_t dst, uintptr_t s) {
         p.pull(reinterpret_cast<float*>(dst), S(s));
       })
+      .def("pull_replicas", [](ShardedParameterServer& p, uintptr_t dst, uintptr_t P, long long sP, int R, uintptr_t s) {
+        p.pull_replicas(reinterpret_cast<float*>(dst), reinterpret_cast<float*>(P), sP, R, S(s));
+      })
       .def("push_replicas", [](ShardedParameterServer& p, uintptr_t P, long long sP, int R, uintptr_t before,
                                uintptr_t s) {
         p.push_replicas(reinterpret_cast<const float*>(P), sP, R, reinterpret_cast<const float*>(before), S(s));

@@ -5,7 +5,8 @@
 #include <stdexcept>
 
 extern "C" hipError_t ea_allreduce_peer(const ea::PeerArgs* a, int twoshot, int nblocks, hipStream_t s);
-extern "C" hipError_t ea_ps_gather(const ea::PsArgs* a, float* dst, int consistent, hipStream_t s);
+extern "C" hipError_t ea_ps_gather(const ea::PsArgs* a, float* dst, int consistent, float* P, long long sP, int R,
+                                   hipStream_t s);
 extern "C" hipError_t ea_ps_push(const ea::PsArgs* a, const float* P, long long sP, int R, const float* before,
                                  hipStream_t s);
 extern "C" hipError_t ea_ps_set(const ea::PsArgs* a, const float* src, hipStream_t s);
@@ -189,7 +190,14 @@ void ShardedParameterServer::set(const float* src, hipStream_t s) {
 void ShardedParameterServer::pull(float* dst, hipStream_t s) {
   if (reinterpret_cast<uintptr_t>(dst) & 15) throw std::invalid_argument("ps pull: destination must be 16-byte aligned");
   const PsArgs a = args();
-  chk(ea_ps_gather(&a, dst, consistent_, s), "ps_gather");
+  chk(ea_ps_gather(&a, dst, consistent_, nullptr, 0, 0, s), "ps_gather");
+}
+
+void ShardedParameterServer::pull_replicas(float* dst, float* P, long long sP, int R, hipStream_t s) {
+  if (reinterpret_cast<uintptr_t>(dst) & 15) throw std::invalid_argument("ps pull: destination must be 16-byte aligned");
+  if (reinterpret_cast<uintptr_t>(P) & 15) throw std::invalid_argument("ps pull: replica rows must start 16-byte aligned");
+  const PsArgs a = args();
+  chk(ea_ps_gather(&a, dst, consistent_, P, sP, R, s), "ps_gather");
 }
 
 void ShardedParameterServer::push_replicas(const float* P, long long sP, int R, const float* before, hipStream_t s) {

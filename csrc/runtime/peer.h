@@ -96,6 +96,7 @@ class ShardedParameterServer {
   void open(const std::vector<std::string>& handles) { buf_.open(handles); }
   void set(const float* src, hipStream_t s);          // theta = src (no concurrent pushes)
   void pull(float* dst, hipStream_t s);               // dst = theta
+  void pull_replicas(float* dst, float* P, long long sP, int R, hipStream_t s);  // dst = P[r] = theta
   // theta += sum_r (P[r] - before), P rows of stride sP
   void push_replicas(const float* P, long long sP, int R, const float* before, hipStream_t s);
   void push_delta(const float* delta, hipStream_t s);  // theta -= delta (reference update semantics)

@@ -197,6 +197,10 @@ class DeviceClient(BaseParameterClient):
     def pull_into(self, dst_ptr: int, stream: int) -> None:
         self._native().pull(dst_ptr, stream)
 
+    def pull_into_replicas(self, dst_ptr: int, P_ptr: int, sP: int, R: int, stream: int) -> None:
+        """dst = theta and every replica row P[r] = theta, one gather kernel."""
+        self._native().pull_replicas(dst_ptr, P_ptr, sP, R, stream)
+
     def push_from(self, delta_ptr: int, stream: int) -> None:
         """theta -= delta (the reference's update semantics)."""
         self._native().push_delta(delta_ptr, stream)

@@ -408,7 +408,12 @@ class BatchedAsynchronousWorker:
             for _ in range(epochs):
                 for g in live:                 # each group runs its epoch on its own stream
                     g.t.begin_epoch()
-                    g.steps(self, g.t.steps_per_epoch())
+                steps = {g.t.steps_per_epoch() for g in live}
+                if len(steps) == 1:
+                    run_group_rounds(live, self, steps.pop())
+                else:
+                    for g in live:
+                        g.steps(self, g.t.steps_per_epoch())
         for g in groups:
             g.t.stream.synchronize()
         if hasattr(self.client, "check"):
@@ -424,6 +429,13 @@ class BatchedAsynchronousWorker:
         t = g.t
         with torch.cuda.stream(t.stream):
             if hasattr(self.client, "pull_refresh"):
+                if getattr(t, "persistent", False) and hasattr(self.client, "pull_into_replicas"):
+                    # the persistent kernel reads only the masters: theta straight into
+                    # every replica's P by the gather itself, weight images left to their
+                    # next reader
+                    self.client.pull_into_replicas(g.before.data_ptr(), t.P.data_ptr(), t.P.stride(0), t.R, t.s)
+                    t._images_stale = True
+                    return
                 self.client.pull_refresh(t, g.before.data_ptr())
                 return
             self.client.pull_into(t.P[0].data_ptr(), t.s)
@@ -445,6 +457,18 @@ class BatchedAsynchronousWorker:
             # for close values; R*before - sum P rounds at ulp(R*|w|) and loses the deltas)
             delta = (g.before.unsqueeze(0) - t.P).sum(0)
             self.client.push_from(delta.data_ptr(), t.s)
+
+
+def run_group_rounds(groups, worker, n):
+    """Enqueue n pull/step/push rounds for every group, each on its own stream.
+
+    Measured, not kept: submitting every group's graph replays from a thread of its own
+    (graph replay drops the GIL) -- no change (8 groups, 'batch': 1.87 vs 1.89 M
+    samples/s). A round is ~6 kernels per group and the groups' rounds overlap ~2.3x on
+    the GPU (profiles/async_batch_trace_r3.txt), so kernel count per round, not host
+    submission, bounds frequency='batch'."""
+    for g in groups:
+        g.steps(worker, n)
 
 
 class _Group:

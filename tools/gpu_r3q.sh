@@ -1,0 +1,15 @@
+#!/bin/bash
+# gather-into-replica-masters for async pulls, persistent flags back on the memset node:
+# GPU suite, A/B vs the previous build on the driver shape, async batch numbers
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/gpu_tests.txt 2>&1 || { echo "tests failed: $?"; tail -60 gpurun_out/gpu_tests.txt; exit 1; }
+tail -2 gpurun_out/gpu_tests.txt
+bash tools/ab_drv.sh || exit 1
+O=gpurun_out/r3q.log; : > $O
+run() { timeout -k 10 200 python bench.py "$@" 2>/dev/null | tail -n1 | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('$*', d['ms_per_step'], round(d['value']))" >> $O; }
+for i in 1 2; do
+run --mode asynchronous --frequency batch --steps 300 --warmup 30 || exit 1
+run --mode hogwild --frequency batch --steps 300 --warmup 30 || exit 1
+done
+cat $O
