@@ -1143,7 +1143,7 @@ static hipError_t launch_cfg(const GroupArgs& ga, hipStream_t s) {
       hipError_t e = hipSuccess;
       if (launch_if<T, WM, WN, WAVES_M, WAVES_N, KSPLIT, KM_FWD, KM_GATHER>(ga, lds, s, e) ||
           launch_if<T, WM, WN, WAVES_M, WAVES_N, KSPLIT, KM_LOSS, KM_NONE>(ga, lds, s, e) ||
-          launch_if<T, WM, WN, WAVES_M, WAVES_N, KSPLIT, KM_DW, KM_DX>(ga, lds, s, e) ||
+          launch_if<T, WM, WN, WAVES_M, WAVES_N, KSPLIT, KM_DW, KM_DX | KM_DW>(ga, lds, s, e) ||
           launch_if<T, WM, WN, WAVES_M, WAVES_N, KSPLIT, KM_PARTIAL, KM_NONE>(ga, lds, s, e))
         return e;
     }
@@ -1187,7 +1187,7 @@ static void set_attr_spec() {
   set_attr<T, WM, WN, WAVES_M, WAVES_N, KSPLIT>();
   set_attr<T, WM, WN, WAVES_M, WAVES_N, KSPLIT, KM_FWD, KM_GATHER>();
   set_attr<T, WM, WN, WAVES_M, WAVES_N, KSPLIT, KM_LOSS, KM_NONE>();
-  set_attr<T, WM, WN, WAVES_M, WAVES_N, KSPLIT, KM_DW, KM_DX>();
+  set_attr<T, WM, WN, WAVES_M, WAVES_N, KSPLIT, KM_DW, KM_DX | KM_DW>();
   set_attr<T, WM, WN, WAVES_M, WAVES_N, KSPLIT, KM_PARTIAL, KM_NONE>();
 }
 
