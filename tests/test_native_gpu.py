@@ -596,6 +596,19 @@ def test_ps_replica_pull_push(consistent):
     ps.pull(got.data_ptr(), s.cuda_stream)
     s.synchronize()
     torch.testing.assert_close(got, want - d, rtol=0, atol=1e-5)
+    # pull straight into every replica master (the persistent trainers' async pull): the
+    # replica rows of an odd-sized vector are only 8-byte aligned, the copy must cope
+    for stride in (n, n + 6):
+        Q = torch.zeros(R, stride, dtype=torch.float32, device="cuda")
+        dst = torch.empty(n, dtype=torch.float32, device="cuda")
+        s.wait_stream(torch.cuda.current_stream())
+        ps.pull_replicas(dst.data_ptr(), Q.data_ptr(), stride, R, s.cuda_stream)
+        s.synchronize()
+        assert torch.equal(dst, got)    # the server's theta, as pulled above
+        for r in range(R):
+            assert torch.equal(Q[r, :n], got), (stride, r)
+        if stride > n:
+            assert not Q[:, n:].any()   # nothing written past each row
     assert ps.error() == 0
 
 
