@@ -345,7 +345,8 @@ __global__ __launch_bounds__(BIG_NT) void gemm_big(GroupArgs ga) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   stamp(ga, 0);
   const int r = blockIdx.x, bid = blockIdx.y;
-  const int pi = (KM1 != KM_NONE && ga.nprob > 1 && bid >= ga.p[1].block_begin) ? 1 : 0;
+  const int b0 = ga.p[0].block_begin, b1 = ga.p[1].block_begin;
+  const int pi = (KM1 != KM_NONE && ga.nprob > 1 && bid >= b1 && (b1 > b0 || bid < b0)) ? 1 : 0;
   const Prob& p = pi ? ga.p[1] : ga.p[0];
   int lb = bid - p.block_begin;
   const int nt = p.tiles_m * p.tiles_n;

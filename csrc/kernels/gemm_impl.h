@@ -1051,7 +1051,10 @@ __global__ __launch_bounds__(256) void gemm_grouped(GroupArgs ga) {
   stamp(ga, 0);
   stamp_clk(ga, 10);
   const int r = blockIdx.x, bid = blockIdx.y;
-  if (KM1 != KM_NONE && ga.nprob > 1 && bid >= ga.p[1].block_begin)
+  // problem 1 owns [p[1].block_begin, ...) up to p[0]'s range when that comes after it
+  // (the executor puts the problem with the deeper tiles first: longest tiles dispatched first)
+  const int b0 = ga.p[0].block_begin, b1 = ga.p[1].block_begin;
+  if (KM1 != KM_NONE && ga.nprob > 1 && bid >= b1 && (b1 > b0 || bid < b0))
     run_prob<T, WM, WN, WAVES_M, WAVES_N, KSPLIT, KM1>(ga, ga.p[1], r, bid - ga.p[1].block_begin, smem);
   else
     run_prob<T, WM, WN, WAVES_M, WAVES_N, KSPLIT, KM0>(ga, ga.p[0], r, bid - ga.p[0].block_begin, smem);

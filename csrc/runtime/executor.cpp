@@ -486,6 +486,18 @@ void Executor::finalize(Launch& L) const {
     // tiles per replica: grid (R, tiles); split-K problems have tiles_k slabs each
     begin += p.tiles_m * p.tiles_n * (p.kind == PK_PARTIAL ? std::max(1, p.tiles_k) : 1);
   }
+  // A weight-gradient + input-gradient pair: the problem with the deeper reduction (the
+  // longer tiles -- Wide DX, K = 4096, against DW's K = batch) takes the first block
+  // range, so its tiles are dispatched first and the short ones fill in around them
+  // instead of trailing at the end of the launch
+  if (L.ga.nprob == 2) {
+    Prob &p0 = L.ga.p[0], &p1 = L.ga.p[1];
+    auto gemm_kind = [](int k) { return k == PK_DW_UPDATE || k == PK_DW_GRAD || k == PK_DX; };
+    if (gemm_kind(p0.kind) && gemm_kind(p1.kind) && p1.K > p0.K && !c_.no_reorder) {
+      p1.block_begin = 0;
+      p0.block_begin = p1.tiles_m * p1.tiles_n;
+    }
+  }
   L.ga.R = c_.R;
   L.ga.total_blocks = begin;
   L.ga.ctr = reinterpret_cast<long long*>(c_.ctr);

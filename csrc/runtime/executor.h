@@ -75,6 +75,7 @@ struct ExecCfg {
   int persist = -1;    // persistent chunk kernel (persist.hip): -1 when eligible, 0 off, 1 required
   long long persist_timeout_ms = 2000;  // spin limit of its in-launch waits
   int persist_cus = 0;  // > 0: CUs the persistent grid may occupy (several executors side by side)
+  int no_reorder = 0;   // A/B: keep a DW + DX launch's problems in declaration order
 };
 
 struct EvalSource {
