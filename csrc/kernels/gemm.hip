@@ -10,6 +10,8 @@ hipError_t ea_gemm_launch_thr64_bf16(const ea::GroupArgs* ga, hipStream_t s);
 hipError_t ea_gemm_launch_big_bf16(const ea::GroupArgs* ga, hipStream_t s);
 hipError_t ea_gemm_launch_big_var_bf16(const ea::GroupArgs* ga, int v, hipStream_t s);
 hipError_t ea_gemm_launch_f32(const ea::GroupArgs* ga, int cfg, hipStream_t s);
+hipError_t ea_gemm_dual_f32(const ea::GroupArgs* ga, int a, int b, hipStream_t s);
+hipError_t ea_gemm_dual_bf16(const ea::GroupArgs* ga, int a, int b, hipStream_t s);
 hipError_t ea_gemm_table_lat_bf16(const ea::TableArgs* ta, int dw, hipStream_t s);
 hipError_t ea_gemm_table_f32(const ea::TableArgs* ta, int dw, hipStream_t s);
 void ea_gemm_init_lat_bf16();
@@ -34,6 +36,9 @@ extern "C" hipError_t ea_gemm_grouped(const ea::GroupArgs* ga, int bf16, int cfg
       hipLaunchKernelGGL(loss_rows_kernel<float>, dim3(ga->R, ga->total_blocks), dim3(256), lds, s, *ga);
     return hipGetLastError();
   }
+  // 100 + 10 a + b: problem 0 on config a, problem 1 on config b (gemm_dual)
+  if (cfg >= 100) return bf16 ? ea_gemm_dual_bf16(ga, (cfg - 100) / 10, cfg % 10, s)
+                              : ea_gemm_dual_f32(ga, (cfg - 100) / 10, cfg % 10, s);
   if (!bf16) return ea_gemm_launch_f32(ga, cfg >= 4 ? 1 : cfg, s);
   if (cfg == 4) return ea_gemm_launch_big_bf16(ga, s);
   if (cfg >= 5) return ea_gemm_launch_big_var_bf16(ga, cfg - 4, s);
@@ -61,8 +66,13 @@ extern "C" void ea_gemm_init() {
 
 // cfg 3: the 64x64 tile of the row-chain weight-gradient table launch (not a
 // grouped-launch config)
-extern "C" int ea_gemm_tile_m(int cfg) { return cfg >= 4 ? 256 : ((cfg == 0 || cfg == 3) ? 64 : 128); }
+// (a dual config 100 + 10 a + b reports its first problem's tile)
+extern "C" int ea_gemm_tile_m(int cfg) {
+  if (cfg >= 100) cfg = (cfg - 100) / 10;
+  return cfg >= 4 ? 256 : ((cfg == 0 || cfg == 3) ? 64 : 128);
+}
 extern "C" int ea_gemm_tile_n(int cfg) {
+  if (cfg >= 100) cfg = (cfg - 100) / 10;
   return cfg >= 4 ? 256 : (cfg == 0 ? 32 : ((cfg == 2 || cfg == 3) ? 64 : 128));
 }
 extern "C" int ea_gather_tile() { return 64; }

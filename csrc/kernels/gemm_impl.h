@@ -1063,6 +1063,27 @@ __global__ __launch_bounds__(256) void gemm_grouped(GroupArgs ga) {
   stamp_clk(ga, 11);
 }
 
+// Two problems whose best tiles differ in ONE launch (a layer's weight gradient and input
+// gradient: Otto DW 513x512x128 wants 128x64 tiles, DX 128x512x512 the 64x32 split-K
+// tile): problem 0 on tile A, problem 1 on tile B, each block runs its problem's tile
+// (every config is 4 waves of 64; LDS = the larger of the two). Replaces two dependent
+// launches by one.
+template <typename T, int WMa, int WNa, int WAMa, int WANa, int KSa, int WMb, int WNb, int WAMb, int WANb, int KSb,
+          unsigned KM0, unsigned KM1>
+__global__ __launch_bounds__(256) void gemm_dual(GroupArgs ga) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  stamp(ga, 0);
+  stamp_clk(ga, 10);
+  const int r = blockIdx.x, bid = blockIdx.y;
+  const int b0 = ga.p[0].block_begin, b1 = ga.p[1].block_begin;
+  if (bid >= b1 && (b1 > b0 || bid < b0))
+    run_prob<T, WMb, WNb, WAMb, WANb, KSb, KM1>(ga, ga.p[1], r, bid - b1, smem);
+  else
+    run_prob<T, WMa, WNa, WAMa, WANa, KSa, KM0>(ga, ga.p[0], r, bid - b0, smem);
+  stamp(ga, 4);
+  stamp_clk(ga, 11);
+}
+
 // Wide-output loss rows run in a kernel of their own: inside gemm_grouped their
 // register-resident row (16 z + 16 y values per lane) raised every GEMM tile's
 // VGPR allocation (104 -> 132 on the 128x128 config, plus scratch) and slowed
@@ -1175,6 +1196,26 @@ static hipError_t launch_table(const TableArgs& ta, int dw, hipStream_t s) {
                        s, ta);
   }
   return hipGetLastError();
+}
+
+// the supported dual pair: problem 0 (DW) on the 128x64 THR-N64 tile (cfg 2), problem 1
+// (DX) on the 64x32 LAT split-K tile (cfg 0)
+template <typename T>
+static size_t dual20_lds() {
+  return std::max(lds_bytes<T, 4, 2, 2, 2, 1>(false), lds_bytes<T, 4, 2, 1, 1, 4>(false));
+}
+template <typename T>
+static hipError_t launch_dual(const GroupArgs& ga, int a, int b, hipStream_t s) {
+  if (a != 2 || b != 0 || ga.nprob != 2) return hipErrorInvalidValue;
+  if (ga.total_blocks <= 0) return hipSuccess;
+  hipLaunchKernelGGL((gemm_dual<T, 4, 2, 2, 2, 1, 4, 2, 1, 1, 4, KM_DW, KM_DX>), dim3(ga.R, ga.total_blocks), dim3(256),
+                     dual20_lds<T>(), s, ga);
+  return hipGetLastError();
+}
+template <typename T>
+static void set_attr_dual() {
+  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_dual<T, 4, 2, 2, 2, 1, 4, 2, 1, 1, 4, KM_DW, KM_DX>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)dual20_lds<T>());
 }
 
 template <typename T>

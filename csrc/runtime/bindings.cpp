@@ -76,6 +76,7 @@ static ExecCfg parse_cfg(const py::dict& d) {
   c.rc_split = get<int>(d, "rc_split", 0);
   c.tail = get<int>(d, "tail", -1);
   c.no_reorder = get<int>(d, "no_reorder", 0);
+  c.dual = get<int>(d, "dual", 1);
   c.persist = get<int>(d, "persist", -1);
   c.persist_timeout_ms = get<long long>(d, "persist_timeout_ms", 2000);
   c.persist_cus = get<int>(d, "persist_cus", 0);

@@ -339,7 +339,7 @@ bool Executor::build_tail() {
     std::memset(&La, 0, sizeof(La));
     La.ga.p[0] = dw_last;
     La.ga.nprob = 1;
-    La.cfg = bwd_[0].cfg;
+    La.cfg = bwd_[0].cfg >= 100 ? (bwd_[0].cfg - 100) / 10 : bwd_[0].cfg;
     finalize(La);
     tl_.post.insert(tl_.post.begin(), La);
   }
@@ -463,9 +463,11 @@ Prob Executor::base_prob() const {
 }
 
 void Executor::finalize(Launch& L) const {
-  const int bm = ea_gemm_tile_m(L.cfg), bn = ea_gemm_tile_n(L.cfg);
   int begin = 0;
   for (int i = 0; i < L.ga.nprob; ++i) {
+    // a dual launch (cfg 100 + 10 a + b) tiles problem 0 with config a, problem 1 with b
+    const int pc = L.cfg >= 100 ? (i == 0 ? (L.cfg - 100) / 10 : L.cfg % 10) : L.cfg;
+    const int bm = ea_gemm_tile_m(pc), bn = ea_gemm_tile_n(pc);
     Prob& p = L.ga.p[i];
     // the epilogues' transposed stores move 8 consecutive elements at a time
     if (p.DT && (p.lddt % 8 || p.sDT % 8))
@@ -763,6 +765,15 @@ void Executor::build() {
         return (long long)c_.R * cdiv(p.M, ea_gemm_tile_m(c)) * cdiv(p.N, ea_gemm_tile_n(c));
       };
       const bool underfilled = cw != cx && tiles(w, cs) + tiles(x, cs) < 512;
+      if (underfilled && cw == 2 && cx == 0 && c_.dual) {
+        // the two products in ONE launch, each on its own tile (gemm_dual)
+        La.ga.p[1] = x;
+        La.ga.nprob = 2;
+        La.cfg = 100 + 10 * cw + cx;
+        finalize(La);
+        bwd_.push_back(La);
+        continue;
+      }
       if ((cw == 4) != (cx == 4) || underfilled) {
         // one of the two products fills the chip with 256x256 tiles, the other
         // would leave most CUs idle on them: two launches, each on its own tile

@@ -76,6 +76,7 @@ struct ExecCfg {
   long long persist_timeout_ms = 2000;  // spin limit of its in-launch waits
   int persist_cus = 0;  // > 0: CUs the persistent grid may occupy (several executors side by side)
   int no_reorder = 0;   // A/B: keep a DW + DX launch's problems in declaration order
+  int dual = 1;         // a layer's DW and DX on different tiles in one launch (0: two launches)
 };
 
 struct EvalSource {

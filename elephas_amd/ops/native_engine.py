@@ -199,6 +199,7 @@ class NativeTrainer(TrainerBase):
             rc_split=int(os.environ.get("ELEPHAS_AMD_RC_SPLIT", "0")),
             tail=int(os.environ.get("ELEPHAS_AMD_TAIL", "-1")) if ws is self.ws else 0,
             no_reorder=int(os.environ.get("ELEPHAS_AMD_NO_REORDER", "0")),
+            dual=int(os.environ.get("ELEPHAS_AMD_DUAL", "1")),
             layers=layers,
             X=self.X.data_ptr(), sX=self.nmax * self.Kp0, ldx=self.Kp0,
             Y=self.Y.data_ptr(), sY=self.nmax * self.ldy, ldy=self.ldy,
