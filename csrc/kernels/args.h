@@ -207,7 +207,7 @@ struct PersistArgs {
   unsigned long long seed;
   float* ws; long long ws_stride;   // per-replica exchange workspace (floats)
   long long o_part, o_dz0, o_a0, o_a1, o_dz1, o_dz2, o_w1, o_w2, o_b1, o_b2;
-  unsigned* flags;                  // [R][PMF_N][PM_MAXWG], zeroed before every launch
+  unsigned* flags;                  // [R][PMF_N][PM_MAXWG], zero at launch (cleared by the chunk's post node)
   unsigned* err;                    // sticky error word (a timed-out wait), read by the host
   long long timeout;                // spin limit in s_memrealtime ticks (100 MHz)
   long long* stamps;                // diagnostics: [block][PM_STAMP_STEPS][32] s_memrealtime (null = off)

@@ -54,6 +54,22 @@ __global__ __launch_bounds__(64) void advance_kernel(long long* ctr, const int* 
   if (threadIdx.x == 0) ctr[0] = s0 + n;
 }
 
+// After a persistent chunk (persist.hip): clear the launch's flag block for the next
+// launch and advance the step counters -- one node instead of a flag memset ahead of
+// the next launch plus advance_kernel (one block; the flag block is a few thousand words)
+__global__ __launch_bounds__(256) void persist_post_kernel(unsigned* flags, int nflags, long long* ctr, const int* ntrain,
+                                                           int R, int B, int n) {
+  for (int e = threadIdx.x; e < nflags; e += 256) flags[e] = 0u;
+  const long long s0 = ctr[0];
+  for (int r = threadIdx.x; r < R; r += 256) {
+    const long long nb = ((long long)ntrain[r] + B - 1) / B;
+    const long long d = nb - s0;
+    ctr[2 + r] += d < 0 ? 0 : (d > n ? n : d);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) ctr[0] = s0 + n;
+}
+
 // grid: total_blocks over R*n elements
 template <typename T>
 __global__ __launch_bounds__(256) void apply_update_kernel(FlatArgs a) {
@@ -263,6 +279,12 @@ extern "C" hipError_t ea_apply_update(FlatArgs* a, int bf16, hipStream_t s) {
   if (a->total_blocks <= 0) return hipSuccess;
   if (bf16) hipLaunchKernelGGL((shadow_tiles_kernel<__bf16, true>), dim3(a->total_blocks), dim3(256), 0, s, *a, tiles);
   else hipLaunchKernelGGL((shadow_tiles_kernel<float, true>), dim3(a->total_blocks), dim3(256), 0, s, *a, tiles);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t ea_persist_post(unsigned* flags, int nflags, long long* ctr, const int* ntrain, int R, int B, int n,
+                                      hipStream_t s) {
+  hipLaunchKernelGGL(persist_post_kernel, dim3(1), dim3(256), 0, s, flags, nflags, ctr, ntrain, R, B, n);
   return hipGetLastError();
 }
 

@@ -16,6 +16,8 @@ extern "C" hipError_t ea_rowchain(const ea::RcArgs* a, int bf16, int nbw, hipStr
 extern "C" hipError_t ea_apply_update(ea::FlatArgs* a, int bf16, hipStream_t s);
 extern "C" hipError_t ea_refresh_shadows(ea::FlatArgs* a, int bf16, hipStream_t s);
 extern "C" hipError_t ea_advance(long long* ctr, const int* ntrain, int R, int B, int n, hipStream_t s);
+extern "C" hipError_t ea_persist_post(unsigned* flags, int nflags, long long* ctr, const int* ntrain, int R, int B, int n,
+                                      hipStream_t s);
 extern "C" hipError_t ea_persist(const ea::PersistArgs* a, hipStream_t s);
 extern "C" int ea_persist_lds_bytes();
 
@@ -144,8 +146,8 @@ bool Executor::build_persist() {
   a.flags = d_pflags_;
   a.err = d_perr_;
   a.timeout = std::max<long long>(1, c_.persist_timeout_ms) * 100000LL;  // s_memrealtime: 100 MHz
-  // the zeroed error word must be in memory before the first launch, which goes to a
-  // caller's (non-blocking) stream that does not order after hipMemset's
+  // the zeroed flags and error word must be in memory before the first launch, which
+  // goes to a caller's (non-blocking) stream that does not order after hipMemset's
   check(hipDeviceSynchronize(), "hipDeviceSynchronize(persistent plan setup)");
   return true;
 }
@@ -172,14 +174,17 @@ void Executor::persist_clear_error() {
 
 void Executor::run_chunk(hipStream_t s, int nsteps) const {
   if (pm_.on) {
-    // flags zeroed by a memset node ahead of every launch (tags restart at 1). Measured,
-    // not kept: the last workgroup out clearing them and advancing the counters itself
-    // (two nodes fewer per chunk): async 'batch' rounds +15 %, but the step loop of the
-    // kernel ran 2-3 % slower (profiles/persist_exit_ab_r3.txt)
-    check(hipMemsetAsync(d_pflags_, 0, pm_.flag_bytes, s), "hipMemsetAsync(persistent flags)");
+    // the flags are zero at launch (setup, then the post node of every chunk: tags
+    // restart at 1), and one post node clears them again and advances the counters
+    // (instead of a flag memset ahead of the launch plus the advance node after it).
+    // Measured, not kept: the kernel's last workgroup doing both (async 'batch' +15 %,
+    // but the step loop ran 2-3 % slower: profiles/persist_exit_ab_r3.txt)
     PersistArgs a = pm_.args;
     a.nsteps = nsteps;
     check(ea_persist(&a, s), "persistent step kernel");
+    check(ea_persist_post(d_pflags_, (int)(pm_.flag_bytes / sizeof(unsigned)), reinterpret_cast<long long*>(c_.ctr),
+                          reinterpret_cast<const int*>(c_.ntrain), c_.R, c_.B, nsteps, s),
+          "persistent chunk post");
     return;
   }
   for (int i = 0; i < nsteps; ++i) run_step(s, i);
@@ -908,13 +913,13 @@ std::vector<int> Executor::launch_cfgs() const {
 
 void Executor::train_step(hipStream_t s) {
   run_chunk(s, 1);
-  advance(1, s);
+  if (!pm_.on) advance(1, s);   // the persistent chunk's post node advanced the counters
 }
 
 void Executor::train_chunk(int nsteps, hipStream_t s) {
   if (nsteps <= 0) return;
   run_chunk(s, nsteps);
-  advance(nsteps, s);
+  if (!pm_.on) advance(nsteps, s);
 }
 
 void Executor::forward_backward(hipStream_t s) {
@@ -1011,8 +1016,9 @@ int Executor::capture(int nsteps, int mode, hipStream_t s) {
   try {
     if (mode == 0) {
       // one chunk: steps at offsets 0..nsteps-1 from the counter base, then one advance
+      // (the persistent plan's post node includes it)
       run_chunk(s, nsteps);
-      advance(nsteps, s);
+      if (!pm_.on) advance(nsteps, s);
     } else {
       for (int i = 0; i < nsteps; ++i) {
         if (mode == 1) forward_backward(s);
