@@ -179,13 +179,27 @@ constexpr int PM_ROWS = 64;    // batch rows per replica (B <= 64)
 constexpr int PM_MAXH = 128;   // hidden widths: 64 or 128
 constexpr int PM_MAXC = 16;    // last layer units
 constexpr int PM_MAXWG = 64;   // workgroups of one kind per replica (one polling wave watches them)
-constexpr int PM_NTU = 2;      // layer-1 column tiles (and layer-2 row tiles) a chain workgroup owns
-enum PmFlag : int { PMF_PART = 0, PMF_BWD = 1, PMF_W = 2, PMF_N = 3 };
+constexpr int PM_NTU = 2;      // layer-1 column tiles (and layer-2 row tiles) a chain / DW workgroup owns
+// hand-off flag kinds: PART (layer-0 partials of a step), BWD (a chain's dZ_0 rows), W
+// (updated W1 / W2 columns), A0 / D2 (V2: a chain's layer-0 activations / dZ_2 and
+// layer-1 activations for the weight-gradient workgroups), GO (residency: every
+// workgroup raises it on entry; the chain workgroups see the whole grid before they
+// touch any state)
+enum PmFlag : int { PMF_PART = 0, PMF_BWD = 1, PMF_W = 2, PMF_A0 = 3, PMF_D2 = 4, PMF_GO = 5, PMF_N = 6 };
+// sticky error codes: the wait that timed out (PERR_GRID: the grid was not resident --
+// nothing was modified, the chunk can be re-run on another plan)
+enum PmErr : unsigned { PERR_L0_BWD = 1, PERR_CHAIN_PART = 2, PERR_CHAIN_BWD = 3, PERR_CHAIN_PREV = 4,
+                        PERR_DW_A0 = 5, PERR_DW_D2 = 6, PERR_GRID = 9 };
 struct PersistArgs {
   int R, B, nsteps;
   int K0, H0, H1, C;            // layer widths (H0, H1 in {64, 128}; C <= 16)
   int nk0, nc0, kc0, cw;        // layer-0 tiles: nk0 k-chunks of kc0 rows x nc0 column blocks of cw
-  int nch, wgs;                 // chain workgroups per replica; workgroups per replica (nk0*nc0 + nch)
+  int nch, wgs;                 // chain workgroups per replica; workgroups per replica (nk0*nc0 + nch [+ nd])
+  // V2 (plain SGD, ReLU, fit granularity): nd weight-gradient workgroups per replica own
+  // the W1 columns / W2 rows; the chain rebuilds Z_0 from Pold + Gram corrections
+  int v2, nd;
+  long long o_g;                    // Gram partials [2][nk0][64][64] (V2)
+  long long part_par, g_par, dz0_par;   // parity strides of the double-buffered partials / Gram / dZ_0 (V2; 0 in V1)
   int act0, act1, act2;
   float rate0, rate1;
   int bias0, bias1, bias2;

@@ -58,8 +58,11 @@ __global__ __launch_bounds__(64) void advance_kernel(long long* ctr, const int* 
 // launch and advance the step counters -- one node instead of a flag memset ahead of
 // the next launch plus advance_kernel (one block; the flag block is a few thousand words)
 __global__ __launch_bounds__(256) void persist_post_kernel(unsigned* flags, int nflags, long long* ctr, const int* ntrain,
-                                                           int R, int B, int n) {
+                                                           int R, int B, int n, const unsigned* err) {
   for (int e = threadIdx.x; e < nflags; e += 256) flags[e] = 0u;
+  // a launch that gave up (sticky error word) did not run its steps: the counters stay
+  // (the host re-plans and re-runs them, native_engine.py NativeTrainer.check)
+  if (*err != 0u) return;
   const long long s0 = ctr[0];
   for (int r = threadIdx.x; r < R; r += 256) {
     const long long nb = ((long long)ntrain[r] + B - 1) / B;
@@ -283,8 +286,8 @@ extern "C" hipError_t ea_apply_update(FlatArgs* a, int bf16, hipStream_t s) {
 }
 
 extern "C" hipError_t ea_persist_post(unsigned* flags, int nflags, long long* ctr, const int* ntrain, int R, int B, int n,
-                                      hipStream_t s) {
-  hipLaunchKernelGGL(persist_post_kernel, dim3(1), dim3(256), 0, s, flags, nflags, ctr, ntrain, R, B, n);
+                                      const unsigned* err, hipStream_t s) {
+  hipLaunchKernelGGL(persist_post_kernel, dim3(1), dim3(256), 0, s, flags, nflags, ctr, ntrain, R, B, n, err);
   return hipGetLastError();
 }
 

@@ -26,7 +26,8 @@
 // loaded with sc1 buffer instructions, each storing wave drains (s_waitcnt vmcnt(0)),
 // the workgroup barriers, one lane stores the flag (agent-scope relaxed = sc1); one
 // wave polls the producers' flags with sc1 loads.  Tags are the step index + 1 within
-// the launch; the flag block is zeroed by a memset node before every launch.  Every
+// the launch; the flag block is zero at every launch (hipMemset + hipDeviceSynchronize
+// at setup, then the 1-block post kernel after each launch clears it again).  Every
 // spin is bounded (timeout -> sticky error word, the workgroup returns; the host
 // raises), and a launch that finds the error word set does nothing.
 //
@@ -75,10 +76,14 @@ struct ChainLds {
   static constexpr int o_b1 = o_y + 16 * 32;          // [H1]
   static constexpr int o_b2 = o_b1 + H1;              // [16]
   static constexpr int o_row = o_b2 + 16;             // [16] ints
-  static constexpr int TOTAL = o_row + 16;
+  static constexpr int o_gs = o_row + 16;             // [16][65] V2: this chain's Gram rows (+ 1)
+  static constexpr int TOTAL = o_gs + 16 * 65;
 };
 constexpr int L0_LDS = 2 * 64 * 129 + 128 * 33 + 64 * 33;
-constexpr int LDS_FLOATS = ((ChainLds<128, 128>::TOTAL > L0_LDS ? ChainLds<128, 128>::TOTAL : L0_LDS) + 3) & ~3;
+constexpr int L0V2_LDS = 2 * 64 * 129 + 128 * 65 + 64 * 65;   // X chunks, W0 tile (cw <= 64), dZ_0 columns
+constexpr int DW_LDS = 64 * 129 + 2 * 64 * 33 + 64 * 17 + 32 * 17;
+constexpr int cmax(int x, int y) { return x > y ? x : y; }
+constexpr int LDS_FLOATS = (cmax(cmax(ChainLds<128, 128>::TOTAL, L0_LDS), cmax(L0V2_LDS, DW_LDS)) + 3) & ~3;
 
 __device__ __forceinline__ f32x4 mma(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
@@ -92,6 +97,9 @@ __device__ __forceinline__ rsrc_t ws_rsrc(const float* base) {
 }
 __device__ __forceinline__ f32x4 ldw4(rsrc_t r, int v, int s) {
   return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, v * 4, s * 4, 16));
+}
+__device__ __forceinline__ float ldw1(rsrc_t r, int v, int s) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, v * 4, s * 4, 16));
 }
 __device__ __forceinline__ void stw1(rsrc_t r, int v, int s, float x) {
   __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, x), r, v * 4, s * 4, 16);
@@ -163,6 +171,34 @@ __device__ __forceinline__ bool wait_two(const PersistArgs& a, const unsigned* f
   }
   ok = __syncthreads_and(ok);
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  return ok != 0;
+}
+
+// residency: wave 0 polls the GO flag of every workgroup of the grid (R replicas x wgs)
+// until all are raised.  A workgroup that is not resident never raises
+// it, so the waiting ones time out (PERR_GRID) before any of them modified state.
+__device__ __forceinline__ bool wait_grid(const PersistArgs& a) {
+  int ok = 1;
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x, tot = a.R * a.wgs;
+    const unsigned long long t0 = wall_clock64();
+    for (;;) {
+      bool all = true;
+      for (int f = lane; f < tot; f += 64) {
+        const int rr = f % a.R, qq = f / a.R;
+        all &= __hip_atomic_load((gu32*)(flag_at(a, rr, PMF_GO) + qq), __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT) != 0u;
+      }
+      if (__all(all)) break;
+      if ((long long)(wall_clock64() - t0) > a.timeout) {
+        ok = 0;
+        if (lane == 0) __hip_atomic_store((gu32*)(a.err), (unsigned)PERR_GRID, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  ok = __syncthreads_and(ok);
   return ok != 0;
 }
 
@@ -584,6 +620,262 @@ __device__ __forceinline__ void l0_role(const PersistArgs& a, float* smem, int r
   }
 }
 
+// ============================================================== V2: layer-0 tiles
+// Plain SGD, fit granularity.  W0_s = W0_{s-2} - lr_{s-1} gs X_{s-1}^T dZ0_{s-1} (and
+// b0 likewise with the column sums of dZ0_{s-1}), so
+//   Z0_s = X_s W0_{s-2} + b0_{s-2}  -  lr_{s-1} gs (X_s X_{s-1}^T + 1) dZ0_{s-1}.
+// The workgroup publishes, two steps ahead of use, Pold_s = its k-chunk's share of the
+// first product (+ b0 on k-chunk 0) and its slice of the Gram block X_s X_{s-1}^T (this
+// k-chunk, rows cb * 64 / nc0 ...); the chain workgroups add the correction with the
+// dZ0_{s-1} rows they hand to each other.  dZ0 reaches this workgroup only for the
+// update of its tile (DW0 = X^T dZ0), which is off the step's critical path.
+// Step 0 is the direct product; buffers of step s live in parity s & 1.
+template <int H0, int NCT>
+__device__ __forceinline__ void l0_role_v2(const PersistArgs& a, float* smem, int r, int kc, int cb, int q) {
+  static_assert(NCT == 2 || NCT == 4, "column blocks of 32 or 64");
+  constexpr int XS = 129, CW = NCT * 16, WS = CW + 1, TU0 = 2 * NCT;   // DW0 tiles per wave (<= 8 row tiles)
+  const int tid = threadIdx.x, lane = tid & 63, i16 = lane & 15, g = lane >> 4;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6) & 3;
+  const int k0 = kc * a.kc0;
+  const int kreal = a.K0 - k0 < a.kc0 ? a.K0 - k0 : a.kc0;
+  const int KCP = (kreal + 63) & ~63;           // reductions over the k-chunk, zero padded to 64
+  const int n0 = cb * CW;
+  const int nrt = (kreal + 15) >> 4, ntiles = nrt * NCT;
+  const int BR = a.nch * 16;
+  float* sX = smem;                             // [2][64][XS] X chunks (steps of parity 0 / 1)
+  float* sW = sX + 2 * 64 * XS;                 // [128][WS]   the W0 tile (master, in place)
+  float* sdZ = sW + 128 * WS;                   // [64][WS]    dZ_0 columns of this tile
+  __shared__ float sB0[64];
+  __shared__ float sBg[64];
+  __shared__ float sRedL[256];
+  const rsrc_t rs = ws_rsrc(a.ws + (long long)r * a.ws_stride);
+  float* P = a.P + (long long)r * a.sP;
+  const bool has_b = kc == 0 && a.bias0;
+  Steps st{ld_inv(a.ctr), ld_inv(a.ntrain + r)};
+
+  for (int e = tid; e < L0V2_LDS; e += 256) smem[e] = 0.f;
+  __syncthreads();
+  for (int base = 0; base < kreal * CW; base += 16 * 256) {
+    float v[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int e = base + tid + 256 * u, el = e < kreal * CW ? e : 0;
+      const int k = el / CW, nn = el - k * CW;
+      v[u] = P[a.p_off0 + (long long)(k0 + k) * H0 + n0 + nn];
+    }
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int e = base + tid + 256 * u;
+      if (e < kreal * CW) sW[(e / CW) * WS + (e % CW)] = v[u];
+    }
+  }
+  int rt[TU0], ct[TU0];
+#pragma unroll
+  for (int u = 0; u < TU0; ++u) {
+    const int t = w + 4 * u;
+    rt[u] = t < ntiles ? t / NCT : 0;
+    ct[u] = t < ntiles ? t - rt[u] * NCT : 0;
+  }
+  float bw = 0.f;
+  const bool bown = has_b && tid < CW;
+  if (bown) bw = P[a.p_off0 + (long long)a.K0 * H0 + n0 + tid];
+  if (tid < 64) sB0[tid] = 0.f;
+  __syncthreads();
+  if (bown) sB0[tid] = bw;
+
+  auto load_x = [&](int i) {   // as l0_role: LDS-DMA of step i's X chunk into buffer i & 1
+    const int valid = st.valid(a, i);
+    const int* pr = a.perm + (long long)r * a.sPerm + (st.s0 + i) * a.B;
+    const float* Xr = a.X + (long long)r * a.sX + k0;
+    float* dst = sX + (i & 1) * 64 * XS;
+    const int myrow = pr[lane < valid ? lane : 0];
+    for (int v = 0; v < 16; ++v) {
+      const int b = w + 4 * v;
+      if (b >= BR) break;
+      const int row = __builtin_amdgcn_readlane(myrow, b);
+      const float* src = Xr + (long long)row * a.ldx;
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+        if (64 * h + lane < kreal) __builtin_amdgcn_global_load_lds(src + 64 * h + lane, dst + b * XS + 64 * h, 4, 0, 0);
+    }
+  };
+
+  // X_i . W0 tile (+ b0 on k-chunk 0) -> partial slab of step i (parity i & 1)
+  auto fwd = [&](int i) {
+    const float* A = sX + (i & 1) * 64 * XS;
+    if (w * 16 < BR) {
+      f32x4 acc[NCT];
+#pragma unroll
+      for (int jj = 0; jj < NCT; ++jj) acc[jj] = zero4f();
+      const float* arow = A + (w * 16 + i16) * XS;
+#pragma unroll 1
+      for (int kb = 0; kb < KCP; kb += 64) {
+        float av[16], bv[NCT][16];
+#pragma unroll
+        for (int ks = 0; ks < 16; ++ks) {
+          const int k = kb + 16 * g + ks;
+          av[ks] = arow[k];
+#pragma unroll
+          for (int jj = 0; jj < NCT; ++jj) bv[jj][ks] = sW[k * WS + jj * 16 + i16];
+        }
+#pragma unroll
+        for (int ks = 0; ks < 16; ++ks) {
+#pragma unroll
+          for (int jj = 0; jj < NCT; ++jj) acc[jj] = mma(av[ks], bv[jj][ks], acc[jj]);
+        }
+      }
+      const int base = (int)(a.o_part + (i & 1) * a.part_par) + kc * 64 * H0 + n0;
+      const int v = (w * 16 + 4 * g) * H0 + i16;
+#pragma unroll
+      for (int jj = 0; jj < NCT; ++jj) {
+        const float bv = has_b ? sB0[jj * 16 + i16] : 0.f;
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq) stw1(rs, v + qq * H0 + jj * 16, base, acc[jj][qq] + bv);
+      }
+    }
+  };
+
+  // rows [cb * 64 / nc0, (cb + 1) * 64 / nc0) of this k-chunk's X_i . X_{i-1}^T -> Gram
+  // slab of step i (parity i & 1)
+  auto gram = [&](int i) {
+    const float* A = sX + (i & 1) * 64 * XS;
+    const float* Bm = sX + ((i - 1) & 1) * 64 * XS;
+    const int rows = 64 / a.nc0, r0 = cb * rows;
+    const int ntg = (rows >> 4) * 4;   // 16 x 16 tiles of the slice (4 column tiles of 16)
+    const int base = (int)(a.o_g + (i & 1) * a.g_par) + kc * 64 * 64;
+#pragma unroll 1
+    for (int t = w; t < ntg; t += 4) {
+      const int tr = t >> 2, tc = t & 3;
+      f32x4 acc = zero4f();
+      const float* arow = A + (r0 + tr * 16 + i16) * XS;
+      const float* brow = Bm + (tc * 16 + i16) * XS;
+#pragma unroll 1
+      for (int kb = 0; kb < KCP; kb += 64) {
+        float av[16], bv[16];
+#pragma unroll
+        for (int ks = 0; ks < 16; ++ks) {
+          const int k = kb + 16 * g + ks;
+          av[ks] = arow[k];
+          bv[ks] = brow[k];
+        }
+#pragma unroll
+        for (int ks = 0; ks < 16; ++ks) acc = mma(av[ks], bv[ks], acc);
+      }
+      const int v = (r0 + tr * 16 + 4 * g) * 64 + tc * 16 + i16;
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq) stw1(rs, v + qq * 64, base, acc[qq]);
+    }
+  };
+
+  const int n = a.nsteps;
+  pstamp(a, 0, 0);
+  const bool v0 = st.valid(a, 0) > 0, v1 = n > 1 && st.valid(a, 1) > 0;
+  if (v0) load_x(0);
+  if (v1) load_x(1);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (v0) {
+    fwd(0);
+    publish(flag_at(a, r, PMF_PART) + q, 1u);
+  }
+  if (v1) {
+    fwd(1);
+    gram(1);
+    publish(flag_at(a, r, PMF_PART) + q, 2u);
+  }
+  pstamp(a, 0, 1);
+  for (int i = 0; i < n; ++i) {
+    if (st.valid(a, i) == 0) break;
+    pstamp(a, i, 2);
+    if (!wait_all(a, flag_at(a, r, PMF_BWD), a.nch, (unsigned)(i + 1), PERR_L0_BWD)) return;
+    pstamp(a, i, 3);
+    stage<NCT>(rs, (int)(a.o_dz0 + (i & 1) * a.dz0_par) + n0, H0, BR, CW, sdZ, WS);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    pstamp(a, i, 4);
+    // DW0 tile = X_i^T dZ_0 (reduction over the batch rows), SGD update in place
+    {
+      const float* Xi = sX + (i & 1) * 64 * XS;
+      f32x4 dw[TU0];
+#pragma unroll
+      for (int u = 0; u < TU0; ++u) dw[u] = zero4f();
+      // tile t = w + 4u: its column tile is w % NCT for every u (NCT divides 4)
+      const int ctw = w % NCT;
+#pragma unroll
+      for (int half = 0; half < 2; ++half) {
+        float xa[TU0][8], zb[8];
+#pragma unroll
+        for (int h8 = 0; h8 < 8; ++h8) {
+          const int b = 16 * g + 8 * half + h8;
+          zb[h8] = sdZ[b * WS + ctw * 16 + i16];
+#pragma unroll
+          for (int u = 0; u < TU0; ++u) xa[u][h8] = Xi[b * XS + rt[u] * 16 + i16];
+        }
+        // branch-free: tiles past ntiles compute garbage that is never stored
+#pragma unroll
+        for (int h8 = 0; h8 < 8; ++h8) {
+#pragma unroll
+          for (int u = 0; u < TU0; ++u) dw[u] = mma(xa[u][h8], zb[h8], dw[u]);
+        }
+      }
+      pstamp(a, i, 7);
+      if (has_b) {   // bias gradient: column sums of dZ_0, 32 columns per pass
+#pragma unroll
+        for (int hc = 0; hc < (CW + 31) / 32; ++hc) {
+          const float t = col_sums(sdZ + 32 * hc, WS, 32, sRedL);
+          if (tid < 32) sBg[hc * 32 + tid] = t;
+          __syncthreads();
+        }
+      }
+      pstamp(a, i, 8);
+      // the plain-SGD rule of pm_update<0>, in the same operation order
+      const long long it = iter_at(a.ctr, a.ntrain, a.B, r, st.s0, i);
+      const float lr = a.op.lr / (1.f + a.op.decay * (float)it), gs = a.op.grad_scale;
+#pragma unroll
+      for (int u = 0; u < TU0; ++u) {
+        if (w + 4 * u >= ntiles) continue;
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq) {
+          const int k = rt[u] * 16 + 4 * g + qq;
+          if (k < kreal) sW[k * WS + ct[u] * 16 + i16] -= lr * (dw[u][qq] * gs);
+        }
+      }
+      if (bown) {
+        bw -= lr * (sBg[tid] * gs);
+        sB0[tid] = bw;
+      }
+    }
+    __syncthreads();
+    pstamp(a, i, 5);
+    // step i + 2: its X chunk into the buffer X_i leaves, then Pold and the Gram slice
+    if (i + 2 < n && st.valid(a, i + 2) > 0) {
+      load_x(i + 2);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      fwd(i + 2);
+      gram(i + 2);
+      publish(flag_at(a, r, PMF_PART) + q, (unsigned)(i + 3));
+    }
+    pstamp(a, i, 6);
+  }
+
+  // ---- epilogue: master tile and both weight-image parities (plain SGD: no state)
+  __syncthreads();
+  float* Wsh = a.Wsh + (long long)r * a.sWsh + a.wsh_off[0];
+  float* WTsh = a.WTsh + (long long)r * a.sWTsh + a.wtsh_off[0];
+  for (int e = tid; e < kreal * CW; e += 256) {
+    const int k = e / CW, nn = e - k * CW;
+    const float v = sW[k * WS + nn];
+    P[a.p_off0 + (long long)(k0 + k) * H0 + n0 + nn] = v;
+#pragma unroll
+    for (int par = 0; par < 2; ++par) {
+      Wsh[par * a.wsh_par + (long long)(k0 + k) * a.Np[0] + n0 + nn] = v;
+      WTsh[par * a.wtsh_par + (long long)(n0 + nn) * a.Kp[0] + k0 + k] = v;
+    }
+  }
+  if (bown) P[a.p_off0 + (long long)a.K0 * H0 + n0 + tid] = bw;
+}
+
 // ============================================================== chain (rows)
 // acc[jj] (jj < 2: column tiles ct0 + 4jj) += A[16][K] . B[K][16 cols], fragments from
 // LDS: A(i, k) = A[i * SAI + k], B(k, n) = B[k * SBK + n * SBN]; the 16 fragments of a
@@ -616,7 +908,11 @@ __device__ __forceinline__ void rows_mm(const float* A, const float* B, int ct0,
   }
 }
 
-template <int H0, int H1, bool FAST, int NPT, bool RELU>
+// V2 (plain SGD + ReLU, fit granularity): the weight gradients leave this role (dw_role_v2
+// owns W1 / W2), the layer-0 pre-activations of step i >= 1 are rebuilt from the L0
+// workgroups' Pold / Gram slabs and the previous step's dZ_0 rows of every chain
+// workgroup (l0_role_v2), and two more flags (A0, D2) hand the rows the DW workgroups need.
+template <int H0, int H1, bool FAST, int NPT, bool RELU, bool V2>
 __device__ __forceinline__ void chain_role(const PersistArgs& a, float* smem, int r, int j) {
   using Lo = ChainLds<H0, H1>;
   constexpr int L0S = Lo::L0S, L1S = Lo::L1S;
@@ -682,6 +978,12 @@ __device__ __forceinline__ void chain_role(const PersistArgs& a, float* smem, in
   for (int u = 0; u < TU; ++u) {
     const int t = w + 4 * u;
     const int rt = t / nown, c = t - rt * nown;
+    if constexpr (V2) {   // the DW workgroups own the masters
+      wm[4 * u] = wm[4 * u + 1] = wm[4 * u + 2] = wm[4 * u + 3] = 0.f;
+      ws0[4 * u] = ws0[4 * u + 1] = ws0[4 * u + 2] = ws0[4 * u + 3] = 0.f;
+      ws1[4 * u] = ws1[4 * u + 1] = ws1[4 * u + 2] = ws1[4 * u + 3] = 0.f;
+      continue;
+    }
 #pragma unroll
     for (int qq = 0; qq < 4; ++qq) {
       const int k = rt * 16 + 4 * g + qq, nn = (j + a.nch * c) * 16 + i16;
@@ -692,7 +994,7 @@ __device__ __forceinline__ void chain_role(const PersistArgs& a, float* smem, in
       ws1[4 * u + qq] = (in && np > 1) ? S[a.op.s_plane + pi] : 0.f;
     }
   }
-  const bool w2own = w < nown;
+  const bool w2own = !V2 && w < nown;
 #pragma unroll
   for (int qq = 0; qq < 4; ++qq) {
     const int k = (j + a.nch * w) * 16 + 4 * g + qq;
@@ -705,9 +1007,9 @@ __device__ __forceinline__ void chain_role(const PersistArgs& a, float* smem, in
   // owned biases, where their gradients come out of the bias MFMAs (all-ones A rows):
   // b1 of the owned column tiles in wave 2 (lane -> unit (j + nch*(lane/16))*16 + lane%16),
   // b2 (chain workgroup 0) in wave 3, lanes < C -- the waves without a layer-2 tile
-  const bool b1own = a.bias1 && w == 2 && lane < 16 * nown;
+  const bool b1own = !V2 && a.bias1 && w == 2 && lane < 16 * nown;
   const int b1n = (j + a.nch * (lane >> 4)) * 16 + (lane & 15);
-  const bool b2own = a.bias2 && j == 0 && w == 3 && lane < C;
+  const bool b2own = !V2 && a.bias2 && j == 0 && w == 3 && lane < C;
   float bm = 0.f, bst0 = 0.f, bst1 = 0.f;
   if (b1own || b2own) {
     const long long pi = b1own ? a.p_off1 + (long long)H0 * H1 + b1n : a.p_off2 + (long long)H1 * C + lane;
@@ -716,6 +1018,9 @@ __device__ __forceinline__ void chain_role(const PersistArgs& a, float* smem, in
     bst1 = np > 1 ? S[a.op.s_plane + pi] : 0.f;
   }
   __syncthreads();
+  // every workgroup of the grid resident before any state (metric sums, hand-offs that
+  // lead to weight updates) is touched: otherwise give up with PERR_GRID, state intact
+  if (!wait_grid(a)) return;
 
   const int n = a.nsteps;
   for (int i = 0; i < n; ++i) {
@@ -739,8 +1044,8 @@ __device__ __forceinline__ void chain_role(const PersistArgs& a, float* smem, in
     pstamp(a, i, 0);
     // this step's partials and (after step 0) every chain workgroup's updated W1 / W2
     // columns of the previous step, watched by one wave
-    if (!wait_two(a, flag_at(a, r, PMF_PART), nl0, (unsigned)(i + 1), flag_at(a, r, PMF_W), i > 0 ? a.nch : 0,
-                  (unsigned)i, 2u))
+    if (!wait_two(a, flag_at(a, r, PMF_PART), nl0, (unsigned)(i + 1), flag_at(a, r, PMF_W),
+                  i > 0 ? (V2 ? a.nd : a.nch) : 0, (unsigned)i, PERR_CHAIN_PART))
       return;
     pstamp(a, i, 1);
     // the weight loads go first: their latency overlaps the partial sums below
@@ -760,7 +1065,7 @@ __device__ __forceinline__ void chain_role(const PersistArgs& a, float* smem, in
       const int m = m0 + rr;
       const bool cin = c0 < H0;
       const int v = rr * H0 + c0;
-      const int pbase = (int)a.o_part + m0 * H0;
+      const int pbase = (int)(a.o_part + (i & 1) * a.part_par) + m0 * H0;
       float z[8];
 #pragma unroll
       for (int e = 0; e < 8; ++e) z[e] = 0.f;
@@ -771,6 +1076,30 @@ __device__ __forceinline__ void chain_role(const PersistArgs& a, float* smem, in
         const int uc = u < a.nk0 ? u : a.nk0 - 1;
         pv[2 * u] = ldw4(rs, vv, pbase + uc * 64 * H0);
         pv[2 * u + 1] = ldw4(rs, vv + 4, pbase + uc * 64 * H0);
+      }
+      // V2, i >= 1: this chain's rows of the Gram slabs (requested before the wait for
+      // the previous step's dZ_0 rows of every chain, whose fragments follow)
+      f32x4 gl[RC_MAXSPLIT];
+      float bz[2][16];
+      const int grow = tid >> 4, gc4 = (tid & 15) * 4;
+      if constexpr (V2) {
+        if (i > 0) {
+#pragma unroll
+          for (int u = 0; u < RC_MAXSPLIT; ++u) {
+            const int uc = u < a.nk0 ? u : a.nk0 - 1;
+            gl[u] = ldw4(rs, grow * 64 + gc4, (int)(a.o_g + (i & 1) * a.g_par) + uc * 64 * 64 + m0 * 64);
+          }
+          pstamp(a, i, 11);
+          if (!wait_all(a, flag_at(a, r, PMF_BWD), a.nch, (unsigned)i, PERR_CHAIN_PREV)) return;
+          pstamp(a, i, 12);
+          const int zs = (int)(a.o_dz0 + ((i - 1) & 1) * a.dz0_par);
+#pragma unroll
+          for (int jj = 0; jj < 2; ++jj) {
+            const int ct = w + 4 * jj < nt0 ? w + 4 * jj : w;   // branch-free: unused past nt0
+#pragma unroll
+            for (int ks = 0; ks < 16; ++ks) bz[jj][ks] = ldw1(rs, (16 * g + ks) * H0 + ct * 16 + i16, zs);
+          }
+        }
       }
 #pragma unroll
       for (int u = 0; u < RC_MAXSPLIT; ++u) {
@@ -784,6 +1113,42 @@ __device__ __forceinline__ void chain_role(const PersistArgs& a, float* smem, in
       }
       pstamp(a, i, 13);
       pcycle(a, i, 28);
+      if constexpr (V2) {
+        if (i > 0) {
+          // Z_0 += -lr_{i-1} gs (G + 1) dZ0_{i-1}: the G rows (+ 1 for the bias) -> LDS,
+          // the product on the MFMAs, back through LDS in the row layout of z
+          float* sG = smem + Lo::o_gs;
+          f32x4 gsum = f32x4{1.f, 1.f, 1.f, 1.f};
+#pragma unroll
+          for (int u = 0; u < RC_MAXSPLIT; ++u)
+            if (u < a.nk0) gsum += gl[u];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) sG[grow * 65 + gc4 + e] = gsum[e];
+          __syncthreads();
+          const long long itp = iter_at(a.ctr, a.ntrain, a.B, r, st.s0, i - 1);
+          const float coef = -(a.op.lr / (1.f + a.op.decay * (float)itp)) * a.op.grad_scale;
+          float ag[16];
+#pragma unroll
+          for (int ks = 0; ks < 16; ++ks) ag[ks] = sG[i16 * 65 + 16 * g + ks];
+#pragma unroll
+          for (int jj = 0; jj < 2; ++jj) {
+            const int ct = w + 4 * jj;
+            f32x4 acc = zero4f();
+#pragma unroll
+            for (int ks = 0; ks < 16; ++ks) acc = mma(ag[ks], bz[jj][ks], acc);
+            if (ct < nt0) {
+#pragma unroll
+              for (int qq = 0; qq < 4; ++qq) sZ0[(4 * g + qq) * L0S + ct * 16 + i16] = coef * acc[qq];
+            }
+          }
+          __syncthreads();
+          if (cin) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) z[e] += sZ0[rr * L0S + c0 + e];
+          }
+          pstamp(a, i, 27);
+        }
+      }
       if (i > 0) {   // the previous step's weights -> LDS (read after the barrier below)
         stage_commit(w1s, H0, sW1, L1S);
         stage_commit(w2s, H1, sW2, S17);
@@ -858,7 +1223,8 @@ __device__ __forceinline__ void chain_role(const PersistArgs& a, float* smem, in
       }
       pstamp(a, i, 17);
     }
-    __syncthreads();
+    if constexpr (V2) publish(flag_at(a, r, PMF_A0) + j, (unsigned)(i + 1));   // the A_0 rows (phase 0) are out
+    else __syncthreads();
     pstamp(a, i, 3);
     publish_rows16<H1>(rs, (int)a.o_a1 + m0 * H1, sA1, L1S);   // weight-gradient operand
     // ---- FWD2: logits, the reduction split over the 4 waves (H1 / 16 k-steps each)
@@ -957,8 +1323,12 @@ __device__ __forceinline__ void chain_role(const PersistArgs& a, float* smem, in
       }
       pstamp(a, i, 21);
     }
-    __syncthreads();
-    publish_rows16<H1>(rs, (int)a.o_dz1 + m0 * H1, sD1, L1S);
+    if constexpr (V2) {
+      publish(flag_at(a, r, PMF_D2) + j, (unsigned)(i + 1));   // A_1 and dZ_2 rows are out
+    } else {
+      __syncthreads();
+      publish_rows16<H1>(rs, (int)a.o_dz1 + m0 * H1, sD1, L1S);
+    }
     pstamp(a, i, 22);
     // ---- DX1: dZ_0 = (dZ_1 . W1^T) * G_0 -> LDS, then published for the L0 tiles
     {
@@ -978,10 +1348,11 @@ __device__ __forceinline__ void chain_role(const PersistArgs& a, float* smem, in
       }
     }
     __syncthreads();
-    publish_rows16<H0>(rs, (int)a.o_dz0 + m0 * H0, sZ0, L0S);
+    publish_rows16<H0>(rs, (int)(a.o_dz0 + (i & 1) * a.dz0_par) + m0 * H0, sZ0, L0S);
     pstamp(a, i, 5);
     publish(flag_at(a, r, PMF_BWD) + j, (unsigned)(i + 1));
     pstamp(a, i, 6);
+    if constexpr (V2) continue;   // weight gradients: dw_role_v2
 
     // ---- weight gradients of the owned layer-1 columns / layer-2 rows, update
     if (!wait_all(a, flag_at(a, r, PMF_BWD), a.nch, (unsigned)(i + 1), 3u)) return;
@@ -1086,6 +1457,7 @@ __device__ __forceinline__ void chain_role(const PersistArgs& a, float* smem, in
   }
 
   // ---- epilogue: owned masters, both weight-image parities, state
+  if constexpr (V2) return;
   float* Wsh = a.Wsh + (long long)r * a.sWsh;
   float* WTsh = a.WTsh + (long long)r * a.sWTsh;
 #pragma unroll
@@ -1130,17 +1502,249 @@ __device__ __forceinline__ void chain_role(const PersistArgs& a, float* smem, in
   }
 }
 
+// ============================================================== V2: weight gradients
+// nd workgroups per replica; workgroup d owns the layer-1 column tiles d + nd*c (c <
+// nown) = the layer-2 row tiles of the same index, their biases, and b2 (d == 0): the
+// chain's DW block of V1 on a workgroup of its own.  Per step it stages A_0 of every
+// row once the chains raise A0, then (D2) the A_1 columns and dZ_2 it needs, rebuilds
+// its dZ_1 columns = (dZ_2 . W2_own^T) * relu'(.) * keep / (1 - rate) -- the factor
+// recovered from A_1 > 0 (ReLU, so the same MFMA as the chain's DX2 gives the same bits)
+// -- computes DW1 / DW2 / the bias sums, applies plain SGD and publishes the columns.
+template <int H0, int H1>
+__device__ __forceinline__ void dw_role_v2(const PersistArgs& a, float* smem, int r, int d) {
+  constexpr int L0S = H0 + 1;
+  constexpr int nt0 = H0 / 16, nt1 = H1 / 16;
+  const int tid = threadIdx.x, lane = tid & 63, i16 = lane & 15, g = lane >> 4;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6) & 3;
+  const int C = a.C;
+  const int BR = a.nch * 16;
+  const int nd = a.nd;
+  float* uA0 = smem;                 // [64][L0S] layer-0 activations of every row
+  float* uD1 = uA0 + 64 * L0S;       // [64][33] dZ_1 of the owned layer-1 columns
+  float* uA1 = uD1 + 64 * 33;        // [64][33] layer-1 activations of the owned W2 rows
+  float* uD2 = uA1 + 64 * 33;        // [64][17] dZ_2
+  float* sW2o = uD2 + 64 * S17;      // [32][17] the owned W2 rows (operand of the dZ_1 rebuild)
+  const rsrc_t rs = ws_rsrc(a.ws + (long long)r * a.ws_stride);
+  float* P = a.P + (long long)r * a.sP;
+  Steps st{ld_inv(a.ctr), ld_inv(a.ntrain + r)};
+
+  const int nown = (nt1 - d + nd - 1) / nd;   // <= PM_NTU (host checks)
+  const int ndw1 = nt0 * nown;
+  int urt[TU], uct[TU];
+#pragma unroll
+  for (int u = 0; u < TU; ++u) {
+    const int t = w + 4 * u;
+    urt[u] = t < ndw1 ? t / nown : 0;
+    uct[u] = t < ndw1 ? t - (t / nown) * nown : 0;
+  }
+  for (int e = tid; e < DW_LDS; e += 256) smem[e] = 0.f;
+  __syncthreads();
+  constexpr int NM = TU * 4 + 4;
+  float wm[NM];
+#pragma unroll
+  for (int u = 0; u < TU; ++u) {
+    const int t = w + 4 * u;
+    const int rt = t / nown, c = t - rt * nown;
+#pragma unroll
+    for (int qq = 0; qq < 4; ++qq) {
+      const int k = rt * 16 + 4 * g + qq, nn = (d + nd * c) * 16 + i16;
+      wm[4 * u + qq] = t < ndw1 ? P[a.p_off1 + (long long)k * H1 + nn] : 0.f;
+    }
+  }
+  const bool w2own = w < nown;
+#pragma unroll
+  for (int qq = 0; qq < 4; ++qq) {
+    const int k = (d + nd * w) * 16 + 4 * g + qq;
+    const bool in = w2own && i16 < C;
+    wm[4 * TU + qq] = in ? P[a.p_off2 + (long long)k * C + i16] : 0.f;
+    if (w2own) sW2o[(w * 16 + 4 * g + qq) * S17 + i16] = wm[4 * TU + qq];
+  }
+  const bool b1own = a.bias1 && w == 2 && lane < 16 * nown;
+  const int b1n = (d + nd * (lane >> 4)) * 16 + (lane & 15);
+  const bool b2own = a.bias2 && d == 0 && w == 3 && lane < C;
+  float bm = 0.f;
+  if (b1own || b2own) bm = P[b1own ? a.p_off1 + (long long)H0 * H1 + b1n : a.p_off2 + (long long)H1 * C + lane];
+  const float ks1 = a.rate1 > 0.f ? 1.f / (1.f - a.rate1) : 1.f;
+  __syncthreads();
+
+  const int n = a.nsteps;
+  for (int i = 0; i < n; ++i) {
+    if (st.valid(a, i) == 0) break;
+    const long long it = iter_at(a.ctr, a.ntrain, a.B, r, st.s0, i);
+    pstamp(a, i, 0);
+    if (!wait_all(a, flag_at(a, r, PMF_A0), a.nch, (unsigned)(i + 1), PERR_DW_A0)) return;
+    pstamp(a, i, 1);
+    stage<H0 / 16>(rs, (int)a.o_a0, H0, BR, H0, uA0, L0S);
+    if (!wait_all(a, flag_at(a, r, PMF_D2), a.nch, (unsigned)(i + 1), PERR_DW_D2)) return;
+    pstamp(a, i, 2);
+#pragma unroll
+    for (int c = 0; c < PM_NTU; ++c) {
+      if (c < nown) stage<1>(rs, (int)a.o_a1 + (d + nd * c) * 16, H1, BR, 16, uA1 + c * 16, 33);
+    }
+    stage<1>(rs, (int)a.o_dz2, 16, BR, 16, uD2, S17);
+    // rows BR..63 of the staging must be zero for the 64-deep reductions
+    for (int e = tid; e < (64 - BR) * L0S; e += 256) uA0[BR * L0S + e] = 0.f;
+    for (int e = tid; e < (64 - BR) * 33; e += 256) uA1[BR * 33 + e] = 0.f;
+    for (int e = tid; e < (64 - BR) * S17; e += 256) uD2[BR * S17 + e] = 0.f;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    pstamp(a, i, 3);
+    // dZ_1 of the owned columns, 16 rows per wave: the chain's DX2 MFMA on the same
+    // operands, times relu'(z) * keep / (1 - rate) = (A_1 > 0 ? 1 / (1 - rate) : 0)
+#pragma unroll
+    for (int c = 0; c < PM_NTU; ++c) {
+      if (c >= nown) continue;
+      float av[4], bv[4];
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {
+        const int cc = 4 * kk + g;
+        av[kk] = uD2[(w * 16 + i16) * S17 + cc];
+        bv[kk] = sW2o[(c * 16 + i16) * S17 + cc];
+      }
+      f32x4 acc = zero4f();
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) acc = mma(av[kk], bv[kk], acc);
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq) {
+        const int row = w * 16 + 4 * g + qq;
+        const float a1 = uA1[row * 33 + c * 16 + i16];
+        uD1[row * 33 + c * 16 + i16] = acc[qq] * (a1 > 0.f ? ks1 : 0.f);
+      }
+    }
+    __syncthreads();
+    pstamp(a, i, 4);
+    {
+      f32x4 dw[TU + 1], db[2] = {zero4f(), zero4f()};
+#pragma unroll
+      for (int u = 0; u <= TU; ++u) dw[u] = zero4f();
+#pragma unroll
+      for (int half = 0; half < 2; ++half) {
+        float xa[TU][8], zb[2][8], a1v[8], d2v[8];
+#pragma unroll
+        for (int h8 = 0; h8 < 8; ++h8) {
+          const int b = 16 * g + 8 * half + h8;
+          zb[0][h8] = uD1[b * 33 + i16];
+          zb[1][h8] = uD1[b * 33 + 16 + i16];
+#pragma unroll
+          for (int u = 0; u < TU; ++u) xa[u][h8] = uA0[b * L0S + urt[u] * 16 + i16];
+          a1v[h8] = uA1[b * 33 + (w2own ? w : 0) * 16 + i16];
+          d2v[h8] = uD2[b * S17 + i16];
+        }
+#pragma unroll
+        for (int h8 = 0; h8 < 8; ++h8) {
+#pragma unroll
+          for (int u = 0; u < TU; ++u) dw[u] = mma(xa[u][h8], uct[u] ? zb[1][h8] : zb[0][h8], dw[u]);
+          dw[TU] = mma(a1v[h8], d2v[h8], dw[TU]);
+        }
+        if (w >= 2) {
+#pragma unroll
+          for (int h8 = 0; h8 < 8; ++h8) {
+            db[0] = mma(1.f, w == 2 ? zb[0][h8] : d2v[h8], db[0]);
+            db[1] = mma(1.f, zb[1][h8], db[1]);
+          }
+        }
+      }
+      pstamp(a, i, 5);
+      // plain SGD in the operation order of pm_update<0>
+      const float lr = a.op.lr / (1.f + a.op.decay * (float)it), gs = a.op.grad_scale;
+#pragma unroll
+      for (int u = 0; u <= TU; ++u)
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq)
+          if (u < TU || i16 < C) wm[4 * u + qq] -= lr * (dw[u][qq] * gs);
+      const float gb = (b1own && lane >= 16) ? db[1][0] : db[0][0];
+      if (b1own || b2own) bm -= lr * (gb * gs);
+    }
+    // ---- publish the owned columns (the chains read them at the next step's start)
+    const bool nxt = i + 1 < n && st.valid(a, i + 1) > 0;
+    if (w2own) {
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq) sW2o[(w * 16 + 4 * g + qq) * S17 + i16] = wm[4 * TU + qq];
+    }
+    if (nxt) {
+#pragma unroll
+      for (int u = 0; u < TU; ++u) {
+        const int t = w + 4 * u;
+        if (t >= ndw1) continue;
+        const int rt = t / nown, c = t - rt * nown;
+        const int v = (rt * 16 + 4 * g) * H1 + i16;
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq) stw1(rs, v + qq * H1, (int)a.o_w1 + (d + nd * c) * 16, wm[4 * u + qq]);
+      }
+      if (w2own && i16 < C) {
+        const int v = (4 * g) * 16 + i16;
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq) stw1(rs, v + qq * 16, (int)a.o_w2 + (d + nd * w) * 256, wm[4 * TU + qq]);
+      }
+      if (b1own) stw1(rs, b1n, (int)a.o_b1, bm);
+      if (b2own) stw1(rs, lane, (int)a.o_b2, bm);
+      publish(flag_at(a, r, PMF_W) + d, (unsigned)(i + 1));
+    } else {
+      __syncthreads();
+    }
+    pstamp(a, i, 6);
+  }
+
+  // ---- epilogue: owned masters and both weight-image parities (plain SGD: no state)
+  float* Wsh = a.Wsh + (long long)r * a.sWsh;
+  float* WTsh = a.WTsh + (long long)r * a.sWTsh;
+#pragma unroll
+  for (int u = 0; u < TU; ++u) {
+    const int t = w + 4 * u;
+    if (t >= ndw1) continue;
+    const int rt = t / nown, c = t - rt * nown;
+#pragma unroll
+    for (int qq = 0; qq < 4; ++qq) {
+      const int k = rt * 16 + 4 * g + qq, nn = (d + nd * c) * 16 + i16;
+      P[a.p_off1 + (long long)k * H1 + nn] = wm[4 * u + qq];
+#pragma unroll
+      for (int par = 0; par < 2; ++par) {
+        Wsh[par * a.wsh_par + a.wsh_off[1] + (long long)k * a.Np[1] + nn] = wm[4 * u + qq];
+        WTsh[par * a.wtsh_par + a.wtsh_off[1] + (long long)nn * a.Kp[1] + k] = wm[4 * u + qq];
+      }
+    }
+  }
+  if (w2own && i16 < C) {
+#pragma unroll
+    for (int qq = 0; qq < 4; ++qq) {
+      const int k = (d + nd * w) * 16 + 4 * g + qq;
+      P[a.p_off2 + (long long)k * C + i16] = wm[4 * TU + qq];
+#pragma unroll
+      for (int par = 0; par < 2; ++par) {
+        Wsh[par * a.wsh_par + a.wsh_off[2] + (long long)k * a.Np[2] + i16] = wm[4 * TU + qq];
+        WTsh[par * a.wtsh_par + a.wtsh_off[2] + (long long)i16 * a.Kp[2] + k] = wm[4 * TU + qq];
+      }
+    }
+  }
+  if (b1own || b2own) P[b1own ? a.p_off1 + (long long)H0 * H1 + b1n : a.p_off2 + (long long)H1 * C + lane] = bm;
+}
+
 }  // namespace
 
-template <int H0, int H1, bool FAST, int NPT, bool RELU>
+template <int H0, int H1, bool FAST, int NPT, bool RELU, bool V2>
 __global__ __launch_bounds__(256) void mlp_persist_kernel(PersistArgs a) {
   __shared__ __attribute__((aligned(16))) float smem[LDS_FLOATS];
   if (__hip_atomic_load((gu32*)(a.err), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) return;
   const int b = blockIdx.x;
   const int r = b % a.R, q = b / a.R;
+  // residency: raise this workgroup's GO flag (the chain workgroups wait for the grid)
+  if (threadIdx.x == 0) __hip_atomic_store((gu32*)(flag_at(a, r, PMF_GO) + q), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const int nl0 = a.nk0 * a.nc0;
-  if (q < nl0) l0_role<H0, NPT>(a, smem, r, q / a.nc0, q - (q / a.nc0) * a.nc0, q);
-  else chain_role<H0, H1, FAST, NPT, RELU>(a, smem, r, q - nl0);
+  if constexpr (V2) {
+    static_assert(NPT == 0 && RELU, "V2: plain SGD, ReLU hidden layers");
+    if (q < nl0) {
+      const int kc = q / a.nc0, cb = q - kc * a.nc0;
+      if (a.cw == 64) l0_role_v2<H0, 4>(a, smem, r, kc, cb, q);
+      else l0_role_v2<H0, 2>(a, smem, r, kc, cb, q);
+    } else if (q < nl0 + a.nch) {
+      chain_role<H0, H1, FAST, NPT, RELU, true>(a, smem, r, q - nl0);
+    } else {
+      dw_role_v2<H0, H1>(a, smem, r, q - nl0 - a.nch);
+    }
+  } else {
+    if (q < nl0) l0_role<H0, NPT>(a, smem, r, q / a.nc0, q - (q / a.nc0) * a.nc0, q);
+    else chain_role<H0, H1, FAST, NPT, RELU, false>(a, smem, r, q - nl0);
+  }
 }
 
 // the instances of one hidden width: the specialised MNIST-style one (relu, softmax +
@@ -1154,9 +1758,16 @@ hipError_t persist_launch(const PersistArgs* a, hipStream_t s) {
   const bool relu = a->act0 == ACT_RELU && a->act1 == ACT_RELU;
   const bool sgd = !a->S || (a->op.opt == OPT_SGD && a->op.mom == 0.f);
   const dim3 grid(a->R * a->wgs);
-  if (fast && relu && sgd) hipLaunchKernelGGL((mlp_persist_kernel<H, H, true, 0, true>), grid, dim3(256), 0, s, *a);
-  else if (fast) hipLaunchKernelGGL((mlp_persist_kernel<H, H, true, -1, false>), grid, dim3(256), 0, s, *a);
-  else hipLaunchKernelGGL((mlp_persist_kernel<H, H, false, -1, false>), grid, dim3(256), 0, s, *a);
+  if (a->v2) {   // the host checked plain SGD + ReLU
+    if (fast) hipLaunchKernelGGL((mlp_persist_kernel<H, H, true, 0, true, true>), grid, dim3(256), 0, s, *a);
+    else hipLaunchKernelGGL((mlp_persist_kernel<H, H, false, 0, true, true>), grid, dim3(256), 0, s, *a);
+  } else if (fast && relu && sgd) {
+    hipLaunchKernelGGL((mlp_persist_kernel<H, H, true, 0, true, false>), grid, dim3(256), 0, s, *a);
+  } else if (fast) {
+    hipLaunchKernelGGL((mlp_persist_kernel<H, H, true, -1, false, false>), grid, dim3(256), 0, s, *a);
+  } else {
+    hipLaunchKernelGGL((mlp_persist_kernel<H, H, false, -1, false, false>), grid, dim3(256), 0, s, *a);
+  }
   return hipGetLastError();
 }
 

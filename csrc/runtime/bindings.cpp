@@ -80,6 +80,7 @@ static ExecCfg parse_cfg(const py::dict& d) {
   c.persist = get<int>(d, "persist", -1);
   c.persist_timeout_ms = get<long long>(d, "persist_timeout_ms", 2000);
   c.persist_cus = get<int>(d, "persist_cus", 0);
+  c.persist_v2 = get<int>(d, "persist_v2", -1);
   for (auto item : d["layers"].cast<py::list>()) {
     py::dict l = item.cast<py::dict>();
     LayerCfg lc;
@@ -190,6 +191,7 @@ PYBIND11_MODULE(_C, m) {
       .def("tailchain", &Executor::tailchain)
       .def("persistent", &Executor::persistent)
       .def("persist_geometry", &Executor::persist_geometry)
+      .def("persist_variant", &Executor::persist_variant)
       .def("persist_error", &Executor::persist_error)
       .def("persist_clear_error", &Executor::persist_clear_error)
       .def("set_stamps", &Executor::set_stamps)

@@ -17,7 +17,7 @@ extern "C" hipError_t ea_apply_update(ea::FlatArgs* a, int bf16, hipStream_t s);
 extern "C" hipError_t ea_refresh_shadows(ea::FlatArgs* a, int bf16, hipStream_t s);
 extern "C" hipError_t ea_advance(long long* ctr, const int* ntrain, int R, int B, int n, hipStream_t s);
 extern "C" hipError_t ea_persist_post(unsigned* flags, int nflags, long long* ctr, const int* ntrain, int R, int B, int n,
-                                      hipStream_t s);
+                                      const unsigned* err, hipStream_t s);
 extern "C" hipError_t ea_persist(const ea::PersistArgs* a, hipStream_t s);
 extern "C" int ea_persist_lds_bytes();
 
@@ -71,22 +71,40 @@ bool Executor::build_persist() {
   check(hipGetDevice(&dev), "hipGetDevice");
   check(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev), "hipDeviceGetAttribute");
   if (const char* e = std::getenv("ELEPHAS_AMD_PERSIST_CUS")) ncu = std::min(ncu, std::atoi(e));  // tests: a smaller grid
+  // tests only: pretend the GPU has more CUs than it does, so the grid cannot be resident
+  // (the kernel's GO-flag wait must fail cleanly and the host fall back)
+  if (const char* e = std::getenv("ELEPHAS_AMD_PERSIST_OVERSUBSCRIBE")) ncu = std::max(ncu, std::atoi(e));
   if (c_.persist_cus > 0) ncu = std::min(ncu, c_.persist_cus);  // a share of the GPU (concurrent executors)
   int lds_max = 0;
   check(hipDeviceGetAttribute(&lds_max, hipDeviceAttributeMaxSharedMemoryPerBlock, dev), "hipDeviceGetAttribute");
   if (ea_persist_lds_bytes() > lds_max) return false;
   const int cap = std::min(ncu / c_.R - nch, PM_MAXWG);
   if (cap < 1) return false;
-  // layer-0 tiles: the cheapest (kc0, cw) whose tile count fits; cost ~ the tile's
-  // MFMA work (FWD reduction padded to 64) + the partials every chain workgroup sums
+  // V2 (persist.hip l0_role_v2 / dw_role_v2): plain SGD, ReLU hidden layers, independent
+  // replicas -- the step's critical path runs through the chain workgroups only
+  const bool v2 = c_.persist_v2 != 0 && c_.op.opt == OPT_SGD && c_.op.mom == 0.f && l0.act == ACT_RELU &&
+                  l1.act == ACT_RELU;
+  const int nd = v2 ? cdiv(l1.N / 16, PM_NTU) : 0;
+  // layer-0 tiles: the cheapest (kc0, cw) whose tile count fits.  V1: cost ~ the tile's
+  // MFMA work (FWD reduction padded to 64) + the partials every chain workgroup sums.
+  // V2: the L0 work is off the critical path; the chain's slab loads (nk0 Pold + Gram
+  // slabs) are not -- fewest k-chunks first, then the smaller tile
   int best_kc = 0, best_cw = 0;
   long long best_cost = -1;
-  for (int cw : {16, 32}) {
+  for (int cw : {16, 32, 64}) {
     if (l0.N % cw) continue;
     const int nc0 = l0.N / cw;
+    if (v2 ? (cw == 16 || nc0 > 4) : cw == 64) continue;
     for (int kc = 16; kc <= PM_MAXH; kc += 16) {
       const int nk0 = cdiv(l0.K, kc);
-      if (nk0 * nc0 > cap || (kc / 16) * (cw / 16) > 16 || nk0 > RC_MAXSPLIT) continue;
+      if (nk0 > RC_MAXSPLIT) continue;
+      if (v2) {
+        if (nk0 * nc0 + nd > cap) continue;
+        const long long cost = 100000LL * nk0 + (long long)kc * cw;
+        if (best_cost < 0 || cost < best_cost) { best_cost = cost; best_kc = kc; best_cw = cw; }
+        continue;
+      }
+      if (nk0 * nc0 > cap || (kc / 16) * (cw / 16) > 16) continue;
       const long long cost = (long long)(cdiv(std::min(kc, l0.K), 64) * 64 + kc) * cw + 512LL * nk0;
       if (best_cost < 0 || cost < best_cost) { best_cost = cost; best_kc = kc; best_cw = cw; }
     }
@@ -97,7 +115,8 @@ bool Executor::build_persist() {
   a.R = c_.R; a.B = c_.B;
   a.K0 = l0.K; a.H0 = l0.N; a.H1 = l1.N; a.C = l2.N;
   a.kc0 = best_kc; a.cw = best_cw; a.nc0 = l0.N / best_cw; a.nk0 = cdiv(l0.K, best_kc);
-  a.nch = nch; a.wgs = a.nk0 * a.nc0 + nch;
+  a.nch = nch; a.v2 = v2 ? 1 : 0; a.nd = nd;
+  a.wgs = a.nk0 * a.nc0 + nch + nd;
   a.act0 = l0.act; a.act1 = l1.act; a.act2 = l2.act;
   a.rate0 = l0.rate; a.rate1 = l1.rate;
   a.bias0 = l0.has_bias; a.bias1 = l1.has_bias; a.bias2 = l2.has_bias;
@@ -123,8 +142,14 @@ bool Executor::build_persist() {
   // exchange workspace per replica (floats; every region 64-float aligned)
   long long off = 0;
   auto take = [&](long long n) { const long long o = off; off += (n + 63) / 64 * 64; return o; };
-  a.o_part = take((long long)a.nk0 * PM_ROWS * a.H0);
-  a.o_dz0 = take((long long)PM_ROWS * a.H0);
+  // V2 double-buffers the partials, the Gram slabs and dZ_0 by step parity
+  const int npar = v2 ? 2 : 1;
+  a.part_par = v2 ? (long long)a.nk0 * PM_ROWS * a.H0 : 0;
+  a.o_part = take(npar * (long long)a.nk0 * PM_ROWS * a.H0);
+  a.g_par = v2 ? (long long)a.nk0 * PM_ROWS * PM_ROWS : 0;
+  a.o_g = v2 ? take(npar * (long long)a.nk0 * PM_ROWS * PM_ROWS) : 0;
+  a.dz0_par = v2 ? (long long)PM_ROWS * a.H0 : 0;
+  a.o_dz0 = take(npar * (long long)PM_ROWS * a.H0);
   a.o_a0 = take((long long)PM_ROWS * a.H0);
   a.o_a1 = take((long long)PM_ROWS * a.H1);
   a.o_dz1 = take((long long)PM_ROWS * a.H1);
@@ -158,6 +183,11 @@ std::vector<int> Executor::persist_geometry() const {
   return {a.nk0, a.nc0, a.kc0, a.cw, a.nch, a.wgs, a.R * a.wgs};
 }
 
+std::vector<int> Executor::persist_variant() const {
+  if (!pm_.on) return {};
+  return {pm_.args.v2 ? 2 : 1, pm_.args.nd};
+}
+
 unsigned Executor::persist_error() const {
   if (!d_perr_) return 0;
   unsigned v = 0;
@@ -183,7 +213,7 @@ void Executor::run_chunk(hipStream_t s, int nsteps) const {
     a.nsteps = nsteps;
     check(ea_persist(&a, s), "persistent step kernel");
     check(ea_persist_post(d_pflags_, (int)(pm_.flag_bytes / sizeof(unsigned)), reinterpret_cast<long long*>(c_.ctr),
-                          reinterpret_cast<const int*>(c_.ntrain), c_.R, c_.B, nsteps, s),
+                          reinterpret_cast<const int*>(c_.ntrain), c_.R, c_.B, nsteps, d_perr_, s),
           "persistent chunk post");
     return;
   }

@@ -16,7 +16,7 @@
 //                   the last layer's backward launch of the grouped plan disappear
 //   persistent plan (3-layer MLPs with 64/128-wide hidden layers, fp32;
 //                   csrc/kernels/persist.hip): a whole chunk of steps in ONE launch
-//                   (+ a flag memset node and the counter advance)
+//                   (+ a 1-block post kernel: flag clear and counter advance)
 //
 // The step reads its batch index, dropout counter and optimizer iteration from
 // device counters, so one captured hipGraph of a step is replayed for every
@@ -75,6 +75,7 @@ struct ExecCfg {
   int persist = -1;    // persistent chunk kernel (persist.hip): -1 when eligible, 0 off, 1 required
   long long persist_timeout_ms = 2000;  // spin limit of its in-launch waits
   int persist_cus = 0;  // > 0: CUs the persistent grid may occupy (several executors side by side)
+  int persist_v2 = -1;  // persistent V2 roles when eligible (plain SGD, ReLU, independent replicas); 0 off
   int no_reorder = 0;   // A/B: keep a DW + DX launch's problems in declaration order
   int dual = 1;         // a layer's DW and DX on different tiles in one launch (0: two launches)
 };
@@ -125,6 +126,7 @@ class Executor {
   // persistent plan: {L0 k-chunks, L0 column blocks, k-chunk rows, block columns, chain
   // workgroups, workgroups per replica, grid}
   std::vector<int> persist_geometry() const;
+  std::vector<int> persist_variant() const;   // {1 or 2, DW workgroups per replica}
   unsigned persist_error() const;  // sticky error word (a timed-out in-launch wait), synchronous read
   void persist_clear_error();
   int rowchain_split() const { return rc_.on ? rc_.nsplitk : 0; }
@@ -180,7 +182,7 @@ class Executor {
     size_t flag_bytes = 0;
   } pm_;
   float* d_pws_ = nullptr;         // persistent plan: per-replica exchange workspace
-  unsigned* d_pflags_ = nullptr;   // [R][PMF_N][PM_MAXWG] flags (zeroed before every launch)
+  unsigned* d_pflags_ = nullptr;   // [R][PMF_N][PM_MAXWG] flags (zero at every launch: setup, then the post kernel)
   unsigned* d_perr_ = nullptr;     // sticky error word
   bool build_persist();
   void run_chunk(hipStream_t s, int nsteps) const;   // nsteps training steps (no counter advance)

@@ -146,7 +146,10 @@ class LabeledPoint:
     __slots__ = ("label", "features")
 
     def __init__(self, label, features):
-        self.label = float(np.asarray(label, dtype=np.float64).reshape(-1)[0])
+        lab = np.asarray(label, dtype=np.float64)
+        if lab.size != 1:   # pyspark: float(label) -- a multi-element label is an error
+            raise TypeError(f"LabeledPoint label must be a scalar, got shape {lab.shape}")
+        self.label = float(lab.reshape(-1)[0])
         self.features = features if isinstance(features, Vector) else DenseVector(features)
 
     def __repr__(self):

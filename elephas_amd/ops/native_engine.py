@@ -20,8 +20,10 @@ batch index, dropout counter and optimizer iteration are read from device counte
 """
 from __future__ import annotations
 
+import logging
 import math
 import os
+import threading
 from typing import Dict, List, Optional
 
 import numpy as np
@@ -33,15 +35,20 @@ from . import native
 from .plan import flatten_weights
 from .trainer import TrainerBase, prepare_features, prepare_targets, split_point
 
+_log = logging.getLogger("elephas_amd.native")
 
-def _gpu_shared() -> bool:
-    """More local ranks than visible GPUs (the single-GPU multi-rank rehearsals): ranks
-    share a device, so a persistent grid cannot count on owning every CU."""
-    try:
-        local = int(os.environ.get("LOCAL_WORLD_SIZE", "1"))
-        return local > max(1, torch.cuda.device_count())
-    except ValueError:
-        return False
+
+def _shared_cu_share(dev: torch.device) -> int:
+    """CUs a persistent grid of this rank may assume when ranks of the job share its
+    GPU (single-GPU multi-rank rehearsals; detected from device UUIDs at init,
+    parallel/dist.py): an equal share, so the sharers' grids are co-resident.
+    0 = the GPU is this process's alone."""
+    from ..parallel import dist
+    n = dist.device_sharers()
+    if n <= 1:
+        return 0
+    ncu = torch.cuda.get_device_properties(dev).multi_processor_count
+    return max(1, ncu // n)
 
 
 # The persistent chunk kernel needs every workgroup of its grid resident at once (they
@@ -50,6 +57,35 @@ def _gpu_shared() -> bool:
 # all trainers of a device are therefore serialised: each waits for the device's most
 # recent one (an event) unless that one was issued on its own stream.
 _PERSIST_LAST: Dict[int, tuple] = {}
+# fence -> launch(es) -> mark is one critical section per device: threaded workers (one
+# native trainer per thread) must not interleave it, or two grids could be in flight at once
+_PERSIST_LOCKS: Dict[int, threading.Lock] = {}
+_PERSIST_LOCKS_GUARD = threading.Lock()
+
+
+def _persist_lock(dev_index: int) -> threading.Lock:
+    with _PERSIST_LOCKS_GUARD:
+        lk = _PERSIST_LOCKS.get(dev_index)
+        if lk is None:
+            lk = _PERSIST_LOCKS[dev_index] = threading.Lock()
+        return lk
+
+
+class PersistentPlanError(RuntimeError):
+    """A persistent launch gave up waiting inside the kernel (its sticky error word).
+    The trainer has already cleared the word and re-planned onto the row-chain plan,
+    so later calls run; ``clean`` is True when the launch modified nothing (the grid was
+    not resident: PERR_GRID), False when a wait timed out mid-chunk (weights may be
+    partially updated -- ``fit`` restores its entry snapshot and re-runs either way)."""
+
+    def __init__(self, code: int):
+        self.code = int(code)
+        self.clean = self.code == 9
+        super().__init__(
+            f"persistent step kernel: an in-launch wait timed out (code {self.code}; "
+            + ("the grid was not resident, nothing was modified" if self.clean else
+               "mid-chunk: weights may be partially updated")
+            + "); the trainer now runs the row-chain plan")
 
 
 def pad8(n: int) -> int:
@@ -75,21 +111,24 @@ class NativeTrainer(TrainerBase):
         self.rowchain_mode = int(os.environ.get("ELEPHAS_AMD_ROWCHAIN", "-1")) if rowchain is None else int(rowchain)
         # persistent chunk kernel (csrc/kernels/persist.hip): None -> $ELEPHAS_AMD_PERSIST
         # (default -1: whenever eligible), 0 off, 1 required.  It keeps a whole cluster of
-        # workgroups per replica resident and waiting on each other, so two processes
-        # sharing one GPU must turn it off (their grids could not both be resident)
+        # workgroups per replica resident and waiting on each other
         self.persist_mode = int(os.environ.get("ELEPHAS_AMD_PERSIST", "-1")) if persist is None else int(persist)
-        if persist is None and self.persist_mode < 0 and _gpu_shared():
-            self.persist_mode = 0
         # persist_cus: the persistent grid is sized to this share of the GPU's CUs, so
         # several trainers whose shares sum to at most the CU count run their persistent
-        # kernels side by side (async worker groups); without it a trainer assumes the
-        # whole GPU and its persistent launches are serialised with every other trainer's
+        # kernels side by side (async worker groups, ranks sharing one GPU); without it a
+        # trainer assumes the whole GPU and its persistent launches are serialised with
+        # every other trainer's of the process
         self.persist_cus = int(persist_cus) if persist_cus else 0
         if not plan.native_ok:
             raise ValueError(f"model is not supported by the native engine: {plan.reason}")
         self.dev = torch.device(device) if device is not None else config.get_device()
         if self.dev.type != "cuda":
             raise ValueError("NativeTrainer needs a GPU device")
+        if not self.persist_cus:
+            share = _shared_cu_share(self.dev)
+            if share:
+                self.persist_cus = share
+                _log.info("ranks share this GPU: persistent grids sized to %d CUs each", share)
         policy = policy or config.get_policy()
         self.bf16 = policy == "mixed_bfloat16"
         self.T = torch.bfloat16 if self.bf16 else torch.float32
@@ -196,6 +235,7 @@ class NativeTrainer(TrainerBase):
             persist=self.persist_mode if ws is self.ws else 0,
             persist_timeout_ms=int(os.environ.get("ELEPHAS_AMD_PERSIST_TIMEOUT_MS", "2000")),
             persist_cus=self.persist_cus,
+            persist_v2=int(os.environ.get("ELEPHAS_AMD_PERSIST_V2", "-1")),
             rc_split=int(os.environ.get("ELEPHAS_AMD_RC_SPLIT", "0")),
             tail=int(os.environ.get("ELEPHAS_AMD_TAIL", "-1")) if ws is self.ws else 0,
             no_reorder=int(os.environ.get("ELEPHAS_AMD_NO_REORDER", "0")),
@@ -273,7 +313,8 @@ class NativeTrainer(TrainerBase):
         summed over ranks by ``allreduce`` (issued on this trainer's stream, so every
         read of the sum is stream-ordered after it), scaled, and written back into every
         replica's master and both weight-image parities by one kernel.  No host sync.
-        Returns the mean as a device tensor valid in this trainer's stream order."""
+        Returns the mean as a device tensor; the caller's current stream is ordered after
+        it (an event wait), so reading it there needs no explicit synchronisation."""
         n_total = int(n_total or self.R)
         with torch.cuda.stream(self.stream):
             avg = getattr(self, "_avg_buf", None)
@@ -293,18 +334,20 @@ class NativeTrainer(TrainerBase):
                     avg.mul_(1.0 / n_total)
                     self.P.copy_(avg.expand_as(self.P))
                 self._images_stale = True
-                return avg
-            if include:
-                scale = 1.0 if allreduce is not None else 1.0 / n_total
-                self.C.replica_average(self.P.data_ptr(), self.P.stride(0), self.R, self.n, avg.data_ptr(), 0,
-                                       self.s, scale)
             else:
-                avg.zero_()
-            if allreduce is not None:
-                allreduce(avg)
-                avg.mul_(1.0 / n_total)
-            self.exe.refresh_from(avg.data_ptr(), 0, self.s)
-        self._images_stale = False
+                if include:
+                    scale = 1.0 if allreduce is not None else 1.0 / n_total
+                    self.C.replica_average(self.P.data_ptr(), self.P.stride(0), self.R, self.n, avg.data_ptr(), 0,
+                                           self.s, scale)
+                else:
+                    avg.zero_()
+                if allreduce is not None:
+                    allreduce(avg)
+                    avg.mul_(1.0 / n_total)
+                self.exe.refresh_from(avg.data_ptr(), 0, self.s)
+                self._images_stale = False
+        # the caller reads the mean on its own stream (mean.cpu(), checkpoints): join it
+        self._exit()
         return avg
 
     def reset_for_fit(self, flat, seed: Optional[int] = None):
@@ -451,20 +494,24 @@ class NativeTrainer(TrainerBase):
         """Launch nsteps fused training steps on self.stream (asynchronous)."""
         if nsteps <= 0:
             return
-        persistent = self._persist_fence()
-        try:
+        if not self.exe.persistent() or self.persist_cus:
             self._run_steps(nsteps, use_graph)
-        finally:
-            if persistent:
+            return
+        with _persist_lock(self.dev.index):
+            self._persist_fence()
+            try:
+                self._run_steps(nsteps, use_graph)
+            finally:
                 self._persist_mark()
 
     def _run_steps(self, nsteps: int, use_graph: bool):
         if self.exe.persistent():
             # one persistent launch per chunk of up to PERSIST_CHUNK steps, a remainder
-            # included (the kernel takes its step count at launch): a chunk is three
-            # stream operations (flag memset, kernel, counter advance), so there is
-            # nothing for a graph to save, and every extra launch would pay the
-            # kernel's fill / drain (weights, optimizer state, first forward) again
+            # included (the kernel takes its step count at launch): a chunk is two
+            # stream operations (the kernel, then a 1-block post kernel that clears the
+            # hand-off flags and advances the counters), so there is nothing for a graph
+            # to save, and every extra launch would pay the kernel's fill / drain
+            # (weights, optimizer state, first forward) again
             while nsteps > 0:
                 n = min(nsteps, self.GRAPH_CHUNK)
                 self.exe.train_chunk(n, self.s)
@@ -593,6 +640,34 @@ class NativeTrainer(TrainerBase):
             self.exe = self.C.Executor(cfg)
 
     def fit(self, epochs, verbose=0, allreduce=None):
+        """Keras-style fit of every replica. On the persistent plan the entry state
+        (masters, optimizer state, counters, shuffle epoch) is snapshotted on the device
+        first: if a persistent launch gives up (GPU shared, grid not resident -- see
+        check()), the trainer re-plans onto the row chain, restores the snapshot and
+        runs the whole fit again, so the caller sees a slower fit, not an exception."""
+        snap = self._snapshot() if self.exe.persistent() else None
+        try:
+            return self._fit(epochs, verbose, allreduce)
+        except PersistentPlanError:
+            if snap is None:
+                raise
+            self._restore(snap)
+            return self._fit(epochs, verbose, allreduce)
+
+    def _snapshot(self):
+        with torch.cuda.stream(self.stream):
+            return dict(P=self.P.clone(), S=self.S.clone(), ctr=self.ctr.clone(),
+                        perm_epoch=getattr(self, "_perm_epoch", 0))
+
+    def _restore(self, snap):
+        with torch.cuda.stream(self.stream):
+            self.P.copy_(snap["P"])
+            self.S.copy_(snap["S"])
+            self.ctr.copy_(snap["ctr"])
+        self._perm_epoch = snap["perm_epoch"]
+        self.sync_shadows()
+
+    def _fit(self, epochs, verbose=0, allreduce=None):
         hist = self.new_history()
         self._enter()
         epochs = int(epochs)
@@ -684,14 +759,21 @@ class NativeTrainer(TrainerBase):
         return t.detach().cpu().numpy().copy()
 
     def check(self):
-        """Raise if a persistent-plan launch gave up waiting inside the kernel (its sticky
-        error word; every later launch of the executor then does nothing)."""
+        """Raise PersistentPlanError if a persistent-plan launch gave up waiting inside the
+        kernel (its sticky error word: later launches of that executor did nothing and
+        their post kernels did not advance the counters).  Before raising, the error word
+        is cleared and the trainer re-planned onto the row chain (logged), so it stays
+        usable; fit() restores its snapshot and re-runs."""
         if self.exe is not None and self.exe.persistent():
             e = self.exe.persist_error()
             if e:
-                raise RuntimeError(f"persistent step kernel: an in-launch wait timed out (code {e}); "
-                                   "the GPU was shared or a workgroup was not resident -- set "
-                                   "ELEPHAS_AMD_PERSIST=0 to use the 3-launch row-chain plan")
+                _log.warning("persistent step kernel gave up (code %d%s); falling back to the row-chain plan",
+                             e, ", grid not resident" if e == 9 else "")
+                self.exe.persist_clear_error()
+                self.persist_mode = 0
+                self._build_executor()
+                self._images_stale = True   # P may hold a partial chunk: images from P first
+                raise PersistentPlanError(e)
 
     # ------------------------------------------------------------------- eval
     def _eval_buffers(self, n: int, with_y: bool, want_pred: bool):
@@ -817,10 +899,27 @@ class NativeTrainer(TrainerBase):
         return [float(s[0] / cnt)] + [float(s[2 + i] / cnt) for i in range(len(self.metrics))]
 
     def launch_count(self):
-        """Kernel launches per training step (the persistent plan: one per chunk)."""
+        """Kernel launches per training step of a long run (the persistent plan: the kernel
+        and its 1-block post kernel per chunk of up to PERSIST_CHUNK steps)."""
         if self.exe.persistent():
-            return 1.0 / self.GRAPH_CHUNK
+            return 2.0 / self.GRAPH_CHUNK
         return self.exe.launches_per_step()
+
+    def launches_for(self, nsteps: int) -> int:
+        """Kernels a run_steps(nsteps) call issues (what a timed region of nsteps holds)."""
+        if nsteps <= 0:
+            return 0
+        if self.exe.persistent():
+            return 2 * ((nsteps + self.GRAPH_CHUNK - 1) // self.GRAPH_CHUNK)
+        full, rest = divmod(nsteps, self.GRAPH_CHUNK)
+        graphs = full + bin(rest).count("1")
+        return nsteps * self.exe.launches_per_step() + graphs   # + one counter advance per graph
+
+    @property
+    def persist_variant(self) -> int:
+        """2: the V2 roles (plain SGD, ReLU: L0 Gram corrections, DW workgroups), 1: V1,
+        0: not persistent."""
+        return int(self.exe.persist_variant()[0]) if self.exe.persistent() else 0
 
     @property
     def persistent(self) -> bool:
@@ -830,8 +929,11 @@ class NativeTrainer(TrainerBase):
     def plan_name(self) -> str:
         if self.exe.persistent():
             nk0, nc0, kc0, cw, nch, wgs, grid = self.exe.persist_geometry()
-            return (f"persistent (1 launch per <= {self.GRAPH_CHUNK}-step chunk; per replica {nk0}x{nc0} "
-                    f"layer-0 tiles of {kc0}x{cw} + {nch} row-chain workgroups; grid {grid})")
+            var, nd = self.exe.persist_variant()
+            dw = f" + {nd} weight-gradient workgroups" if var == 2 else ""
+            return (f"persistent V{var} (1 kernel + 1 post kernel per <= {self.GRAPH_CHUNK}-step chunk; per "
+                    f"replica {nk0}x{nc0} layer-0 tiles of {kc0}x{cw} + {nch} row-chain workgroups{dw}; "
+                    f"grid {grid})")
         if self.exe.rowchain():
             return "row-chain (3 launches per step)"
         if self.exe.tailchain():

@@ -46,7 +46,36 @@ def init_from_env(backend: str = None, timeout_s: int = None) -> bool:
         local = int(os.environ.get("LOCAL_RANK", "0"))
         torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
     dist.init_process_group(backend=backend, timeout=timedelta(seconds=timeout_s))
+    _detect_device_sharing()
     return True
+
+
+_SHARERS = 1
+
+
+def _device_key():
+    import socket
+    if not torch.cuda.is_available():
+        return (socket.gethostname(), "cpu", os.getpid())
+    p = torch.cuda.get_device_properties(torch.cuda.current_device())
+    uuid = str(getattr(p, "uuid", "")) or "%x:%x" % (getattr(p, "pci_bus_id", -1), getattr(p, "pci_device_id", -1))
+    return (socket.gethostname(), uuid)
+
+
+def _detect_device_sharing():
+    """How many ranks of the job run on this rank's GPU (same host and device UUID / PCI
+    id): > 1 only in single-GPU multi-rank rehearsals.  A rank that sees ONE device of
+    an 8-GPU node (HIP_VISIBLE_DEVICES per rank) is not sharing, whatever
+    LOCAL_WORLD_SIZE says.  Collective: called by every rank in init_from_env."""
+    global _SHARERS
+    keys = all_gather_object(_device_key())
+    me = keys[rank()]
+    _SHARERS = max(1, sum(1 for k in keys if k == me))
+
+
+def device_sharers() -> int:
+    """Ranks of this job that share this process's GPU (1 when it owns it)."""
+    return _SHARERS
 
 
 def rank() -> int:

@@ -24,8 +24,10 @@ def to_labeled_point(sc, features: np.ndarray, labels: np.ndarray, categorical: 
     iterate as LabeledPoint objects, and lp_to_simple_rdd converts them as arrays."""
     from ..data.rdd import LabeledPointPartition, RDD
     features, labels = np.asarray(features), np.asarray(labels)
-    if features.ndim != 2 or len(features) != len(labels):
-        # anything not a row matrix keeps the per-row construction (and its errors)
+    scalar_labels = labels.ndim == 1 or (labels.ndim == 2 and labels.shape[1] == 1)
+    if features.ndim != 2 or len(features) != len(labels) or (not categorical and not scalar_labels):
+        # anything not a row matrix (or multi-column labels without ``categorical``) keeps
+        # the reference's per-row construction, and its errors
         return sc.parallelize([LabeledPoint(np.argmax(y) if categorical else y, to_vector(x))
                                for x, y in zip(features, labels)])
     lab = np.argmax(labels.reshape(len(labels), -1), axis=1) if categorical else labels.reshape(len(labels), -1)[:, 0]

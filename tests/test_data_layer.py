@@ -29,6 +29,12 @@ def test_labeled_point_roundtrips(spark_context):
     assert r.first()[1].shape == (3,)
     r2 = rdd_utils.lp_to_simple_rdd(lp2, categorical=False, nb_classes=3)
     assert r2.first()[1] == 2.0
+    # (n, 1) labels take the columnar path; multi-column labels without ``categorical``
+    # take the reference's per-row LabeledPoint construction, which rejects them
+    lp3 = rdd_utils.to_labeled_point(spark_context, features, np.asarray([[2.0], [1.0]]), False)
+    assert lp3.first().label == 2.0
+    with pytest.raises(TypeError):
+        rdd_utils.to_labeled_point(spark_context, features, cat, False)
 
 
 def test_encode_label():

@@ -22,9 +22,10 @@ def _run(scenario, world=2, timeout=150, env_extra=None):
         port = so.getsockname()[1]
     procs = []
     for r in range(world):
+        # the ranks share the GPU: parallel/dist.py detects it (device UUIDs) and sizes
+        # every persistent grid to an equal CU share, so both stay resident
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
-                   MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0",
-                   ELEPHAS_AMD_PERSIST="0")   # ranks share the GPU: no persistent grids
+                   MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
         env.update(env_extra or {})
         cmd = [sys.executable, "-u", os.path.join(HERE, "_peer_worker.py"), scenario]
         prof = os.environ.get("ELEPHAS_AMD_PEER_PROF_DIR")   # tools: kernel trace of rank 0
@@ -126,12 +127,13 @@ def test_spark_model_synchronous_two_ranks_equals_single_process(tmp_path, gran)
 @pytest.mark.parametrize("gran", ["fit", "epoch"])
 def test_spark_model_sync_persistent_plan_two_ranks_match_one(gran, tmp_path):
     """The persistent plan under SparkModel(mode='synchronous') across 2 ranks (each rank's
-    persistent grid limited to half the CUs, so both stay resident on the shared GPU):
+    persistent grid sized to half the CUs by the device-sharing detection, so both stay
+    resident on the shared GPU):
     the averaging writes the mean into the masters and leaves the weight images to the
     next reader (NativeTrainer._ensure_images) -- both ranks agree bit for bit and match a
     single-process run; predict / evaluate / transform read refreshed images."""
     env = {"ELEPHAS_AMD_TEST_OUT": str(tmp_path), "ELEPHAS_AMD_P2P_ANY_BACKEND": "1",
-           "ELEPHAS_AMD_PERSIST": "1", "ELEPHAS_AMD_PERSIST_CUS": "128"}
+           "ELEPHAS_AMD_PERSIST": "1"}
     two = _run(f"spark_sync_{gran}p", env_extra=env)
     one = _run(f"spark_sync_{gran}p", world=1, env_extra=env)
     for r in two + one:

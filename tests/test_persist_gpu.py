@@ -67,6 +67,8 @@ def test_persist_matches_fp32_reference_with_same_masks(opt):
     xs, ys = _shards([96, 96], 40, 6, seed=3)
     nat = _trainer(model, 2, 32, persist=1)
     assert nat.persistent
+    # plain SGD + ReLU takes the V2 roles (Gram-corrected layer 0, DW workgroups)
+    assert nat.persist_variant == (2 if opt == "sgd" else 1), nat.plan_name()
     ref = TorchTrainer(model, build_plan(model), 2, 32, torch.device("cuda"), hash_dropout_seed=12345)
     w0 = nat.get_weights_flat()[0].copy()
     for t in (nat, ref):
@@ -182,3 +184,84 @@ def test_persist_headline_shape_plan_and_progress():
     for hr in h:
         assert hr["loss"][-1] < hr["loss"][0]
     t.check()
+
+
+@pytest.mark.parametrize("hidden", [128, 64])
+def test_persist_v2_matches_v1(monkeypatch, hidden):
+    """The V2 roles (layer-0 pre-activations rebuilt from Pold + Gram corrections, weight
+    gradients on their own workgroups) against V1 on the headline shape: 8 replicas x B
+    64, dropout, shuffling, a validation split, a partial last batch -- the same
+    training within fp32 rounding (V2 adds the last update to the product, not the tile)."""
+    from elephas_amd.models import initializers
+    from elephas_amd.models.optimizers import SGD
+    initializers.set_seed(77)
+    model = _mlp(784, [hidden, hidden], 10, dropout=0.2)
+    model.compile(SGD(learning_rate=0.1, decay=1e-3), "categorical_crossentropy", ["acc"])
+    xs, ys = _shards([700] * 7 + [300], 784, 10, seed=8)
+    out = []
+    for v2 in ("1", "0"):
+        monkeypatch.setenv("ELEPHAS_AMD_PERSIST_V2", v2)
+        t = _trainer(model, 8, 64, persist=1, seed=3)
+        assert t.persist_variant == (2 if v2 == "1" else 1), t.plan_name()
+        t.set_data(xs, ys, 0.1, shuffle=True)
+        torch.manual_seed(1)
+        h = t.fit(2)
+        out.append((t.get_weights_flat(), h))
+    (w2, h2), (w1, h1) = out
+    scale = np.abs(w1).max()
+    assert np.abs(w2 - w1).max() <= 2e-5 * scale, (np.abs(w2 - w1).max(), scale)
+    for a, b in zip(h2, h1):
+        for key in a:
+            np.testing.assert_allclose(a[key], b[key], rtol=5e-4, atol=5e-4)
+
+
+def test_persist_v2_chunking_close():
+    """V2 across launch boundaries: 37 steps in chunks of 16 + 16 + 4 + 1 vs 37 one-step
+    launches (the first step of a launch is the direct product, later ones corrected):
+    equal within fp32 rounding."""
+    from elephas_amd.models import initializers
+    from elephas_amd.models.optimizers import SGD
+    initializers.set_seed(9)
+    model = _mlp(784, [128, 128], 10, dropout=0.2)
+    model.compile(SGD(0.05), "categorical_crossentropy", ["acc"])
+    xs, ys = _shards([64 * 40] * 2, 784, 10, seed=2)
+    ws = []
+    for chunk in (16, 1):
+        t = _trainer(model, 2, 64, persist=1, seed=99)
+        assert t.persist_variant == 2
+        t.set_data(xs, ys, 0.0, shuffle=False)
+        t.GRAPH_CHUNK = chunk   # steps per persistent launch (set_data may rebuild the executor)
+        w0 = t.get_weights_flat()
+        t.begin_epoch()
+        t.run_steps(37)
+        ws.append(t.get_weights_flat())
+    step = np.abs(ws[1] - w0).max()
+    assert np.abs(ws[0] - ws[1]).max() <= 1e-4 * step, (np.abs(ws[0] - ws[1]).max(), step)
+
+
+def test_persist_oversubscribed_grid_falls_back(monkeypatch):
+    """A persistent grid larger than the GPU can hold (the CU count overridden upwards)
+    cannot be resident: the kernel's GO-flag wait gives up before touching any state, the
+    trainer re-plans onto the row chain and fit() re-runs from its snapshot -- the caller
+    gets the row-chain result, not an exception."""
+    from elephas_amd.models import initializers
+    from elephas_amd.models.optimizers import SGD
+    initializers.set_seed(4)
+    model = _mlp(784, [128, 128], 10, dropout=0.2)
+    model.compile(SGD(0.1), "categorical_crossentropy", ["acc"])
+    xs, ys = _shards([256] * 8, 784, 10, seed=6)
+    monkeypatch.setenv("ELEPHAS_AMD_PERSIST_TIMEOUT_MS", "200")
+    monkeypatch.setenv("ELEPHAS_AMD_PERSIST_OVERSUBSCRIBE", "1024")
+    t = _trainer(model, 8, 64, persist=-1, seed=21)
+    nk0, nc0, kc0, cw, nch, wgs, grid = t.exe.persist_geometry()
+    assert grid > torch.cuda.get_device_properties(0).multi_processor_count, t.plan_name()
+    t.set_data(xs, ys, 0.0, shuffle=False)
+    h = t.fit(1)
+    assert not t.persistent and t.rowchain, t.plan_name()
+    monkeypatch.delenv("ELEPHAS_AMD_PERSIST_OVERSUBSCRIBE")
+    ref = _trainer(model, 8, 64, persist=0, seed=21, rowchain=1)
+    ref.set_data(xs, ys, 0.0, shuffle=False)
+    hr = ref.fit(1)
+    assert np.array_equal(t.get_weights_flat(), ref.get_weights_flat())
+    for a, b in zip(h, hr):
+        np.testing.assert_allclose(a["loss"], b["loss"], rtol=1e-6)
