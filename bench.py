@@ -177,15 +177,19 @@ def main():
         W = args.workers_per_gpu
     B = args.batch
     batch_mode = args.granularity == "batch"
-    R = 1 if batch_mode else W
-    Bloc = B * W if batch_mode else B
+    # per-step sync DP on ONE GPU: the W workers are replicas of one sync trainer whose
+    # gradients are summed every step inside the persistent launch (native_engine sync);
+    # across ranks: one replica of the rank's W * B rows and a per-step all-reduce
+    sync_local = batch_mode and world == 1 and gpu and not args.rccl and not args.overlap
+    R = W if (not batch_mode or sync_local) else 1
+    Bloc = B if (not batch_mode or sync_local) else B * W
 
     # synthetic MNIST-shaped shards, one per worker
     rng = np.random.default_rng(1000 + rank)
     centers = rng.normal(0, 1, size=(classes, dims[0])).astype(np.float32)
     xs, ys = [], []
     for r in range(R):
-        n = rows * (W if batch_mode else 1)
+        n = rows * (W if R == 1 and batch_mode else 1)
         y = rng.integers(0, classes, n)
         x = centers[y] + rng.normal(0, 2.0, size=(n, dims[0])).astype(np.float32)
         x = (x - x.min()) / (x.max() - x.min())
@@ -194,7 +198,7 @@ def main():
 
     if gpu:
         from elephas_amd.ops.native_engine import NativeTrainer
-        t = NativeTrainer(model, plan, R, Bloc, dev, seed=4321 + rank)
+        t = NativeTrainer(model, plan, R, Bloc, dev, seed=4321 + rank, sync=sync_local)
     else:
         from elephas_amd.ops.torch_engine import TorchTrainer
         t = TorchTrainer(model, plan, R, Bloc, dev, seed=4321 + rank)
@@ -205,7 +209,7 @@ def main():
     def allreduce_grads(G):
         dist.all_reduce_sum_(G)
 
-    if batch_mode and gpu and (world > 1 or args.overlap):
+    if batch_mode and gpu and not sync_local and (world > 1 or args.overlap):
         t.set_grad_scale(1.0 / world)   # mean of the ranks' gradients after the sum all-reduce
     channel = None
     if batch_mode and gpu and world > 1 and not args.overlap and not args.no_graph and not args.rccl:
@@ -281,7 +285,7 @@ def main():
 
     dts = dist.all_gather_object(dt)
     dt_max = max(dts)
-    samples = rows_done * (R if not batch_mode else 1) * world
+    samples = rows_done * R * world
     # evidence for the multi-GPU record, gathered after the timed region: every rank's
     # HIP device, the all-reduce path actually taken, and a bit-exact digest of the
     # averaged theta (equal on every rank iff the all-reduce gave all ranks one result)
@@ -305,9 +309,13 @@ def main():
         path = f"torch.distributed {dist.backend()}" if not gpu else p2p.describe(nbytes)
     else:
         path = None
+    provenance = None
+    if gpu:
+        from elephas_amd.ops import native
+        provenance = native.provenance()   # the loaded _C's source digest vs this tree's csrc/
     if rank == 0:
         value = samples / dt_max
-        launches = t.launch_count() if gpu else None
+        launches = round(t.launches_for(args.steps) / args.steps, 4) if gpu else None
         names = {"mnist": "MNIST-MLP 784-128-128-10", "otto": "Otto-MLP 93-512-512-512-9",
                  "wide": "Wide-MLP 4096-4096-4096-1000"}
         metric = ("samples/sec (whole node) MNIST-MLP 784-128-128-10 sync DP at 1/2/4/8 MI355X"
@@ -337,7 +345,9 @@ def main():
                 "workers_total": W * world,
                 "batch_per_worker": B,
                 "rows_per_worker": rows,
-                "sync": "reference (one-shot averaging per fit)" if not batch_mode else "per-step gradient all-reduce",
+                "sync": ("reference (one-shot averaging per fit)" if not batch_mode else
+                         "per-step synchronous DP of the GPU's workers (gradient sum over the replicas every step)"
+                         if sync_local else "per-step gradient all-reduce"),
                 "allreduce": path,
                 "allreduce_bytes": nbytes if world > 1 else None,
                 "comm_world_size": dist.world_size(),
@@ -345,8 +355,10 @@ def main():
                 "theta_sha1_16": digests[0],
                 "theta_equal_on_all_ranks": all(d == digests[0] for d in digests),
                 "optimizer": "SGD(lr=%g)" % MODELS[args.model][4],
-                "engine": ("native HIP executor + hipGraph: " + t.plan_name()) if gpu else "torch CPU reference",
-                "launches_per_step": launches,
+                "engine": (("native HIP executor: " if t.persistent else "native HIP executor + hipGraph: ")
+                           + t.plan_name()) if gpu else "torch CPU reference",
+                "launches_per_step": launches,   # kernels the timed region issued / steps
+                "native_provenance": provenance,
                 "policy": args.policy,
                 "validation_passes_timed": state["val_passes"],
             },

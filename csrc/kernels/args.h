@@ -185,11 +185,13 @@ constexpr int PM_NTU = 2;      // layer-1 column tiles (and layer-2 row tiles) a
 // layer-1 activations for the weight-gradient workgroups), GO (residency: every
 // workgroup raises it on entry; the chain workgroups see the whole grid before they
 // touch any state)
-enum PmFlag : int { PMF_PART = 0, PMF_BWD = 1, PMF_W = 2, PMF_A0 = 3, PMF_D2 = 4, PMF_GO = 5, PMF_N = 6 };
+// X (sync: a workgroup's weight-gradient tile is in the exchange slab, see PersistArgs::sync)
+enum PmFlag : int { PMF_PART = 0, PMF_BWD = 1, PMF_W = 2, PMF_A0 = 3, PMF_D2 = 4, PMF_GO = 5, PMF_X = 6, PMF_N = 7 };
 // sticky error codes: the wait that timed out (PERR_GRID: the grid was not resident --
 // nothing was modified, the chunk can be re-run on another plan)
 enum PmErr : unsigned { PERR_L0_BWD = 1, PERR_CHAIN_PART = 2, PERR_CHAIN_BWD = 3, PERR_CHAIN_PREV = 4,
-                        PERR_DW_A0 = 5, PERR_DW_D2 = 6, PERR_GRID = 9 };
+                        PERR_DW_A0 = 5, PERR_DW_D2 = 6, PERR_XCHG = 7, PERR_GRID = 9 };
+constexpr int PM_XSLOT = 7 * 1024;   // floats of one workgroup's exchange slab (sync)
 struct PersistArgs {
   int R, B, nsteps;
   int K0, H0, H1, C;            // layer widths (H0, H1 in {64, 128}; C <= 16)
@@ -200,6 +202,13 @@ struct PersistArgs {
   int v2, nd;
   long long o_g;                    // Gram partials [2][nk0][64][64] (V2)
   long long part_par, g_par, dz0_par;   // parity strides of the double-buffered partials / Gram / dZ_0 (V2; 0 in V1)
+  // sync (V1 roles, per-step synchronous DP of the R replicas = one model): after its
+  // weight-gradient MFMAs every owning workgroup puts its tile into its exchange slab
+  // (parity of the step), raises X, waits for the same workgroup of every replica and
+  // sums the R slabs in replica order -- the same bits everywhere, so the replicas'
+  // updates (grad_scale = 1 / R) keep their weights identical
+  int sync;
+  long long o_xg;                   // exchange slabs [2][wgs][PM_XSLOT] in every replica's workspace
   int act0, act1, act2;
   float rate0, rate1;
   int bias0, bias1, bias2;

@@ -202,6 +202,50 @@ __device__ __forceinline__ bool wait_grid(const PersistArgs& a) {
   return ok != 0;
 }
 
+// sync: sum the weight-gradient fragments v[0 .. N) (f32x4 per lane, lane-linear slab
+// layout) of workgroup q over the R replicas, in replica order.  Every storing wave drains
+// its sc1 stores before the flag (publish); the slabs alternate by step parity, so a
+// replica running a step ahead never overwrites one a peer still reads.
+template <int N>
+__device__ __forceinline__ bool xchg_sum(const PersistArgs& a, int r, int q, int i, f32x4 (&v)[N]) {
+  const int tid = threadIdx.x;
+  const long long slab = a.o_xg + ((long long)(i & 1) * a.wgs + q) * PM_XSLOT;
+  const rsrc_t all = ws_rsrc(a.ws);   // every replica's workspace (offsets r * ws_stride)
+#pragma unroll
+  for (int u = 0; u < N; ++u) stw4(all, (u * 256 + tid) * 4, (int)((long long)r * a.ws_stride + slab), v[u]);
+  publish(flag_at(a, r, PMF_X) + q, (unsigned)(i + 1));
+  // one lane per replica watches that replica's flag of workgroup q
+  int ok = 1;
+  if (tid < 64) {
+    const unsigned long long t0 = wall_clock64();
+    for (;;) {
+      const unsigned f = tid < a.R ? __hip_atomic_load((gu32*)(flag_at(a, tid, PMF_X) + q), __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT)
+                                   : (unsigned)(i + 1);
+      if (__all(f >= (unsigned)(i + 1))) break;
+      if ((long long)(wall_clock64() - t0) > a.timeout) {
+        ok = 0;
+        if (tid == 0) __hip_atomic_store((gu32*)(a.err), (unsigned)PERR_XCHG, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  ok = __syncthreads_and(ok);
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  if (!ok) return false;
+#pragma unroll
+  for (int u = 0; u < N; ++u) v[u] = zero4f();
+  for (int rr = 0; rr < a.R; ++rr) {
+    f32x4 x[N];
+#pragma unroll
+    for (int u = 0; u < N; ++u) x[u] = ldw4(all, (u * 256 + tid) * 4, (int)((long long)rr * a.ws_stride + slab));
+#pragma unroll
+    for (int u = 0; u < N; ++u) v[u] += x[u];
+  }
+  return true;
+}
+
 __device__ __forceinline__ float dropout_u1(uint32_t base, int row, int c) {
   // the per-column-pair hash of dropout_u8 (common.h): the row-chain / grouped masks
   const uint32_t h = fmix32(base ^ (((uint32_t)row << 16) | (uint32_t)(c >> 1)));
@@ -545,7 +589,17 @@ __device__ __forceinline__ void l0_role(const PersistArgs& a, float* smem, int r
       }
       pstamp(a, i, 7);
       // bias gradient (first k-chunk): column sums of dZ_0 over the batch rows
-      const float gsum = has_b ? col_sums(sdZ, WS, cw, sRedL) : 0.f;
+      float gsum = has_b ? col_sums(sdZ, WS, cw, sRedL) : 0.f;
+      if (a.sync) {   // per-step synchronous DP: the R replicas' tiles summed, same bits everywhere
+        f32x4 xv[TU + 1];
+#pragma unroll
+        for (int u = 0; u < TU; ++u) xv[u] = dw[u];
+        xv[TU] = f32x4{gsum, 0.f, 0.f, 0.f};
+        if (!xchg_sum<TU + 1>(a, r, q, i, xv)) return;
+#pragma unroll
+        for (int u = 0; u < TU; ++u) dw[u] = xv[u];
+        gsum = xv[TU][0];
+      }
       pstamp(a, i, 8);
       const long long it = iter_at(a.ctr, a.ntrain, a.B, r, st.s0, i);
       float wv[TU * 4], gv[TU * 4];
@@ -1412,6 +1466,18 @@ __device__ __forceinline__ void chain_role(const PersistArgs& a, float* smem, in
         }
       }
       pstamp(a, i, 24);
+      if (a.sync) {   // per-step synchronous DP (see xchg_sum)
+        f32x4 xv[TU + 3];
+#pragma unroll
+        for (int u = 0; u <= TU; ++u) xv[u] = dw[u];
+        xv[TU + 1] = db[0];
+        xv[TU + 2] = db[1];
+        if (!xchg_sum<TU + 3>(a, r, nl0 + j, i, xv)) return;
+#pragma unroll
+        for (int u = 0; u <= TU; ++u) dw[u] = xv[u];
+        db[0] = xv[TU + 1];
+        db[1] = xv[TU + 2];
+      }
       pstamp(a, i, 25);
       const float gb = (b1own && lane >= 16) ? db[1][0] : db[0][0];
       const float gs = a.op.grad_scale;

@@ -81,6 +81,7 @@ static ExecCfg parse_cfg(const py::dict& d) {
   c.persist_timeout_ms = get<long long>(d, "persist_timeout_ms", 2000);
   c.persist_cus = get<int>(d, "persist_cus", 0);
   c.persist_v2 = get<int>(d, "persist_v2", -1);
+  c.persist_sync = get<int>(d, "persist_sync", 0);
   for (auto item : d["layers"].cast<py::list>()) {
     py::dict l = item.cast<py::dict>();
     LayerCfg lc;
@@ -157,6 +158,11 @@ static EvalSource parse_src(const py::dict& d) {
 
 PYBIND11_MODULE(_C, m) {
   m.doc() = "elephas_amd native runtime: CDNA4 (gfx950) HIP kernels + executor";
+#ifndef EA_SRC_DIGEST
+#define EA_SRC_DIGEST "unknown"
+#endif
+  // sha256 prefix of the csrc/ sources this binary was built from (elephas_amd/_build.py)
+  m.attr("source_digest") = EA_SRC_DIGEST;
 
   py::class_<Executor>(m, "Executor")
       .def(py::init([](py::dict cfg) { return new Executor(parse_cfg(cfg)); }))

@@ -82,8 +82,8 @@ bool Executor::build_persist() {
   if (cap < 1) return false;
   // V2 (persist.hip l0_role_v2 / dw_role_v2): plain SGD, ReLU hidden layers, independent
   // replicas -- the step's critical path runs through the chain workgroups only
-  const bool v2 = c_.persist_v2 != 0 && c_.op.opt == OPT_SGD && c_.op.mom == 0.f && l0.act == ACT_RELU &&
-                  l1.act == ACT_RELU;
+  const bool v2 = c_.persist_v2 != 0 && !c_.persist_sync && c_.op.opt == OPT_SGD && c_.op.mom == 0.f &&
+                  l0.act == ACT_RELU && l1.act == ACT_RELU;
   const int nd = v2 ? cdiv(l1.N / 16, PM_NTU) : 0;
   // layer-0 tiles: the cheapest (kc0, cw) whose tile count fits.  V1: cost ~ the tile's
   // MFMA work (FWD reduction padded to 64) + the partials every chain workgroup sums.
@@ -117,6 +117,7 @@ bool Executor::build_persist() {
   a.kc0 = best_kc; a.cw = best_cw; a.nc0 = l0.N / best_cw; a.nk0 = cdiv(l0.K, best_kc);
   a.nch = nch; a.v2 = v2 ? 1 : 0; a.nd = nd;
   a.wgs = a.nk0 * a.nc0 + nch + nd;
+  a.sync = c_.persist_sync ? 1 : 0;
   a.act0 = l0.act; a.act1 = l1.act; a.act2 = l2.act;
   a.rate0 = l0.rate; a.rate1 = l1.rate;
   a.bias0 = l0.has_bias; a.bias1 = l1.has_bias; a.bias2 = l2.has_bias;
@@ -158,6 +159,7 @@ bool Executor::build_persist() {
   a.o_w2 = take((long long)a.H1 * 16);
   a.o_b1 = take(a.H1);
   a.o_b2 = take(16);
+  a.o_xg = a.sync ? take(2LL * a.wgs * PM_XSLOT) : 0;
   a.ws_stride = off;
   const size_t ws_bytes = sizeof(float) * (size_t)off * c_.R;
   check(hipMalloc(&d_pws_, ws_bytes), "hipMalloc(persistent workspace)");
@@ -185,7 +187,7 @@ std::vector<int> Executor::persist_geometry() const {
 
 std::vector<int> Executor::persist_variant() const {
   if (!pm_.on) return {};
-  return {pm_.args.v2 ? 2 : 1, pm_.args.nd};
+  return {pm_.args.v2 ? 2 : 1, pm_.args.nd, pm_.args.sync};
 }
 
 unsigned Executor::persist_error() const {

@@ -76,6 +76,7 @@ struct ExecCfg {
   long long persist_timeout_ms = 2000;  // spin limit of its in-launch waits
   int persist_cus = 0;  // > 0: CUs the persistent grid may occupy (several executors side by side)
   int persist_v2 = -1;  // persistent V2 roles when eligible (plain SGD, ReLU, independent replicas); 0 off
+  int persist_sync = 0;  // persistent plan as per-step synchronous DP of the R replicas (in-launch exchange)
   int no_reorder = 0;   // A/B: keep a DW + DX launch's problems in declaration order
   int dual = 1;         // a layer's DW and DX on different tiles in one launch (0: two launches)
 };
@@ -126,7 +127,7 @@ class Executor {
   // persistent plan: {L0 k-chunks, L0 column blocks, k-chunk rows, block columns, chain
   // workgroups, workgroups per replica, grid}
   std::vector<int> persist_geometry() const;
-  std::vector<int> persist_variant() const;   // {1 or 2, DW workgroups per replica}
+  std::vector<int> persist_variant() const;   // {1 or 2, DW workgroups per replica, sync}
   unsigned persist_error() const;  // sticky error word (a timed-out in-launch wait), synchronous read
   void persist_clear_error();
   int rowchain_split() const { return rc_.on ? rc_.nsplitk : 0; }

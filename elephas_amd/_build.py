@@ -40,6 +40,22 @@ SOURCES = [
 ]
 
 
+def source_digest() -> str:
+    """sha256 (first 16 hex digits) over every native source under csrc/ (path + bytes, in
+    path order): compiled into _C as ``source_digest`` so a run can show that the loaded
+    binary was built from the sources it ships with (ops/native.py provenance())."""
+    import hashlib
+    h = hashlib.sha256()
+    for dirpath, _, files in sorted(os.walk(CSRC)):
+        for fn in sorted(files):
+            if fn.endswith((".hip", ".h", ".cpp")) and "tests" not in os.path.relpath(dirpath, CSRC).split(os.sep):
+                path = os.path.join(dirpath, fn)
+                h.update(os.path.relpath(path, CSRC).encode())
+                with open(path, "rb") as f:
+                    h.update(f.read())
+    return h.hexdigest()[:16]
+
+
 def ext_path() -> str:
     return os.path.join(ROOT, "elephas_amd", "_C" + sysconfig.get_config_var("EXT_SUFFIX"))
 
@@ -82,13 +98,21 @@ def build(verbose: bool = False, force: bool = False, jobs: int = 6) -> str:
     flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-fvisibility=hidden",
              "-Wno-unused-result"]
     objs, cmds = [], []
+    digest = source_digest()
+    stamp = os.path.join(BUILD, "source_digest.txt")
+    old_digest = open(stamp).read().strip() if os.path.exists(stamp) else ""
     for src in SOURCES:
         s = os.path.join(CSRC, src)
         o = os.path.join(BUILD, src.replace("/", "_") + ".o")
         objs.append(o)
-        if force or not os.path.exists(o) or os.path.getmtime(o) < _newest(_deps(s)):
+        extra = []
+        stale = force or not os.path.exists(o) or os.path.getmtime(o) < _newest(_deps(s))
+        if src == "runtime/bindings.cpp":
+            extra = [f'-DEA_SRC_DIGEST="{digest}"']
+            stale = stale or old_digest != digest   # the digest covers every source
+        if stale:
             lang = [] if src.endswith(".hip") else ["-x", "hip"]
-            cmds.append([_hipcc()] + flags + inc + lang + ["-c", s, "-o", o])
+            cmds.append([_hipcc()] + flags + extra + inc + lang + ["-c", s, "-o", o])
 
     def run(cmd):
         if verbose:
@@ -100,6 +124,8 @@ def build(verbose: bool = False, force: bool = False, jobs: int = 6) -> str:
 
     with ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
         list(ex.map(run, cmds))
+    with open(stamp, "w") as f:
+        f.write(digest)
     out = ext_path()
     if force or cmds or not os.path.exists(out) or os.path.getmtime(out) < _newest(objs):
         run([_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC"] + objs + ["-o", out, "-lrt", "-lpthread"])

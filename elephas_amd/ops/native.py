@@ -71,6 +71,16 @@ def require():
     return m
 
 
+def provenance() -> dict:
+    """Which sources the loaded binary was built from: the digest compiled into _C vs the
+    digest of the csrc/ tree next to it (equal = the binary matches these sources)."""
+    from .._build import source_digest
+    m = load(build_if_missing=False)
+    built = getattr(m, "source_digest", None) if m is not None else None
+    tree = source_digest()
+    return dict(built=built, tree=tree, match=built == tree, path=_path() if m is not None else None)
+
+
 def stream_handle(stream=None) -> int:
     s = stream if stream is not None else torch.cuda.current_stream()
     return int(s.cuda_stream)

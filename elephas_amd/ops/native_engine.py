@@ -88,6 +88,12 @@ class PersistentPlanError(RuntimeError):
             + "); the trainer now runs the row-chain plan")
 
 
+def _replica_sum(G: torch.Tensor):
+    """Gradient exchange of a sync trainer's replicas (one GPU): every replica gets the
+    sum (the optimizer applies grad_scale = 1/R)."""
+    G.copy_(G.sum(0, keepdim=True).expand_as(G))
+
+
 def pad8(n: int) -> int:
     return (int(n) + 7) // 8 * 8
 
@@ -103,9 +109,16 @@ class NativeTrainer(TrainerBase):
     def __init__(self, model, plan, R: int = 1, batch_size: int = 32, device=None, seed: Optional[int] = None,
                  policy: Optional[str] = None, eval_batch: int = 2048, rowchain: Optional[int] = None,
                  persist: Optional[int] = None, stream: Optional[torch.cuda.Stream] = None,
-                 persist_cus: Optional[int] = None):
+                 persist_cus: Optional[int] = None, sync: bool = False):
         super().__init__(model, plan, R, batch_size)
         self.C = native.require()
+        # sync: the R replicas are ONE model trained with per-step synchronous data
+        # parallelism (reference SURVEY §2.3 DP-sync 'batch'): every step each replica's
+        # gradient over its own batch, summed over the replicas, scaled 1/R, applied by all.
+        # On the persistent plan the exchange happens inside the launch (persist.hip
+        # xchg_sum); otherwise forward/backward -> replica sum -> apply per step.
+        self.sync = bool(sync) and R > 1
+        self._grad_scale = 1.0
         # row-chain step plan (3 launches, csrc/kernels/rowchain.hip): None ->
         # $ELEPHAS_AMD_ROWCHAIN (default -1: whenever the model is eligible), 0 off, 1 required
         self.rowchain_mode = int(os.environ.get("ELEPHAS_AMD_ROWCHAIN", "-1")) if rowchain is None else int(rowchain)
@@ -222,7 +235,8 @@ class NativeTrainer(TrainerBase):
                                Z=w["Z"].data_ptr(), D=w["D"].data_ptr(), DT=w["DT"].data_ptr(),
                                dZ=w["dZ"].data_ptr(), dZT=w["dZT"].data_ptr(),
                                wsh_off=d["wsh_off"], wtsh_off=d["wtsh_off"]))
-        opt = dict(opt=self.opt_id, s_plane=self.n, grad_scale=1.0)
+        opt = dict(opt=self.opt_id, s_plane=self.n,
+                   grad_scale=self._grad_scale / (self.R if self.sync else 1))
         opt.update({k: v for k, v in self.opt_hp.items() if k != "state_init"})
         return dict(
             R=self.R, B=ws["B"], Bp=ws["Bp"], bf16=int(self.bf16), seed=self.seed,
@@ -236,6 +250,7 @@ class NativeTrainer(TrainerBase):
             persist_timeout_ms=int(os.environ.get("ELEPHAS_AMD_PERSIST_TIMEOUT_MS", "2000")),
             persist_cus=self.persist_cus,
             persist_v2=int(os.environ.get("ELEPHAS_AMD_PERSIST_V2", "-1")),
+            persist_sync=int(self.sync) if ws is self.ws else 0,
             rc_split=int(os.environ.get("ELEPHAS_AMD_RC_SPLIT", "0")),
             tail=int(os.environ.get("ELEPHAS_AMD_TAIL", "-1")) if ws is self.ws else 0,
             no_reorder=int(os.environ.get("ELEPHAS_AMD_NO_REORDER", "0")),
@@ -439,6 +454,8 @@ class NativeTrainer(TrainerBase):
             vs.append(sp)
             vc.append(n - sp if self.active[r] else 0)
         self.ntrain_h, self.vcount_h = nt, vc
+        # in-launch gradient exchange needs every replica to run the same steps
+        self._sync_equal = len(set(nt)) == 1
         with torch.cuda.stream(self.stream):
             self.ntrain.copy_(torch.tensor(nt, dtype=torch.int32))
             self.vstart.copy_(torch.tensor(vs, dtype=torch.int32))
@@ -494,6 +511,11 @@ class NativeTrainer(TrainerBase):
         """Launch nsteps fused training steps on self.stream (asynchronous)."""
         if nsteps <= 0:
             return
+        if self.sync and not self._sync_in_launch():
+            # per-step synchronous DP without the in-launch exchange: forward/backward of
+            # every replica -> gradient sum over the replicas -> apply (grad_scale 1/R)
+            self.run_steps_allreduce(nsteps, _replica_sum, use_graph=use_graph)
+            return
         if not self.exe.persistent() or self.persist_cus:
             self._run_steps(nsteps, use_graph)
             return
@@ -503,6 +525,9 @@ class NativeTrainer(TrainerBase):
                 self._run_steps(nsteps, use_graph)
             finally:
                 self._persist_mark()
+
+    def _sync_in_launch(self) -> bool:
+        return bool(self.exe.persistent() and self.exe.persist_variant()[2] and getattr(self, "_sync_equal", False))
 
     def _run_steps(self, nsteps: int, use_graph: bool):
         if self.exe.persistent():
@@ -632,12 +657,11 @@ class NativeTrainer(TrainerBase):
         self._new_perm(gen)
 
     def set_grad_scale(self, scale: float):
-        if abs(scale - 1.0) > 0:
-            cfg = self._cfg(self.ws)
-            cfg["opt"]["grad_scale"] = float(scale)
-            self.exe.destroy_graphs()
-            self._graphs = {}
-            self.exe = self.C.Executor(cfg)
+        """Scale every gradient by ``scale`` before the optimizer (the mean over ranks after
+        a sum all-reduce); sync trainers add their 1/R on top."""
+        if float(scale) != self._grad_scale:
+            self._grad_scale = float(scale)
+            self._build_executor()
 
     def fit(self, epochs, verbose=0, allreduce=None):
         """Keras-style fit of every replica. On the persistent plan the entry state
@@ -929,9 +953,10 @@ class NativeTrainer(TrainerBase):
     def plan_name(self) -> str:
         if self.exe.persistent():
             nk0, nc0, kc0, cw, nch, wgs, grid = self.exe.persist_geometry()
-            var, nd = self.exe.persist_variant()
+            var, nd, sync = self.exe.persist_variant()
             dw = f" + {nd} weight-gradient workgroups" if var == 2 else ""
-            return (f"persistent V{var} (1 kernel + 1 post kernel per <= {self.GRAPH_CHUNK}-step chunk; per "
+            sy = ", per-step gradient exchange of the replicas inside the launch" if sync else ""
+            return (f"persistent V{var}{sy} (1 kernel + 1 post kernel per <= {self.GRAPH_CHUNK}-step chunk; per "
                     f"replica {nk0}x{nc0} layer-0 tiles of {kc0}x{cw} + {nch} row-chain workgroups{dw}; "
                     f"grid {grid})")
         if self.exe.rowchain():

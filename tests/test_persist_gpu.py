@@ -265,3 +265,40 @@ def test_persist_oversubscribed_grid_falls_back(monkeypatch):
     assert np.array_equal(t.get_weights_flat(), ref.get_weights_flat())
     for a, b in zip(h, hr):
         np.testing.assert_allclose(a["loss"], b["loss"], rtol=1e-6)
+
+
+@pytest.mark.parametrize("opt", ["sgd", "sgd_mom"])
+def test_persist_sync_replicas_match_eager_exchange(opt):
+    """Per-step synchronous DP of the replicas inside the persistent launch (every owning
+    workgroup sums the R replicas' weight-gradient tiles in replica order): the replicas
+    stay bit-identical, and the training equals the eager per-step path (forward /
+    backward, replica sum of G, apply) within fp32 summation order."""
+    from elephas_amd.models import initializers, optimizers as O
+    from elephas_amd.ops.plan import build_plan
+    from elephas_amd.ops.native_engine import NativeTrainer
+    from elephas_amd import config
+    config.set_policy("float32")
+    initializers.set_seed(12)
+    model = _mlp(784, [128, 128], 10, dropout=0.2)
+    model.compile({"sgd": O.SGD(0.1), "sgd_mom": O.SGD(0.05, momentum=0.9)}[opt], "categorical_crossentropy",
+                  ["acc"])
+    xs, ys = _shards([450] * 4, 784, 10, seed=13)
+    out = []
+    for persist in (1, 0):
+        t = NativeTrainer(model, build_plan(model), 4, 64, torch.device("cuda"), seed=5, persist=persist,
+                          sync=True)
+        assert t.persistent == bool(persist)
+        if persist:
+            assert t.exe.persist_variant()[2] == 1, t.plan_name()
+        t.set_data(xs, ys, 0.1, shuffle=True)
+        torch.manual_seed(3)
+        h = t.fit(2)
+        w = t.get_weights_flat()
+        out.append((w, h))
+    (wp, hp), (we, he) = out
+    for r in range(1, 4):
+        assert np.array_equal(wp[r], wp[0]), r          # one model: identical replicas
+    scale = np.abs(we).max()
+    assert np.abs(wp - we).max() <= 1e-4 * scale, (np.abs(wp - we).max(), scale)
+    for a, b in zip(hp, he):
+        np.testing.assert_allclose(a["loss"], b["loss"], rtol=5e-4, atol=5e-4)
