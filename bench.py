@@ -122,6 +122,8 @@ def main():
                     help="batch granularity: per-layer gradient buckets all-reduced beside the backward")
     ap.add_argument("--dropout", type=float, default=None, help="override the model's dropout (diagnostics)")
     ap.add_argument("--out", default=None, help="also append the JSON line to this file")
+    ap.add_argument("--no-sub", action="store_true",
+                    help="skip the extra per-step-sync / strong-split measurements of the headline line")
     ap.add_argument("--async-groups", type=int, default=None,
                     help="async/hogwild: independently progressing worker groups per GPU (default: one per worker)")
     ap.add_argument("--frequency", default="batch", choices=["epoch", "batch"],
@@ -167,16 +169,106 @@ def main():
         return bench_infer(args, model, dist, rank, world, dev)
     if args.mode != "synchronous":
         return bench_async(args, model, dist, rank, world, dev)
+    if args.scaling == "strong" and 8 % world:
+        raise SystemExit("bench.py --scaling strong: the 8 reference partitions must split evenly over the GPUs")
+    W = 8 // world if args.scaling == "strong" else args.workers_per_gpu
+    batch_mode = args.granularity == "batch"
+    m = measure_train(args, model, dist, rank, world, dev, gpu, W, batch_mode, args.steps, args.warmup)
+    # extra measurements in the same line (after the headline's timed region, never inside
+    # it), so a multi-GPU record also exercises the per-step exchange and the reference
+    # job's strong split: per-step sync DP at the same workers per GPU, and 8 // N workers
+    # per GPU (only for the default headline invocation; --no-sub skips them)
+    subs = {}
+    if (not args.no_sub and args.model == "mnist" and not batch_mode and args.scaling == "weak"
+            and args.workers_per_gpu == 8):
+        sk, sw = max(1, args.steps), max(1, args.warmup)
+        strong_w = 8 // world if 8 % world == 0 and 8 // world != W else None   # N = 1: the headline itself
+        for name, w_, bm in (("per_step_sync", W, True), ("strong", strong_w, False)):
+            if w_ is None:
+                continue
+            r = measure_train(args, model, dist, rank, world, dev, gpu, w_, bm, sk, sw)
+            subs[name] = {"value": round(r["samples"] / r["dt_max"], 1), "ms_per_step": round(r["dt_max"] / sk * 1e3, 4),
+                          "steps": sk, "workers_per_gpu": w_, "sync": r["sync"], "engine": r["engine"],
+                          "scaling": "weak" if name != "strong" else "strong",
+                          "theta_equal_on_all_ranks": r["theta_equal"], "allreduce": r["path"]}
+    provenance = None
+    if gpu:
+        from elephas_amd.ops import native
+        provenance = native.provenance()   # the loaded _C's source digest vs this tree's csrc/
+    B, rows, R, samples, dt_max = args.batch, m["rows"], m["R"], m["samples"], m["dt_max"]
+    batch_mode, t, state, digests = m["batch_mode"], m["t"], m["state"], m["digests"]
+    devices, path, nbytes = m["devices"], m["path"], m["nbytes"]
+    if rank == 0:
+        value = samples / dt_max
+        launches = round(t.launches_for(args.steps) / args.steps, 4) if gpu else None
+        names = {"mnist": "MNIST-MLP 784-128-128-10", "otto": "Otto-MLP 93-512-512-512-9",
+                 "wide": "Wide-MLP 4096-4096-4096-1000"}
+        metric = ("samples/sec (whole node) MNIST-MLP 784-128-128-10 sync DP at 1/2/4/8 MI355X"
+                  if args.model == "mnist" else f"samples/sec (whole node) {names[args.model]} sync DP")
+        line = {
+            "metric": metric,
+            "value": round(value, 1),
+            "unit": "samples/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(dt_max / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": args.scaling,
+            "vs_baseline": None,
+            "dtype": "bf16" if args.policy == "mixed_bfloat16" else "fp32",
+            "data": (f"synthetic {args.model.upper()}-shaped ({MODELS[args.model][0][0]} features, "
+                     f"{MODELS[args.model][2]} classes), random-init weights"),
+            "config": {
+                "model": names[args.model],
+                "global_batch": B * W * world,
+                "seq_len": None,
+                "parallelism": f"dp{world}",
+                "ranks": world,
+                "backend": dist.backend(),
+                "workers_per_gpu": W,
+                "workers_total": W * world,
+                "batch_per_worker": B,
+                "rows_per_worker": rows,
+                "sync": m["sync"],
+                "allreduce": path,
+                "allreduce_bytes": nbytes if world > 1 else None,
+                "comm_world_size": dist.world_size(),
+                "rank_devices": devices,
+                "theta_sha1_16": digests[0],
+                "theta_equal_on_all_ranks": all(d == digests[0] for d in digests),
+                "optimizer": "SGD(lr=%g)" % MODELS[args.model][4],
+                "engine": m["engine"],
+                "launches_per_step": launches,   # kernels the timed region issued / steps
+                "native_provenance": provenance,
+                "policy": args.policy,
+                "validation_passes_timed": state["val_passes"],
+                "sub_measurements": subs or None,
+            },
+        }
+        s = json.dumps(line)
+        print(s, flush=True)
+        if args.out:
+            with open(args.out, "a") as f:
+                f.write(s + "\n")
+    if dist.is_initialized():
+        dist.barrier()
+        import torch.distributed as tdist
+        from elephas_amd.parallel import p2p
+        p2p.shutdown()   # peer buffers freed only after every rank is done with them
+        tdist.destroy_process_group()
+
+
+def measure_train(args, model, dist, rank, world, dev, gpu, W, batch_mode, steps, warmup):
+    """One timed training measurement (W workers per GPU, fit or per-step sync
+    granularity): warmup steps, then EXACTLY ``steps`` steps (+ the fit averaging) between
+    a barrier and device synchronisation on both sides; the max over ranks is returned
+    with the evidence fields of the JSON line."""
+    import torch
+    from elephas_amd.ops.plan import build_plan
     plan = build_plan(model)
     dims, drop, classes, rows, _ = MODELS[args.model]
-    if args.scaling == "strong":
-        if 8 % world:
-            raise SystemExit("bench.py --scaling strong: the 8 reference partitions must split evenly over the GPUs")
-        W = 8 // world
-    else:
-        W = args.workers_per_gpu
     B = args.batch
-    batch_mode = args.granularity == "batch"
     # per-step sync DP on ONE GPU: the W workers are replicas of one sync trainer whose
     # gradients are summed every step inside the persistent launch (native_engine sync);
     # across ranks: one replica of the rank's W * B rows and a per-step all-reduce
@@ -274,11 +366,11 @@ def main():
         t.prepare_graphs(allreduce_path=batch_mode and world > 1 and not args.overlap)
     if gpu and args.validation_split > 0:
         t._eval_exe()   # the epoch-end validation executor exists before the timed region
-    run(args.warmup)
+    run(warmup)
     average()
     sync()
     t0 = time.perf_counter()
-    rows_done = run(args.steps)
+    rows_done = run(steps)
     average()
     sync()
     dt = time.perf_counter() - t0
@@ -313,67 +405,15 @@ def main():
     if gpu:
         from elephas_amd.ops import native
         provenance = native.provenance()   # the loaded _C's source digest vs this tree's csrc/
-    if rank == 0:
-        value = samples / dt_max
-        launches = round(t.launches_for(args.steps) / args.steps, 4) if gpu else None
-        names = {"mnist": "MNIST-MLP 784-128-128-10", "otto": "Otto-MLP 93-512-512-512-9",
-                 "wide": "Wide-MLP 4096-4096-4096-1000"}
-        metric = ("samples/sec (whole node) MNIST-MLP 784-128-128-10 sync DP at 1/2/4/8 MI355X"
-                  if args.model == "mnist" else f"samples/sec (whole node) {names[args.model]} sync DP")
-        line = {
-            "metric": metric,
-            "value": round(value, 1),
-            "unit": "samples/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(dt_max / args.steps * 1e3, 4),
-            "higher_is_better": True,
-            "scaling": args.scaling,
-            "vs_baseline": None,
-            "dtype": "bf16" if args.policy == "mixed_bfloat16" else "fp32",
-            "data": (f"synthetic {args.model.upper()}-shaped ({MODELS[args.model][0][0]} features, "
-                     f"{MODELS[args.model][2]} classes), random-init weights"),
-            "config": {
-                "model": names[args.model],
-                "global_batch": B * W * world,
-                "seq_len": None,
-                "parallelism": f"dp{world}",
-                "ranks": world,
-                "backend": dist.backend(),
-                "workers_per_gpu": W,
-                "workers_total": W * world,
-                "batch_per_worker": B,
-                "rows_per_worker": rows,
-                "sync": ("reference (one-shot averaging per fit)" if not batch_mode else
-                         "per-step synchronous DP of the GPU's workers (gradient sum over the replicas every step)"
-                         if sync_local else "per-step gradient all-reduce"),
-                "allreduce": path,
-                "allreduce_bytes": nbytes if world > 1 else None,
-                "comm_world_size": dist.world_size(),
-                "rank_devices": devices,
-                "theta_sha1_16": digests[0],
-                "theta_equal_on_all_ranks": all(d == digests[0] for d in digests),
-                "optimizer": "SGD(lr=%g)" % MODELS[args.model][4],
-                "engine": (("native HIP executor: " if t.persistent else "native HIP executor + hipGraph: ")
-                           + t.plan_name()) if gpu else "torch CPU reference",
-                "launches_per_step": launches,   # kernels the timed region issued / steps
-                "native_provenance": provenance,
-                "policy": args.policy,
-                "validation_passes_timed": state["val_passes"],
-            },
-        }
-        s = json.dumps(line)
-        print(s, flush=True)
-        if args.out:
-            with open(args.out, "a") as f:
-                f.write(s + "\n")
-    if dist.is_initialized():
-        dist.barrier()
-        import torch.distributed as tdist
-        from elephas_amd.parallel import p2p
-        p2p.shutdown()   # peer buffers freed only after every rank is done with them
-        tdist.destroy_process_group()
+    sync_desc = ("reference (one-shot averaging per fit)" if not batch_mode else
+                 "per-step synchronous DP of the GPU's workers (gradient sum over the replicas every step)"
+                 if sync_local else "per-step gradient all-reduce")
+    engine = ((("native HIP executor: " if t.persistent else "native HIP executor + hipGraph: ") + t.plan_name())
+              if gpu else "torch CPU reference")
+    out = dict(t=t, R=R, rows=rows, samples=samples, dt_max=dt_max, state=state, digests=digests, devices=devices,
+               path=path, nbytes=nbytes, batch_mode=batch_mode, sync=sync_desc, engine=engine,
+               theta_equal=all(d == digests[0] for d in digests), W=W)
+    return out
 
 
 def bench_fit(args, model, dist, rank, world, dev):

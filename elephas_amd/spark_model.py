@@ -340,8 +340,14 @@ class SparkModel:
         gran = self.sync_granularity
         epochs = int(train_config.get("epochs", 1))
         verbose = int(train_config.get("verbose", 0))
+        # per-step sync DP on one rank: the partitions are replicas of ONE sync trainer whose
+        # gradients are summed every step (inside the persistent launch on the native
+        # engine) instead of a host-issued all-reduce per step
+        bs = int(train_config.get("batch_size", 32))
+        sync_local = (gran == "batch" and dist.world_size() == 1 and len(local) > 1
+                      and all(len(p) > bs for p in local))
         with self._timer.phase("setup"):
-            trainer, active = worker.prepare_partitions(local)
+            trainer, active = worker.prepare_partitions(local, sync=sync_local)
         start = 0
         if checkpoint_dir and resume and ckpt.exists(checkpoint_dir):
             with self._timer.phase("checkpoint"):
@@ -364,7 +370,8 @@ class SparkModel:
                 self._save_checkpoint(checkpoint_dir, epochs, epochs, mean, trainer, local)
         else:
             mean = None
-            allreduce = self._grad_allreduce(n_parts) if gran == "batch" else None
+            allreduce = (self._grad_allreduce(n_parts) if gran == "batch" and not getattr(trainer, "sync", False)
+                         else None)
             for e in range(start, epochs):
                 if local and any(active):
                     fault.maybe_inject("train", dist.rank())

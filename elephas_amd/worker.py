@@ -169,11 +169,16 @@ class SparkWorker:
         yield [subtract_params(before, after), history]
 
     def prepare_partitions(self, partitions: Sequence[list], engine: Optional[str] = None,
-                           seed: Optional[int] = None):
+                           seed: Optional[int] = None, sync: bool = False):
         """Build the shared executor with one replica per partition and load the
-        shards (no training). Returns (trainer, active)."""
+        shards (no training). Returns (trainer, active). ``sync``: the replicas are one
+        model trained with per-step synchronous DP (native engine; NativeTrainer sync)."""
         from .ops.engine import make_trainer
         bs, epochs, verbose, vs, shuffle = self._cfg()
+        native_kw = {"sync": True} if sync else {}
+        base_engine = engine
+        if sync:   # a sync trainer is cached apart from an independent-replica one
+            engine = f"{engine or ''}|sync"
         xs, ys = [], []
         for p in partitions:
             x, y = partition_to_numpy(p)
@@ -195,7 +200,7 @@ class SparkWorker:
             return trainer, active
         self.model = _build_model(self.json, self.custom_objects, self.master_optimizer, self.master_loss,
                                   self.master_metrics, _value(self.parameters))
-        trainer = make_trainer(self.model, max(1, len(partitions)), bs, engine=engine, seed=seed)
+        trainer = make_trainer(self.model, max(1, len(partitions)), bs, engine=base_engine, seed=seed, **native_kw)
         if partitions:
             trainer.set_data(xs, ys, vs, active=active, shuffle=shuffle)
         _trainer_cache.store(self, len(partitions), engine, trainer, self.model,
