@@ -606,10 +606,12 @@ def bench_async(args, model, dist, rank, world, dev):
     for g in range(G):
         lo, hi = bounds[g], bounds[g + 1]
         t = NativeTrainer(model, plan, hi - lo, B, dev, seed=4321 + 97 * rank + g,
-                          persist_cus=group_persist_cus(G, dev) if G > 1 else None)
+                          persist_cus=group_persist_cus(G, dev) if G > 1 else None, ps_hook=freq == "batch")
         t.set_data(dx[lo:hi], dy[lo:hi], args.validation_split, shuffle=True)
         t.begin_epoch()
         grp = _Group(t, [True] * (hi - lo))
+        if freq == "batch":
+            grp.attach(client)   # push / pull per step inside the persistent launch
         if not args.no_graph:
             if freq == "batch":
                 grp.capture(worker)
@@ -675,6 +677,8 @@ def bench_async(args, model, dist, rank, world, dev):
                        "plan": groups[0].t.plan_name() if hasattr(groups[0].t, "plan_name") else None,
                        "ps": f"sharded over {world} GPU(s), 4096-parameter chunks, IPC-mapped",
                        "exchange": ("pull / push per epoch around hipGraph training chunks" if freq == "epoch"
+                                    else "per step inside the persistent launch (push delta, pull theta; "
+                                         "host pull per chunk)" if getattr(groups[0], "inlaunch", False)
                                     else "hipGraph per group-step (pull, refresh, train, push)" if groups[0].graph
                                     else "eager launches")},
         }

@@ -3,6 +3,8 @@
 #pragma once
 #include <stdint.h>
 
+#include "peer_args.h"
+
 namespace ea {
 
 // ---------------------------------------------------------------- enums ----
@@ -190,7 +192,7 @@ enum PmFlag : int { PMF_PART = 0, PMF_BWD = 1, PMF_W = 2, PMF_A0 = 3, PMF_D2 = 4
 // sticky error codes: the wait that timed out (PERR_GRID: the grid was not resident --
 // nothing was modified, the chunk can be re-run on another plan)
 enum PmErr : unsigned { PERR_L0_BWD = 1, PERR_CHAIN_PART = 2, PERR_CHAIN_BWD = 3, PERR_CHAIN_PREV = 4,
-                        PERR_DW_A0 = 5, PERR_DW_D2 = 6, PERR_XCHG = 7, PERR_GRID = 9 };
+                        PERR_DW_A0 = 5, PERR_DW_D2 = 6, PERR_XCHG = 7, PERR_PS = 8, PERR_GRID = 9 };
 constexpr int PM_XSLOT = 7 * 1024;   // floats of one workgroup's exchange slab (sync)
 struct PersistArgs {
   int R, B, nsteps;
@@ -209,6 +211,14 @@ struct PersistArgs {
   // updates (grad_scale = 1 / R) keep their weights identical
   int sync;
   long long o_xg;                   // exchange slabs [2][wgs][PM_XSLOT] in every replica's workspace
+  // parameter-server hook (V1 roles; async / hogwild frequency='batch', reference
+  // elephas/worker.py:114-127): after its update every owning workgroup pushes its
+  // delta (theta_new - theta_pulled, fp32 atomics into the sharded device PS) and pulls
+  // its slice of theta for the next step, inside the launch.  ps_mode 0 off, 1 hogwild,
+  // 2 asynchronous (a pull never sees a half-applied push of a slice: per-slice
+  // began / ended counters, slice = the owning workgroup's index, in rank 0's flag area)
+  int ps_mode;
+  PsArgs ps;
   int act0, act1, act2;
   float rate0, rate1;
   int bias0, bias1, bias2;

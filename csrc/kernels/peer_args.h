@@ -33,6 +33,7 @@ struct PsArgs {
   long long ctr_off;            // byte offset of the per-chunk began/ended counters
   unsigned long long timeout_ticks;
   int world, rank;
+  long long shard_begin[PEER_MAX_RANKS];   // first parameter of every rank's shard (n past the last)
 };
 
 }  // namespace ea

@@ -79,7 +79,7 @@ struct ChainLds {
   static constexpr int o_gs = o_row + 16;             // [16][65] V2: this chain's Gram rows (+ 1)
   static constexpr int TOTAL = o_gs + 16 * 65;
 };
-constexpr int L0_LDS = 2 * 64 * 129 + 128 * 33 + 64 * 33;
+constexpr int L0_LDS = 2 * 64 * 129 + 128 * 33 + 64 * 33 + 128 * 33;   // + the pulled tile (PS hook)
 constexpr int L0V2_LDS = 2 * 64 * 129 + 128 * 65 + 64 * 65;   // X chunks, W0 tile (cw <= 64), dZ_0 columns
 constexpr int DW_LDS = 64 * 129 + 2 * 64 * 33 + 64 * 17 + 32 * 17;
 constexpr int cmax(int x, int y) { return x > y ? x : y; }
@@ -244,6 +244,76 @@ __device__ __forceinline__ bool xchg_sum(const PersistArgs& a, int r, int q, int
     for (int u = 0; u < N; ++u) v[u] += x[u];
   }
   return true;
+}
+
+// ---- in-launch parameter-server hook (PersistArgs::ps_mode; layout: peer_args.h,
+//      kernels: peer.hip).  theta element i lives in the buffer of the rank owning its
+//      4096-parameter chunk; the memory is uncached (hipDeviceMallocUncached), so plain
+//      loads and system-scope atomics see every rank's latest writes.
+__device__ __forceinline__ float* ps_elem(const PsArgs& ps, long long i) {
+  // the shard holding i, by selects against the (uniform) shard starts: no per-lane
+  // indexing of the kernel-argument array (that would go through scratch)
+  char* b = ps.base[0];
+#pragma unroll
+  for (int rr = 1; rr < PEER_MAX_RANKS; ++rr) b = (rr < ps.world && i >= ps.shard_begin[rr]) ? ps.base[rr] : b;
+  return reinterpret_cast<float*>(b + PEER_DATA_OFF) + i;
+}
+__device__ __forceinline__ unsigned* ps_slice_ctr(const PsArgs& ps, int slice, int which) {
+  // rank 0's flag area (unused by the parameter server's own kernels): 64-byte words
+  return reinterpret_cast<unsigned*>(ps.base[0] + PEER_FLAG_OFF + (long long)which * PEER_MAX_BLOCKS * 64 +
+                                     (long long)slice * 64);
+}
+__device__ __forceinline__ unsigned ps_ld_ctr(const unsigned* c) {
+  return __hip_atomic_load(const_cast<unsigned*>(c), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+// push bracket (asynchronous mode): writers of a slice never wait
+__device__ __forceinline__ void ps_push_begin(const PersistArgs& a, int slice) {
+  if (a.ps_mode == 2 && threadIdx.x == 0)
+    __hip_atomic_fetch_add(ps_slice_ctr(a.ps, slice, 0), 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_SYSTEM);
+  __syncthreads();
+}
+__device__ __forceinline__ void ps_push_end(const PersistArgs& a, int slice) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every wave's atomics are done
+  __syncthreads();
+  if (a.ps_mode == 2 && threadIdx.x == 0)
+    __hip_atomic_fetch_add(ps_slice_ctr(a.ps, slice, 1), 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+// pull: copy(); in asynchronous mode only while no writer is inside the slice (ended ==
+// began before the copy, began unchanged after it), retried otherwise.  false: timed out
+template <typename Copy>
+__device__ __forceinline__ bool ps_pull(const PersistArgs& a, int slice, unsigned* sh, Copy copy) {
+  if (a.ps_mode != 2) {
+    copy();
+    return true;
+  }
+  unsigned& snap_sh = sh[0];   // two words of the caller's LDS
+  unsigned& state_sh = sh[1];
+  const unsigned long long t0 = wall_clock64();
+  for (;;) {
+    if (threadIdx.x == 0) {
+      for (;;) {
+        const unsigned e = ps_ld_ctr(ps_slice_ctr(a.ps, slice, 1));
+        const unsigned b = ps_ld_ctr(ps_slice_ctr(a.ps, slice, 0));
+        if (b == e) { snap_sh = b; break; }
+        if ((long long)(wall_clock64() - t0) > a.timeout) { snap_sh = b; break; }
+        __builtin_amdgcn_s_sleep(1);
+      }
+    }
+    __syncthreads();
+    copy();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the copy's loads complete before the re-check
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const unsigned b2 = ps_ld_ctr(ps_slice_ctr(a.ps, slice, 0));
+      const bool late = (long long)(wall_clock64() - t0) > a.timeout;
+      state_sh = b2 == snap_sh ? 1 : (late ? 2 : 0);
+      if (late && b2 != snap_sh)
+        __hip_atomic_store((gu32*)(a.err), (unsigned)PERR_PS, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (state_sh == 1) return true;
+    if (state_sh == 2) return false;
+  }
 }
 
 __device__ __forceinline__ float dropout_u1(uint32_t base, int row, int c) {
@@ -416,7 +486,7 @@ struct Steps {
 };
 
 // ============================================================== layer-0 tiles
-template <int H0, int NPT>
+template <int H0, int NPT, bool PS>
 __device__ __forceinline__ void l0_role(const PersistArgs& a, float* smem, int r, int kc, int cb, int q) {
   constexpr int XS = 129;                       // X chunk rows (<= 128 columns)
   const int tid = threadIdx.x, lane = tid & 63, i16 = lane & 15, g = lane >> 4;
@@ -431,6 +501,7 @@ __device__ __forceinline__ void l0_role(const PersistArgs& a, float* smem, int r
   float* sX = smem;                             // [2][64][XS] X chunks of two steps
   float* sW = sX + 2 * 64 * XS;                 // [128][WS]  the W0 tile (master, in place)
   float* sdZ = sW + 128 * WS;                   // [64][WS]   dZ_0 columns of this tile
+  float* sWp = sdZ + 64 * 33;                   // [128][WS]  parameter-server hook: the tile as pulled
   __shared__ float sB0[32];
   __shared__ float sRedL[256];
   const rsrc_t rs = ws_rsrc(a.ws + (long long)r * a.ws_stride);
@@ -485,6 +556,15 @@ __device__ __forceinline__ void l0_role(const PersistArgs& a, float* smem, int r
   if (tid < 32) sB0[tid] = 0.f;
   __syncthreads();
   if (bown) sB0[tid] = bw;
+  float bwp = bw;   // parameter-server hook: b0 as pulled
+  if constexpr (PS) {
+    for (int e = tid; e < 128 * WS; e += 256) sWp[e] = sW[e];
+  }
+  // parameter-server hook: the tile's flat parameter indices
+  auto w0_index = [&](int e) -> long long {
+    const int k = e / cw, nn = e - k * cw;
+    return a.p_off0 + (long long)(k0 + k) * H0 + n0 + nn;
+  };
 
   // X chunk of step i into sX buffer (i & 1): LDS-DMA, one 64-column row segment per
   // wave instruction (rows past the valid batch repeat its first row: finite values
@@ -633,6 +713,48 @@ __device__ __forceinline__ void l0_role(const PersistArgs& a, float* smem, int r
       }
     }
     __syncthreads();
+    if constexpr (PS) {
+      // reference worker.py:114-127 per batch: push theta_new - theta_pulled of this tile
+      // (and b0), then pull the tile of theta for the next step
+      ps_push_begin(a, q);
+      for (int e = tid; e < kreal * cw; e += 256) {
+        const int k = e / cw, nn = e - k * cw;
+        const float dlt = sW[k * WS + nn] - sWp[k * WS + nn];
+        if (dlt != 0.f) __hip_atomic_fetch_add(ps_elem(a.ps, w0_index(e)), dlt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+      if (bown && bw != bwp)
+        __hip_atomic_fetch_add(ps_elem(a.ps, a.p_off0 + (long long)a.K0 * H0 + n0 + tid), bw - bwp, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+      ps_push_end(a, q);
+      if (nxt) {
+        const bool ok = ps_pull(a, q, reinterpret_cast<unsigned*>(sRedL), [&]() {
+          for (int base = 0; base < kreal * cw; base += 8 * 256) {
+            float v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+              const int e = base + tid + 256 * u;
+              v[u] = *ps_elem(a.ps, w0_index(e < kreal * cw ? e : 0));
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+              const int e = base + tid + 256 * u;
+              if (e < kreal * cw) {
+                const int k = e / cw, nn = e - k * cw;
+                sW[k * WS + nn] = v[u];
+                sWp[k * WS + nn] = v[u];
+              }
+            }
+          }
+          if (bown) {
+            bw = *ps_elem(a.ps, a.p_off0 + (long long)a.K0 * H0 + n0 + tid);
+            bwp = bw;
+          }
+        });
+        if (!ok) return;
+        if (bown) sB0[tid] = bw;
+        __syncthreads();
+      }
+    }
     pstamp(a, i, 5);
     if (nxt) fwd(i + 1);
     pstamp(a, i, 6);
@@ -966,7 +1088,7 @@ __device__ __forceinline__ void rows_mm(const float* A, const float* B, int ct0,
 // owns W1 / W2), the layer-0 pre-activations of step i >= 1 are rebuilt from the L0
 // workgroups' Pold / Gram slabs and the previous step's dZ_0 rows of every chain
 // workgroup (l0_role_v2), and two more flags (A0, D2) hand the rows the DW workgroups need.
-template <int H0, int H1, bool FAST, int NPT, bool RELU, bool V2>
+template <int H0, int H1, bool FAST, int NPT, bool RELU, bool V2, bool PS>
 __device__ __forceinline__ void chain_role(const PersistArgs& a, float* smem, int r, int j) {
   using Lo = ChainLds<H0, H1>;
   constexpr int L0S = Lo::L0S, L1S = Lo::L1S;
@@ -1071,6 +1193,23 @@ __device__ __forceinline__ void chain_role(const PersistArgs& a, float* smem, in
     bst0 = np > 0 ? S[pi] : 0.f;
     bst1 = np > 1 ? S[a.op.s_plane + pi] : 0.f;
   }
+  // parameter-server hook: the owned masters as pulled, and their flat indices (-1: none)
+  float wpl[PS ? NM : 1], bpl = bm;
+  if constexpr (PS) {
+#pragma unroll
+    for (int e = 0; e < NM; ++e) wpl[e] = wm[e];
+  }
+  auto chain_index = [&](int u, int qq) -> long long {
+    if (u < TU) {
+      const int t = w + 4 * u;
+      if (t >= ndw1) return -1;
+      const int rt = t / nown, c = t - rt * nown;
+      return a.p_off1 + (long long)(rt * 16 + 4 * g + qq) * H1 + (j + a.nch * c) * 16 + i16;
+    }
+    if (!(w2own && i16 < C)) return -1;
+    return a.p_off2 + (long long)((j + a.nch * w) * 16 + 4 * g + qq) * C + i16;
+  };
+  const long long bias_index = b1own ? a.p_off1 + (long long)H0 * H1 + b1n : a.p_off2 + (long long)H1 * C + lane;
   __syncthreads();
   // every workgroup of the grid resident before any state (metric sums, hand-offs that
   // lead to weight updates) is touched: otherwise give up with PERR_GRID, state intact
@@ -1498,6 +1637,49 @@ __device__ __forceinline__ void chain_role(const PersistArgs& a, float* smem, in
     }
     pstamp(a, i, 9);
     const bool nxt = i + 1 < n && st.valid(a, i + 1) > 0;
+    if constexpr (PS) {
+      // parameter-server hook: push the owned columns' theta_new - theta_pulled, then pull
+      // them for the next step (published to the other chain workgroups below)
+      ps_push_begin(a, nl0 + j);
+#pragma unroll
+      for (int u = 0; u <= TU; ++u) {
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq) {
+          const long long idx = chain_index(u, qq);
+          const float dlt = wm[4 * u + qq] - wpl[4 * u + qq];
+          if (idx >= 0 && dlt != 0.f)
+            __hip_atomic_fetch_add(ps_elem(a.ps, idx), dlt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+      }
+      if ((b1own || b2own) && bm != bpl) __hip_atomic_fetch_add(ps_elem(a.ps, bias_index), bm - bpl, __ATOMIC_RELAXED,
+                                                                 __HIP_MEMORY_SCOPE_SYSTEM);
+      ps_push_end(a, nl0 + j);
+      if (nxt) {
+        const bool ok = ps_pull(a, nl0 + j, reinterpret_cast<unsigned*>(sRed), [&]() {
+          float v[NM];
+#pragma unroll
+          for (int u = 0; u <= TU; ++u) {
+#pragma unroll
+            for (int qq = 0; qq < 4; ++qq) {
+              const long long idx = chain_index(u, qq);
+              v[4 * u + qq] = *ps_elem(a.ps, idx >= 0 ? idx : a.p_off1);
+            }
+          }
+#pragma unroll
+          for (int e = 0; e < NM; ++e) {
+            if (chain_index(e >> 2, e & 3) >= 0) {
+              wm[e] = v[e];
+              wpl[e] = v[e];
+            }
+          }
+          if (b1own || b2own) {
+            bm = *ps_elem(a.ps, bias_index);
+            bpl = bm;
+          }
+        });
+        if (!ok) return;
+      }
+    }
     if (!nxt) break;
     // ---- publish the owned weights, gather everyone's into LDS for the next step
 #pragma unroll
@@ -1787,7 +1969,7 @@ __device__ __forceinline__ void dw_role_v2(const PersistArgs& a, float* smem, in
 
 }  // namespace
 
-template <int H0, int H1, bool FAST, int NPT, bool RELU, bool V2>
+template <int H0, int H1, bool FAST, int NPT, bool RELU, bool V2, bool PS = false>
 __global__ __launch_bounds__(256) void mlp_persist_kernel(PersistArgs a) {
   __shared__ __attribute__((aligned(16))) float smem[LDS_FLOATS];
   if (__hip_atomic_load((gu32*)(a.err), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) return;
@@ -1803,13 +1985,13 @@ __global__ __launch_bounds__(256) void mlp_persist_kernel(PersistArgs a) {
       if (a.cw == 64) l0_role_v2<H0, 4>(a, smem, r, kc, cb, q);
       else l0_role_v2<H0, 2>(a, smem, r, kc, cb, q);
     } else if (q < nl0 + a.nch) {
-      chain_role<H0, H1, FAST, NPT, RELU, true>(a, smem, r, q - nl0);
+      chain_role<H0, H1, FAST, NPT, RELU, true, false>(a, smem, r, q - nl0);
     } else {
       dw_role_v2<H0, H1>(a, smem, r, q - nl0 - a.nch);
     }
   } else {
-    if (q < nl0) l0_role<H0, NPT>(a, smem, r, q / a.nc0, q - (q / a.nc0) * a.nc0, q);
-    else chain_role<H0, H1, FAST, NPT, RELU, false>(a, smem, r, q - nl0);
+    if (q < nl0) l0_role<H0, NPT, PS>(a, smem, r, q / a.nc0, q - (q / a.nc0) * a.nc0, q);
+    else chain_role<H0, H1, FAST, NPT, RELU, false, PS>(a, smem, r, q - nl0);
   }
 }
 
@@ -1827,6 +2009,10 @@ hipError_t persist_launch(const PersistArgs* a, hipStream_t s) {
   if (a->v2) {   // the host checked plain SGD + ReLU
     if (fast) hipLaunchKernelGGL((mlp_persist_kernel<H, H, true, 0, true, true>), grid, dim3(256), 0, s, *a);
     else hipLaunchKernelGGL((mlp_persist_kernel<H, H, false, 0, true, true>), grid, dim3(256), 0, s, *a);
+  } else if (a->ps_mode) {   // V1 with the in-launch parameter-server exchange
+    if (fast && relu && sgd) hipLaunchKernelGGL((mlp_persist_kernel<H, H, true, 0, true, false, true>), grid, dim3(256), 0, s, *a);
+    else if (fast) hipLaunchKernelGGL((mlp_persist_kernel<H, H, true, -1, false, false, true>), grid, dim3(256), 0, s, *a);
+    else hipLaunchKernelGGL((mlp_persist_kernel<H, H, false, -1, false, false, true>), grid, dim3(256), 0, s, *a);
   } else if (fast && relu && sgd) {
     hipLaunchKernelGGL((mlp_persist_kernel<H, H, true, 0, true, false>), grid, dim3(256), 0, s, *a);
   } else if (fast) {

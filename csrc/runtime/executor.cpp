@@ -185,6 +185,13 @@ std::vector<int> Executor::persist_geometry() const {
   return {a.nk0, a.nc0, a.kc0, a.cw, a.nch, a.wgs, a.R * a.wgs};
 }
 
+bool Executor::set_param_server(const PsArgs& ps, int mode) {
+  if (!pm_.on || pm_.args.v2 || pm_.args.sync) return mode == 0;
+  pm_.args.ps = ps;
+  pm_.args.ps_mode = mode;
+  return true;
+}
+
 std::vector<int> Executor::persist_variant() const {
   if (!pm_.on) return {};
   return {pm_.args.v2 ? 2 : 1, pm_.args.nd, pm_.args.sync};

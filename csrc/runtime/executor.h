@@ -128,6 +128,10 @@ class Executor {
   // workgroups, workgroups per replica, grid}
   std::vector<int> persist_geometry() const;
   std::vector<int> persist_variant() const;   // {1 or 2, DW workgroups per replica, sync}
+  // parameter-server hook of the persistent plan (V1 roles only): every step pushes the
+  // owned parameters' deltas into the server and pulls the next step's (mode 1 hogwild,
+  // 2 asynchronous, 0 off); false when the plan cannot (not persistent, or V2 roles)
+  bool set_param_server(const PsArgs& ps, int mode);
   unsigned persist_error() const;  // sticky error word (a timed-out in-launch wait), synchronous read
   void persist_clear_error();
   int rowchain_split() const { return rc_.on ? rc_.nsplitk : 0; }

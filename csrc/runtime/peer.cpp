@@ -171,6 +171,7 @@ PsArgs ShardedParameterServer::args() const {
   a.timeout_ticks = timeout_ticks_;
   a.world = buf_.world();
   a.rank = buf_.rank();
+  for (int r = 0; r < PEER_MAX_RANKS; ++r) a.shard_begin[r] = r < a.world ? shard_begin(r) : n_;
   return a;
 }
 

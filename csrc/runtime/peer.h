@@ -107,6 +107,8 @@ class ShardedParameterServer {
   int consistent() const { return consistent_; }
   long long nchunks() const { return nchunks_; }
   long long shard_begin(int r) const;                 // first parameter owned by rank r
+  // the kernel view of the server (a persistent step kernel's in-launch hook, persist.hip)
+  PsArgs kernel_args() const { return args(); }
 
  private:
   static long long padded(long long n) { return (n + 3) / 4 * 4 + 4; }

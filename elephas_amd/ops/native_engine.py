@@ -109,7 +109,7 @@ class NativeTrainer(TrainerBase):
     def __init__(self, model, plan, R: int = 1, batch_size: int = 32, device=None, seed: Optional[int] = None,
                  policy: Optional[str] = None, eval_batch: int = 2048, rowchain: Optional[int] = None,
                  persist: Optional[int] = None, stream: Optional[torch.cuda.Stream] = None,
-                 persist_cus: Optional[int] = None, sync: bool = False):
+                 persist_cus: Optional[int] = None, sync: bool = False, ps_hook: bool = False):
         super().__init__(model, plan, R, batch_size)
         self.C = native.require()
         # sync: the R replicas are ONE model trained with per-step synchronous data
@@ -119,6 +119,10 @@ class NativeTrainer(TrainerBase):
         # xchg_sum); otherwise forward/backward -> replica sum -> apply per step.
         self.sync = bool(sync) and R > 1
         self._grad_scale = 1.0
+        # ps_hook: the persistent plan will push / pull a device parameter server every
+        # step inside the launch (attach_param_server), so it keeps the V1 roles
+        self.ps_hook = bool(ps_hook)
+        self._ps = None
         # row-chain step plan (3 launches, csrc/kernels/rowchain.hip): None ->
         # $ELEPHAS_AMD_ROWCHAIN (default -1: whenever the model is eligible), 0 off, 1 required
         self.rowchain_mode = int(os.environ.get("ELEPHAS_AMD_ROWCHAIN", "-1")) if rowchain is None else int(rowchain)
@@ -249,7 +253,7 @@ class NativeTrainer(TrainerBase):
             persist=self.persist_mode if ws is self.ws else 0,
             persist_timeout_ms=int(os.environ.get("ELEPHAS_AMD_PERSIST_TIMEOUT_MS", "2000")),
             persist_cus=self.persist_cus,
-            persist_v2=int(os.environ.get("ELEPHAS_AMD_PERSIST_V2", "-1")),
+            persist_v2=0 if self.ps_hook else int(os.environ.get("ELEPHAS_AMD_PERSIST_V2", "-1")),
             persist_sync=int(self.sync) if ws is self.ws else 0,
             rc_split=int(os.environ.get("ELEPHAS_AMD_RC_SPLIT", "0")),
             tail=int(os.environ.get("ELEPHAS_AMD_TAIL", "-1")) if ws is self.ws else 0,
@@ -275,6 +279,25 @@ class NativeTrainer(TrainerBase):
         self._graphs = {}
         self.exe = self.C.Executor(self._cfg(self.ws))
         self.GRAPH_CHUNK = self.PERSIST_CHUNK if self.exe.persistent() else type(self).GRAPH_CHUNK
+        if self._ps is not None and not self.exe.set_param_server(*self._ps):
+            self._ps = None   # the rebuilt plan cannot (e.g. the row-chain fallback): host-side exchange
+
+    def attach_param_server(self, ps, consistent: bool) -> bool:
+        """Per-step parameter-server exchange INSIDE the persistent launch (reference
+        worker.py:114-127 frequency='batch': pull, train_on_batch, push): after every
+        step each owning workgroup pushes theta_new - theta_pulled of its parameters into
+        the sharded device server and pulls its slice for the next step.  The host then
+        only pulls theta into P before each chunk.  Returns False when the plan cannot
+        (not persistent / V2 roles): the caller keeps the per-step host-side rounds."""
+        mode = 2 if consistent else 1
+        if not self.exe.persistent() or not self.exe.set_param_server(ps, mode):
+            return False
+        self._ps = (ps, mode)
+        return True
+
+    @property
+    def param_server_in_launch(self) -> bool:
+        return self._ps is not None
 
     def _eval_exe(self):
         if self.exe_eval is None:

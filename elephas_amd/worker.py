@@ -388,14 +388,19 @@ class BatchedAsynchronousWorker:
             xs, ys = zip(*data[bounds[g]:bounds[g + 1]])
             # several groups run concurrently on their own streams: each persistent grid
             # gets its share of the CUs so all of them are resident at once
-            t = make_trainer(self.model, len(xs), bs, engine="native",
-                             **({"persist_cus": group_persist_cus(G)} if G > 1 else {}))
+            kw = {"persist_cus": group_persist_cus(G)} if G > 1 else {}
+            if self.frequency == "batch":
+                kw["ps_hook"] = True   # the per-batch exchange inside the persistent launch
+            t = make_trainer(self.model, len(xs), bs, engine="native", **kw)
             active = [len(x) > bs for x in xs]   # inactive replicas push a zero delta
             if self.frequency == "epoch":
                 t.set_data(list(xs), list(ys), vs, active=active, shuffle=True)
             else:
                 t.set_data(list(xs), list(ys), 0.0, active=active, shuffle=False)
-            groups.append(_Group(t, active))
+            grp = _Group(t, active)
+            if self.frequency == "batch":
+                grp.attach(self.client)
+            groups.append(grp)
         if self.frequency == "epoch":
             for e in range(epochs):
                 for g in groups:          # enqueue every group's epoch, then read histories
@@ -498,10 +503,26 @@ class _Group:
     def graph(self):
         return bool(self.graphs)
 
+    def attach(self, client):
+        """frequency='batch' on the persistent plan: the server's push / pull per step runs
+        inside the launch (NativeTrainer.attach_param_server); the host pulls theta
+        into the masters once per chunk. ELEPHAS_AMD_ASYNC_INLAUNCH=0 keeps host rounds."""
+        self.inlaunch = False
+        ps = getattr(client, "ps", None)
+        if (ps is None or os.environ.get("ELEPHAS_AMD_ASYNC_INLAUNCH", "1") == "0"
+                or not hasattr(self.t, "attach_param_server")):
+            return
+        from .parallel import fault
+        if fault.injection_active():
+            return
+        self.inlaunch = bool(self.t.attach_param_server(ps, bool(ps.consistent)))
+
     def capture(self, worker):
         """Capture the CHUNK-round and 1-round graphs; eager launches (logged) if capture fails."""
         import torch
         from .parallel import fault
+        if getattr(self, "inlaunch", False):
+            return   # one persistent launch per chunk, exchange inside it
         if os.environ.get("ELEPHAS_AMD_ASYNC_GRAPH", "1") == "0" or fault.injection_active():
             return
         try:
@@ -528,6 +549,15 @@ class _Group:
     def steps(self, worker, n):
         """Enqueue n pull/step/push rounds (no host synchronisation)."""
         import torch
+        if getattr(self, "inlaunch", False):
+            # one host pull of theta into every replica's masters per persistent chunk; the
+            # kernel pushes each step's delta and pulls the next step's theta itself
+            while n > 0:
+                k = min(n, self.t.GRAPH_CHUNK)
+                worker._pull(self)
+                self.t.run_steps(k)
+                n -= k
+            return
         if self.graphs:
             full, rest = divmod(n, self.CHUNK)
             with torch.cuda.stream(self.t.stream):
