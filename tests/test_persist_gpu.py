@@ -302,3 +302,88 @@ def test_persist_sync_replicas_match_eager_exchange(opt):
     assert np.abs(wp - we).max() <= 1e-4 * scale, (np.abs(wp - we).max(), scale)
     for a, b in zip(hp, he):
         np.testing.assert_allclose(a["loss"], b["loss"], rtol=5e-4, atol=5e-4)
+
+
+@pytest.mark.parametrize("mode", ["asynchronous", "hogwild"])
+def test_async_inlaunch_single_worker_equals_plain_training(mode):
+    """frequency='batch' with the exchange inside the persistent launch (every step each
+    owning workgroup pushes theta_new - theta_pulled into the device PS and pulls its
+    slice for the next step; the host pulls once per chunk): with ONE worker the server
+    always returns that worker's own latest weights, so the run equals plain V1 training
+    on the same batches, across launch boundaries (chunks of 8 steps)."""
+    from elephas_amd.models import initializers
+    from elephas_amd.models.optimizers import SGD
+    from elephas_amd.ops.plan import build_plan, flatten_weights
+    from elephas_amd.ops.native_engine import NativeTrainer
+    from elephas_amd.parameter.client import DeviceClient
+    from elephas_amd.worker import BatchedAsynchronousWorker, _Group
+    from elephas_amd import config
+    config.set_policy("float32")
+    initializers.set_seed(41)
+    model = _mlp(784, [128, 128], 10, dropout=0.2)
+    model.compile(SGD(0.1), "categorical_crossentropy", ["acc"])
+    xs, ys = _shards([64 * 30], 784, 10, seed=17)
+    init = flatten_weights(model.get_weights())
+    client = DeviceClient().connect(len(init), mode, rank=0, world=1, allgather=lambda h: [h])
+    th = torch.from_numpy(init).cuda()
+    torch.cuda.synchronize()
+    client.ps.set(th.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    t = NativeTrainer(model, build_plan(model), 1, 64, torch.device("cuda"), seed=3, ps_hook=True)
+    assert t.persistent and t.persist_variant == 1, t.plan_name()
+    t.set_data(xs, ys, 0.0, shuffle=False)
+    t.GRAPH_CHUNK = 8
+    grp = _Group(t, [True])
+    grp.attach(client)
+    assert grp.inlaunch
+    worker = BatchedAsynchronousWorker(None, None, client, {}, "batch", None, None, None, None)
+    t.begin_epoch()
+    grp.steps(worker, 27)
+    torch.cuda.synchronize()
+    t.check()
+    got = torch.empty(len(init), dtype=torch.float32, device="cuda")
+    client.ps.pull(got.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert client.ps.error() == 0
+    import os
+    os.environ["ELEPHAS_AMD_PERSIST_V2"] = "0"
+    try:
+        ref = NativeTrainer(model, build_plan(model), 1, 64, torch.device("cuda"), seed=3, persist=1)
+    finally:
+        del os.environ["ELEPHAS_AMD_PERSIST_V2"]
+    ref.set_data(xs, ys, 0.0, shuffle=False)
+    ref.begin_epoch()
+    ref.run_steps(27)
+    wr = ref.get_weights_flat()[0]
+    step = np.abs(wr - init).max()
+    err = np.abs(got.cpu().numpy() - wr).max()
+    assert err <= 1e-5 * step + 1e-7, (err, step)
+
+
+@pytest.mark.parametrize("mode", ["asynchronous", "hogwild"])
+def test_spark_model_async_batch_inlaunch_learns(mode):
+    """SparkModel(mode, frequency='batch') on the fp32 persistent plan: four partitions as
+    four concurrently running worker groups, each pushing / pulling the device PS every
+    step inside its persistent launch; the master network learns, the distributed
+    evaluate agrees with the master's (reference tests/integration/test_end_to_end.py)."""
+    from elephas_amd import config
+    from elephas_amd.data import SparkContext
+    from elephas_amd.models import initializers
+    from elephas_amd.models.optimizers import SGD
+    from elephas_amd.spark_model import SparkModel
+    from elephas_amd.utils.rdd_utils import to_simple_rdd
+    from elephas_amd.models.datasets import synthetic_classification
+    config.set_policy("float32")
+    initializers.set_seed(6)
+    x, yi = synthetic_classification(4096, 784, 10, seed=2)
+    x = (x / 10).astype(np.float32)
+    y = np.eye(10, dtype=np.float32)[yi]
+    model = _mlp(784, [128, 128], 10, dropout=0.2)
+    model.compile(SGD(learning_rate=0.05), "categorical_crossentropy", ["acc"])
+    acc0 = model.evaluate(x, y)[1]
+    sm = SparkModel(model, mode=mode, frequency="batch", parameter_server_mode="device", num_workers=4)
+    sm.fit(to_simple_rdd(SparkContext.getOrCreate(), x, y), epochs=3, batch_size=64, verbose=0)
+    ev = sm.evaluate(x, y)
+    ref = sm.master_network.evaluate(x, y)
+    assert np.allclose(ev, ref, atol=0.01), (ev, ref)
+    assert np.isfinite(ev).all() and ref[1] > max(0.6, acc0 + 0.3), (acc0, ref)
