@@ -219,6 +219,7 @@ struct PersistArgs {
   // began / ended counters, slice = the owning workgroup's index, in rank 0's flag area)
   int ps_mode;
   PsArgs ps;
+  int bf16;                         // V2 only: X and the weight images are bf16 (mixed_bfloat16 policy)
   int act0, act1, act2;
   float rate0, rate1;
   int bias0, bias1, bias2;

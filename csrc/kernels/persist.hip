@@ -90,6 +90,38 @@ __device__ __forceinline__ f32x4 mma(float a, float b, f32x4 c) {
 }
 __device__ __forceinline__ f32x4 zero4f() { return f32x4{0.f, 0.f, 0.f, 0.f}; }
 
+// mixed_bfloat16 policy (BF instances): every MFMA operand rounded to bf16 (round to
+// nearest even) at its fragment load -- a bf16 x bf16 product is exact in fp32, so the
+// fp32 MFMA on rounded operands gives the numerics of a bf16 MFMA with fp32 accumulation
+// (the latency-bound step gains nothing from the faster bf16 matrix rate; the data shard
+// itself is bf16, half the bytes per step)
+template <bool BF>
+__device__ __forceinline__ float rb(float x) {
+  if constexpr (BF) {
+    const unsigned u = __builtin_bit_cast(unsigned, x);
+    return __builtin_bit_cast(float, (u + 0x7fffu + ((u >> 16) & 1u)) & 0xffff0000u);
+  } else {
+    return x;
+  }
+}
+// one element of a bf16 row packed two per dword in LDS (element k of a row at dword k / 2)
+__device__ __forceinline__ float bf_at(const float* row, int k) {
+  const unsigned d = __builtin_bit_cast(unsigned, row[k >> 1]);
+  return __builtin_bit_cast(float, (k & 1) ? (d & 0xffff0000u) : (d << 16));
+}
+// replica r's weight image (elements of the compute dtype), as the float* img_store takes
+template <bool BF>
+__device__ __forceinline__ float* img_base(float* base, long long off) {
+  if constexpr (BF) return reinterpret_cast<float*>(reinterpret_cast<__bf16*>(base) + off);
+  else return base + off;
+}
+// weight-image store in the trainer's compute dtype
+template <bool BF>
+__device__ __forceinline__ void img_store(float* base, long long i, float v) {
+  if constexpr (BF) reinterpret_cast<__bf16*>(base)[i] = (__bf16)v;
+  else base[i] = v;
+}
+
 // ---- write-through (sc1) accesses of handed-off bytes through a buffer resource of
 //      the replica's workspace: per-lane offset v + uniform offset s (SGPR), in floats
 __device__ __forceinline__ rsrc_t ws_rsrc(const float* base) {
@@ -806,10 +838,12 @@ __device__ __forceinline__ void l0_role(const PersistArgs& a, float* smem, int r
 // dZ0_{s-1} rows they hand to each other.  dZ0 reaches this workgroup only for the
 // update of its tile (DW0 = X^T dZ0), which is off the step's critical path.
 // Step 0 is the direct product; buffers of step s live in parity s & 1.
-template <int H0, int NCT>
+template <int H0, int NCT, bool BF>
 __device__ __forceinline__ void l0_role_v2(const PersistArgs& a, float* smem, int r, int kc, int cb, int q) {
   static_assert(NCT == 2 || NCT == 4, "column blocks of 32 or 64");
-  constexpr int XS = 129, CW = NCT * 16, WS = CW + 1, TU0 = 2 * NCT;   // DW0 tiles per wave (<= 8 row tiles)
+  // X rows in LDS: fp32 (stride 129 floats), or bf16 packed two per dword (stride 65 dwords)
+  constexpr int XS = BF ? 65 : 129, CW = NCT * 16, WS = CW + 1, TU0 = 2 * NCT;   // DW0 tiles per wave (<= 8 row tiles)
+  auto xat = [](const float* row, int k) -> float { if constexpr (BF) return bf_at(row, k); else return row[k]; };
   const int tid = threadIdx.x, lane = tid & 63, i16 = lane & 15, g = lane >> 4;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6) & 3;
   const int k0 = kc * a.kc0;
@@ -819,7 +853,7 @@ __device__ __forceinline__ void l0_role_v2(const PersistArgs& a, float* smem, in
   const int nrt = (kreal + 15) >> 4, ntiles = nrt * NCT;
   const int BR = a.nch * 16;
   float* sX = smem;                             // [2][64][XS] X chunks (steps of parity 0 / 1)
-  float* sW = sX + 2 * 64 * XS;                 // [128][WS]   the W0 tile (master, in place)
+  float* sW = sX + 2 * 64 * 129;                // [128][WS]   the W0 tile (master, in place)
   float* sdZ = sW + 128 * WS;                   // [64][WS]    dZ_0 columns of this tile
   __shared__ float sB0[64];
   __shared__ float sBg[64];
@@ -869,10 +903,16 @@ __device__ __forceinline__ void l0_role_v2(const PersistArgs& a, float* smem, in
       const int b = w + 4 * v;
       if (b >= BR) break;
       const int row = __builtin_amdgcn_readlane(myrow, b);
-      const float* src = Xr + (long long)row * a.ldx;
+      if constexpr (BF) {   // bf16 shard: one dword (two elements) per lane, <= 128 elements per row
+        const float* src = reinterpret_cast<const float*>(reinterpret_cast<const __bf16*>(a.X) +
+                                                          (long long)r * a.sX + (long long)row * a.ldx + k0);
+        if (lane < (kreal + 1) / 2) __builtin_amdgcn_global_load_lds(src + lane, dst + b * XS, 4, 0, 0);
+      } else {
+        const float* src = Xr + (long long)row * a.ldx;
 #pragma unroll
-      for (int h = 0; h < 2; ++h)
-        if (64 * h + lane < kreal) __builtin_amdgcn_global_load_lds(src + 64 * h + lane, dst + b * XS + 64 * h, 4, 0, 0);
+        for (int h = 0; h < 2; ++h)
+          if (64 * h + lane < kreal) __builtin_amdgcn_global_load_lds(src + 64 * h + lane, dst + b * XS + 64 * h, 4, 0, 0);
+      }
     }
   };
 
@@ -890,9 +930,9 @@ __device__ __forceinline__ void l0_role_v2(const PersistArgs& a, float* smem, in
 #pragma unroll
         for (int ks = 0; ks < 16; ++ks) {
           const int k = kb + 16 * g + ks;
-          av[ks] = arow[k];
+          av[ks] = xat(arow, k);
 #pragma unroll
-          for (int jj = 0; jj < NCT; ++jj) bv[jj][ks] = sW[k * WS + jj * 16 + i16];
+          for (int jj = 0; jj < NCT; ++jj) bv[jj][ks] = rb<BF>(sW[k * WS + jj * 16 + i16]);
         }
 #pragma unroll
         for (int ks = 0; ks < 16; ++ks) {
@@ -931,8 +971,8 @@ __device__ __forceinline__ void l0_role_v2(const PersistArgs& a, float* smem, in
 #pragma unroll
         for (int ks = 0; ks < 16; ++ks) {
           const int k = kb + 16 * g + ks;
-          av[ks] = arow[k];
-          bv[ks] = brow[k];
+          av[ks] = xat(arow, k);
+          bv[ks] = xat(brow, k);
         }
 #pragma unroll
         for (int ks = 0; ks < 16; ++ks) acc = mma(av[ks], bv[ks], acc);
@@ -968,6 +1008,10 @@ __device__ __forceinline__ void l0_role_v2(const PersistArgs& a, float* smem, in
     stage<NCT>(rs, (int)(a.o_dz0 + (i & 1) * a.dz0_par) + n0, H0, BR, CW, sdZ, WS);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    if constexpr (BF) {   // the weight gradient's dZ_0 operand (and the bias sums) in bf16
+      for (int e = tid; e < 64 * WS; e += 256) sdZ[e] = rb<true>(sdZ[e]);
+      __syncthreads();
+    }
     pstamp(a, i, 4);
     // DW0 tile = X_i^T dZ_0 (reduction over the batch rows), SGD update in place
     {
@@ -985,7 +1029,7 @@ __device__ __forceinline__ void l0_role_v2(const PersistArgs& a, float* smem, in
           const int b = 16 * g + 8 * half + h8;
           zb[h8] = sdZ[b * WS + ctw * 16 + i16];
 #pragma unroll
-          for (int u = 0; u < TU0; ++u) xa[u][h8] = Xi[b * XS + rt[u] * 16 + i16];
+          for (int u = 0; u < TU0; ++u) xa[u][h8] = xat(Xi + b * XS, rt[u] * 16 + i16);
         }
         // branch-free: tiles past ntiles compute garbage that is never stored
 #pragma unroll
@@ -1037,16 +1081,16 @@ __device__ __forceinline__ void l0_role_v2(const PersistArgs& a, float* smem, in
 
   // ---- epilogue: master tile and both weight-image parities (plain SGD: no state)
   __syncthreads();
-  float* Wsh = a.Wsh + (long long)r * a.sWsh + a.wsh_off[0];
-  float* WTsh = a.WTsh + (long long)r * a.sWTsh + a.wtsh_off[0];
+  float* Wsh = img_base<BF>(a.Wsh, (long long)r * a.sWsh + a.wsh_off[0]);
+  float* WTsh = img_base<BF>(a.WTsh, (long long)r * a.sWTsh + a.wtsh_off[0]);
   for (int e = tid; e < kreal * CW; e += 256) {
     const int k = e / CW, nn = e - k * CW;
     const float v = sW[k * WS + nn];
     P[a.p_off0 + (long long)(k0 + k) * H0 + n0 + nn] = v;
 #pragma unroll
     for (int par = 0; par < 2; ++par) {
-      Wsh[par * a.wsh_par + (long long)(k0 + k) * a.Np[0] + n0 + nn] = v;
-      WTsh[par * a.wtsh_par + (long long)(n0 + nn) * a.Kp[0] + k0 + k] = v;
+      img_store<BF>(Wsh, par * a.wsh_par + (long long)(k0 + k) * a.Np[0] + n0 + nn, v);
+      img_store<BF>(WTsh, par * a.wtsh_par + (long long)(n0 + nn) * a.Kp[0] + k0 + k, v);
     }
   }
   if (bown) P[a.p_off0 + (long long)a.K0 * H0 + n0 + tid] = bw;
@@ -1056,7 +1100,7 @@ __device__ __forceinline__ void l0_role_v2(const PersistArgs& a, float* smem, in
 // acc[jj] (jj < 2: column tiles ct0 + 4jj) += A[16][K] . B[K][16 cols], fragments from
 // LDS: A(i, k) = A[i * SAI + k], B(k, n) = B[k * SBK + n * SBN]; the 16 fragments of a
 // 64-deep block are read before its MFMAs
-template <int K, int SAI, int SBK, int SBN>
+template <int K, int SAI, int SBK, int SBN, bool BF = false>
 __device__ __forceinline__ void rows_mm(const float* A, const float* B, int ct0, int nct, f32x4 (&acc)[2], int i16,
                                         int g) {
   acc[0] = zero4f();
@@ -1072,9 +1116,9 @@ __device__ __forceinline__ void rows_mm(const float* A, const float* B, int ct0,
 #pragma unroll
     for (int ks = 0; ks < 16; ++ks) {
       const int k = kb + 16 * g + ks;
-      av[ks] = arow[k];
-      bv0[ks] = b0[k * SBK];
-      bv1[ks] = b1[k * SBK];
+      av[ks] = rb<BF>(arow[k]);
+      bv0[ks] = rb<BF>(b0[k * SBK]);
+      bv1[ks] = rb<BF>(b1[k * SBK]);
     }
 #pragma unroll
     for (int ks = 0; ks < 16; ++ks) {
@@ -1088,7 +1132,7 @@ __device__ __forceinline__ void rows_mm(const float* A, const float* B, int ct0,
 // owns W1 / W2), the layer-0 pre-activations of step i >= 1 are rebuilt from the L0
 // workgroups' Pold / Gram slabs and the previous step's dZ_0 rows of every chain
 // workgroup (l0_role_v2), and two more flags (A0, D2) hand the rows the DW workgroups need.
-template <int H0, int H1, bool FAST, int NPT, bool RELU, bool V2, bool PS>
+template <int H0, int H1, bool FAST, int NPT, bool RELU, bool V2, bool PS, bool BF = false>
 __device__ __forceinline__ void chain_role(const PersistArgs& a, float* smem, int r, int j) {
   using Lo = ChainLds<H0, H1>;
   constexpr int L0S = Lo::L0S, L1S = Lo::L1S;
@@ -1290,7 +1334,7 @@ __device__ __forceinline__ void chain_role(const PersistArgs& a, float* smem, in
           for (int jj = 0; jj < 2; ++jj) {
             const int ct = w + 4 * jj < nt0 ? w + 4 * jj : w;   // branch-free: unused past nt0
 #pragma unroll
-            for (int ks = 0; ks < 16; ++ks) bz[jj][ks] = ldw1(rs, (16 * g + ks) * H0 + ct * 16 + i16, zs);
+            for (int ks = 0; ks < 16; ++ks) bz[jj][ks] = rb<BF>(ldw1(rs, (16 * g + ks) * H0 + ct * 16 + i16, zs));
           }
         }
       }
@@ -1386,7 +1430,7 @@ __device__ __forceinline__ void chain_role(const PersistArgs& a, float* smem, in
     float G1[8];
     {
       f32x4 acc[2];
-      rows_mm<H0, L0S, L1S, 1>(sA0, sW1, w, nt1, acc, i16, g);
+      rows_mm<H0, L0S, L1S, 1, BF>(sA0, sW1, w, nt1, acc, i16, g);
       pstamp(a, i, 16);
       const float ks = a.rate1 > 0.f ? 1.f / (1.f - a.rate1) : 1.f;
       const uint32_t db = dropout_base(a.seed, r, 1, it);
@@ -1429,8 +1473,8 @@ __device__ __forceinline__ void chain_role(const PersistArgs& a, float* smem, in
       for (int s2 = 0; s2 < PER; ++s2) {
         const int sx = w * PER + s2;
         const int k = (sx >> 4) * 64 + 16 * g + (sx & 15);
-        av[s2] = sA1[i16 * L1S + k];
-        bv[s2] = sW2[k * S17 + i16];
+        av[s2] = rb<BF>(sA1[i16 * L1S + k]);
+        bv[s2] = rb<BF>(sW2[k * S17 + i16]);
       }
 #pragma unroll
       for (int s2 = 0; s2 < PER; ++s2) acc = mma(av[s2], bv[s2], acc);
@@ -1505,8 +1549,8 @@ __device__ __forceinline__ void chain_role(const PersistArgs& a, float* smem, in
 #pragma unroll
         for (int ks = 0; ks < 4; ++ks) {
           const int c = 4 * ks + g;
-          av[ks] = sD2[i16 * S17 + c];
-          bv[ks] = sW2[col * S17 + c];
+          av[ks] = rb<BF>(sD2[i16 * S17 + c]);
+          bv[ks] = rb<BF>(sW2[col * S17 + c]);
         }
         f32x4 acc = zero4f();
 #pragma unroll
@@ -1526,7 +1570,7 @@ __device__ __forceinline__ void chain_role(const PersistArgs& a, float* smem, in
     // ---- DX1: dZ_0 = (dZ_1 . W1^T) * G_0 -> LDS, then published for the L0 tiles
     {
       f32x4 acc[2];
-      rows_mm<H1, L1S, 1, L1S>(sD1, sW1, w, nt0, acc, i16, g);
+      rows_mm<H1, L1S, 1, L1S, BF>(sD1, sW1, w, nt0, acc, i16, g);
       pstamp(a, i, 23);
 #pragma unroll
       for (int jj = 0; jj < 2; ++jj) {
@@ -1758,7 +1802,7 @@ __device__ __forceinline__ void chain_role(const PersistArgs& a, float* smem, in
 // its dZ_1 columns = (dZ_2 . W2_own^T) * relu'(.) * keep / (1 - rate) -- the factor
 // recovered from A_1 > 0 (ReLU, so the same MFMA as the chain's DX2 gives the same bits)
 // -- computes DW1 / DW2 / the bias sums, applies plain SGD and publishes the columns.
-template <int H0, int H1>
+template <int H0, int H1, bool BF>
 __device__ __forceinline__ void dw_role_v2(const PersistArgs& a, float* smem, int r, int d) {
   constexpr int L0S = H0 + 1;
   constexpr int nt0 = H0 / 16, nt1 = H1 / 16;
@@ -1846,8 +1890,8 @@ __device__ __forceinline__ void dw_role_v2(const PersistArgs& a, float* smem, in
 #pragma unroll
       for (int kk = 0; kk < 4; ++kk) {
         const int cc = 4 * kk + g;
-        av[kk] = uD2[(w * 16 + i16) * S17 + cc];
-        bv[kk] = sW2o[(c * 16 + i16) * S17 + cc];
+        av[kk] = rb<BF>(uD2[(w * 16 + i16) * S17 + cc]);
+        bv[kk] = rb<BF>(sW2o[(c * 16 + i16) * S17 + cc]);
       }
       f32x4 acc = zero4f();
 #pragma unroll
@@ -1871,12 +1915,12 @@ __device__ __forceinline__ void dw_role_v2(const PersistArgs& a, float* smem, in
 #pragma unroll
         for (int h8 = 0; h8 < 8; ++h8) {
           const int b = 16 * g + 8 * half + h8;
-          zb[0][h8] = uD1[b * 33 + i16];
-          zb[1][h8] = uD1[b * 33 + 16 + i16];
+          zb[0][h8] = rb<BF>(uD1[b * 33 + i16]);
+          zb[1][h8] = rb<BF>(uD1[b * 33 + 16 + i16]);
 #pragma unroll
-          for (int u = 0; u < TU; ++u) xa[u][h8] = uA0[b * L0S + urt[u] * 16 + i16];
-          a1v[h8] = uA1[b * 33 + (w2own ? w : 0) * 16 + i16];
-          d2v[h8] = uD2[b * S17 + i16];
+          for (int u = 0; u < TU; ++u) xa[u][h8] = rb<BF>(uA0[b * L0S + urt[u] * 16 + i16]);
+          a1v[h8] = rb<BF>(uA1[b * 33 + (w2own ? w : 0) * 16 + i16]);
+          d2v[h8] = rb<BF>(uD2[b * S17 + i16]);
         }
 #pragma unroll
         for (int h8 = 0; h8 < 8; ++h8) {
@@ -1934,8 +1978,8 @@ __device__ __forceinline__ void dw_role_v2(const PersistArgs& a, float* smem, in
   }
 
   // ---- epilogue: owned masters and both weight-image parities (plain SGD: no state)
-  float* Wsh = a.Wsh + (long long)r * a.sWsh;
-  float* WTsh = a.WTsh + (long long)r * a.sWTsh;
+  float* Wsh = img_base<BF>(a.Wsh, (long long)r * a.sWsh);
+  float* WTsh = img_base<BF>(a.WTsh, (long long)r * a.sWTsh);
 #pragma unroll
   for (int u = 0; u < TU; ++u) {
     const int t = w + 4 * u;
@@ -1947,8 +1991,8 @@ __device__ __forceinline__ void dw_role_v2(const PersistArgs& a, float* smem, in
       P[a.p_off1 + (long long)k * H1 + nn] = wm[4 * u + qq];
 #pragma unroll
       for (int par = 0; par < 2; ++par) {
-        Wsh[par * a.wsh_par + a.wsh_off[1] + (long long)k * a.Np[1] + nn] = wm[4 * u + qq];
-        WTsh[par * a.wtsh_par + a.wtsh_off[1] + (long long)nn * a.Kp[1] + k] = wm[4 * u + qq];
+        img_store<BF>(Wsh, par * a.wsh_par + a.wsh_off[1] + (long long)k * a.Np[1] + nn, wm[4 * u + qq]);
+        img_store<BF>(WTsh, par * a.wtsh_par + a.wtsh_off[1] + (long long)nn * a.Kp[1] + k, wm[4 * u + qq]);
       }
     }
   }
@@ -1959,8 +2003,8 @@ __device__ __forceinline__ void dw_role_v2(const PersistArgs& a, float* smem, in
       P[a.p_off2 + (long long)k * C + i16] = wm[4 * TU + qq];
 #pragma unroll
       for (int par = 0; par < 2; ++par) {
-        Wsh[par * a.wsh_par + a.wsh_off[2] + (long long)k * a.Np[2] + i16] = wm[4 * TU + qq];
-        WTsh[par * a.wtsh_par + a.wtsh_off[2] + (long long)i16 * a.Kp[2] + k] = wm[4 * TU + qq];
+        img_store<BF>(Wsh, par * a.wsh_par + a.wsh_off[2] + (long long)k * a.Np[2] + i16, wm[4 * TU + qq]);
+        img_store<BF>(WTsh, par * a.wtsh_par + a.wtsh_off[2] + (long long)i16 * a.Kp[2] + k, wm[4 * TU + qq]);
       }
     }
   }
@@ -1969,7 +2013,7 @@ __device__ __forceinline__ void dw_role_v2(const PersistArgs& a, float* smem, in
 
 }  // namespace
 
-template <int H0, int H1, bool FAST, int NPT, bool RELU, bool V2, bool PS = false>
+template <int H0, int H1, bool FAST, int NPT, bool RELU, bool V2, bool PS = false, bool BF = false>
 __global__ __launch_bounds__(256) void mlp_persist_kernel(PersistArgs a) {
   __shared__ __attribute__((aligned(16))) float smem[LDS_FLOATS];
   if (__hip_atomic_load((gu32*)(a.err), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) return;
@@ -1982,12 +2026,12 @@ __global__ __launch_bounds__(256) void mlp_persist_kernel(PersistArgs a) {
     static_assert(NPT == 0 && RELU, "V2: plain SGD, ReLU hidden layers");
     if (q < nl0) {
       const int kc = q / a.nc0, cb = q - kc * a.nc0;
-      if (a.cw == 64) l0_role_v2<H0, 4>(a, smem, r, kc, cb, q);
-      else l0_role_v2<H0, 2>(a, smem, r, kc, cb, q);
+      if (a.cw == 64) l0_role_v2<H0, 4, BF>(a, smem, r, kc, cb, q);
+      else l0_role_v2<H0, 2, BF>(a, smem, r, kc, cb, q);
     } else if (q < nl0 + a.nch) {
-      chain_role<H0, H1, FAST, NPT, RELU, true, false>(a, smem, r, q - nl0);
+      chain_role<H0, H1, FAST, NPT, RELU, true, false, BF>(a, smem, r, q - nl0);
     } else {
-      dw_role_v2<H0, H1>(a, smem, r, q - nl0 - a.nch);
+      dw_role_v2<H0, H1, BF>(a, smem, r, q - nl0 - a.nch);
     }
   } else {
     if (q < nl0) l0_role<H0, NPT, PS>(a, smem, r, q / a.nc0, q - (q / a.nc0) * a.nc0, q);
@@ -2006,7 +2050,10 @@ hipError_t persist_launch(const PersistArgs* a, hipStream_t s) {
   const bool relu = a->act0 == ACT_RELU && a->act1 == ACT_RELU;
   const bool sgd = !a->S || (a->op.opt == OPT_SGD && a->op.mom == 0.f);
   const dim3 grid(a->R * a->wgs);
-  if (a->v2) {   // the host checked plain SGD + ReLU
+  if (a->v2 && a->bf16) {   // mixed_bfloat16: bf16 shard, bf16-rounded MFMA operands, fp32 masters
+    if (fast) hipLaunchKernelGGL((mlp_persist_kernel<H, H, true, 0, true, true, false, true>), grid, dim3(256), 0, s, *a);
+    else hipLaunchKernelGGL((mlp_persist_kernel<H, H, false, 0, true, true, false, true>), grid, dim3(256), 0, s, *a);
+  } else if (a->v2) {   // the host checked plain SGD + ReLU
     if (fast) hipLaunchKernelGGL((mlp_persist_kernel<H, H, true, 0, true, true>), grid, dim3(256), 0, s, *a);
     else hipLaunchKernelGGL((mlp_persist_kernel<H, H, false, 0, true, true>), grid, dim3(256), 0, s, *a);
   } else if (a->ps_mode) {   // V1 with the in-launch parameter-server exchange

@@ -59,7 +59,7 @@ Executor::~Executor() {
 // workgroup must be resident: they wait for each other inside the launch).
 bool Executor::build_persist() {
   const int L = (int)c_.layers.size();
-  if (c_.bf16 || L != 3) return false;
+  if (L != 3) return false;
   const LayerCfg &l0 = c_.layers[0], &l1 = c_.layers[1], &l2 = c_.layers[2];
   // hidden widths (64, 64) or (128, 128): the kernel is compiled for those two shapes
   if (!((l0.N == 64 && l1.N == 64) || (l0.N == 128 && l1.N == 128))) return false;
@@ -85,6 +85,8 @@ bool Executor::build_persist() {
   const bool v2 = c_.persist_v2 != 0 && !c_.persist_sync && c_.op.opt == OPT_SGD && c_.op.mom == 0.f &&
                   l0.act == ACT_RELU && l1.act == ACT_RELU;
   const int nd = v2 ? cdiv(l1.N / 16, PM_NTU) : 0;
+  // bf16 (mixed_bfloat16): the V2 roles only (bf16-rounded operands, bf16 shard and images)
+  if (c_.bf16 && !v2) return false;
   // layer-0 tiles: the cheapest (kc0, cw) whose tile count fits.  V1: cost ~ the tile's
   // MFMA work (FWD reduction padded to 64) + the partials every chain workgroup sums.
   // V2: the L0 work is off the critical path; the chain's slab loads (nk0 Pold + Gram
@@ -118,6 +120,7 @@ bool Executor::build_persist() {
   a.nch = nch; a.v2 = v2 ? 1 : 0; a.nd = nd;
   a.wgs = a.nk0 * a.nc0 + nch + nd;
   a.sync = c_.persist_sync ? 1 : 0;
+  a.bf16 = c_.bf16 ? 1 : 0;
   a.act0 = l0.act; a.act1 = l1.act; a.act2 = l2.act;
   a.rate0 = l0.rate; a.rate1 = l1.rate;
   a.bias0 = l0.has_bias; a.bias1 = l1.has_bias; a.bias2 = l2.has_bias;

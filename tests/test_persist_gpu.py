@@ -387,3 +387,39 @@ def test_spark_model_async_batch_inlaunch_learns(mode):
     ref = sm.master_network.evaluate(x, y)
     assert np.allclose(ev, ref, atol=0.01), (ev, ref)
     assert np.isfinite(ev).all() and ref[1] > max(0.6, acc0 + 0.3), (acc0, ref)
+
+
+def test_persist_bf16_policy_matches_rowchain_bf16():
+    """mixed_bfloat16 on the persistent plan (V2 roles with the bf16 data shard and every
+    MFMA operand rounded to bf16 -- exact bf16 products, fp32 accumulation and masters)
+    against the bf16 row-chain plan: the same training within bf16 resolution, and the
+    bf16 weight images written back at the end of the launch serve evaluation."""
+    from elephas_amd import config
+    from elephas_amd.models import initializers
+    from elephas_amd.models.optimizers import SGD
+    from elephas_amd.ops.plan import build_plan
+    from elephas_amd.ops.native_engine import NativeTrainer
+    initializers.set_seed(15)
+    model = _mlp(784, [128, 128], 10, dropout=0.2)
+    model.compile(SGD(learning_rate=0.1), "categorical_crossentropy", ["acc"])
+    xs, ys = _shards([640] * 8, 784, 10, seed=19)
+    w0 = None
+    out = []
+    for persist in (1, 0):
+        t = NativeTrainer(model, build_plan(model), 8, 64, torch.device("cuda"), seed=9, persist=persist,
+                          rowchain=None if persist else 1, policy="mixed_bfloat16")
+        assert t.persistent == bool(persist), t.plan_name()
+        if persist:
+            assert t.persist_variant == 2
+        w0 = t.get_weights_flat()
+        t.set_data(xs, ys, 0.1, shuffle=False)
+        h = t.fit(2)
+        out.append((t.get_weights_flat(), h, t.evaluate(xs[0], ys[0])))
+    config.set_policy("float32")
+    (wp, hp, ep), (wr, hr, er) = out
+    step = np.abs(wr - w0).mean()
+    err = np.abs(wp - wr).mean()
+    assert err <= 0.05 * step, (err, step)
+    for a, b in zip(hp, hr):
+        np.testing.assert_allclose(a["loss"], b["loss"], rtol=2e-2, atol=2e-2)
+    np.testing.assert_allclose(ep, er, rtol=3e-2, atol=3e-2)
