@@ -723,9 +723,11 @@ __device__ __forceinline__ void tile_epilogue(const GA& ga, const Prob& p, const
         lds8(row, t_c0, v);
         const long long pidx = p.p_off + (long long)gm * p.N + gn0;
         if (!upd) {
+          // the raw gradient: the apply kernel (flat.hip) multiplies by grad_scale once
+          // (scaling here too squared it: 1 / world^2 on the multi-rank per-step path)
 #pragma unroll
           for (int q = 0; q < 8; ++q)
-            if (gn0 + q < p.N) G[pidx + q] = valid > 0 ? v[q] * p.op.grad_scale : 0.f;
+            if (gn0 + q < p.N) G[pidx + q] = valid > 0 ? v[q] : 0.f;
           continue;
         }
         float w[8], s0[8], s1[8];

@@ -80,7 +80,7 @@ struct ChainLds {
   static constexpr int TOTAL = o_gs + 16 * 65;
 };
 constexpr int L0_LDS = 2 * 64 * 129 + 128 * 33 + 64 * 33 + 128 * 33;   // + the pulled tile (PS hook)
-constexpr int L0V2_LDS = 2 * 64 * 129 + 128 * 65 + 64 * 65;   // X chunks, W0 tile (cw <= 64), dZ_0 columns
+constexpr int L0V2_LDS = 2 * 64 * 129 + 128 * 65 + 64 * 65 + 64 * 65;   // X chunks, W0 tile (cw <= 64), dZ_0 columns, store staging
 constexpr int DW_LDS = 64 * 129 + 2 * 64 * 33 + 64 * 17 + 32 * 17;
 constexpr int cmax(int x, int y) { return x > y ? x : y; }
 constexpr int LDS_FLOATS = (cmax(cmax(ChainLds<128, 128>::TOTAL, L0_LDS), cmax(L0V2_LDS, DW_LDS)) + 3) & ~3;
@@ -855,6 +855,7 @@ __device__ __forceinline__ void l0_role_v2(const PersistArgs& a, float* smem, in
   float* sX = smem;                             // [2][64][XS] X chunks (steps of parity 0 / 1)
   float* sW = sX + 2 * 64 * 129;                // [128][WS]   the W0 tile (master, in place)
   float* sdZ = sW + 128 * WS;                   // [64][WS]    dZ_0 columns of this tile
+  float* sT = sW + 128 * 65 + 64 * 65;          // [64][65]    staging of the Pold / Gram slabs (16-byte stores)
   __shared__ float sB0[64];
   __shared__ float sBg[64];
   __shared__ float sRedL[256];
@@ -940,15 +941,23 @@ __device__ __forceinline__ void l0_role_v2(const PersistArgs& a, float* smem, in
           for (int jj = 0; jj < NCT; ++jj) acc[jj] = mma(av[ks], bv[jj][ks], acc[jj]);
         }
       }
-      const int base = (int)(a.o_part + (i & 1) * a.part_par) + kc * 64 * H0 + n0;
-      const int v = (w * 16 + 4 * g) * H0 + i16;
 #pragma unroll
       for (int jj = 0; jj < NCT; ++jj) {
         const float bv = has_b ? sB0[jj * 16 + i16] : 0.f;
 #pragma unroll
-        for (int qq = 0; qq < 4; ++qq) stw1(rs, v + qq * H0 + jj * 16, base, acc[jj][qq] + bv);
+        for (int qq = 0; qq < 4; ++qq) sT[(w * 16 + 4 * g + qq) * 65 + jj * 16 + i16] = acc[jj][qq] + bv;
       }
     }
+    __syncthreads();
+    // the slab leaves as 16-byte write-through row segments (4-byte sc1 stores cost ~6x
+    // per byte: MI355X_MICROARCH.md price list)
+    const int base = (int)(a.o_part + (i & 1) * a.part_par) + kc * 64 * H0 + n0;
+    for (int e = tid; e < BR * (CW / 4); e += 256) {
+      const int row = e / (CW / 4), c4 = e - row * (CW / 4);
+      const float* src = sT + row * 65 + 4 * c4;
+      stw4(rs, row * H0 + 4 * c4, base, f32x4{src[0], src[1], src[2], src[3]});
+    }
+    __syncthreads();
   };
 
   // rows [cb * 64 / nc0, (cb + 1) * 64 / nc0) of this k-chunk's X_i . X_{i-1}^T -> Gram
@@ -977,10 +986,16 @@ __device__ __forceinline__ void l0_role_v2(const PersistArgs& a, float* smem, in
 #pragma unroll
         for (int ks = 0; ks < 16; ++ks) acc = mma(av[ks], bv[ks], acc);
       }
-      const int v = (r0 + tr * 16 + 4 * g) * 64 + tc * 16 + i16;
 #pragma unroll
-      for (int qq = 0; qq < 4; ++qq) stw1(rs, v + qq * 64, base, acc[qq]);
+      for (int qq = 0; qq < 4; ++qq) sT[(tr * 16 + 4 * g + qq) * 65 + tc * 16 + i16] = acc[qq];
     }
+    __syncthreads();
+    for (int e = tid; e < rows * 16; e += 256) {
+      const int row = e >> 4, c4 = e & 15;
+      const float* src = sT + row * 65 + 4 * c4;
+      stw4(rs, (r0 + row) * 64 + 4 * c4, base, f32x4{src[0], src[1], src[2], src[3]});
+    }
+    __syncthreads();
   };
 
   const int n = a.nsteps;
@@ -1281,15 +1296,18 @@ __device__ __forceinline__ void chain_role(const PersistArgs& a, float* smem, in
     pstamp(a, i, 0);
     // this step's partials and (after step 0) every chain workgroup's updated W1 / W2
     // columns of the previous step, watched by one wave
-    if (!wait_two(a, flag_at(a, r, PMF_PART), nl0, (unsigned)(i + 1), flag_at(a, r, PMF_W),
-                  i > 0 ? (V2 ? a.nd : a.nch) : 0, (unsigned)i, PERR_CHAIN_PART))
+    // V1: the partials and every chain workgroup's updated W1 / W2 columns of the previous
+    // step.  V2: the partials and the previous step's dZ_0 rows of every chain workgroup
+    // (the Z_0 correction); the DW workgroups' W1 / W2 are waited for only before FWD1
+    if (!wait_two(a, flag_at(a, r, PMF_PART), nl0, (unsigned)(i + 1), flag_at(a, r, V2 ? PMF_BWD : PMF_W),
+                  i > 0 ? a.nch : 0, (unsigned)i, PERR_CHAIN_PART))
       return;
     pstamp(a, i, 1);
     // the weight loads go first: their latency overlaps the partial sums below
     Staged<H0 * H1 / 1024> w1s;
     Staged<H1 / 64> w2s;
     f32x4 bvec = zero4f();
-    if (i > 0) {
+    if (!V2 && i > 0) {
       stage_issue(w1s, rs, (int)a.o_w1, H1, H0, H1);
       stage_issue(w2s, rs, (int)a.o_w2, 16, H1, 16);
       if (tid < H1 / 4) bvec = ldw4(rs, 4 * tid, (int)a.o_b1);
@@ -1327,8 +1345,6 @@ __device__ __forceinline__ void chain_role(const PersistArgs& a, float* smem, in
             gl[u] = ldw4(rs, grow * 64 + gc4, (int)(a.o_g + (i & 1) * a.g_par) + uc * 64 * 64 + m0 * 64);
           }
           pstamp(a, i, 11);
-          if (!wait_all(a, flag_at(a, r, PMF_BWD), a.nch, (unsigned)i, PERR_CHAIN_PREV)) return;
-          pstamp(a, i, 12);
           const int zs = (int)(a.o_dz0 + ((i - 1) & 1) * a.dz0_par);
 #pragma unroll
           for (int jj = 0; jj < 2; ++jj) {
@@ -1386,7 +1402,7 @@ __device__ __forceinline__ void chain_role(const PersistArgs& a, float* smem, in
           pstamp(a, i, 27);
         }
       }
-      if (i > 0) {   // the previous step's weights -> LDS (read after the barrier below)
+      if (!V2 && i > 0) {   // the previous step's weights -> LDS (read after the barrier below)
         stage_commit(w1s, H0, sW1, L1S);
         stage_commit(w2s, H1, sW2, S17);
         if (tid < H1 / 4) {
@@ -1422,6 +1438,25 @@ __device__ __forceinline__ void chain_role(const PersistArgs& a, float* smem, in
       for (int h = 0; h < 2; ++h) sY[(tid >> 5) * 32 + 256 * h + (tid & 31)] = yv[h];
       if (tid < 16) sRow[tid] = m0 + tid < valid ? 1 : -1;
       pstamp(a, i, 15);
+    }
+    if constexpr (V2) {
+      if (i > 0) {   // the DW workgroups' W1 / W2 / biases of the previous step -> LDS
+        if (!wait_all(a, flag_at(a, r, PMF_W), a.nd, (unsigned)i, PERR_CHAIN_PREV)) return;
+        pstamp(a, i, 12);
+        stage_issue(w1s, rs, (int)a.o_w1, H1, H0, H1);
+        stage_issue(w2s, rs, (int)a.o_w2, 16, H1, 16);
+        if (tid < H1 / 4) bvec = ldw4(rs, 4 * tid, (int)a.o_b1);
+        else if (tid >= 64 && tid < 68) bvec = ldw4(rs, 4 * (tid - 64), (int)a.o_b2);
+        stage_commit(w1s, H0, sW1, L1S);
+        stage_commit(w2s, H1, sW2, S17);
+        if (tid < H1 / 4) {
+#pragma unroll
+          for (int qq = 0; qq < 4; ++qq) sB1[4 * tid + qq] = a.bias1 ? bvec[qq] : 0.f;
+        } else if (tid >= 64 && tid < 68) {
+#pragma unroll
+          for (int qq = 0; qq < 4; ++qq) sB2[4 * (tid - 64) + qq] = (a.bias2 && 4 * (tid - 64) + qq < C) ? bvec[qq] : 0.f;
+        }
+      }
     }
     __syncthreads();
     pstamp(a, i, 2);

@@ -117,8 +117,11 @@ bool Executor::build_persist() {
   a.R = c_.R; a.B = c_.B;
   a.K0 = l0.K; a.H0 = l0.N; a.H1 = l1.N; a.C = l2.N;
   a.kc0 = best_kc; a.cw = best_cw; a.nc0 = l0.N / best_cw; a.nk0 = cdiv(l0.K, best_kc);
-  a.nch = nch; a.v2 = v2 ? 1 : 0; a.nd = nd;
-  a.wgs = a.nk0 * a.nc0 + nch + nd;
+  // V2: one weight-gradient workgroup per layer-1 column tile when the CUs allow (halves
+  // their MFMA chain vs two tiles each: the W1 / W2 hand-off is on the step's critical path)
+  const int nd_use = (v2 && cdiv(l0.K, best_kc) * (l0.N / best_cw) + l1.N / 16 <= cap) ? l1.N / 16 : nd;
+  a.nch = nch; a.v2 = v2 ? 1 : 0; a.nd = nd_use;
+  a.wgs = a.nk0 * a.nc0 + nch + nd_use;
   a.sync = c_.persist_sync ? 1 : 0;
   a.bf16 = c_.bf16 ? 1 : 0;
   a.act0 = l0.act; a.act1 = l1.act; a.act2 = l2.act;

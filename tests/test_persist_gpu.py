@@ -271,37 +271,46 @@ def test_persist_oversubscribed_grid_falls_back(monkeypatch):
 def test_persist_sync_replicas_match_eager_exchange(opt):
     """Per-step synchronous DP of the replicas inside the persistent launch (every owning
     workgroup sums the R replicas' weight-gradient tiles in replica order): the replicas
-    stay bit-identical, and the training equals the eager per-step path (forward /
-    backward, replica sum of G, apply) within fp32 summation order."""
+    stay bit-identical, and both it and the eager per-step path (forward / backward,
+    replica sum of G, apply) equal ONE fp32 torch model trained on the replicas' batches
+    stacked (4 x 64 rows per step; no dropout, so no masks to match)."""
     from elephas_amd.models import initializers, optimizers as O
     from elephas_amd.ops.plan import build_plan
     from elephas_amd.ops.native_engine import NativeTrainer
+    from elephas_amd.ops.torch_engine import TorchTrainer
     from elephas_amd import config
     config.set_policy("float32")
     initializers.set_seed(12)
-    model = _mlp(784, [128, 128], 10, dropout=0.2)
+    model = _mlp(784, [128, 128], 10)
     model.compile({"sgd": O.SGD(0.1), "sgd_mom": O.SGD(0.05, momentum=0.9)}[opt], "categorical_crossentropy",
                   ["acc"])
-    xs, ys = _shards([450] * 4, 784, 10, seed=13)
+    R, B, steps = 4, 64, 7
+    xs, ys = _shards([B * steps] * R, 784, 10, seed=13)
+    w0 = None
     out = []
     for persist in (1, 0):
-        t = NativeTrainer(model, build_plan(model), 4, 64, torch.device("cuda"), seed=5, persist=persist,
+        t = NativeTrainer(model, build_plan(model), R, B, torch.device("cuda"), seed=5, persist=persist,
                           sync=True)
         assert t.persistent == bool(persist)
         if persist:
             assert t.exe.persist_variant()[2] == 1, t.plan_name()
-        t.set_data(xs, ys, 0.1, shuffle=True)
-        torch.manual_seed(3)
-        h = t.fit(2)
-        w = t.get_weights_flat()
-        out.append((w, h))
-    (wp, hp), (we, he) = out
-    for r in range(1, 4):
-        assert np.array_equal(wp[r], wp[0]), r          # one model: identical replicas
-    scale = np.abs(we).max()
-    assert np.abs(wp - we).max() <= 1e-4 * scale, (np.abs(wp - we).max(), scale)
-    for a, b in zip(hp, he):
-        np.testing.assert_allclose(a["loss"], b["loss"], rtol=5e-4, atol=5e-4)
+        w0 = t.get_weights_flat()[0].copy()
+        t.set_data(xs, ys, 0.0, shuffle=False)
+        t.fit(2)
+        out.append(t.get_weights_flat())
+    # the reference: one model, batch i = the replicas' batch i stacked in replica order
+    xc = np.concatenate([np.concatenate([x[i * B:(i + 1) * B] for x in xs]) for i in range(steps)])
+    yc = np.concatenate([np.concatenate([y[i * B:(i + 1) * B] for y in ys]) for i in range(steps)])
+    ref = TorchTrainer(model, build_plan(model), 1, R * B, torch.device("cuda"))
+    ref.set_data([xc], [yc], 0.0, shuffle=False)
+    ref.fit(2)
+    wt = ref.get_weights_flat()[0]
+    step = np.abs(wt - w0).max()
+    for name, w in zip(("in-launch", "eager"), out):
+        for r in range(1, R):
+            assert np.array_equal(w[r], w[0]), (name, r)          # one model: identical replicas
+        err = np.abs(w[0] - wt).max() / step
+        assert err < 1e-3, (name, err)
 
 
 @pytest.mark.parametrize("mode", ["asynchronous", "hogwild"])
@@ -392,8 +401,10 @@ def test_spark_model_async_batch_inlaunch_learns(mode):
 def test_persist_bf16_policy_matches_rowchain_bf16():
     """mixed_bfloat16 on the persistent plan (V2 roles with the bf16 data shard and every
     MFMA operand rounded to bf16 -- exact bf16 products, fp32 accumulation and masters)
-    against the bf16 row-chain plan: the same training within bf16 resolution, and the
-    bf16 weight images written back at the end of the launch serve evaluation."""
+    against the bf16 row-chain plan: their distance is of the order of the bf16 plan's
+    own distance to fp32 (bf16 rounding noise, not a different training), the loss
+    histories agree, and the bf16 weight images written back at the end of the launch
+    serve evaluation."""
     from elephas_amd import config
     from elephas_amd.models import initializers
     from elephas_amd.models.optimizers import SGD
@@ -403,23 +414,22 @@ def test_persist_bf16_policy_matches_rowchain_bf16():
     model = _mlp(784, [128, 128], 10, dropout=0.2)
     model.compile(SGD(learning_rate=0.1), "categorical_crossentropy", ["acc"])
     xs, ys = _shards([640] * 8, 784, 10, seed=19)
-    w0 = None
-    out = []
-    for persist in (1, 0):
+    out = {}
+    for name, persist, pol in (("p_bf16", 1, "mixed_bfloat16"), ("rc_bf16", 0, "mixed_bfloat16"),
+                               ("rc_f32", 0, "float32")):
         t = NativeTrainer(model, build_plan(model), 8, 64, torch.device("cuda"), seed=9, persist=persist,
-                          rowchain=None if persist else 1, policy="mixed_bfloat16")
+                          rowchain=None if persist else 1, policy=pol)
         assert t.persistent == bool(persist), t.plan_name()
         if persist:
             assert t.persist_variant == 2
         w0 = t.get_weights_flat()
         t.set_data(xs, ys, 0.1, shuffle=False)
         h = t.fit(2)
-        out.append((t.get_weights_flat(), h, t.evaluate(xs[0], ys[0])))
+        out[name] = (t.get_weights_flat(), h, t.evaluate(xs[0], ys[0]))
     config.set_policy("float32")
-    (wp, hp, ep), (wr, hr, er) = out
-    step = np.abs(wr - w0).mean()
-    err = np.abs(wp - wr).mean()
-    assert err <= 0.05 * step, (err, step)
-    for a, b in zip(hp, hr):
-        np.testing.assert_allclose(a["loss"], b["loss"], rtol=2e-2, atol=2e-2)
-    np.testing.assert_allclose(ep, er, rtol=3e-2, atol=3e-2)
+    dist = lambda a, b: np.abs(out[a][0] - out[b][0]).mean() / np.abs(out[b][0] - w0).mean()
+    assert dist("p_bf16", "rc_bf16") <= 1.5 * dist("rc_bf16", "rc_f32") + 0.02, \
+        (dist("p_bf16", "rc_bf16"), dist("rc_bf16", "rc_f32"))
+    for a, b in zip(out["p_bf16"][1], out["rc_bf16"][1]):
+        np.testing.assert_allclose(a["loss"], b["loss"], rtol=1e-2, atol=1e-2)
+    np.testing.assert_allclose(out["p_bf16"][2], out["rc_bf16"][2], rtol=3e-2, atol=3e-2)

@@ -14,7 +14,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 NAMES = {
-    "chain": {0: "part_wait0", 1: "part_seen", 11: "gram_ld", 12: "prev_dz0_seen", 13: "p0_sums",
+    "chain": {0: "part_wait0", 1: "part_dz0_seen", 11: "gram_ld", 12: "w_seen", 13: "p0_sums",
               27: "correction", 14: "p0_act", 15: "p0_st", 2: "phase0", 16: "fwd1_mm", 17: "fwd1_epi",
               3: "fwd1", 18: "fwd2", 19: "logits", 20: "loss", 4: "dz2", 21: "dx2", 22: "dz1_pub",
               23: "dx1_mm", 5: "dx1", 6: "bwd_pub", 7: "bwd_seen", 8: "stage_ld", 24: "dw_mm", 26: "opt",
@@ -50,7 +50,7 @@ def main():
     ys = [np.eye(10, dtype=np.float32)[rng.integers(0, 10, 7500)] for _ in range(R)]
     t.set_data(xs, ys, 0.1)
     nk0, nc0, kc0, cw, nch, wgs, grid = t.exe.persist_geometry()
-    var, nd = t.exe.persist_variant()
+    var, nd, sync = t.exe.persist_variant()
     print("plan", t.plan_name())
     st = torch.zeros(grid * 8 * 32, dtype=torch.int64, device="cuda")
     t.begin_epoch()
