@@ -80,7 +80,8 @@ struct ChainLds {
   static constexpr int TOTAL = o_gs + 16 * 65;
 };
 constexpr int L0_LDS = 2 * 64 * 129 + 128 * 33 + 64 * 33 + 128 * 33;   // + the pulled tile (PS hook)
-constexpr int L0V2_LDS = 2 * 64 * 129 + 128 * 65 + 64 * 65 + 64 * 65;   // X chunks, W0 tile (cw <= 64), dZ_0 columns, store staging
+// V2 layer-0: three X chunks (kc0 <= 112: stride 113), W0 tile (cw <= 64), dZ_0 columns, store staging
+constexpr int L0V2_LDS = 3 * 64 * 113 + 128 * 65 + 64 * 65 + 64 * 65;
 constexpr int DW_LDS = 64 * 129 + 2 * 64 * 33 + 64 * 17 + 32 * 17;
 constexpr int cmax(int x, int y) { return x > y ? x : y; }
 constexpr int LDS_FLOATS = (cmax(cmax(ChainLds<128, 128>::TOTAL, L0_LDS), cmax(L0V2_LDS, DW_LDS)) + 3) & ~3;
@@ -841,8 +842,10 @@ __device__ __forceinline__ void l0_role(const PersistArgs& a, float* smem, int r
 template <int H0, int NCT, bool BF>
 __device__ __forceinline__ void l0_role_v2(const PersistArgs& a, float* smem, int r, int kc, int cb, int q) {
   static_assert(NCT == 2 || NCT == 4, "column blocks of 32 or 64");
-  // X rows in LDS: fp32 (stride 129 floats), or bf16 packed two per dword (stride 65 dwords)
-  constexpr int XS = BF ? 65 : 129, CW = NCT * 16, WS = CW + 1, TU0 = 2 * NCT;   // DW0 tiles per wave (<= 8 row tiles)
+  // X rows in LDS: fp32 (stride kc0 + 1 floats), or bf16 packed two per dword (stride
+  // kc0 / 2 + 1 dwords); three chunks (steps s % 3), kc0 <= 112 (host)
+  constexpr int CW = NCT * 16, WS = CW + 1, TU0 = 2 * NCT;   // DW0 tiles per wave (<= 8 row tiles)
+  const int XS = BF ? a.kc0 / 2 + 1 : a.kc0 + 1;
   auto xat = [](const float* row, int k) -> float { if constexpr (BF) return bf_at(row, k); else return row[k]; };
   const int tid = threadIdx.x, lane = tid & 63, i16 = lane & 15, g = lane >> 4;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6) & 3;
@@ -852,8 +855,8 @@ __device__ __forceinline__ void l0_role_v2(const PersistArgs& a, float* smem, in
   const int n0 = cb * CW;
   const int nrt = (kreal + 15) >> 4, ntiles = nrt * NCT;
   const int BR = a.nch * 16;
-  float* sX = smem;                             // [2][64][XS] X chunks (steps of parity 0 / 1)
-  float* sW = sX + 2 * 64 * 129;                // [128][WS]   the W0 tile (master, in place)
+  float* sX = smem;                             // [3][64][XS] X chunks of steps s % 3
+  float* sW = sX + 3 * 64 * XS;                 // [128][WS]   the W0 tile (master, in place)
   float* sdZ = sW + 128 * WS;                   // [64][WS]    dZ_0 columns of this tile
   float* sT = sW + 128 * 65 + 64 * 65;          // [64][65]    staging of the Pold / Gram slabs (16-byte stores)
   __shared__ float sB0[64];
@@ -898,7 +901,7 @@ __device__ __forceinline__ void l0_role_v2(const PersistArgs& a, float* smem, in
     const int valid = st.valid(a, i);
     const int* pr = a.perm + (long long)r * a.sPerm + (st.s0 + i) * a.B;
     const float* Xr = a.X + (long long)r * a.sX + k0;
-    float* dst = sX + (i & 1) * 64 * XS;
+    float* dst = sX + (i % 3) * 64 * XS;
     const int myrow = pr[lane < valid ? lane : 0];
     for (int v = 0; v < 16; ++v) {
       const int b = w + 4 * v;
@@ -919,7 +922,7 @@ __device__ __forceinline__ void l0_role_v2(const PersistArgs& a, float* smem, in
 
   // X_i . W0 tile (+ b0 on k-chunk 0) -> partial slab of step i (parity i & 1)
   auto fwd = [&](int i) {
-    const float* A = sX + (i & 1) * 64 * XS;
+    const float* A = sX + (i % 3) * 64 * XS;
     if (w * 16 < BR) {
       f32x4 acc[NCT];
 #pragma unroll
@@ -963,11 +966,11 @@ __device__ __forceinline__ void l0_role_v2(const PersistArgs& a, float* smem, in
   // rows [cb * 64 / nc0, (cb + 1) * 64 / nc0) of this k-chunk's X_i . X_{i-1}^T -> Gram
   // slab of step i (parity i & 1)
   auto gram = [&](int i) {
-    const float* A = sX + (i & 1) * 64 * XS;
-    const float* Bm = sX + ((i - 1) & 1) * 64 * XS;
+    const float* A = sX + (i % 3) * 64 * XS;
+    const float* Bm = sX + ((i - 1) % 3) * 64 * XS;
     const int rows = 64 / a.nc0, r0 = cb * rows;
     const int ntg = (rows >> 4) * 4;   // 16 x 16 tiles of the slice (4 column tiles of 16)
-    const int base = (int)(a.o_g + (i & 1) * a.g_par) + kc * 64 * 64;
+    const int base = (int)(a.o_g + (i % 3) * a.g_par) + kc * 64 * 64;   // three Gram slabs (written a step early)
 #pragma unroll 1
     for (int t = w; t < ntg; t += 4) {
       const int tr = t >> 2, tc = t & 3;
@@ -1017,6 +1020,17 @@ __device__ __forceinline__ void l0_role_v2(const PersistArgs& a, float* smem, in
   pstamp(a, 0, 1);
   for (int i = 0; i < n; ++i) {
     if (st.valid(a, i) == 0) break;
+    // step i + 2's X chunk and its Gram slice depend on no hand-off: done while the
+    // chains still run step i (the X chunk goes to buffer (i + 2) % 3, which X_{i-1} left)
+    const bool ahead = i + 2 < n && st.valid(a, i + 2) > 0;
+    if (ahead) {
+      load_x(i + 2);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      pstamp(a, i, 9);
+      gram(i + 2);
+      pstamp(a, i, 10);
+    }
     pstamp(a, i, 2);
     if (!wait_all(a, flag_at(a, r, PMF_BWD), a.nch, (unsigned)(i + 1), PERR_L0_BWD)) return;
     pstamp(a, i, 3);
@@ -1030,7 +1044,7 @@ __device__ __forceinline__ void l0_role_v2(const PersistArgs& a, float* smem, in
     pstamp(a, i, 4);
     // DW0 tile = X_i^T dZ_0 (reduction over the batch rows), SGD update in place
     {
-      const float* Xi = sX + (i & 1) * 64 * XS;
+      const float* Xi = sX + (i % 3) * 64 * XS;
       f32x4 dw[TU0];
 #pragma unroll
       for (int u = 0; u < TU0; ++u) dw[u] = zero4f();
@@ -1082,13 +1096,9 @@ __device__ __forceinline__ void l0_role_v2(const PersistArgs& a, float* smem, in
     }
     __syncthreads();
     pstamp(a, i, 5);
-    // step i + 2: its X chunk into the buffer X_i leaves, then Pold and the Gram slice
-    if (i + 2 < n && st.valid(a, i + 2) > 0) {
-      load_x(i + 2);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
+    // step i + 2's Pold = X_{i+2} . W0 after step i; PART covers the Gram slab too
+    if (ahead) {
       fwd(i + 2);
-      gram(i + 2);
       publish(flag_at(a, r, PMF_PART) + q, (unsigned)(i + 3));
     }
     pstamp(a, i, 6);
@@ -1342,7 +1352,7 @@ __device__ __forceinline__ void chain_role(const PersistArgs& a, float* smem, in
 #pragma unroll
           for (int u = 0; u < RC_MAXSPLIT; ++u) {
             const int uc = u < a.nk0 ? u : a.nk0 - 1;
-            gl[u] = ldw4(rs, grow * 64 + gc4, (int)(a.o_g + (i & 1) * a.g_par) + uc * 64 * 64 + m0 * 64);
+            gl[u] = ldw4(rs, grow * 64 + gc4, (int)(a.o_g + (i % 3) * a.g_par) + uc * 64 * 64 + m0 * 64);
           }
           pstamp(a, i, 11);
           const int zs = (int)(a.o_dz0 + ((i - 1) & 1) * a.dz0_par);

@@ -101,6 +101,7 @@ bool Executor::build_persist() {
       const int nk0 = cdiv(l0.K, kc);
       if (nk0 > RC_MAXSPLIT) continue;
       if (v2) {
+        if (kc > 112) continue;   // three X chunks of kc + 1 columns in LDS (persist.hip L0V2_LDS)
         if (nk0 * nc0 + nd > cap) continue;
         const long long cost = 100000LL * nk0 + (long long)kc * cw;
         if (best_cost < 0 || cost < best_cost) { best_cost = cost; best_kc = kc; best_cw = cw; }
@@ -154,7 +155,7 @@ bool Executor::build_persist() {
   a.part_par = v2 ? (long long)a.nk0 * PM_ROWS * a.H0 : 0;
   a.o_part = take(npar * (long long)a.nk0 * PM_ROWS * a.H0);
   a.g_par = v2 ? (long long)a.nk0 * PM_ROWS * PM_ROWS : 0;
-  a.o_g = v2 ? take(npar * (long long)a.nk0 * PM_ROWS * PM_ROWS) : 0;
+  a.o_g = v2 ? take(3LL * a.nk0 * PM_ROWS * PM_ROWS) : 0;   // three Gram slabs (step % 3)
   a.dz0_par = v2 ? (long long)PM_ROWS * a.H0 : 0;
   a.o_dz0 = take(npar * (long long)PM_ROWS * a.H0);
   a.o_a0 = take((long long)PM_ROWS * a.H0);

@@ -19,8 +19,8 @@ NAMES = {
               3: "fwd1", 18: "fwd2", 19: "logits", 20: "loss", 4: "dz2", 21: "dx2", 22: "dz1_pub",
               23: "dx1_mm", 5: "dx1", 6: "bwd_pub", 7: "bwd_seen", 8: "stage_ld", 24: "dw_mm", 26: "opt",
               9: "upd", 10: "w_pub"},
-    "l0": {0: "start", 1: "part_pub", 2: "bwd_wait0", 3: "bwd_seen", 4: "dz_ld", 7: "dw_mm", 8: "colsum",
-           9: "opt", 5: "dw_upd", 10: "fwd_mm", 6: "next_pub"},
+    "l0": {0: "start", 1: "part_pub", 9: "x_next", 10: "gram_next", 2: "bwd_wait0", 3: "bwd_seen", 4: "dz_ld",
+           7: "dw_mm", 8: "colsum", 5: "dw_upd", 6: "next_pub"},
     "dw": {0: "a0_wait0", 1: "a0_seen", 2: "d2_seen", 3: "staged", 4: "dz1", 5: "dw_mm", 6: "w_pub"},
 }
 
