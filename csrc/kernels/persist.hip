@@ -934,7 +934,8 @@ __device__ __forceinline__ void l0_role_v2(const PersistArgs& a, float* smem, in
 #pragma unroll
         for (int ks = 0; ks < 16; ++ks) {
           const int k = kb + 16 * g + ks;
-          av[ks] = xat(arow, k);
+          // rows are kc0 + 1 wide: k past the chunk reads the next row -- masked to zero
+          av[ks] = k < kreal ? xat(arow, k) : 0.f;
 #pragma unroll
           for (int jj = 0; jj < NCT; ++jj) bv[jj][ks] = rb<BF>(sW[k * WS + jj * 16 + i16]);
         }
@@ -983,7 +984,7 @@ __device__ __forceinline__ void l0_role_v2(const PersistArgs& a, float* smem, in
 #pragma unroll
         for (int ks = 0; ks < 16; ++ks) {
           const int k = kb + 16 * g + ks;
-          av[ks] = xat(arow, k);
+          av[ks] = k < kreal ? xat(arow, k) : 0.f;   // (finite X past the chunk) x 0
           bv[ks] = xat(brow, k);
         }
 #pragma unroll
