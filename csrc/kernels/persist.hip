@@ -1018,14 +1018,14 @@ __device__ __forceinline__ void l0_role_v2(const PersistArgs& a, float* smem, in
     gram(1);
     publish(flag_at(a, r, PMF_PART) + q, 2u);
   }
+  if (n > 2 && st.valid(a, 2) > 0) load_x(2);   // in flight until iteration 0 needs it
   pstamp(a, 0, 1);
   for (int i = 0; i < n; ++i) {
     if (st.valid(a, i) == 0) break;
     // step i + 2's X chunk and its Gram slice depend on no hand-off: done while the
     // chains still run step i (the X chunk goes to buffer (i + 2) % 3, which X_{i-1} left)
     const bool ahead = i + 2 < n && st.valid(a, i + 2) > 0;
-    if (ahead) {
-      load_x(i + 2);
+    if (ahead) {   // X_{i+2} was issued at the end of the previous iteration (or the prologue)
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       pstamp(a, i, 9);
@@ -1097,6 +1097,8 @@ __device__ __forceinline__ void l0_role_v2(const PersistArgs& a, float* smem, in
     }
     __syncthreads();
     pstamp(a, i, 5);
+    // X_{i+3} into the buffer X_i just left: its DMA overlaps the Pold MFMAs below
+    if (i + 3 < n && st.valid(a, i + 3) > 0) load_x(i + 3);
     // step i + 2's Pold = X_{i+2} . W0 after step i; PART covers the Gram slab too
     if (ahead) {
       fwd(i + 2);
