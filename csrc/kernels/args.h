@@ -187,12 +187,15 @@ constexpr int PM_NTU = 2;      // layer-1 column tiles (and layer-2 row tiles) a
 // layer-1 activations for the weight-gradient workgroups), GO (residency: every
 // workgroup raises it on entry; the chain workgroups see the whole grid before they
 // touch any state)
-// X (sync: a workgroup's weight-gradient tile is in the exchange slab, see PersistArgs::sync)
-enum PmFlag : int { PMF_PART = 0, PMF_BWD = 1, PMF_W = 2, PMF_A0 = 3, PMF_D2 = 4, PMF_GO = 5, PMF_X = 6, PMF_N = 7 };
+// X (sync: a workgroup's weight-gradient tile is in the exchange slab, see PersistArgs::sync),
+// GR (V2 with ng > 0: a weight-gradient workgroup's Gram slab of a step is out)
+enum PmFlag : int { PMF_PART = 0, PMF_BWD = 1, PMF_W = 2, PMF_A0 = 3, PMF_D2 = 4, PMF_GO = 5, PMF_X = 6, PMF_GR = 7,
+                    PMF_N = 8 };
 // sticky error codes: the wait that timed out (PERR_GRID: the grid was not resident --
 // nothing was modified, the chunk can be re-run on another plan)
 enum PmErr : unsigned { PERR_L0_BWD = 1, PERR_CHAIN_PART = 2, PERR_CHAIN_BWD = 3, PERR_CHAIN_PREV = 4,
-                        PERR_DW_A0 = 5, PERR_DW_D2 = 6, PERR_XCHG = 7, PERR_PS = 8, PERR_GRID = 9 };
+                        PERR_DW_A0 = 5, PERR_DW_D2 = 6, PERR_XCHG = 7, PERR_PS = 8, PERR_GRID = 9,
+                        PERR_CHAIN_GR = 10 };
 constexpr int PM_XSLOT = 7 * 1024;   // floats of one workgroup's exchange slab (sync)
 struct PersistArgs {
   int R, B, nsteps;
@@ -202,7 +205,11 @@ struct PersistArgs {
   // V2 (plain SGD, ReLU, fit granularity): nd weight-gradient workgroups per replica own
   // the W1 columns / W2 rows; the chain rebuilds Z_0 from Pold + Gram corrections
   int v2, nd;
-  long long o_g;                    // Gram partials [2][nk0][64][64] (V2)
+  // V2 Gram slabs X_s . X_{s-1}^T: ng > 0 -- computed by the weight-gradient workgroups
+  // d < ng over k-chunks of gk columns (their idle window between W and A0), one slab each;
+  // ng = 0 -- by the layer-0 tiles, one slab per k-chunk of kc0 (nk0 slabs)
+  int ng, gk;
+  long long o_g;                    // Gram partials [3][max(nk0, ng)][64][64] (V2)
   long long part_par, g_par, dz0_par;   // parity strides of the double-buffered partials / Gram / dZ_0 (V2; 0 in V1)
   // sync (V1 roles, per-step synchronous DP of the R replicas = one model): after its
   // weight-gradient MFMAs every owning workgroup puts its tile into its exchange slab
@@ -220,6 +227,10 @@ struct PersistArgs {
   int ps_mode;
   PsArgs ps;
   int bf16;                         // V2 only: X and the weight images are bf16 (mixed_bfloat16 policy)
+  // the epilogue also writes both weight-image parities (V2: 0 -- the host marks them stale
+  // and rebuilds them from the masters before the next reader; the transposed image's
+  // stores are strided)
+  int imgs;
   int act0, act1, act2;
   float rate0, rate1;
   int bias0, bias1, bias2;

@@ -77,14 +77,19 @@ struct ChainLds {
   static constexpr int o_b2 = o_b1 + H1;              // [16]
   static constexpr int o_row = o_b2 + 16;             // [16] ints
   static constexpr int o_gs = o_row + 16;             // [16][65] V2: this chain's Gram rows (+ 1)
-  static constexpr int TOTAL = o_gs + 16 * 65;
+  static constexpr int o_wr = o_gs + 16 * 65;         // [4] V2: the W hand-off seen early (broadcast)
+  static constexpr int TOTAL = o_wr + 4;
 };
 constexpr int L0_LDS = 2 * 64 * 129 + 128 * 33 + 64 * 33 + 128 * 33;   // + the pulled tile (PS hook)
 // V2 layer-0: three X chunks (kc0 <= 112: stride 113), W0 tile (cw <= 64), dZ_0 columns, store staging
 constexpr int L0V2_LDS = 3 * 64 * 113 + 128 * 65 + 64 * 65 + 64 * 65;
 constexpr int DW_LDS = 64 * 129 + 2 * 64 * 33 + 64 * 17 + 32 * 17;
+// + the Gram k-chunk (ng > 0): two X chunks of <= 112 columns (row stride <= 116) and
+// the 64 x 64 slab staging
+constexpr int DWG_LDS = DW_LDS + 2 * 64 * 116 + 64 * 65;
+constexpr int DWP_LDS = DWG_LDS;
 constexpr int cmax(int x, int y) { return x > y ? x : y; }
-constexpr int LDS_FLOATS = (cmax(cmax(ChainLds<128, 128>::TOTAL, L0_LDS), cmax(L0V2_LDS, DW_LDS)) + 3) & ~3;
+constexpr int LDS_FLOATS = (cmax(cmax(ChainLds<128, 128>::TOTAL, L0_LDS), cmax(L0V2_LDS, DWP_LDS)) + 3) & ~3;
 
 __device__ __forceinline__ f32x4 mma(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
@@ -193,6 +198,46 @@ __device__ __forceinline__ bool wait_two(const PersistArgs& a, const unsigned* f
       const unsigned v = (inA || inB) ? __hip_atomic_load((gu32*)(const_cast<unsigned*>(f)), __ATOMIC_RELAXED,
                                                           __HIP_MEMORY_SCOPE_AGENT)
                                       : want;
+      if (__all(v >= want)) break;
+      if ((long long)(wall_clock64() - t0) > a.timeout) {
+        ok = 0;
+        if (lane == 0) __hip_atomic_store((gu32*)(a.err), code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  ok = __syncthreads_and(ok);
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  return ok != 0;
+}
+
+// the same for up to four producer sets (lanes [o_s, o_s + n_s) watch set s; <= 64 in all):
+// one poll, one barrier for every hand-off a phase depends on
+struct WaitSet {
+  const unsigned* f;
+  int n;
+  unsigned tag;
+};
+__device__ __forceinline__ bool wait_sets(const PersistArgs& a, const WaitSet (&ws)[4], unsigned code) {
+  int ok = 1;
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    const unsigned* f = nullptr;
+    unsigned want = 0;
+    int o = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (lane >= o && lane < o + ws[k].n) {
+        f = ws[k].f + (lane - o);
+        want = ws[k].tag;
+      }
+      o += ws[k].n;
+    }
+    const unsigned long long t0 = wall_clock64();
+    for (;;) {
+      const unsigned v = f ? __hip_atomic_load((gu32*)(const_cast<unsigned*>(f)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                           : want;
       if (__all(v >= want)) break;
       if ((long long)(wall_clock64() - t0) > a.timeout) {
         ok = 0;
@@ -1015,7 +1060,7 @@ __device__ __forceinline__ void l0_role_v2(const PersistArgs& a, float* smem, in
   }
   if (v1) {
     fwd(1);
-    gram(1);
+    if (a.ng == 0) gram(1);
     publish(flag_at(a, r, PMF_PART) + q, 2u);
   }
   if (n > 2 && st.valid(a, 2) > 0) load_x(2);   // in flight until iteration 0 needs it
@@ -1025,7 +1070,7 @@ __device__ __forceinline__ void l0_role_v2(const PersistArgs& a, float* smem, in
     // step i + 2's X chunk and its Gram slice depend on no hand-off: done while the
     // chains still run step i (the X chunk goes to buffer (i + 2) % 3, which X_{i-1} left)
     const bool ahead = i + 2 < n && st.valid(a, i + 2) > 0;
-    if (ahead) {   // X_{i+2} was issued at the end of the previous iteration (or the prologue)
+    if (ahead && a.ng == 0) {   // X_{i+2} was issued at the end of the previous iteration (or the prologue)
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       pstamp(a, i, 9);
@@ -1097,14 +1142,16 @@ __device__ __forceinline__ void l0_role_v2(const PersistArgs& a, float* smem, in
     }
     __syncthreads();
     pstamp(a, i, 5);
-    // X_{i+3} into the buffer X_i just left: its DMA overlaps the Pold MFMAs below
-    if (i + 3 < n && st.valid(a, i + 3) > 0) load_x(i + 3);
-    // step i + 2's Pold = X_{i+2} . W0 after step i; PART covers the Gram slab too
+    // step i + 2's Pold = X_{i+2} . W0 after step i (ng == 0: PART covers the Gram slab too)
     if (ahead) {
       fwd(i + 2);
       publish(flag_at(a, r, PMF_PART) + q, (unsigned)(i + 3));
     }
     pstamp(a, i, 6);
+    // X_{i+3} into the buffer X_i just left, after the Pold MFMAs: an LDS-DMA in flight
+    // makes the compiler wait for it before every later LDS access (measured: issued
+    // before fwd, the Pold phase took 6.9 instead of 3.7 us)
+    if (i + 3 < n && st.valid(a, i + 3) > 0) load_x(i + 3);
   }
 
   // ---- epilogue: master tile and both weight-image parities (plain SGD: no state)
@@ -1115,10 +1162,12 @@ __device__ __forceinline__ void l0_role_v2(const PersistArgs& a, float* smem, in
     const int k = e / CW, nn = e - k * CW;
     const float v = sW[k * WS + nn];
     P[a.p_off0 + (long long)(k0 + k) * H0 + n0 + nn] = v;
+    if (a.imgs) {
 #pragma unroll
-    for (int par = 0; par < 2; ++par) {
-      img_store<BF>(Wsh, par * a.wsh_par + (long long)(k0 + k) * a.Np[0] + n0 + nn, v);
-      img_store<BF>(WTsh, par * a.wtsh_par + (long long)(n0 + nn) * a.Kp[0] + k0 + k, v);
+      for (int par = 0; par < 2; ++par) {
+        img_store<BF>(Wsh, par * a.wsh_par + (long long)(k0 + k) * a.Np[0] + n0 + nn, v);
+        img_store<BF>(WTsh, par * a.wtsh_par + (long long)(n0 + nn) * a.Kp[0] + k0 + k, v);
+      }
     }
   }
   if (bown) P[a.p_off0 + (long long)a.K0 * H0 + n0 + tid] = bw;
@@ -1288,44 +1337,71 @@ __device__ __forceinline__ void chain_role(const PersistArgs& a, float* smem, in
   if (!wait_grid(a)) return;
 
   const int n = a.nsteps;
+  // V2: this chain's rows of step s's Gram slabs (X_s . X_{s-1}^T, one per k-chunk)
+  f32x4 gl[V2 ? RC_MAXSPLIT : 1];
+  const int grow = tid >> 4, gc4 = (tid & 15) * 4;
+  auto load_gram = [&](int s) {
+    if constexpr (V2) {
+      const int ngs = a.ng > 0 ? a.ng : a.nk0;
+#pragma unroll
+      for (int u = 0; u < RC_MAXSPLIT; ++u) {   // branch-free: slabs past ngs re-read the last one
+        const int uc = u < ngs ? u : ngs - 1;
+        gl[u] = ldw4(rs, grow * 64 + gc4, (int)(a.o_g + (s % 3) * a.g_par) + uc * 64 * 64 + m0 * 64);
+      }
+    }
+  };
+  // data rows of this workgroup's targets (thread: rows tid / 32 + 8h, target column
+  // tid % 32), read one step ahead so the target loads have no dependent address load
+  auto target_rows = [&](int s, int (&prow)[2]) {
+    const int vs = st.valid(a, s);
+    const int* pr = a.perm + (long long)r * a.sPerm + (st.s0 + s) * a.B + m0;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int rr = (tid >> 5) + 8 * h;
+      prow[h] = (m0 + rr < vs && (tid & 31) < a.ldy) ? pr[rr] : -1;
+    }
+  };
+  int prow[2];
+  target_rows(0, prow);
   for (int i = 0; i < n; ++i) {
     const int valid = st.valid(a, i);
     if (valid == 0) break;
     const long long it = iter_at(a.ctr, a.ntrain, a.B, r, st.s0, i);
-    const long long step = st.s0 + i;
     // batch rows of this workgroup: targets requested before the wait
     float yv[2];
     {
-      const int* pr = a.perm + (long long)r * a.sPerm + step * a.B + m0;
       const float* Yb = a.Y + (long long)r * a.sY;
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int rr = (tid >> 5) + 8 * h, c = tid & 31;
-        const bool in = m0 + rr < valid && c < a.ldy;
-        const int prow = in ? pr[rr] : 0;
-        yv[h] = in ? Yb[(long long)prow * a.ldy + c] : 0.f;
-      }
+      for (int h = 0; h < 2; ++h) yv[h] = prow[h] >= 0 ? Yb[(long long)prow[h] * a.ldy + (tid & 31)] : 0.f;
     }
     pstamp(a, i, 0);
-    // this step's partials and (after step 0) every chain workgroup's updated W1 / W2
-    // columns of the previous step, watched by one wave
     // V1: the partials and every chain workgroup's updated W1 / W2 columns of the previous
-    // step.  V2: the partials and the previous step's dZ_0 rows of every chain workgroup
-    // (the Z_0 correction); the DW workgroups' W1 / W2 are waited for only before FWD1
-    if (!wait_two(a, flag_at(a, r, PMF_PART), nl0, (unsigned)(i + 1), flag_at(a, r, V2 ? PMF_BWD : PMF_W),
-                  i > 0 ? a.nch : 0, (unsigned)i, PERR_CHAIN_PART))
-      return;
+    // step.  V2: the partials, the previous step's dZ_0 rows of every chain workgroup (the
+    // Z_0 correction) and (ng > 0) this step's Gram slabs -- one poll.  The DW workgroups'
+    // W1 / W2 come later in the step (below)
+    {
+      const bool prev = i > 0;
+      const WaitSet sets[4] = {
+          {flag_at(a, r, PMF_PART), nl0, (unsigned)(i + 1)},
+          {flag_at(a, r, V2 ? PMF_BWD : PMF_W), prev ? a.nch : 0, (unsigned)i},
+          {flag_at(a, r, PMF_GR), (V2 && prev) ? a.ng : 0, (unsigned)(i + 1)},
+          {nullptr, 0, 0u}};
+      if (!wait_sets(a, sets, PERR_CHAIN_PART)) return;
+    }
     pstamp(a, i, 1);
-    // the weight loads go first: their latency overlaps the partial sums below
+    if (i + 1 < n) target_rows(i + 1, prow);
     Staged<H0 * H1 / 1024> w1s;
     Staged<H1 / 64> w2s;
     f32x4 bvec = zero4f();
-    if (!V2 && i > 0) {
+    // V1: the weight loads go first: their latency overlaps the partial sums below
+    auto issue_w = [&]() {
       stage_issue(w1s, rs, (int)a.o_w1, H1, H0, H1);
       stage_issue(w2s, rs, (int)a.o_w2, 16, H1, 16);
       if (tid < H1 / 4) bvec = ldw4(rs, 4 * tid, (int)a.o_b1);
       else if (tid >= 64 && tid < 68) bvec = ldw4(rs, 4 * (tid - 64), (int)a.o_b2);
-    }
+    };
+    if (!V2 && i > 0) issue_w();
+    bool wready = false;   // V2: the W1 / W2 loads were issued during phase 0
 
     // ---- phase 0: z_0 = sum of the split-K partials (b0 is in chunk 0's) -> act, dropout
     {
@@ -1347,16 +1423,11 @@ __device__ __forceinline__ void chain_role(const PersistArgs& a, float* smem, in
       }
       // V2, i >= 1: this chain's rows of the Gram slabs (requested before the wait for
       // the previous step's dZ_0 rows of every chain, whose fragments follow)
-      f32x4 gl[RC_MAXSPLIT];
       float bz[2][16];
-      const int grow = tid >> 4, gc4 = (tid & 15) * 4;
+      unsigned wflag = 0;
       if constexpr (V2) {
         if (i > 0) {
-#pragma unroll
-          for (int u = 0; u < RC_MAXSPLIT; ++u) {
-            const int uc = u < a.nk0 ? u : a.nk0 - 1;
-            gl[u] = ldw4(rs, grow * 64 + gc4, (int)(a.o_g + (i % 3) * a.g_par) + uc * 64 * 64 + m0 * 64);
-          }
+          load_gram(i);
           pstamp(a, i, 11);
           const int zs = (int)(a.o_dz0 + ((i - 1) & 1) * a.dz0_par);
 #pragma unroll
@@ -1365,6 +1436,12 @@ __device__ __forceinline__ void chain_role(const PersistArgs& a, float* smem, in
 #pragma unroll
             for (int ks = 0; ks < 16; ++ks) bz[jj][ks] = rb<BF>(ldw1(rs, (16 * g + ks) * H0 + ct * 16 + i16, zs));
           }
+          // one non-blocking look at the DW workgroups' W flags, returning with the loads
+          // above; read after the sums (the correction's barrier broadcasts it)
+          if (tid < 64)
+            wflag = tid < a.nd ? __hip_atomic_load((gu32*)(flag_at(a, r, PMF_W) + tid), __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_AGENT)
+                               : (unsigned)i;
         }
       }
 #pragma unroll
@@ -1385,12 +1462,24 @@ __device__ __forceinline__ void chain_role(const PersistArgs& a, float* smem, in
           // the product on the MFMAs, back through LDS in the row layout of z
           float* sG = smem + Lo::o_gs;
           f32x4 gsum = f32x4{1.f, 1.f, 1.f, 1.f};
+          const int ngs = a.ng > 0 ? a.ng : a.nk0;
 #pragma unroll
           for (int u = 0; u < RC_MAXSPLIT; ++u)
-            if (u < a.nk0) gsum += gl[u];
+            if (u < ngs) gsum += gl[u];
 #pragma unroll
           for (int e = 0; e < 4; ++e) sG[grow * 65 + gc4 + e] = gsum[e];
+          int* sWr = reinterpret_cast<int*>(smem + Lo::o_wr);
+          if (tid < 64) {
+            const bool rdy = __all(wflag >= (unsigned)i);
+            if (tid == 0) sWr[0] = rdy ? 1 : 0;
+          }
           __syncthreads();
+          // W1 / W2 already out: their loads overlap the correction and the act below
+          wready = sWr[0] != 0;
+          if (wready) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            issue_w();
+          }
           const long long itp = iter_at(a.ctr, a.ntrain, a.B, r, st.s0, i - 1);
           const float coef = -(a.op.lr / (1.f + a.op.decay * (float)itp)) * a.op.grad_scale;
           float ag[16];
@@ -1454,12 +1543,11 @@ __device__ __forceinline__ void chain_role(const PersistArgs& a, float* smem, in
     }
     if constexpr (V2) {
       if (i > 0) {   // the DW workgroups' W1 / W2 / biases of the previous step -> LDS
-        if (!wait_all(a, flag_at(a, r, PMF_W), a.nd, (unsigned)i, PERR_CHAIN_PREV)) return;
+        if (!wready) {
+          if (!wait_all(a, flag_at(a, r, PMF_W), a.nd, (unsigned)i, PERR_CHAIN_PREV)) return;
+          issue_w();
+        }
         pstamp(a, i, 12);
-        stage_issue(w1s, rs, (int)a.o_w1, H1, H0, H1);
-        stage_issue(w2s, rs, (int)a.o_w2, 16, H1, 16);
-        if (tid < H1 / 4) bvec = ldw4(rs, 4 * tid, (int)a.o_b1);
-        else if (tid >= 64 && tid < 68) bvec = ldw4(rs, 4 * (tid - 64), (int)a.o_b2);
         stage_commit(w1s, H0, sW1, L1S);
         stage_commit(w2s, H1, sW2, S17);
         if (tid < H1 / 4) {
@@ -1683,7 +1771,8 @@ __device__ __forceinline__ void chain_role(const PersistArgs& a, float* smem, in
 #pragma unroll
         for (int h8 = 0; h8 < 8; ++h8) {
 #pragma unroll
-          for (int u = 0; u < TU; ++u) dw[u] = mma(xa[u][h8], uct[u] ? zb[1][h8] : zb[0][h8], dw[u]);
+          for (int u = 0; u < TU; ++u)   // wave-uniform: no MFMAs for tiles past ndw1
+            if (w + 4 * u < ndw1) dw[u] = mma(xa[u][h8], uct[u] ? zb[1][h8] : zb[0][h8], dw[u]);
           dw[TU] = mma(a1v[h8], d2v[h8], dw[TU]);
         }
         // bias gradients = column sums over the batch rows: an all-ones A operand (every
@@ -1877,7 +1966,17 @@ __device__ __forceinline__ void dw_role_v2(const PersistArgs& a, float* smem, in
     urt[u] = t < ndw1 ? t / nown : 0;
     uct[u] = t < ndw1 ? t - (t / nown) * nown : 0;
   }
-  for (int e = tid; e < DW_LDS; e += 256) smem[e] = 0.f;
+  // Gram k-chunk of this workgroup (ng > 0): X_s . X_{s-1}^T over columns [k0g, k0g + kg)
+  const bool gown = a.ng > 0 && d < a.ng;
+  const int k0g = d * a.gk;
+  const int kg = gown ? (a.K0 - k0g < a.gk ? a.K0 - k0g : a.gk) : 0;
+  // row stride: fp32 = 4 (mod 8) floats, bf16 = 2 (mod 4) dwords -- the fragment reads
+  // below (16 rows x 4 consecutive k per MFMA) hit 64 distinct banks
+  const int xneed = BF ? (kg + 1) / 2 + 1 : kg + 1;
+  const int XSg = BF ? xneed + ((2 - xneed) % 4 + 4) % 4 : xneed + ((4 - xneed) % 8 + 8) % 8;
+  float* sXg = smem + DW_LDS;        // [2][64][XSg] X chunks of steps s & 1
+  float* sTg = sXg + 2 * 64 * 116;   // [64][65] slab staging (16-byte stores)
+  for (int e = tid; e < DWP_LDS; e += 256) smem[e] = 0.f;
   __syncthreads();
   constexpr int NM = TU * 4 + 4;
   float wm[NM];
@@ -1907,10 +2006,81 @@ __device__ __forceinline__ void dw_role_v2(const PersistArgs& a, float* smem, in
   const float ks1 = a.rate1 > 0.f ? 1.f / (1.f - a.rate1) : 1.f;
   __syncthreads();
 
+  // step s's X chunk (rows gathered through the permutation) -> buffer s & 1, LDS-DMA
+  auto load_xg = [&](int s) {
+    const int valid = st.valid(a, s);
+    const int* pr = a.perm + (long long)r * a.sPerm + (st.s0 + s) * a.B;
+    float* dst = sXg + (s & 1) * 64 * XSg;
+    const int myrow = pr[lane < valid ? lane : 0];
+    for (int v = 0; v < 16; ++v) {
+      const int b = w + 4 * v;
+      if (b >= BR) break;
+      const int row = __builtin_amdgcn_readlane(myrow, b);
+      if constexpr (BF) {
+        const float* src = reinterpret_cast<const float*>(reinterpret_cast<const __bf16*>(a.X) +
+                                                          (long long)r * a.sX + (long long)row * a.ldx + k0g);
+        if (lane < (kg + 1) / 2) __builtin_amdgcn_global_load_lds(src + lane, dst + b * XSg, 4, 0, 0);
+      } else {
+        const float* src = a.X + (long long)r * a.sX + (long long)row * a.ldx + k0g;
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+          if (64 * h + lane < kg) __builtin_amdgcn_global_load_lds(src + 64 * h + lane, dst + b * XSg + 64 * h, 4, 0, 0);
+      }
+    }
+  };
+  // Gram slab of step s = X_s . X_{s-1}^T over this k-chunk: wave w owns column tile w
+  // and all four row tiles (the B fragments read once, four independent accumulators)
+  auto gram_dw = [&](int s) {
+    const float* A = sXg + (s & 1) * 64 * XSg;
+    const float* Bm = sXg + ((s - 1) & 1) * 64 * XSg;
+    auto xat = [](const float* row, int k) -> float { if constexpr (BF) return bf_at(row, k); else return row[k]; };
+    f32x4 acc[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acc[u] = zero4f();
+    const float* brow = Bm + (w * 16 + i16) * XSg;
+#pragma unroll 1
+    for (int kb = 0; kb < kg; kb += 16) {
+      float av[4][4], bv[4];
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const int k = kb + 4 * ks + g;
+        bv[ks] = xat(brow, k);   // finite (X or zero padding) past the chunk, times a zero A
+#pragma unroll
+        for (int u = 0; u < 4; ++u) av[u][ks] = k < kg ? xat(A + (u * 16 + i16) * XSg, k) : 0.f;
+      }
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) acc[u] = mma(av[u][ks], bv[ks], acc[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq) sTg[(u * 16 + 4 * g + qq) * 65 + w * 16 + i16] = acc[u][qq];
+    __syncthreads();
+    const int base = (int)(a.o_g + (s % 3) * a.g_par) + d * 64 * 64;
+    for (int e = tid; e < BR * 16; e += 256) {
+      const int row = e >> 4, c4 = e & 15;
+      const float* src = sTg + row * 65 + 4 * c4;
+      stw4(rs, row * 64 + 4 * c4, base, f32x4{src[0], src[1], src[2], src[3]});
+    }
+    publish(flag_at(a, r, PMF_GR) + d, (unsigned)(s + 1));
+  };
+
   const int n = a.nsteps;
+  if (gown && n > 1 && st.valid(a, 1) > 0) {   // Gram(1); Gram(s + 2) follows iteration s
+    load_xg(0);
+    load_xg(1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    gram_dw(1);
+  }
   for (int i = 0; i < n; ++i) {
     if (st.valid(a, i) == 0) break;
     const long long it = iter_at(a.ctr, a.ntrain, a.B, r, st.s0, i);
+    const bool gnext = gown && i + 2 < n && st.valid(a, i + 2) > 0;
+    // X_{i+2} into the buffer X_i left (Gram(i + 1) is out): the DMA runs during the A0 wait
+    if (gnext) load_xg(i + 2);
     pstamp(a, i, 0);
     if (!wait_all(a, flag_at(a, r, PMF_A0), a.nch, (unsigned)(i + 1), PERR_DW_A0)) return;
     pstamp(a, i, 1);
@@ -2023,6 +2193,12 @@ __device__ __forceinline__ void dw_role_v2(const PersistArgs& a, float* smem, in
       __syncthreads();
     }
     pstamp(a, i, 6);
+    if (gnext) {   // Gram(i + 2), in the idle window before the next step's A0
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      gram_dw(i + 2);
+      pstamp(a, i, 7);
+    }
   }
 
   // ---- epilogue: owned masters and both weight-image parities (plain SGD: no state)
@@ -2037,6 +2213,7 @@ __device__ __forceinline__ void dw_role_v2(const PersistArgs& a, float* smem, in
     for (int qq = 0; qq < 4; ++qq) {
       const int k = rt * 16 + 4 * g + qq, nn = (d + nd * c) * 16 + i16;
       P[a.p_off1 + (long long)k * H1 + nn] = wm[4 * u + qq];
+      if (!a.imgs) continue;
 #pragma unroll
       for (int par = 0; par < 2; ++par) {
         img_store<BF>(Wsh, par * a.wsh_par + a.wsh_off[1] + (long long)k * a.Np[1] + nn, wm[4 * u + qq]);
@@ -2049,6 +2226,7 @@ __device__ __forceinline__ void dw_role_v2(const PersistArgs& a, float* smem, in
     for (int qq = 0; qq < 4; ++qq) {
       const int k = (d + nd * w) * 16 + 4 * g + qq;
       P[a.p_off2 + (long long)k * C + i16] = wm[4 * TU + qq];
+      if (!a.imgs) continue;
 #pragma unroll
       for (int par = 0; par < 2; ++par) {
         img_store<BF>(Wsh, par * a.wsh_par + a.wsh_off[2] + (long long)k * a.Np[2] + i16, wm[4 * TU + qq]);

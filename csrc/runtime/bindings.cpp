@@ -198,6 +198,7 @@ PYBIND11_MODULE(_C, m) {
       .def("persistent", &Executor::persistent)
       .def("persist_geometry", &Executor::persist_geometry)
       .def("persist_variant", &Executor::persist_variant)
+      .def("persist_images", &Executor::persist_images)
       .def("set_param_server", [](Executor& e, ShardedParameterServer* ps, int mode) {
         return e.set_param_server(ps ? ps->kernel_args() : PsArgs{}, ps ? mode : 0);
       }, py::arg("ps"), py::arg("mode"))

@@ -122,9 +122,19 @@ bool Executor::build_persist() {
   // their MFMA chain vs two tiles each: the W1 / W2 hand-off is on the step's critical path)
   const int nd_use = (v2 && cdiv(l0.K, best_kc) * (l0.N / best_cw) + l1.N / 16 <= cap) ? l1.N / 16 : nd;
   a.nch = nch; a.v2 = v2 ? 1 : 0; a.nd = nd_use;
+  // V2 Gram slabs on the weight-gradient workgroups (off the layer-0 tiles' loop, which is
+  // on the step's critical path) when every k-chunk fits their LDS (<= 112 columns, even
+  // for the bf16 pairs); otherwise on the layer-0 tiles
+  const char* gl0 = std::getenv("ELEPHAS_AMD_PERSIST_GRAM_L0");   // A/B: keep them on the layer-0 tiles
+  if (v2 && !(gl0 && std::atoi(gl0) != 0)) {
+    const int gk = (cdiv(l0.K, nd_use) + 1) & ~1;
+    if (gk <= 112) { a.gk = gk; a.ng = cdiv(l0.K, gk); }
+  }
   a.wgs = a.nk0 * a.nc0 + nch + nd_use;
   a.sync = c_.persist_sync ? 1 : 0;
   a.bf16 = c_.bf16 ? 1 : 0;
+  const char* pim = std::getenv("ELEPHAS_AMD_PERSIST_IMAGES");   // A/B: V2 epilogue writes the images too
+  a.imgs = (!v2 || (pim && std::atoi(pim) != 0)) ? 1 : 0;
   a.act0 = l0.act; a.act1 = l1.act; a.act2 = l2.act;
   a.rate0 = l0.rate; a.rate1 = l1.rate;
   a.bias0 = l0.has_bias; a.bias1 = l1.has_bias; a.bias2 = l2.has_bias;
@@ -154,8 +164,9 @@ bool Executor::build_persist() {
   const int npar = v2 ? 2 : 1;
   a.part_par = v2 ? (long long)a.nk0 * PM_ROWS * a.H0 : 0;
   a.o_part = take(npar * (long long)a.nk0 * PM_ROWS * a.H0);
-  a.g_par = v2 ? (long long)a.nk0 * PM_ROWS * PM_ROWS : 0;
-  a.o_g = v2 ? take(3LL * a.nk0 * PM_ROWS * PM_ROWS) : 0;   // three Gram slabs (step % 3)
+  const int nslab = std::max(a.nk0, a.ng);
+  a.g_par = v2 ? (long long)nslab * PM_ROWS * PM_ROWS : 0;
+  a.o_g = v2 ? take(3LL * nslab * PM_ROWS * PM_ROWS) : 0;   // three Gram slabs (step % 3)
   a.dz0_par = v2 ? (long long)PM_ROWS * a.H0 : 0;
   a.o_dz0 = take(npar * (long long)PM_ROWS * a.H0);
   a.o_a0 = take((long long)PM_ROWS * a.H0);

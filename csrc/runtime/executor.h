@@ -128,6 +128,7 @@ class Executor {
   // workgroups, workgroups per replica, grid}
   std::vector<int> persist_geometry() const;
   std::vector<int> persist_variant() const;   // {1 or 2, DW workgroups per replica, sync}
+  bool persist_images() const { return pm_.on && pm_.args.imgs != 0; }   // epilogue writes the weight images
   // parameter-server hook of the persistent plan (V1 roles only): every step pushes the
   // owned parameters' deltas into the server and pulls the next step's (mode 1 hogwild,
   // 2 asynchronous, 0 off); false when the plan cannot (not persistent, or V2 roles)

@@ -19,7 +19,9 @@ HostLoader::HostLoader(long long chunk_bytes, int nbuf, int threads) : chunk_(ch
   if (chunk_bytes <= 0 || nbuf < 1) throw std::invalid_argument("HostLoader: bad sizes");
   if (threads <= 0) {
     const char* e = getenv("ELEPHAS_AMD_LOADER_THREADS");
-    threads = e ? atoi(e) : (int)std::min(8u, std::max(1u, std::thread::hardware_concurrency()));
+    // 16: a GPU's CPU share on an MI355X node (8 GPUs per host); the fp32 -> bf16 row
+    // packing of inference inputs is bound by it (Wide predict)
+    threads = e ? atoi(e) : (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
   }
   threads_ = std::max(1, threads);
   for (int i = 0; i < nbuf; ++i) {
@@ -223,9 +225,12 @@ void infer_pipeline(Executor& exe, HostLoader& L, const InferPipeArgs& a, const 
   if (a.B <= 0 || a.stage_rows <= 0 || a.stage_rows % a.B) throw std::invalid_argument("infer_pipeline: bad stage");
   if (a.x_bf16 && !a.dStage) throw std::invalid_argument("infer_pipeline: bf16 rows need a device staging buffer");
   const long long nst = (a.n + a.stage_rows - 1) / a.stage_rows;
-  // bf16 rows: the packing threads convert on the host (half the PCIe bytes; measured
-  // faster than DMA-ing fp32 and converting on the device: Wide predict 9.3 vs 12.8 ms)
-  const HostPin xpin(a.x_bf16 ? nullptr : a.x, (size_t)(((a.n - 1) * a.x_ld + a.k) * 4));
+  // bf16 rows: by default the packing threads convert on the host (half the PCIe bytes);
+  // ELEPHAS_AMD_INFER_DEVICE_CVT=1: pin the fp32 rows, DMA them (one linear copy when
+  // dense) and convert on the device
+  const char* dc = std::getenv("ELEPHAS_AMD_INFER_DEVICE_CVT");
+  const bool dev_cvt = a.x_bf16 && dc && std::atoi(dc) != 0;
+  const HostPin xpin((a.x_bf16 && !dev_cvt) ? nullptr : a.x, (size_t)(((a.n - 1) * a.x_ld + a.k) * 4));
   const HostPin ypin(a.y, a.y ? (size_t)(((a.n - 1) * a.y_ld + a.ky) * 4) : 0);
   const HostPin opin(a.out, a.out ? (size_t)(a.n * a.ldp * 4) : 0);
   std::vector<hipEvent_t> evs;  // [up, done] + one download event per stage (staged copy-out)
@@ -248,9 +253,12 @@ void infer_pipeline(Executor& exe, HostLoader& L, const InferPipeArgs& a, const 
       const long long lo = st * a.stage_rows, nr = std::min(a.stage_rows, a.n - lo);
       const float* xh = a.x + lo * a.x_ld;
       if (xpin && a.x_bf16) {
-        chk(hipMemcpy2DAsync(a.dStage, (size_t)(a.k * 4), xh, (size_t)(a.x_ld * 4), (size_t)(a.k * 4), (size_t)nr,
-                             hipMemcpyHostToDevice, s_up),
-            "infer H2D");
+        if (a.x_ld == a.k)   // dense rows: one linear DMA (the 2D path is a slower copy)
+          chk(hipMemcpyAsync(a.dStage, xh, (size_t)(nr * a.k * 4), hipMemcpyHostToDevice, s_up), "infer H2D");
+        else
+          chk(hipMemcpy2DAsync(a.dStage, (size_t)(a.k * 4), xh, (size_t)(a.x_ld * 4), (size_t)(a.k * 4), (size_t)nr,
+                               hipMemcpyHostToDevice, s_up),
+              "infer H2D");
         chk(ea_cvt_rows_bf16(a.dStage, a.k, a.dX + lo * a.dX_ld, a.dX_ld / 2, nr, a.k, s_up), "infer cvt");
       } else if (xpin) {
         chk(hipMemcpy2DAsync(a.dX + lo * a.dX_ld, (size_t)a.dX_ld, xh, (size_t)(a.x_ld * 4), (size_t)(a.k * 4),

@@ -560,6 +560,8 @@ class NativeTrainer(TrainerBase):
             # hand-off flags and advances the counters), so there is nothing for a graph
             # to save, and every extra launch would pay the kernel's fill / drain
             # (weights, optimizer state, first forward) again
+            if not self.exe.persist_images():
+                self._images_stale = True   # the kernel updates the masters only (V2)
             while nsteps > 0:
                 n = min(nsteps, self.GRAPH_CHUNK)
                 self.exe.train_chunk(n, self.s)

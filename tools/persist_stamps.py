@@ -21,7 +21,7 @@ NAMES = {
               9: "upd", 10: "w_pub"},
     "l0": {0: "start", 1: "part_pub", 9: "x_next", 10: "gram_next", 2: "bwd_wait0", 3: "bwd_seen", 4: "dz_ld",
            7: "dw_mm", 8: "colsum", 5: "dw_upd", 6: "next_pub"},
-    "dw": {0: "a0_wait0", 1: "a0_seen", 2: "d2_seen", 3: "staged", 4: "dz1", 5: "dw_mm", 6: "w_pub"},
+    "dw": {0: "a0_wait0", 1: "a0_seen", 2: "d2_seen", 3: "staged", 4: "dz1", 5: "dw_mm", 6: "w_pub", 7: "gram"},
 }
 
 
@@ -69,17 +69,41 @@ def main():
     roles = {"l0": q < nl0, "chain": (q >= nl0) & (q < nl0 + nch), "dw": q >= nl0 + nch}
     chain = roles["chain"]
     ref_k = 6   # chain: dZ_0 rows published (end of a step)
-    print("ticks of 10 ns -> us; per step, medians relative to the chains' dZ_0 publication of the previous step")
+    rep = np.arange(grid) % R
+    print("ticks of 10 ns -> us; per step, medians relative to the same replica's chains' dZ_0 "
+          "publication of the previous step (replicas run unsynchronised)")
+
+    def base(i):   # per block: its replica's median chain dZ_0 publication of step i - 1
+        b = np.zeros(grid)
+        for rr in range(R):
+            b[rep == rr] = np.median(s[chain & (rep == rr), i - 1, ref_k])
+        return b
+
     for i in range(1, min(8, nst)):
-        b0 = np.median(s[chain, i - 1, ref_k])
-        if b0 == 0:
+        b0 = base(i)
+        if (b0 == 0).any():
             continue
         for role, mask in roles.items():
             if not mask.any():
                 continue
-            vals = {n: (np.median(s[mask, i, k]) - b0) / 100.0 for k, n in NAMES[role].items()
+            vals = {n: np.median((s[mask, i, k] - b0[mask]) / 100.0) for k, n in NAMES[role].items()
                     if (s[mask, i, k] > 0).all()}
             print(f"step {i} {role:5s} " + " ".join(f"{k}={v:.2f}" for k, v in vals.items()))
+    # spread of the hand-offs within a replica: the last chain's dZ_0 publication, the
+    # last PART publication (layer-0 iteration i - 2), each chain's wait end
+    for i in range(2, min(8, nst)):
+        b0 = base(i)
+        if (b0 == 0).any():
+            continue
+        cl, pl, sl, jl = [], [], [], []
+        for rr in range(R):
+            m = rep == rr
+            cl.append((s[chain & m, i - 1, ref_k].max() - b0[m][0]) / 100.0)
+            pl.append((s[roles["l0"] & m, i - 2, 6].max() - b0[m][0]) / 100.0)
+            sl.append((s[chain & m, i, 1].max() - b0[m][0]) / 100.0)
+            jl.append([(s[chain & m & (q == nl0 + j), i - 1, ref_k][0] - b0[m][0]) / 100.0 for j in range(nch)])
+        print(f"step {i} last dz0_pub(i-1) {np.round(np.median(cl), 2)}  last part_pub {np.round(np.median(pl), 2)}"
+              f"  last seen {np.round(np.median(sl), 2)}  per chain j dz0_pub {np.round(np.median(jl, axis=0), 2)}")
     ends = [np.median(s[chain, i, ref_k]) for i in range(min(8, nst))]
     d = np.diff([x for x in ends if x > 0]) / 100.0
     print("step period (us):", np.round(d, 2), "median", np.round(np.median(d), 2) if len(d) else None)
