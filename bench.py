@@ -269,32 +269,51 @@ def measure_train(args, model, dist, rank, world, dev, gpu, W, batch_mode, steps
     plan = build_plan(model)
     dims, drop, classes, rows, _ = MODELS[args.model]
     B = args.batch
-    # per-step sync DP on ONE GPU: the W workers are replicas of one sync trainer whose
-    # gradients are summed every step inside the persistent launch (native_engine sync);
-    # across ranks: one replica of the rank's W * B rows and a per-step all-reduce
-    sync_local = batch_mode and world == 1 and gpu and not args.rccl and not args.overlap
-    R = W if (not batch_mode or sync_local) else 1
-    Bloc = B if (not batch_mode or sync_local) else B * W
+    # per-step sync DP: the W workers are replicas of one sync trainer whose gradients are
+    # summed every step inside the persistent launch (native_engine sync), across ranks too
+    # (the rank exchange over peer-mapped buffers, attach_rank_exchange); where that
+    # cannot run: one replica of the rank's W * B rows and a per-step all-reduce
+    sync_local = (batch_mode and gpu and not args.rccl and not args.overlap
+                  and (world == 1 or os.environ.get("ELEPHAS_AMD_XRANK", "1") != "0"))
 
-    # synthetic MNIST-shaped shards, one per worker
-    rng = np.random.default_rng(1000 + rank)
-    centers = rng.normal(0, 1, size=(classes, dims[0])).astype(np.float32)
-    xs, ys = [], []
-    for r in range(R):
-        n = rows * (W if R == 1 and batch_mode else 1)
-        y = rng.integers(0, classes, n)
-        x = centers[y] + rng.normal(0, 2.0, size=(n, dims[0])).astype(np.float32)
-        x = (x - x.min()) / (x.max() - x.min())
-        xs.append(x.astype(np.float32))
-        ys.append(np.eye(classes, dtype=np.float32)[y])
+    def make(sync_local):
+        R = W if (not batch_mode or sync_local) else 1
+        Bloc = B if (not batch_mode or sync_local) else B * W
+        # synthetic MNIST-shaped shards, one per worker
+        rng = np.random.default_rng(1000 + rank)
+        centers = rng.normal(0, 1, size=(classes, dims[0])).astype(np.float32)
+        xs, ys = [], []
+        for r in range(R):
+            n = rows * (W if R == 1 and batch_mode else 1)
+            y = rng.integers(0, classes, n)
+            x = centers[y] + rng.normal(0, 2.0, size=(n, dims[0])).astype(np.float32)
+            x = (x - x.min()) / (x.max() - x.min())
+            xs.append(x.astype(np.float32))
+            ys.append(np.eye(classes, dtype=np.float32)[y])
+        if gpu:
+            from elephas_amd.ops.native_engine import NativeTrainer
+            t = NativeTrainer(model, plan, R, Bloc, dev, seed=4321 + rank, sync=sync_local)
+        else:
+            from elephas_amd.ops.torch_engine import TorchTrainer
+            t = TorchTrainer(model, plan, R, Bloc, dev, seed=4321 + rank)
+        t.set_data(xs, ys, args.validation_split, shuffle=True)
+        return t, R, Bloc
 
-    if gpu:
-        from elephas_amd.ops.native_engine import NativeTrainer
-        t = NativeTrainer(model, plan, R, Bloc, dev, seed=4321 + rank, sync=sync_local)
-    else:
-        from elephas_amd.ops.torch_engine import TorchTrainer
-        t = TorchTrainer(model, plan, R, Bloc, dev, seed=4321 + rank)
-    t.set_data(xs, ys, args.validation_split, shuffle=True)
+    t, R, Bloc = make(sync_local)
+    if world > 1:
+        # one initial model on every rank (the reference's driver broadcasts the master
+        # weights; per-step sync DP never averages, so the ranks must start equal)
+        init = torch.from_numpy(np.ascontiguousarray(t.get_weights_flat()[0]))
+        dist.broadcast_(init, 0)
+        init_np = init.cpu().numpy()
+        t.set_weights_flat(init_np)
+    xrank = False
+    if sync_local and world > 1:
+        xrank = t.attach_rank_exchange(rank, world)   # collective: the same answer on every rank
+        if not xrank:
+            sync_local = False
+            t, R, Bloc = make(False)
+            t.set_weights_flat(init_np)
     ntrain = t.ntrain_h[0] if gpu else t.split[0]
     steps_per_epoch = int(math.ceil(ntrain / Bloc))
 
@@ -304,7 +323,8 @@ def measure_train(args, model, dist, rank, world, dev, gpu, W, batch_mode, steps
     if batch_mode and gpu and not sync_local and (world > 1 or args.overlap):
         t.set_grad_scale(1.0 / world)   # mean of the ranks' gradients after the sum all-reduce
     channel = None
-    if batch_mode and gpu and world > 1 and not args.overlap and not args.no_graph and not args.rccl:
+    if (batch_mode and gpu and world > 1 and not sync_local and not args.overlap and not args.no_graph
+            and not args.rccl):
         from elephas_amd.parallel import p2p   # per-step peer all-reduce captured with the step
         channel = p2p.graph_channel(t.G.numel())
 
@@ -329,7 +349,7 @@ def measure_train(args, model, dist, rank, world, dev, gpu, W, batch_mode, steps
                     t.run_steps_allreduce_graph(n, channel)
                 elif batch_mode and args.overlap:
                     t.run_steps_allreduce_overlap(n, dist.all_reduce_sum_)
-                elif batch_mode and world > 1:
+                elif batch_mode and world > 1 and not sync_local:
                     t.run_steps_allreduce(n, allreduce_grads, use_graph=not args.no_graph)
                 else:
                     t.run_steps(n, use_graph=not args.no_graph)
@@ -363,7 +383,7 @@ def measure_train(args, model, dist, rank, world, dev, gpu, W, batch_mode, steps
 
     # warmup (includes hipGraph capture of both chunk shapes)
     if gpu and not args.no_graph:
-        t.prepare_graphs(allreduce_path=batch_mode and world > 1 and not args.overlap)
+        t.prepare_graphs(allreduce_path=batch_mode and world > 1 and not args.overlap and not sync_local)
     if gpu and args.validation_split > 0:
         t._eval_exe()   # the epoch-end validation executor exists before the timed region
     run(warmup)
@@ -393,7 +413,9 @@ def measure_train(args, model, dist, rank, world, dev, gpu, W, batch_mode, steps
     digests = dist.all_gather_object(digest)
     from elephas_amd.parallel import p2p
     nbytes = (t.G.numel() if batch_mode and gpu else theta.size) * 4
-    if channel is not None:
+    if xrank:
+        path = "in-launch rank exchange: per-step weight-gradient tiles through peer-mapped buffers (persist.hip)"
+    elif channel is not None:
         path = "peer-memory kernel captured in the step's hipGraph (dedicated channel)"
     elif gpu and world > 1 and not batch_mode:
         path = p2p.describe(nbytes)
@@ -406,7 +428,9 @@ def measure_train(args, model, dist, rank, world, dev, gpu, W, batch_mode, steps
         from elephas_amd.ops import native
         provenance = native.provenance()   # the loaded _C's source digest vs this tree's csrc/
     sync_desc = ("reference (one-shot averaging per fit)" if not batch_mode else
-                 "per-step synchronous DP of the GPU's workers (gradient sum over the replicas every step)"
+                 ("per-step synchronous DP of every worker of the job inside the launch (gradient sum over "
+                  "the replicas, then over the ranks, every step)" if xrank else
+                  "per-step synchronous DP of the GPU's workers (gradient sum over the replicas every step)")
                  if sync_local else "per-step gradient all-reduce")
     engine = ((("native HIP executor: " if t.persistent else "native HIP executor + hipGraph: ") + t.plan_name())
               if gpu else "torch CPU reference")

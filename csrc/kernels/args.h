@@ -195,7 +195,7 @@ enum PmFlag : int { PMF_PART = 0, PMF_BWD = 1, PMF_W = 2, PMF_A0 = 3, PMF_D2 = 4
 // nothing was modified, the chunk can be re-run on another plan)
 enum PmErr : unsigned { PERR_L0_BWD = 1, PERR_CHAIN_PART = 2, PERR_CHAIN_BWD = 3, PERR_CHAIN_PREV = 4,
                         PERR_DW_A0 = 5, PERR_DW_D2 = 6, PERR_XCHG = 7, PERR_PS = 8, PERR_GRID = 9,
-                        PERR_CHAIN_GR = 10 };
+                        PERR_CHAIN_GR = 10, PERR_XRANK = 11 };
 constexpr int PM_XSLOT = 7 * 1024;   // floats of one workgroup's exchange slab (sync)
 struct PersistArgs {
   int R, B, nsteps;
@@ -218,6 +218,16 @@ struct PersistArgs {
   // updates (grad_scale = 1 / R) keep their weights identical
   int sync;
   long long o_xg;                   // exchange slabs [2][wgs][PM_XSLOT] in every replica's workspace
+  // sync across ranks (xr_world > 1; one node, every rank the same step sequence): after
+  // the replica sum, replica 0's owning workgroup q puts the rank's sum into slab
+  // [tag & 1][q] of its rank-exchange buffer (peer-mapped, uncached; peer_args.h offsets)
+  // and raises flag q (system scope, tag = xr_tag0 + step + 1, monotonic over the trainer's
+  // life); every replica then sums the ranks' slabs in rank order -- the same bits on every
+  // rank and replica
+  char* xr_base[PEER_MAX_RANKS];
+  int xr_world, xr_rank;
+  unsigned xr_tag0;
+  long long xr_timeout;             // its waits' spin limit (ticks): ranks may start seconds apart
   // parameter-server hook (V1 roles; async / hogwild frequency='batch', reference
   // elephas/worker.py:114-127): after its update every owning workgroup pushes its
   // delta (theta_new - theta_pulled, fp32 atomics into the sharded device PS) and pulls

@@ -199,6 +199,13 @@ PYBIND11_MODULE(_C, m) {
       .def("persist_geometry", &Executor::persist_geometry)
       .def("persist_variant", &Executor::persist_variant)
       .def("persist_images", &Executor::persist_images)
+      .def("set_rank_exchange", [](Executor& e, std::vector<uintptr_t> bases, int world, int rank, unsigned tag0,
+                                   double timeout_s) {
+        std::vector<char*> b;
+        for (auto p : bases) b.push_back(reinterpret_cast<char*>(p));
+        return e.set_rank_exchange(b, world, rank, tag0, timeout_s);
+      })
+      .def("rank_exchange_steps", &Executor::rank_exchange_steps)
       .def("set_param_server", [](Executor& e, ShardedParameterServer* ps, int mode) {
         return e.set_param_server(ps ? ps->kernel_args() : PsArgs{}, ps ? mode : 0);
       }, py::arg("ps"), py::arg("mode"))
@@ -279,6 +286,24 @@ PYBIND11_MODULE(_C, m) {
   });
 
   // ---- peer-memory collectives and the sharded device PS (peer.h)
+  // a bare peer-mapped buffer (the persistent kernel's rank exchange, PersistArgs::xr_*)
+  py::class_<PeerBuffer>(m, "PeerBuffer")
+      .def(py::init<int, int, long long, int>(), py::arg("rank"), py::arg("world"), py::arg("data_bytes"),
+           py::arg("device"))
+      .def("handle", [](PeerBuffer& p) { return py::bytes(p.handle()); })
+      .def("open", [](PeerBuffer& p, std::vector<py::bytes> hs) {
+        std::vector<std::string> v;
+        for (auto& h : hs) v.emplace_back(std::string(h));
+        p.open(v);
+      })
+      .def("bases", [](PeerBuffer& p) {
+        std::vector<uintptr_t> v;
+        for (int r = 0; r < p.world(); ++r) v.push_back(reinterpret_cast<uintptr_t>(p.base(r)));
+        return v;
+      })
+      .def("error", &PeerBuffer::error)
+      .def("release", &PeerBuffer::release);
+
   py::class_<PeerAllReduce>(m, "PeerAllReduce")
       .def(py::init<int, int, long long, int, double>(), py::arg("rank"), py::arg("world"), py::arg("cap_elems"),
            py::arg("device"), py::arg("timeout_s") = 20.0)

@@ -210,6 +210,20 @@ bool Executor::set_param_server(const PsArgs& ps, int mode) {
   return true;
 }
 
+bool Executor::set_rank_exchange(const std::vector<char*>& bases, int world, int rank, unsigned tag0,
+                                 double timeout_s) {
+  if (!pm_.on || !pm_.args.sync || world > PEER_MAX_RANKS || (int)bases.size() != world || rank < 0 ||
+      rank >= world || pm_.args.wgs > PEER_MAX_BLOCKS)
+    return world <= 1;
+  PersistArgs& a = pm_.args;
+  for (int k = 0; k < PEER_MAX_RANKS; ++k) a.xr_base[k] = k < world ? bases[k] : nullptr;
+  a.xr_world = world;
+  a.xr_rank = rank;
+  a.xr_timeout = (long long)(std::max(1.0, timeout_s) * 1e8);   // s_memrealtime: 100 MHz
+  pm_.xr_steps = tag0;   // a rebuilt executor continues the trainer's tag sequence
+  return true;
+}
+
 std::vector<int> Executor::persist_variant() const {
   if (!pm_.on) return {};
   return {pm_.args.v2 ? 2 : 1, pm_.args.nd, pm_.args.sync};
@@ -238,6 +252,10 @@ void Executor::run_chunk(hipStream_t s, int nsteps) const {
     // but the step loop ran 2-3 % slower: profiles/persist_exit_ab_r3.txt)
     PersistArgs a = pm_.args;
     a.nsteps = nsteps;
+    if (a.xr_world > 1) {   // the rank exchange's flag tags continue over launches
+      a.xr_tag0 = pm_.xr_steps;
+      pm_.xr_steps += (unsigned)nsteps;
+    }
     check(ea_persist(&a, s), "persistent step kernel");
     check(ea_persist_post(d_pflags_, (int)(pm_.flag_bytes / sizeof(unsigned)), reinterpret_cast<long long*>(c_.ctr),
                           reinterpret_cast<const int*>(c_.ntrain), c_.R, c_.B, nsteps, d_perr_, s),

@@ -133,6 +133,10 @@ class Executor {
   // owned parameters' deltas into the server and pulls the next step's (mode 1 hogwild,
   // 2 asynchronous, 0 off); false when the plan cannot (not persistent, or V2 roles)
   bool set_param_server(const PsArgs& ps, int mode);
+  // per-step sync across ranks inside the launch (PersistArgs::xr_*): every rank's
+  // rank-exchange buffer (peer-mapped); false: the plan cannot (not a persistent sync plan)
+  bool set_rank_exchange(const std::vector<char*>& bases, int world, int rank, unsigned tag0, double timeout_s);
+  unsigned rank_exchange_steps() const { return pm_.xr_steps; }
   unsigned persist_error() const;  // sticky error word (a timed-out in-launch wait), synchronous read
   void persist_clear_error();
   int rowchain_split() const { return rc_.on ? rc_.nsplitk : 0; }
@@ -186,6 +190,7 @@ class Executor {
     bool on = false;
     PersistArgs args{};
     size_t flag_bytes = 0;
+    mutable unsigned xr_steps = 0;   // steps run with the rank exchange (its flag tags)
   } pm_;
   float* d_pws_ = nullptr;         // persistent plan: per-replica exchange workspace
   unsigned* d_pflags_ = nullptr;   // [R][PMF_N][PM_MAXWG] flags (zero at every launch: setup, then the post kernel)

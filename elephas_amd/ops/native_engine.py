@@ -239,8 +239,11 @@ class NativeTrainer(TrainerBase):
                                Z=w["Z"].data_ptr(), D=w["D"].data_ptr(), DT=w["DT"].data_ptr(),
                                dZ=w["dZ"].data_ptr(), dZT=w["dZT"].data_ptr(),
                                wsh_off=d["wsh_off"], wtsh_off=d["wtsh_off"]))
+        # sync: the gradient is the sum over the R replicas (and, with the in-launch rank
+        # exchange, over the ranks): the mean
+        xw = self._xr["world"] if getattr(self, "_xr", None) else 1
         opt = dict(opt=self.opt_id, s_plane=self.n,
-                   grad_scale=self._grad_scale / (self.R if self.sync else 1))
+                   grad_scale=self._grad_scale / (self.R * xw if self.sync else 1))
         opt.update({k: v for k, v in self.opt_hp.items() if k != "state_init"})
         return dict(
             R=self.R, B=ws["B"], Bp=ws["Bp"], bf16=int(self.bf16), seed=self.seed,
@@ -274,13 +277,72 @@ class NativeTrainer(TrainerBase):
             acc=self.acc.data_ptr(), acc_stride=6, ctr=self.ctr.data_ptr())
 
     def _build_executor(self):
+        tag0 = 0
         if self.exe is not None:
+            tag0 = self.exe.rank_exchange_steps()
             self.exe.destroy_graphs()
         self._graphs = {}
         self.exe = self.C.Executor(self._cfg(self.ws))
         self.GRAPH_CHUNK = self.PERSIST_CHUNK if self.exe.persistent() else type(self).GRAPH_CHUNK
         if self._ps is not None and not self.exe.set_param_server(*self._ps):
             self._ps = None   # the rebuilt plan cannot (e.g. the row-chain fallback): host-side exchange
+        xr = getattr(self, "_xr", None)
+        if xr is not None:
+            xr["live"] = bool(self.exe.set_rank_exchange(xr["bases"], xr["world"], xr["rank"], tag0, xr["timeout"]))
+
+    def attach_rank_exchange(self, rank: int, world: int, allgather=None, timeout_s: Optional[float] = None) -> bool:
+        """Per-step synchronous DP across ranks INSIDE the persistent launch (reference
+        spark_model.py:217-228 with per-batch exchange; SURVEY §2.3 DP-sync 'batch'): a
+        sync trainer's replica sum of every weight-gradient tile is exchanged with the
+        other ranks through a peer-mapped buffer (HIP IPC, uncached; over xGMI between
+        GPUs) and summed in rank order by the owning workgroups -- the same update on every
+        rank and replica, no host round trip per step.  Collective: every rank calls it
+        with the same shard sizes.  Returns False on every rank (and changes nothing) if
+        any rank cannot: the caller keeps its own per-step exchange."""
+        from ..parallel import dist as _dist
+        from ..parallel.p2p import exchange_handles
+        gather = allgather or _dist.all_gather_object
+        world = int(world)
+        if world <= 1:
+            return False
+        ok = bool(self.sync and self.exe.persistent() and self._sync_in_launch())
+        if not ok:
+            _log.warning("rank exchange: this trainer's plan cannot run it (%s)", self.plan_name())
+        buf = None
+        try:
+            if ok:
+                wgs = int(self.exe.persist_geometry()[5])
+                devi = self.dev.index if self.dev.index is not None else torch.cuda.current_device()
+                buf = self.C.PeerBuffer(int(rank), world, 2 * wgs * 7 * 1024 * 4, int(devi))
+        except Exception as e:  # noqa: BLE001 - voted below
+            _log.warning("rank exchange: buffer setup failed: %r", e)
+            ok, buf = False, None
+        handles = exchange_handles(bytes(buf.handle()) if buf is not None else b"", allgather)
+        if ok and all(handles):
+            try:
+                buf.open(handles)
+            except Exception:  # noqa: BLE001
+                ok = False
+        else:
+            ok = False
+        # every rank must run the same step sequence (the exchange tags): equal shard sizes
+        votes = gather((ok, tuple(self.ntrain_h)))
+        if not all(v[0] for v in votes) or len({v[1] for v in votes}) != 1:
+            return False
+        timeout = float(os.environ.get("ELEPHAS_AMD_P2P_TIMEOUT_S", "60")) if timeout_s is None else float(timeout_s)
+        self._xr = dict(buf=buf, bases=list(buf.bases()), world=world, rank=int(rank), timeout=timeout, live=False)
+        self._build_executor()   # the grad scale now includes 1 / world
+        live = gather(bool(self._xr["live"]))
+        if not all(live):
+            self._xr = None
+            self._build_executor()
+            return False
+        return True
+
+    @property
+    def rank_exchange(self) -> bool:
+        xr = getattr(self, "_xr", None)
+        return bool(xr and xr["live"])
 
     def attach_param_server(self, ps, consistent: bool) -> bool:
         """Per-step parameter-server exchange INSIDE the persistent launch (reference
@@ -534,6 +596,9 @@ class NativeTrainer(TrainerBase):
         """Launch nsteps fused training steps on self.stream (asynchronous)."""
         if nsteps <= 0:
             return
+        if getattr(self, "_xr", None) is not None and not (self._xr["live"] and self._sync_in_launch()):
+            raise RuntimeError("per-step sync across ranks: the rank exchange is attached but this plan / data "
+                               "cannot run it inside the launch (every rank must keep equal shard sizes)")
         if self.sync and not self._sync_in_launch():
             # per-step synchronous DP without the in-launch exchange: forward/backward of
             # every replica -> gradient sum over the replicas -> apply (grad_scale 1/R)

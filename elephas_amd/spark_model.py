@@ -346,8 +346,21 @@ class SparkModel:
         bs = int(train_config.get("batch_size", 32))
         sync_local = (gran == "batch" and dist.world_size() == 1 and len(local) > 1
                       and all(len(p) > bs for p in local))
+        # several ranks: the same, with the replica sums exchanged between the ranks inside
+        # the launch (attach_rank_exchange), when every rank holds equally many partitions
+        # of equal sizes (the exchange needs one step sequence on all ranks)
+        cross = False
+        if gran == "batch" and dist.world_size() > 1:
+            sizes = dist.all_gather_object(tuple(len(p) for p in local))
+            cross = (len(set(sizes)) == 1 and len(set(sizes[0])) == 1 and len(local) >= 2
+                     and all(n > bs for n in sizes[0]) and self._native_ok())
         with self._timer.phase("setup"):
-            trainer, active = worker.prepare_partitions(local, sync=sync_local)
+            trainer, active = worker.prepare_partitions(local, sync=sync_local or cross)
+            if cross:
+                # collective on every rank (all hold >= 2 equal partitions: sync trainers)
+                ok = trainer.attach_rank_exchange(dist.rank(), dist.world_size())
+                if not all(dist.all_gather_object(bool(ok))):
+                    trainer, active = worker.prepare_partitions(local, sync=False)
         start = 0
         if checkpoint_dir and resume and ckpt.exists(checkpoint_dir):
             with self._timer.phase("checkpoint"):

@@ -298,6 +298,57 @@ def step_graph(dist, rank, world):
                 error=int(ch.impl.error()))
 
 
+def sync_inlaunch(dist, rank, world):
+    """Per-step synchronous DP across ranks inside the persistent launch: two ranks x
+    two replicas (each rank's grid on half the CUs), the weight-gradient tiles summed
+    over the replicas and then over the ranks by the owning workgroups.  Every replica
+    of every rank ends bit-identical, and equal (to fp32 summation order) to ONE torch
+    model trained on the four workers' batches stacked in rank-major order."""
+    import hashlib
+    import torch
+    from elephas_amd import config
+    from elephas_amd.models import Sequential, Dense, initializers
+    from elephas_amd.models.optimizers import SGD
+    from elephas_amd.ops.native_engine import NativeTrainer
+    from elephas_amd.ops.plan import build_plan
+    from elephas_amd.ops.torch_engine import TorchTrainer
+    config.set_policy("float32")
+    initializers.set_seed(21)   # the same initial weights on every rank
+    m = Sequential()
+    m.add(Dense(128, activation="relu", input_dim=784))
+    m.add(Dense(128, activation="relu"))
+    m.add(Dense(10, activation="softmax"))
+    m.compile(SGD(0.1), "categorical_crossentropy", ["acc"])
+    R, B, steps = 2, 64, 9
+    rng = np.random.default_rng(77)   # every rank builds every worker's shard
+    xs_all = [rng.random((B * steps, 784), dtype=np.float32) for _ in range(world * R)]
+    ys_all = [np.eye(10, dtype=np.float32)[rng.integers(0, 10, B * steps)] for _ in range(world * R)]
+    xs, ys = xs_all[rank * R:(rank + 1) * R], ys_all[rank * R:(rank + 1) * R]
+    ag = _allgather(dist)
+    t = NativeTrainer(m, build_plan(m), R, B, torch.device("cuda"), seed=5, sync=True, persist_cus=128)
+    w0 = t.get_weights_flat()[0].copy()
+    t.set_data(xs, ys, 0.0, shuffle=False)
+    attached = t.attach_rank_exchange(rank, world, allgather=ag)
+    if not attached:
+        return dict(attached=False, plan=t.plan_name())
+    t.GRAPH_CHUNK = 4   # several launches: the exchange tags continue across them
+    t.fit(2)
+    w = t.get_weights_flat()
+    replicas_equal = all(np.array_equal(w[r], w[0]) for r in range(R))
+    dig = hashlib.sha1(w[0].tobytes()).hexdigest()[:16]
+    digs = ag(dig)
+    xc = np.concatenate([np.concatenate([x[i * B:(i + 1) * B] for x in xs_all]) for i in range(steps)])
+    yc = np.concatenate([np.concatenate([y[i * B:(i + 1) * B] for y in ys_all]) for i in range(steps)])
+    ref = TorchTrainer(m, build_plan(m), 1, world * R * B, torch.device("cuda"))
+    ref.set_data([xc], [yc], 0.0, shuffle=False)
+    ref.fit(2)
+    wt = ref.get_weights_flat()[0]
+    err = float(np.abs(w[0] - wt).max() / np.abs(wt - w0).max())
+    return dict(attached=True, plan=t.plan_name(), replicas_equal=replicas_equal,
+                same_on_all_ranks=len(set(digs)) == 1, err=err, error=int(t.exe.persist_error()),
+                steps_tagged=int(t.exe.rank_exchange_steps()))
+
+
 def main():
     scenario = sys.argv[1]
     dist = _gloo()
@@ -314,6 +365,8 @@ def main():
         res = ps(dist, rank, world)
     elif scenario == "ps_selftest":
         res = ps_selftest(dist, rank, world)
+    elif scenario == "sync_inlaunch":
+        res = sync_inlaunch(dist, rank, world)
     elif scenario.startswith("spark_sync_"):  # spark_sync_<fit|epoch|batch>[p]
         res = spark_sync(dist, rank, world, scenario.rsplit("_", 1)[1])
     elif scenario in ("spark_asynchronous", "spark_hogwild"):

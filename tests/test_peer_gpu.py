@@ -147,3 +147,15 @@ def test_spark_model_sync_persistent_plan_two_ranks_match_one(gran, tmp_path):
     for k in a.files:
         scale = max(1.0, float(np.abs(ref[k]).max()))
         np.testing.assert_allclose(a[k], ref[k], rtol=0, atol=2e-6 * scale, err_msg=k)
+
+
+def test_sync_inlaunch_across_ranks_matches_one_model():
+    """Per-step synchronous DP across ranks inside the persistent launch (the replica sum
+    of every weight-gradient tile exchanged with the other rank through peer-mapped
+    buffers, summed in rank order): all replicas of both ranks stay bit-identical and
+    match one fp32 torch model trained on the stacked batches of the 2 x 2 workers."""
+    for r in _run("sync_inlaunch"):
+        assert r["attached"], r
+        assert r["error"] == 0 and r["replicas_equal"] and r["same_on_all_ranks"], r
+        assert r["err"] < 1e-3, r
+        assert r["steps_tagged"] == 18, r   # 2 epochs x 9 steps ran with the exchange

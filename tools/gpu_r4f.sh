@@ -21,7 +21,7 @@ done
 cat $O
 timeout -k 10 150 python tools/persist_stamps.py 8 64 8 > gpurun_out/stamps_r4f.txt 2>&1 || exit 1
 grep -v -E "amdgpu.ids|Warning|from elephas" gpurun_out/stamps_r4f.txt | tail -32
-bash tools/gpu_pred.sh || exit 1
+[ -n "$PRED" ] && { bash tools/gpu_pred.sh || exit 1; }
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
 timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/prof_drv4 -o k -- python3 bench.py --gpus 1 --steps 20 --warmup 5 --no-sub > gpurun_out/prof_drv4.log 2>&1 || exit 1
 python3 - <<'PY'
