@@ -110,6 +110,15 @@ __device__ __forceinline__ float rb(float x) {
     return x;
   }
 }
+// two fp32 values rounded to bf16 (RNE, as rb<true>) packed in one dword, lo first
+__device__ __forceinline__ unsigned bf2(float lo, float hi) {
+  const unsigned a = __builtin_bit_cast(unsigned, lo), b = __builtin_bit_cast(unsigned, hi);
+  return ((a + 0x7fffu + ((a >> 16) & 1u)) >> 16) | ((b + 0x7fffu + ((b >> 16) & 1u)) & 0xffff0000u);
+}
+__device__ __forceinline__ bf16x8 bf8(const float (&v)[8]) {
+  return __builtin_bit_cast(bf16x8, u32x4{bf2(v[0], v[1]), bf2(v[2], v[3]), bf2(v[4], v[5]), bf2(v[6], v[7])});
+}
+
 // one element of a bf16 row packed two per dword in LDS (element k of a row at dword k / 2)
 __device__ __forceinline__ float bf_at(const float* row, int k) {
   const unsigned d = __builtin_bit_cast(unsigned, row[k >> 1]);
@@ -1025,21 +1034,42 @@ __device__ __forceinline__ void l0_role_v2(const PersistArgs& a, float* smem, in
 #pragma unroll
       for (int jj = 0; jj < NCT; ++jj) acc[jj] = zero4f();
       const float* arow = A + (w * 16 + i16) * XS;
+      if constexpr (BF) {
+        // bf16 X rows straight into v_mfma_f32_16x16x32_bf16 (lane: elements kb + 8g + j,
+        // four packed dwords, masked past the chunk), the W0 tile rounded to bf16
+        const unsigned* au = reinterpret_cast<const unsigned*>(arow);
 #pragma unroll 1
-      for (int kb = 0; kb < KCP; kb += 64) {
-        float av[16], bv[NCT][16];
+        for (int kb = 0; kb < KCP; kb += 32) {
+          const int d0 = (kb + 8 * g) >> 1;
+          u32x4 aq;
 #pragma unroll
-        for (int ks = 0; ks < 16; ++ks) {
-          const int k = kb + 16 * g + ks;
-          // rows are kc0 + 1 wide: k past the chunk reads the next row -- masked to zero
-          av[ks] = k < kreal ? xat(arow, k) : 0.f;
+          for (int e = 0; e < 4; ++e) aq[e] = 2 * (d0 + e) < kreal ? au[d0 + e] : 0u;
+          const bf16x8 a8 = __builtin_bit_cast(bf16x8, aq);
 #pragma unroll
-          for (int jj = 0; jj < NCT; ++jj) bv[jj][ks] = rb<BF>(sW[k * WS + jj * 16 + i16]);
+          for (int jj = 0; jj < NCT; ++jj) {
+            float bv[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) bv[j] = sW[(kb + 8 * g + j) * WS + jj * 16 + i16];
+            acc[jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a8, bf8(bv), acc[jj], 0, 0, 0);
+          }
         }
+      } else {
+#pragma unroll 1
+        for (int kb = 0; kb < KCP; kb += 64) {
+          float av[16], bv[NCT][16];
 #pragma unroll
-        for (int ks = 0; ks < 16; ++ks) {
+          for (int ks = 0; ks < 16; ++ks) {
+            const int k = kb + 16 * g + ks;
+            // rows are kc0 + 1 wide: k past the chunk reads the next row -- masked to zero
+            av[ks] = k < kreal ? xat(arow, k) : 0.f;
 #pragma unroll
-          for (int jj = 0; jj < NCT; ++jj) acc[jj] = mma(av[ks], bv[jj][ks], acc[jj]);
+            for (int jj = 0; jj < NCT; ++jj) bv[jj][ks] = sW[k * WS + jj * 16 + i16];
+          }
+#pragma unroll
+          for (int ks = 0; ks < 16; ++ks) {
+#pragma unroll
+            for (int jj = 0; jj < NCT; ++jj) acc[jj] = mma(av[ks], bv[jj][ks], acc[jj]);
+          }
         }
       }
 #pragma unroll
@@ -1254,6 +1284,36 @@ __device__ __forceinline__ void rows_mm(const float* A, const float* B, int ct0,
       acc[0] = mma(av[ks], bv0[ks], acc[0]);
       acc[1] = mma(av[ks], bv1[ks], acc[1]);
     }
+  }
+}
+
+// rows_mm on the bf16 matrix cores (mixed_bfloat16 policy): the same bf16-rounded
+// operands, one v_mfma_f32_16x16x32_bf16 per 32-deep block instead of eight
+// 16x16x4 f32 MFMAs (lane: k = kb + 8g + j, j < 8)
+template <int K, int SAI, int SBK, int SBN>
+__device__ __forceinline__ void rows_mm_b(const float* A, const float* B, int ct0, int nct, f32x4 (&acc)[2], int i16,
+                                          int g) {
+  static_assert(K % 32 == 0, "32-deep blocks");
+  acc[0] = zero4f();
+  acc[1] = zero4f();
+  if (ct0 >= nct) return;
+  const bool two = ct0 + 4 < nct;
+  const float* arow = A + i16 * SAI;
+  const float* b0 = B + (ct0 * 16 + i16) * SBN;
+  const float* b1 = two ? B + ((ct0 + 4) * 16 + i16) * SBN : b0;
+#pragma unroll
+  for (int kb = 0; kb < K; kb += 32) {
+    float av[8], bv0[8], bv1[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int k = kb + 8 * g + j;
+      av[j] = arow[k];
+      bv0[j] = b0[k * SBK];
+      bv1[j] = b1[k * SBK];
+    }
+    const bf16x8 a8 = bf8(av);
+    acc[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a8, bf8(bv0), acc[0], 0, 0, 0);
+    acc[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a8, bf8(bv1), acc[1], 0, 0, 0);
   }
 }
 
@@ -1486,7 +1546,10 @@ __device__ __forceinline__ void chain_role(const PersistArgs& a, float* smem, in
           for (int jj = 0; jj < 2; ++jj) {
             const int ct = w + 4 * jj < nt0 ? w + 4 * jj : w;   // branch-free: unused past nt0
 #pragma unroll
-            for (int ks = 0; ks < 16; ++ks) bz[jj][ks] = rb<BF>(ldw1(rs, (16 * g + ks) * H0 + ct * 16 + i16, zs));
+            for (int ks = 0; ks < 16; ++ks) {   // BF: the 16x16x32 bf16 layout (two 32-deep blocks)
+              const int kr = BF ? 32 * (ks >> 3) + 8 * g + (ks & 7) : 16 * g + ks;
+              bz[jj][ks] = rb<BF>(ldw1(rs, kr * H0 + ct * 16 + i16, zs));
+            }
           }
           // one non-blocking look at the DW workgroups' W flags, returning with the loads
           // above; read after the sums (the correction's barrier broadcasts it)
@@ -1536,13 +1599,33 @@ __device__ __forceinline__ void chain_role(const PersistArgs& a, float* smem, in
           const float coef = -(a.op.lr / (1.f + a.op.decay * (float)itp)) * a.op.grad_scale;
           float ag[16];
 #pragma unroll
-          for (int ks = 0; ks < 16; ++ks) ag[ks] = sG[i16 * 65 + 16 * g + ks];
+          for (int ks = 0; ks < 16; ++ks) ag[ks] = sG[i16 * 65 + (BF ? 32 * (ks >> 3) + 8 * g + (ks & 7) : 16 * g + ks)];
 #pragma unroll
           for (int jj = 0; jj < 2; ++jj) {
             const int ct = w + 4 * jj;
             f32x4 acc = zero4f();
+            if constexpr (BF) {
+              // dZ_0 is bf16 (rb above); G + 1 stays ~fp32 as a bf16 hi + lo pair: four
+              // 16x16x32 bf16 MFMAs instead of sixteen 16x16x4 f32 ones
+              float h0[8], l0[8], h1[8], l1[8], z0[8], z1[8];
 #pragma unroll
-            for (int ks = 0; ks < 16; ++ks) acc = mma(ag[ks], bz[jj][ks], acc);
+              for (int e = 0; e < 8; ++e) {
+                h0[e] = rb<true>(ag[e]);
+                l0[e] = ag[e] - h0[e];
+                h1[e] = rb<true>(ag[8 + e]);
+                l1[e] = ag[8 + e] - h1[e];
+                z0[e] = bz[jj][e];
+                z1[e] = bz[jj][8 + e];
+              }
+              const bf16x8 zb0 = bf8(z0), zb1 = bf8(z1);
+              acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf8(h0), zb0, acc, 0, 0, 0);
+              acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf8(h1), zb1, acc, 0, 0, 0);
+              acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf8(l0), zb0, acc, 0, 0, 0);
+              acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf8(l1), zb1, acc, 0, 0, 0);
+            } else {
+#pragma unroll
+              for (int ks = 0; ks < 16; ++ks) acc = mma(ag[ks], bz[jj][ks], acc);
+            }
             if (ct < nt0) {
 #pragma unroll
               for (int qq = 0; qq < 4; ++qq) sZ0[(4 * g + qq) * L0S + ct * 16 + i16] = coef * acc[qq];
@@ -1618,7 +1701,8 @@ __device__ __forceinline__ void chain_role(const PersistArgs& a, float* smem, in
     float G1[8];
     {
       f32x4 acc[2];
-      rows_mm<H0, L0S, L1S, 1, BF>(sA0, sW1, w, nt1, acc, i16, g);
+      if constexpr (BF) rows_mm_b<H0, L0S, L1S, 1>(sA0, sW1, w, nt1, acc, i16, g);
+      else rows_mm<H0, L0S, L1S, 1, BF>(sA0, sW1, w, nt1, acc, i16, g);
       pstamp(a, i, 16);
       const float ks = a.rate1 > 0.f ? 1.f / (1.f - a.rate1) : 1.f;
       const uint32_t db = dropout_base(a.seed, r, 1, it);
@@ -1758,7 +1842,8 @@ __device__ __forceinline__ void chain_role(const PersistArgs& a, float* smem, in
     // ---- DX1: dZ_0 = (dZ_1 . W1^T) * G_0 -> LDS, then published for the L0 tiles
     {
       f32x4 acc[2];
-      rows_mm<H1, L1S, 1, L1S, BF>(sD1, sW1, w, nt0, acc, i16, g);
+      if constexpr (BF) rows_mm_b<H1, L1S, 1, L1S>(sD1, sW1, w, nt0, acc, i16, g);
+      else rows_mm<H1, L1S, 1, L1S, BF>(sD1, sW1, w, nt0, acc, i16, g);
       pstamp(a, i, 23);
 #pragma unroll
       for (int jj = 0; jj < 2; ++jj) {
@@ -2090,20 +2175,42 @@ __device__ __forceinline__ void dw_role_v2(const PersistArgs& a, float* smem, in
 #pragma unroll
     for (int u = 0; u < 4; ++u) acc[u] = zero4f();
     const float* brow = Bm + (w * 16 + i16) * XSg;
+    if constexpr (BF) {
+      // the bf16 rows straight into v_mfma_f32_16x16x32_bf16 (lane: elements kb + 8g + j,
+      // four packed dwords); both operands masked past the chunk (kg is even: whole pairs)
+      const unsigned* bu = reinterpret_cast<const unsigned*>(brow);
 #pragma unroll 1
-    for (int kb = 0; kb < kg; kb += 16) {
-      float av[4][4], bv[4];
+      for (int kb = 0; kb < kg; kb += 32) {
+        const int d0 = (kb + 8 * g) >> 1;
+        u32x4 bq;
 #pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        const int k = kb + 4 * ks + g;
-        bv[ks] = xat(brow, k);   // finite (X or zero padding) past the chunk, times a zero A
+        for (int e = 0; e < 4; ++e) bq[e] = 2 * (d0 + e) < kg ? bu[d0 + e] : 0u;
 #pragma unroll
-        for (int u = 0; u < 4; ++u) av[u][ks] = k < kg ? xat(A + (u * 16 + i16) * XSg, k) : 0.f;
+        for (int u = 0; u < 4; ++u) {
+          const unsigned* au = reinterpret_cast<const unsigned*>(A + (u * 16 + i16) * XSg);
+          u32x4 aq;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) aq[e] = 2 * (d0 + e) < kg ? au[d0 + e] : 0u;
+          acc[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, aq), __builtin_bit_cast(bf16x8, bq),
+                                                           acc[u], 0, 0, 0);
+        }
       }
+    } else {
+#pragma unroll 1
+      for (int kb = 0; kb < kg; kb += 16) {
+        float av[4][4], bv[4];
 #pragma unroll
-      for (int ks = 0; ks < 4; ++ks)
+        for (int ks = 0; ks < 4; ++ks) {
+          const int k = kb + 4 * ks + g;
+          bv[ks] = xat(brow, k);   // finite (X or zero padding) past the chunk, times a zero A
 #pragma unroll
-        for (int u = 0; u < 4; ++u) acc[u] = mma(av[u][ks], bv[ks], acc[u]);
+          for (int u = 0; u < 4; ++u) av[u][ks] = k < kg ? xat(A + (u * 16 + i16) * XSg, k) : 0.f;
+        }
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+          for (int u = 0; u < 4; ++u) acc[u] = mma(av[u][ks], bv[ks], acc[u]);
+      }
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u)
@@ -2179,30 +2286,61 @@ __device__ __forceinline__ void dw_role_v2(const PersistArgs& a, float* smem, in
       f32x4 dw[TU + 1], db[2] = {zero4f(), zero4f()};
 #pragma unroll
       for (int u = 0; u <= TU; ++u) dw[u] = zero4f();
+      if constexpr (BF) {
+        // v_mfma_f32_16x16x32_bf16 over two 32-row blocks of the batch (lane: rows
+        // kb + 8g + j), the operands rounded to bf16 as rb<true> does
+        const bf16x8 ones = __builtin_bit_cast(bf16x8, u32x4{0x3f803f80u, 0x3f803f80u, 0x3f803f80u, 0x3f803f80u});
 #pragma unroll
-      for (int half = 0; half < 2; ++half) {
-        float xa[TU][8], zb[2][8], a1v[8], d2v[8];
+        for (int kb = 0; kb < 64; kb += 32) {
+          float xa[TU][8], z0[8], z1[8], a1v[8], d2v[8];
 #pragma unroll
-        for (int h8 = 0; h8 < 8; ++h8) {
-          const int b = 16 * g + 8 * half + h8;
-          zb[0][h8] = rb<BF>(uD1[b * 33 + i16]);
-          zb[1][h8] = rb<BF>(uD1[b * 33 + 16 + i16]);
+          for (int j = 0; j < 8; ++j) {
+            const int b = kb + 8 * g + j;
+            z0[j] = uD1[b * 33 + i16];
+            z1[j] = uD1[b * 33 + 16 + i16];
 #pragma unroll
-          for (int u = 0; u < TU; ++u) xa[u][h8] = rb<BF>(uA0[b * L0S + urt[u] * 16 + i16]);
-          a1v[h8] = rb<BF>(uA1[b * 33 + (w2own ? w : 0) * 16 + i16]);
-          d2v[h8] = rb<BF>(uD2[b * S17 + i16]);
+            for (int u = 0; u < TU; ++u) xa[u][j] = uA0[b * L0S + urt[u] * 16 + i16];
+            a1v[j] = uA1[b * 33 + (w2own ? w : 0) * 16 + i16];
+            d2v[j] = uD2[b * S17 + i16];
+          }
+          const bf16x8 zb0 = bf8(z0), zb1 = bf8(z1), d28 = bf8(d2v);
+#pragma unroll
+          for (int u = 0; u < TU; ++u)   // wave-uniform: no MFMAs for tiles past ndw1
+            if (w + 4 * u < ndw1)
+              dw[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf8(xa[u]), uct[u] ? zb1 : zb0, dw[u], 0, 0, 0);
+          dw[TU] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf8(a1v), d28, dw[TU], 0, 0, 0);
+          if (w >= 2) {
+            db[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, w == 2 ? zb0 : d28, db[0], 0, 0, 0);
+            db[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, zb1, db[1], 0, 0, 0);
+          }
         }
+      } else {
 #pragma unroll
-        for (int h8 = 0; h8 < 8; ++h8) {
-#pragma unroll
-          for (int u = 0; u < TU; ++u) dw[u] = mma(xa[u][h8], uct[u] ? zb[1][h8] : zb[0][h8], dw[u]);
-          dw[TU] = mma(a1v[h8], d2v[h8], dw[TU]);
-        }
-        if (w >= 2) {
+        for (int half = 0; half < 2; ++half) {
+          float xa[TU][8], zb[2][8], a1v[8], d2v[8];
 #pragma unroll
           for (int h8 = 0; h8 < 8; ++h8) {
-            db[0] = mma(1.f, w == 2 ? zb[0][h8] : d2v[h8], db[0]);
-            db[1] = mma(1.f, zb[1][h8], db[1]);
+            const int b = 16 * g + 8 * half + h8;
+            zb[0][h8] = uD1[b * 33 + i16];
+            zb[1][h8] = uD1[b * 33 + 16 + i16];
+#pragma unroll
+            for (int u = 0; u < TU; ++u) xa[u][h8] = uA0[b * L0S + urt[u] * 16 + i16];
+            a1v[h8] = uA1[b * 33 + (w2own ? w : 0) * 16 + i16];
+            d2v[h8] = uD2[b * S17 + i16];
+          }
+#pragma unroll
+          for (int h8 = 0; h8 < 8; ++h8) {
+#pragma unroll
+            for (int u = 0; u < TU; ++u)   // wave-uniform: no MFMAs for tiles past ndw1
+              if (w + 4 * u < ndw1) dw[u] = mma(xa[u][h8], uct[u] ? zb[1][h8] : zb[0][h8], dw[u]);
+            dw[TU] = mma(a1v[h8], d2v[h8], dw[TU]);
+          }
+          if (w >= 2) {
+#pragma unroll
+            for (int h8 = 0; h8 < 8; ++h8) {
+              db[0] = mma(1.f, w == 2 ? zb[0][h8] : d2v[h8], db[0]);
+              db[1] = mma(1.f, zb[1][h8], db[1]);
+            }
           }
         }
       }

@@ -3,7 +3,7 @@ in-kernel s_memrealtime stamps (10 ns ticks): per step, the median stamp of ever
 phase of every role relative to the chain workgroups' publication of the previous
 step's dZ_0 rows (V2: the step's true start; V1: the partials seen), and the step period.
 
-  python tools/persist_stamps.py [R] [B] [steps] [v2: 1|0]
+  python tools/persist_stamps.py [R] [B] [steps] [v2: 1|0|-1] [policy]
 """
 import os
 import sys
@@ -29,14 +29,14 @@ def main():
     R = int(sys.argv[1]) if len(sys.argv) > 1 else 8
     B = int(sys.argv[2]) if len(sys.argv) > 2 else 64
     nst = int(sys.argv[3]) if len(sys.argv) > 3 else 8
-    if len(sys.argv) > 4:
+    if len(sys.argv) > 4 and sys.argv[4] != "-1":
         os.environ["ELEPHAS_AMD_PERSIST_V2"] = sys.argv[4]
     from elephas_amd import config
     from elephas_amd.models import Sequential, Dense, Dropout
     from elephas_amd.models.optimizers import SGD
     from elephas_amd.ops.plan import build_plan
     from elephas_amd.ops.native_engine import NativeTrainer
-    config.set_policy("float32")
+    config.set_policy(sys.argv[5] if len(sys.argv) > 5 else "float32")
     m = Sequential()
     m.add(Dense(128, activation="relu", input_dim=784))
     m.add(Dropout(0.2))
