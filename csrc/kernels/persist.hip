@@ -1475,6 +1475,11 @@ __device__ __forceinline__ void chain_role(const PersistArgs& a, float* smem, in
   };
   int prow[2];
   target_rows(0, prow);
+  // the loss / metric sums of this workgroup's rows over the chunk (threads < 2 + nmet):
+  // one fp64 atomic per value at the end of the launch instead of one per step (an
+  // atomic in flight holds up the next hand-off's drain; float partials summed in fp64
+  // are exact in any order)
+  double msum = 0.0;
   for (int i = 0; i < n; ++i) {
     const int valid = st.valid(a, i);
     if (valid == 0) break;
@@ -1798,7 +1803,7 @@ __device__ __forceinline__ void chain_role(const PersistArgs& a, float* smem, in
         float sv = 0.f;
 #pragma unroll
         for (int rr = 0; rr < 16; ++rr) sv += sAcc[rr * 8 + tid];
-        if (sv != 0.f) atomicAdd(a.acc + (long long)r * a.acc_stride + tid, (double)sv);
+        msum += (double)sv;
       }
       pstamp(a, i, 20);
     }
@@ -2021,6 +2026,7 @@ __device__ __forceinline__ void chain_role(const PersistArgs& a, float* smem, in
     pstamp(a, i, 10);
     pcycle(a, i, 29);
   }
+  if (a.acc && tid < 2 + a.nmet && msum != 0.0) atomicAdd(a.acc + (long long)r * a.acc_stride + tid, msum);
 
   // ---- epilogue: owned masters, both weight-image parities, state
   if constexpr (V2) return;
