@@ -104,6 +104,17 @@ def main():
             jl.append([(s[chain & m & (q == nl0 + j), i - 1, ref_k][0] - b0[m][0]) / 100.0 for j in range(nch)])
         print(f"step {i} last dz0_pub(i-1) {np.round(np.median(cl), 2)}  last part_pub {np.round(np.median(pl), 2)}"
               f"  last seen {np.round(np.median(sl), 2)}  per chain j dz0_pub {np.round(np.median(jl, axis=0), 2)}")
+    # the launch's fill: step 0 relative to the earliest layer-0 start stamp of the replica
+    f = {}
+    for rr in range(R):
+        m = rep == rr
+        t0 = s[roles["l0"] & m, 0, 0].min()
+        f.setdefault("l0 part_pub(0) [last]", []).append((s[roles["l0"] & m, 0, 1].max() - t0) / 100.0)
+        f.setdefault("chain seen(0) [last]", []).append((s[chain & m, 0, 1].max() - t0) / 100.0)
+        f.setdefault("chain bwd_pub(0) [median]", []).append((np.median(s[chain & m, 0, ref_k]) - t0) / 100.0)
+        f.setdefault("chain bwd_pub(1) [median]", []).append((np.median(s[chain & m, 1, ref_k]) - t0) / 100.0)
+    print("fill (us from the first layer-0 stamp, median over replicas):",
+          {k: round(float(np.median(v)), 2) for k, v in f.items()})
     ends = [np.median(s[chain, i, ref_k]) for i in range(min(8, nst))]
     d = np.diff([x for x in ends if x > 0]) / 100.0
     print("step period (us):", np.round(d, 2), "median", np.round(np.median(d), 2) if len(d) else None)
