@@ -914,3 +914,36 @@ def test_tail_chain_matches_fp32_reference_with_same_masks(hidden, B, policy):
     d = np.abs(grp.get_weights_flat() - wn).max() / np.abs(wn - w0).max()
     assert d < tol, d
     config.set_policy("float32")
+
+
+def test_predict_output_pool_never_aliases_a_live_array():
+    """Large predictions come from a pool of pinned host buffers recycled only after the
+    previous array (and its views) is gone: arrays the caller holds never share memory,
+    and a recycled buffer holds exactly the new call's predictions."""
+    import gc
+    from elephas_amd import config
+    from elephas_amd.ops.native_engine import NativeTrainer, _OUT_POOL
+    from elephas_amd.ops.plan import build_plan
+    config.set_policy("float32")
+    m = _mlp(16, [32], 32, out_act="softmax")
+    m.compile("sgd", "categorical_crossentropy", ["acc"])
+    t = NativeTrainer(m, build_plan(m), 1, 256, torch.device("cuda"))
+    rng = np.random.default_rng(3)
+    x1 = rng.random((70000, 16), dtype=np.float32)   # 70000 x 32 fp32 = 9 MB: pooled
+    x2 = rng.random((70000, 16), dtype=np.float32)
+    a = t.predict(x1)
+    b = t.predict(x2)
+    c = t.predict(x1)
+    assert not np.shares_memory(a, b) and not np.shares_memory(a, c) and not np.shares_memory(b, c)
+    assert np.array_equal(a, c) and not np.array_equal(a, b)
+    view = b[:10]
+    del b
+    gc.collect()
+    d = t.predict(x1)                          # b's buffer is still referenced by the view
+    assert not np.shares_memory(d, view) and np.array_equal(d, a)
+    ref_b = view.copy()
+    del a, c, d
+    gc.collect()
+    e = t.predict(x2)                          # may reuse a recycled buffer
+    assert np.array_equal(e[:10], ref_b) and np.array_equal(view, ref_b)
+    assert sum(len(v) for v in _OUT_POOL._free.values()) <= _OUT_POOL.KEEP
