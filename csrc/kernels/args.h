@@ -189,8 +189,10 @@ constexpr int PM_NTU = 2;      // layer-1 column tiles (and layer-2 row tiles) a
 // touch any state)
 // X (sync: a workgroup's weight-gradient tile is in the exchange slab, see PersistArgs::sync),
 // GR (V2 with ng > 0: a weight-gradient workgroup's Gram slab of a step is out)
+// XT (sync across ranks: replica 0's workgroup q has the job-wide sum of its tile in its
+// total slab; the other replicas read it there instead of every rank's slab)
 enum PmFlag : int { PMF_PART = 0, PMF_BWD = 1, PMF_W = 2, PMF_A0 = 3, PMF_D2 = 4, PMF_GO = 5, PMF_X = 6, PMF_GR = 7,
-                    PMF_N = 8 };
+                    PMF_XT = 8, PMF_N = 9 };
 // sticky error codes: the wait that timed out (PERR_GRID: the grid was not resident --
 // nothing was modified, the chunk can be re-run on another plan)
 enum PmErr : unsigned { PERR_L0_BWD = 1, PERR_CHAIN_PART = 2, PERR_CHAIN_BWD = 3, PERR_CHAIN_PREV = 4,
@@ -228,6 +230,7 @@ struct PersistArgs {
   int xr_world, xr_rank;
   unsigned xr_tag0;
   long long xr_timeout;             // its waits' spin limit (ticks): ranks may start seconds apart
+  long long o_xt;                   // total slabs [2][wgs][PM_XSLOT] (replica 0's workspace; xr_world > 1)
   // parameter-server hook (V1 roles; async / hogwild frequency='batch', reference
   // elephas/worker.py:114-127): after its update every owning workgroup pushes its
   // delta (theta_new - theta_pulled, fp32 atomics into the sharded device PS) and pulls

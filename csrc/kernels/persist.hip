@@ -170,8 +170,9 @@ __device__ __forceinline__ void publish(unsigned* flag, unsigned tag) {
 // wave 0 polls flags[0 .. n) (lane q watches producer q) until every one reaches tag;
 // the whole workgroup leaves together.  false: timed out (error word set)
 __device__ __forceinline__ bool wait_all(const PersistArgs& a, const unsigned* flags, int n, unsigned tag,
-                                         unsigned code) {
+                                         unsigned code, long long tmo = -1) {
   int ok = 1;
+  if (tmo < 0) tmo = a.timeout;
   if (threadIdx.x < 64) {
     const int lane = threadIdx.x;
     const unsigned long long t0 = wall_clock64();
@@ -180,7 +181,7 @@ __device__ __forceinline__ bool wait_all(const PersistArgs& a, const unsigned* f
                                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                                   : tag;
       if (__all(v >= tag)) break;
-      if ((long long)(wall_clock64() - t0) > a.timeout) {
+      if ((long long)(wall_clock64() - t0) > tmo) {
         ok = 0;
         if (lane == 0) __hip_atomic_store((gu32*)(a.err), code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
@@ -331,9 +332,13 @@ __device__ __forceinline__ bool xchg_sum(const PersistArgs& a, int r, int q, int
     for (int u = 0; u < N; ++u) v[u] += x[u];
   }
   if (a.xr_world <= 1) return true;
-  // ---- across ranks: replica 0 publishes the rank's sum, every replica sums the ranks'
+  // ---- across ranks: replica 0 publishes the rank's sum, reads every rank's (over xGMI
+  // on a node), sums them in rank order and leaves the total in its local total slab; the
+  // other replicas read that (one remote read set per workgroup and rank, not R of them)
   const unsigned tag = a.xr_tag0 + (unsigned)i + 1u;
   const long long soff = PEER_DATA_OFF + ((long long)(tag & 1u) * a.wgs + q) * PM_XSLOT * 4;
+  const long long tslab = a.o_xt + ((long long)(i & 1) * a.wgs + q) * PM_XSLOT;   // in replica 0's workspace
+  ok = 1;
   if (r == 0) {
     f32x4* dst = reinterpret_cast<f32x4*>(a.xr_base[a.xr_rank] + soff);
 #pragma unroll
@@ -343,45 +348,54 @@ __device__ __forceinline__ bool xchg_sum(const PersistArgs& a, int r, int q, int
     if (tid == 0)
       __hip_atomic_store(reinterpret_cast<unsigned*>(a.xr_base[a.xr_rank] + PEER_FLAG_OFF + (long long)q * 64), tag,
                          __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
-  ok = 1;
-  if (tid < 64) {
-    // lane k watches rank k's flag q (the rank's buffer by selects: no per-lane kernarg indexing)
-    char* b = a.xr_base[0];
+    if (tid < 64) {
+      // lane k watches rank k's flag q (the rank's buffer by selects: no per-lane kernarg indexing)
+      char* b = a.xr_base[0];
 #pragma unroll
-    for (int k = 1; k < PEER_MAX_RANKS; ++k) b = (tid == k) ? a.xr_base[k] : b;
-    const unsigned* fl = reinterpret_cast<const unsigned*>(b + PEER_FLAG_OFF + (long long)q * 64);
-    const unsigned long long t0 = wall_clock64();
-    for (;;) {
-      const unsigned f = tid < a.xr_world ? __hip_atomic_load(const_cast<unsigned*>(fl), __ATOMIC_ACQUIRE,
-                                                              __HIP_MEMORY_SCOPE_SYSTEM)
-                                          : tag;
-      if (__all((int)(f - tag) >= 0)) break;   // wrap-safe: tags only grow
-      if ((long long)(wall_clock64() - t0) > a.xr_timeout) {
-        ok = 0;
-        if (tid == 0) __hip_atomic_store((gu32*)(a.err), (unsigned)PERR_XRANK, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
+      for (int k = 1; k < PEER_MAX_RANKS; ++k) b = (tid == k) ? a.xr_base[k] : b;
+      const unsigned* fl = reinterpret_cast<const unsigned*>(b + PEER_FLAG_OFF + (long long)q * 64);
+      const unsigned long long t0 = wall_clock64();
+      for (;;) {
+        const unsigned f = tid < a.xr_world ? __hip_atomic_load(const_cast<unsigned*>(fl), __ATOMIC_ACQUIRE,
+                                                                __HIP_MEMORY_SCOPE_SYSTEM)
+                                            : tag;
+        if (__all((int)(f - tag) >= 0)) break;   // wrap-safe: tags only grow
+        if ((long long)(wall_clock64() - t0) > a.xr_timeout) {
+          ok = 0;
+          if (tid == 0) __hip_atomic_store((gu32*)(a.err), (unsigned)PERR_XRANK, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
       }
-      __builtin_amdgcn_s_sleep(1);
     }
-  }
-  ok = __syncthreads_and(ok);
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-  if (!ok) return false;
+    ok = __syncthreads_and(ok);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    if (!ok) return false;
 #pragma unroll
-  for (int u = 0; u < N; ++u) v[u] = zero4f();
+    for (int u = 0; u < N; ++u) v[u] = zero4f();
 #pragma unroll 1
-  for (int k = 0; k < a.xr_world; ++k) {   // rank order
-    char* b = a.xr_base[0];
+    for (int k = 0; k < a.xr_world; ++k) {   // rank order
+      char* b = a.xr_base[0];
 #pragma unroll
-    for (int kk = 1; kk < PEER_MAX_RANKS; ++kk) b = (k == kk) ? a.xr_base[kk] : b;
-    const f32x4* src = reinterpret_cast<const f32x4*>(b + soff);
-    f32x4 x[N];
+      for (int kk = 1; kk < PEER_MAX_RANKS; ++kk) b = (k == kk) ? a.xr_base[kk] : b;
+      const f32x4* src = reinterpret_cast<const f32x4*>(b + soff);
+      f32x4 x[N];
 #pragma unroll
-    for (int u = 0; u < N; ++u) x[u] = __builtin_nontemporal_load(src + u * 256 + tid);
+      for (int u = 0; u < N; ++u) x[u] = __builtin_nontemporal_load(src + u * 256 + tid);
 #pragma unroll
-    for (int u = 0; u < N; ++u) v[u] += x[u];
+      for (int u = 0; u < N; ++u) v[u] += x[u];
+    }
+    if (a.R > 1) {   // the total for the other replicas (write-through, then the local flag)
+#pragma unroll
+      for (int u = 0; u < N; ++u) stw4(all, (u * 256 + tid) * 4, (int)tslab, v[u]);
+      publish(flag_at(a, 0, PMF_XT) + q, (unsigned)(i + 1));
+    }
+    return true;
   }
+  // replica 0 may itself wait for a late rank: the rank exchange's patience here too
+  if (!wait_all(a, flag_at(a, 0, PMF_XT) + q, 1, (unsigned)(i + 1), PERR_XRANK, a.xr_timeout)) return false;
+#pragma unroll
+  for (int u = 0; u < N; ++u) v[u] = ldw4(all, (u * 256 + tid) * 4, (int)tslab);
   return true;
 }
 

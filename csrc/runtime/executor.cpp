@@ -178,6 +178,7 @@ bool Executor::build_persist() {
   a.o_b1 = take(a.H1);
   a.o_b2 = take(16);
   a.o_xg = a.sync ? take(2LL * a.wgs * PM_XSLOT) : 0;
+  a.o_xt = a.sync ? take(2LL * a.wgs * PM_XSLOT) : 0;   // used with the rank exchange
   a.ws_stride = off;
   const size_t ws_bytes = sizeof(float) * (size_t)off * c_.R;
   check(hipMalloc(&d_pws_, ws_bytes), "hipMalloc(persistent workspace)");
@@ -220,6 +221,9 @@ bool Executor::set_rank_exchange(const std::vector<char*>& bases, int world, int
   a.xr_world = world;
   a.xr_rank = rank;
   a.xr_timeout = (long long)(std::max(1.0, timeout_s) * 1e8);   // s_memrealtime: 100 MHz
+  // every in-launch wait may now sit behind another rank (startup skew of seconds): the
+  // rank exchange's patience for all of them (residency was checked on the host)
+  a.timeout = std::max(a.timeout, a.xr_timeout);
   pm_.xr_steps = tag0;   // a rebuilt executor continues the trainer's tag sequence
   return true;
 }
