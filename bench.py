@@ -186,7 +186,11 @@ def main():
         for name, w_, bm in (("per_step_sync", W, True), ("strong", strong_w, False)):
             if w_ is None:
                 continue
-            r = measure_train(args, model, dist, rank, world, dev, gpu, w_, bm, sk, sw)
+            try:
+                r = measure_train(args, model, dist, rank, world, dev, gpu, w_, bm, sk, sw)
+            except Exception as e:  # noqa: BLE001 - an extra measurement never costs the headline line
+                subs[name] = {"error": repr(e)[:300]}
+                continue
             subs[name] = {"value": round(r["samples"] / r["dt_max"], 1), "ms_per_step": round(r["dt_max"] / sk * 1e3, 4),
                           "steps": sk, "workers_per_gpu": w_, "sync": r["sync"], "engine": r["engine"],
                           "scaling": "weak" if name != "strong" else "strong",
