@@ -2477,7 +2477,7 @@ __global__ __launch_bounds__(256) void mlp_persist_kernel(PersistArgs a) {
 
 // the instances of one hidden width: the specialised MNIST-style one (relu, softmax +
 // cross-entropy, plain SGD) and the general ones
-template <int H>
+template <int H0, int H1>
 hipError_t persist_launch(const PersistArgs* a, hipStream_t s) {
   bool fast = a->act2 == ACT_SOFTMAX && (a->loss == LOSS_CCE || a->loss == LOSS_SPARSE_CCE);
   for (int i = 0; i < a->nmet; ++i)
@@ -2487,21 +2487,21 @@ hipError_t persist_launch(const PersistArgs* a, hipStream_t s) {
   const bool sgd = !a->S || (a->op.opt == OPT_SGD && a->op.mom == 0.f);
   const dim3 grid(a->R * a->wgs);
   if (a->v2 && a->bf16) {   // mixed_bfloat16: bf16 shard, bf16-rounded MFMA operands, fp32 masters
-    if (fast) hipLaunchKernelGGL((mlp_persist_kernel<H, H, true, 0, true, true, false, true>), grid, dim3(256), 0, s, *a);
-    else hipLaunchKernelGGL((mlp_persist_kernel<H, H, false, 0, true, true, false, true>), grid, dim3(256), 0, s, *a);
+    if (fast) hipLaunchKernelGGL((mlp_persist_kernel<H0, H1, true, 0, true, true, false, true>), grid, dim3(256), 0, s, *a);
+    else hipLaunchKernelGGL((mlp_persist_kernel<H0, H1, false, 0, true, true, false, true>), grid, dim3(256), 0, s, *a);
   } else if (a->v2) {   // the host checked plain SGD + ReLU
-    if (fast) hipLaunchKernelGGL((mlp_persist_kernel<H, H, true, 0, true, true>), grid, dim3(256), 0, s, *a);
-    else hipLaunchKernelGGL((mlp_persist_kernel<H, H, false, 0, true, true>), grid, dim3(256), 0, s, *a);
+    if (fast) hipLaunchKernelGGL((mlp_persist_kernel<H0, H1, true, 0, true, true>), grid, dim3(256), 0, s, *a);
+    else hipLaunchKernelGGL((mlp_persist_kernel<H0, H1, false, 0, true, true>), grid, dim3(256), 0, s, *a);
   } else if (a->ps_mode) {   // V1 with the in-launch parameter-server exchange
-    if (fast && relu && sgd) hipLaunchKernelGGL((mlp_persist_kernel<H, H, true, 0, true, false, true>), grid, dim3(256), 0, s, *a);
-    else if (fast) hipLaunchKernelGGL((mlp_persist_kernel<H, H, true, -1, false, false, true>), grid, dim3(256), 0, s, *a);
-    else hipLaunchKernelGGL((mlp_persist_kernel<H, H, false, -1, false, false, true>), grid, dim3(256), 0, s, *a);
+    if (fast && relu && sgd) hipLaunchKernelGGL((mlp_persist_kernel<H0, H1, true, 0, true, false, true>), grid, dim3(256), 0, s, *a);
+    else if (fast) hipLaunchKernelGGL((mlp_persist_kernel<H0, H1, true, -1, false, false, true>), grid, dim3(256), 0, s, *a);
+    else hipLaunchKernelGGL((mlp_persist_kernel<H0, H1, false, -1, false, false, true>), grid, dim3(256), 0, s, *a);
   } else if (fast && relu && sgd) {
-    hipLaunchKernelGGL((mlp_persist_kernel<H, H, true, 0, true, false>), grid, dim3(256), 0, s, *a);
+    hipLaunchKernelGGL((mlp_persist_kernel<H0, H1, true, 0, true, false>), grid, dim3(256), 0, s, *a);
   } else if (fast) {
-    hipLaunchKernelGGL((mlp_persist_kernel<H, H, true, -1, false, false>), grid, dim3(256), 0, s, *a);
+    hipLaunchKernelGGL((mlp_persist_kernel<H0, H1, true, -1, false, false>), grid, dim3(256), 0, s, *a);
   } else {
-    hipLaunchKernelGGL((mlp_persist_kernel<H, H, false, -1, false, false>), grid, dim3(256), 0, s, *a);
+    hipLaunchKernelGGL((mlp_persist_kernel<H0, H1, false, -1, false, false>), grid, dim3(256), 0, s, *a);
   }
   return hipGetLastError();
 }
@@ -2513,10 +2513,11 @@ using namespace ea;
 extern "C" int ea_persist_lds_bytes() { return (int)(LDS_FLOATS * sizeof(float)); }
 
 // grid: R * wgs workgroups of 256 threads, every one resident (the host sizes the
-// grid to at most one workgroup per CU); hidden widths (64, 64) or (128, 128)
+// grid to at most one workgroup per CU); hidden widths (64, 64), (128, 128), (128, 64)
 extern "C" hipError_t ea_persist(const PersistArgs* a, hipStream_t s) {
   if (a->nsteps <= 0) return hipSuccess;
-  if (a->H0 == 128 && a->H1 == 128) return persist_launch<128>(a, s);
-  if (a->H0 == 64 && a->H1 == 64) return persist_launch<64>(a, s);
+  if (a->H0 == 128 && a->H1 == 128) return persist_launch<128, 128>(a, s);
+  if (a->H0 == 64 && a->H1 == 64) return persist_launch<64, 64>(a, s);
+  if (a->H0 == 128 && a->H1 == 64) return persist_launch<128, 64>(a, s);
   return hipErrorInvalidValue;
 }

@@ -61,8 +61,8 @@ bool Executor::build_persist() {
   const int L = (int)c_.layers.size();
   if (L != 3) return false;
   const LayerCfg &l0 = c_.layers[0], &l1 = c_.layers[1], &l2 = c_.layers[2];
-  // hidden widths (64, 64) or (128, 128): the kernel is compiled for those two shapes
-  if (!((l0.N == 64 && l1.N == 64) || (l0.N == 128 && l1.N == 128))) return false;
+  // hidden widths (64, 64), (128, 128) or (128, 64): the kernel is compiled for those shapes
+  if (!((l0.N == 64 && l1.N == 64) || (l0.N == 128 && l1.N == 128) || (l0.N == 128 && l1.N == 64))) return false;
   if (l1.K != l0.N || l2.K != l1.N || l2.N > PM_MAXC || c_.ldy > 32) return false;
   if (c_.B > PM_ROWS || c_.B < 1) return false;
   const int nch = cdiv(c_.B, 16);

@@ -52,15 +52,17 @@ def _trainer(model, R, B, persist, seed=12345, rowchain=None):
                          rowchain=rowchain)
 
 
-@pytest.mark.parametrize("opt", ["sgd", "sgd_mom", "adam"])
-def test_persist_matches_fp32_reference_with_same_masks(opt):
+@pytest.mark.parametrize("opt,hidden", [("sgd", (64, 64)), ("sgd_mom", (64, 64)), ("adam", (64, 64)),
+                                        ("sgd", (128, 64)), ("sgd_mom", (128, 64))])
+def test_persist_matches_fp32_reference_with_same_masks(opt, hidden):
     """Persistent plan == fp32 torch autograd with the same dropout masks (2 replicas,
-    3 steps per epoch, 2 epochs: every hand-off of every step is exercised)."""
+    3 steps per epoch, 2 epochs: every hand-off of every step is exercised); equal and
+    unequal hidden widths."""
     from elephas_amd.models import initializers, optimizers as O
     from elephas_amd.ops.plan import build_plan
     from elephas_amd.ops.torch_engine import TorchTrainer
     initializers.set_seed(31)
-    model = _mlp(40, [64, 64], 6, dropout=0.3)
+    model = _mlp(40, list(hidden), 6, dropout=0.3)
     optim = {"sgd": O.SGD(0.2), "sgd_mom": O.SGD(0.05, momentum=0.9, nesterov=True),
              "adam": O.Adam(0.003)}[opt]
     model.compile(optim, "categorical_crossentropy", ["acc"])
@@ -186,7 +188,7 @@ def test_persist_headline_shape_plan_and_progress():
     t.check()
 
 
-@pytest.mark.parametrize("hidden", [128, 64])
+@pytest.mark.parametrize("hidden", [(128, 128), (64, 64), (128, 64)])
 def test_persist_v2_matches_v1(monkeypatch, hidden):
     """The V2 roles (layer-0 pre-activations rebuilt from Pold + Gram corrections, weight
     gradients on their own workgroups) against V1 on the headline shape: 8 replicas x B
@@ -195,7 +197,7 @@ def test_persist_v2_matches_v1(monkeypatch, hidden):
     from elephas_amd.models import initializers
     from elephas_amd.models.optimizers import SGD
     initializers.set_seed(77)
-    model = _mlp(784, [hidden, hidden], 10, dropout=0.2)
+    model = _mlp(784, list(hidden), 10, dropout=0.2)
     model.compile(SGD(learning_rate=0.1, decay=1e-3), "categorical_crossentropy", ["acc"])
     xs, ys = _shards([700] * 7 + [300], 784, 10, seed=8)
     out = []
