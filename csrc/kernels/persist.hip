@@ -20,6 +20,12 @@
 //     workgroup computes DW1 / DW2 for the layer-1 columns (layer-2 rows) it owns,
 //     updates them (masters and optimizer state in registers), publishes them, and
 //     loads the whole new W1 / W2 for the next step.
+//   (V2 roles -- plain SGD + ReLU, fit granularity: l0_role_v2 / chain_role<V2> /
+//     dw_role_v2 below; layer-0 pre-activations two steps ahead plus a Gram correction
+//     in the chains, W1 / W2 and the Gram slabs on weight-gradient workgroups.  bf16
+//     instances run their products on v_mfma_f32_16x16x32_bf16.  docs/templates/
+//     persistent-kernel.md has the roles, the modes -- per-step sync inside the launch,
+//     across ranks through peer-mapped buffers, the parameter-server hook -- and safety.)
 //
 // Hand-offs follow the write-through form of the guide's inter-workgroup protocol
 // (cdna_hip_programming.md Guideline 16, R1): every handed-off byte is stored and
@@ -39,8 +45,9 @@
 // Semantics are those of the row-chain plan (reference elephas/worker.py:41-42 ->
 // one Keras fit step per batch): identical dropout masks (dropout_u1), batch windows,
 // optimizer iterations and loss epilogues; master weights and state are read from P / S
-// at the start of the launch and written back (with both weight-image parities) at
-// its end.
+// at the start of the launch and written back at its end (V1 with both weight-image
+// parities; V2 the masters only -- the host rebuilds the images before their next
+// reader).
 #include "common.h"
 #include "loss_tile.h"
 
