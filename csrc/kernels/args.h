@@ -272,6 +272,59 @@ struct PersistArgs {
 };
 constexpr int PM_STAMP_STEPS = 8;
 
+// --------------------------------------- persistent layer pipeline (deep.hip)
+// A chunk of training steps of a 2..DP_MAXL-layer Dense stack whose hidden layers are too
+// wide / too many for PersistArgs (Otto 93-512-512-512-9 at B = 128): nw workgroups per
+// replica (512 threads each, one per CU).  Workgroup j OWNS column tile j (16 units) of
+// every hidden layer: W_0[:, J] (its forward + weight gradient) and, for layers l >= 1, the
+// ROWS J of W_l (the input-gradient stripe dA_{l-1}[:, J] and the weight gradient
+// DW_l[J, :] of the backward); the forward of layer l >= 1 reads the columns J of W_l from a
+// transposed image the row owners rewrite after their update.  Phases of a step are
+// separated by per-replica all-to-all flag barriers (see deep.hip).
+constexpr int DP_MAXL = 5;      // Dense layers
+constexpr int DP_MAXWG = 64;    // workgroups per replica (one polling wave)
+constexpr int DP_ROWS = 128;    // batch rows per replica
+constexpr int DP_MAXC = 32;     // last-layer units (whole rows in one loss tile)
+constexpr int DP_CW = 64;       // dZ columns per backward chunk
+constexpr int DP_STAMP_STEPS = 8;
+struct DeepLayer {
+  int K, N;            // true input / output widths
+  int N16;             // output width padded to 16
+  int Kx;              // input row stride (multiple of 8): layer 0 the shard's ldx, else N16 below
+  int T;               // 16-column tiles of the output
+  int act, has_bias;
+  float rate;
+  long long p_off;     // kernel [K][N] at p_off of the flat vector, bias (N) after it
+  long long o_a, o_dz; // workspace (floats): A_l, dZ_l [Bp][N16] (hidden layers; dZ also last)
+  long long o_wt;      // workspace: W_l^T image [N16][Kx] (l >= 1)
+  long long o_w;       // workspace: row-major image [Kx][N16] (last layer)
+  int l_w;             // LDS: owned master -- layer 0: W^T tile [16][Kx + 4]; l >= 1: rows [16][N16 + 4]
+  int l_b;             // LDS: owned bias tile [16] (last layer: [N16] on workgroup 0)
+  int l_at;            // LDS: A_l^T stripe [16][Bp + 4] (hidden layers)
+};
+struct DeepArgs {
+  int R, B, Bp, RT, KS, nsteps, L, nw;
+  DeepLayer ly[DP_MAXL];
+  long long o_g, o_bl;          // workspace: G_{L-2} [Bp][N16], last-layer bias image [N16]
+  int l_dz0, l_stage, l_red, lds_floats;
+  const float* X; long long sX, ldx;
+  const float* Y; long long sY, ldy;
+  const int* perm; long long sPerm;
+  const int* ntrain;
+  float* P; long long sP;
+  float* S; long long sS;
+  OptParams op;
+  int loss, nmet, met[4];
+  double* acc; int acc_stride;
+  long long* ctr;
+  unsigned long long seed;
+  float* ws; long long ws_stride;   // per-replica workspace (floats)
+  unsigned* flags;                  // [R][2][DP_MAXWG] GO / phase counters, zero at launch
+  unsigned* err;                    // sticky error word (PmErr codes)
+  long long timeout;                // spin limit in s_memrealtime ticks
+  long long* stamps;                // diagnostics: [block][DP_STAMP_STEPS][32] s_memrealtime (null = off)
+};
+
 constexpr int MAX_SEG = 16;
 
 struct Seg {

@@ -1,0 +1,31 @@
+// Dispatch of the persistent layer-pipeline kernel (deep_impl.h) to its per-layer-count
+// instances (deep_l{2,3,4,5}.hip: one translation unit each, built in parallel)
+#include "args.h"
+#include <hip/hip_runtime.h>
+
+extern "C" hipError_t ea_deep_l2(const ea::DeepArgs* a, int fast, int sgd0, hipStream_t s);
+extern "C" hipError_t ea_deep_l3(const ea::DeepArgs* a, int fast, int sgd0, hipStream_t s);
+extern "C" hipError_t ea_deep_l4(const ea::DeepArgs* a, int fast, int sgd0, hipStream_t s);
+extern "C" hipError_t ea_deep_l5(const ea::DeepArgs* a, int fast, int sgd0, hipStream_t s);
+
+using namespace ea;
+
+// grid: R * nw workgroups of 512 threads, every one resident (the host sizes the grid to
+// at most one workgroup per CU); dynamic LDS a->lds_floats floats
+extern "C" hipError_t ea_deep(const DeepArgs* a, hipStream_t s) {
+  if (a->nsteps <= 0) return hipSuccess;
+  // softmax + (sparse) categorical cross-entropy with accuracy / CCE metrics: the quad-per-row
+  // loss tile; everything else the generic one
+  bool fast = a->ly[a->L - 1].act == ACT_SOFTMAX && (a->loss == LOSS_CCE || a->loss == LOSS_SPARSE_CCE);
+  for (int i = 0; i < a->nmet; ++i)
+    fast = fast && (a->met[i] == MET_ACC_CAT || a->met[i] == MET_ACC_SPARSE || a->met[i] == LOSS_CCE ||
+                    a->met[i] == LOSS_SPARSE_CCE);
+  const int sgd0 = a->op.opt == OPT_SGD && a->op.mom == 0.f;   // plain SGD: no optimizer state
+  switch (a->L) {
+    case 2: return ea_deep_l2(a, fast, sgd0, s);
+    case 3: return ea_deep_l3(a, fast, sgd0, s);
+    case 4: return ea_deep_l4(a, fast, sgd0, s);
+    case 5: return ea_deep_l5(a, fast, sgd0, s);
+    default: return hipErrorInvalidValue;
+  }
+}

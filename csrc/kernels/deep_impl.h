@@ -1,0 +1,1020 @@
+// Persistent layer-pipeline training kernel (MI355X / gfx950) -- the kernel templates;
+// deep_l{2,3,4,5}.hip instantiate one layer count each (parallel builds), deep.hip dispatches.
+//
+// Persistent layer-pipeline training kernel (MI355X / gfx950): a whole chunk of training
+// steps of a 2..DP_MAXL-layer Dense stack with wide hidden layers in ONE launch.
+//
+// Why: the Otto MLP (93-512-512-512-9, 8 replicas x B 128, reference examples/
+// ml_pipeline_otto.py:57-68) ran as 7 latency-bound launches per step (tail-chain plan,
+// 174 us, profiles/README.md); its 512-wide layers do not fit persist.hip's chain roles
+// (widths <= 128, B <= 64).  Here a replica is a cluster of nw workgroups of 512 threads
+// (8 waves, one workgroup per CU; block b serves replica b % R, so with R = 8 a replica's
+// cluster is dispatched to one XCD -- speed only, the protocol never depends on placement).
+//
+// Ownership (workgroup j, column tile J = [16j, 16j + 16) of every hidden layer):
+//   * W_0[:, J] (LDS, transposed [16][Kx0 + 4]) and b_0[J]: the layer-0 forward of the
+//     tile and its weight gradient DW_0[:, J] = X^T dZ_0[:, J] -- dZ_0[:, J] is produced by
+//     the same workgroup, so layer 0 needs no hand-off in the backward at all;
+//   * the ROWS J of W_l, l >= 1 (LDS [16][N16 + 4]) and b_l[J]: the backward stripe
+//     dA_{l-1}[:, J] = dZ_l W_l[J, :]^T and DW_l[J, :] = A_{l-1}[:, J]^T dZ_l, both from ONE
+//     pass over dZ_l (streamed through LDS in 64-column chunks); after its update the row
+//     owner rewrites its 16-column segment of the transposed image W_l^T (workspace) that
+//     the forward of the next step reads (columns J of W_l for the owner of output tile J);
+//   * the activation-gradient factors G_l = act'(z) keep / (1 - rate) of the forward stay
+//     in the registers of the lanes that produce dA_l in the backward (same wave, same
+//     lane <-> element map), the activation stripes A_l[:, J] in LDS (the DW operand).
+//   The last layer (<= 32 units) is row-parallel: the tail workgroups (16 batch rows each)
+//   run its forward, the loss / metrics and dZ_{L-2} rows (G_{L-2} is the one factor that
+//   goes through the workspace).
+//
+// Phases of step s (tags = s * (2L - 2) + phase + 1; every workgroup publishes every phase):
+//   FWD_0 -> | FWD_1 -> | ... FWD_{L-2} -> | tail -> | BW_{L-2} (+ DW_{L-1}) -> | ... BW_1 ->
+//   then DW_0 of step s runs at the top of step s + 1 (no wait: its inputs are local).
+// Hand-offs follow the write-through form of the guide's inter-workgroup protocol
+// (cdna_hip_programming.md Guideline 16, R1): every handed-off byte is stored with an sc1
+// buffer store and loaded with an sc1 buffer load, every storing wave drains
+// (s_waitcnt vmcnt(0)) before the workgroup barrier, one lane stores the phase counter
+// (agent-scope relaxed atomic store), one wave polls the replica's counters.  Every spin is
+// bounded (timeout -> sticky error word; the host re-plans), the flags are zero at launch.
+//
+// Semantics are those of the grouped / tail-chain plans (reference elephas/worker.py:41-42 ->
+// one Keras fit step per batch): the same dropout masks (dropout_u1 keyed by replica, Dense
+// index, optimizer iteration, batch row, column), batch windows, optimizer iterations and
+// loss epilogues (loss_tile.h).  Masters are read from P at the start of the launch and
+// written back at its end; optimizer state stays in S (read-modify-write by the owner).
+#pragma once
+#include "common.h"
+#include "loss_tile.h"
+
+namespace ea {
+
+namespace {
+
+using gu32 = __attribute__((address_space(1))) unsigned;
+using rsrc_t = __amdgpu_buffer_rsrc_t;
+typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
+
+constexpr int NWV = 8;          // waves per workgroup
+constexpr int NTH = NWV * 64;   // threads per workgroup
+constexpr int CW = DP_CW;       // dZ columns per backward chunk
+constexpr int LDZ = CW + 4;     // LDS row stride of a dZ chunk
+
+__device__ __forceinline__ f32x4 z4() { return f32x4{0.f, 0.f, 0.f, 0.f}; }
+
+// ---- write-through (sc1) accesses of handed-off bytes: per-lane offset v + uniform offset
+//      s, both in floats, through a buffer resource of the replica's workspace
+__device__ __forceinline__ rsrc_t ws_rsrc(const float* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), (short)0, 0x7fffffff, 0x00020000);
+}
+__device__ __forceinline__ f32x4 ld4(rsrc_t r, int v, long long s) {
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, v * 4, (int)s * 4, 16));
+}
+__device__ __forceinline__ float ld1(rsrc_t r, int v, long long s) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, v * 4, (int)s * 4, 16));
+}
+__device__ __forceinline__ void st1(rsrc_t r, int v, long long s, float x) {
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, x), r, v * 4, (int)s * 4, 16);
+}
+__device__ __forceinline__ void st4(rsrc_t r, int v, long long s, f32x4 x) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, x), r, v * 4, (int)s * 4, 16);
+}
+__device__ __forceinline__ f32x4 lds4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
+__device__ __forceinline__ void lds4(float* p, f32x4 v) { *reinterpret_cast<f32x4*>(p) = v; }
+
+// 16x16 output tile += A . B over 4 k values per lane group (fp32 MFMA, exact):
+// lane group g holds k = 4g .. 4g + 3 of a 16-deep chunk, MFMA e consumes element e
+__device__ __forceinline__ void mma4(f32x4& c, f32x4 a, f32x4 b) {
+  c = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b.x, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, b.y, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, b.z, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, b.w, c, 0, 0, 0);
+}
+
+// Workgroup barrier for LDS hand-offs only (no vmcnt drain: prefetched global loads stay
+// in flight across it)
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+__device__ __forceinline__ unsigned* dflag(const DeepArgs& a, int r, int kind) {
+  return a.flags + ((long long)r * 2 + kind) * DP_MAXWG;
+}
+
+// R1 publish of phase `tag`: every storing wave drains its sc1 stores, the workgroup
+// meets, one lane raises its phase counter
+__device__ __forceinline__ void publish(const DeepArgs& a, int r, int j, unsigned tag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store((gu32*)(dflag(a, r, 1) + j), tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// wave 0 polls the phase counters of the replica's nw workgroups (lane q watches q) until
+// each reaches tag; false: timed out (error word set)
+__device__ __forceinline__ bool wait_phase(const DeepArgs& a, int r, unsigned tag) {
+  int ok = 1;
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    const unsigned* f = dflag(a, r, 1) + lane;
+    const unsigned long long t0 = wall_clock64();
+    for (;;) {
+      const unsigned v = lane < a.nw ? __hip_atomic_load((gu32*)(const_cast<unsigned*>(f)), __ATOMIC_RELAXED,
+                                                         __HIP_MEMORY_SCOPE_AGENT)
+                                     : tag;
+      if (__all(v >= tag)) break;
+      if ((long long)(wall_clock64() - t0) > a.timeout) {
+        ok = 0;
+        if (lane == 0) __hip_atomic_store((gu32*)(a.err), (unsigned)PERR_CHAIN_PREV, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  ok = __syncthreads_and(ok);
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // no load moves above the poll
+  return ok != 0;
+}
+
+// residency: every workgroup of the grid raised its GO flag (a workgroup that is not
+// resident never does: the others time out before touching any state)
+__device__ __forceinline__ bool wait_grid(const DeepArgs& a) {
+  int ok = 1;
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x, tot = a.R * a.nw;
+    const unsigned long long t0 = wall_clock64();
+    for (;;) {
+      bool all = true;
+      for (int f = lane; f < tot; f += 64)
+        all &= __hip_atomic_load((gu32*)(dflag(a, f % a.R, 0) + f / a.R), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+      if (__all(all)) break;
+      if ((long long)(wall_clock64() - t0) > a.timeout) {
+        ok = 0;
+        if (lane == 0) __hip_atomic_store((gu32*)(a.err), (unsigned)PERR_GRID, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  ok = __syncthreads_and(ok);
+  return ok != 0;
+}
+
+__device__ __forceinline__ float dropout_u1(uint32_t base, int row, int c) {
+  // the per-column-pair hash of dropout_u8 (common.h): the grouped / row-chain masks
+  const uint32_t h = fmix32(base ^ (((uint32_t)row << 16) | (uint32_t)(c >> 1)));
+  return (float)((c & 1) ? (h >> 16) : (h & 0xFFFFu)) * (1.0f / 65536.0f);
+}
+
+__device__ __forceinline__ void dstamp(const DeepArgs& a, int s, int k) {
+  if (a.stamps && threadIdx.x == 0 && s >= 0 && s < DP_STAMP_STEPS)
+    a.stamps[((long long)blockIdx.x * DP_STAMP_STEPS + s) * 32 + k] = (long long)__builtin_amdgcn_s_memrealtime();
+}
+
+// per-workgroup constants
+struct Ctx {
+  int r, j, tid, lane, w, g, c16;
+  rsrc_t rs;           // the replica's workspace
+  float* P;            // the replica's masters
+  float* S;            // the replica's optimizer state (null: none)
+  int* prow;           // LDS: the batch rows of two steps [2][DP_ROWS] (by step parity)
+};
+
+// The lane indices, re-derived from threadIdx.x through an opaque move at the top of every
+// phase: otherwise the compiler hoists every per-lane address of every phase out of the
+// step loop and, with far more of them than registers, spills them to scratch (~750
+// scratch stores before the loop and a scratch load in front of most workspace accesses)
+__device__ __forceinline__ Ctx lanes(const Ctx& x0) {
+  int t;
+  asm volatile("v_mov_b32 %0, %1" : "=v"(t) : "v"((int)threadIdx.x));
+  Ctx x = x0;
+  x.tid = t;
+  x.lane = t & 63;
+  x.g = (t & 63) >> 4;
+  x.c16 = t & 15;
+  return x;
+}
+
+// The optimizer rule of one step (Keras 2.10 optimizer_v2, as common.h opt_update) with its
+// per-step scalars hoisted: the decayed learning rate and the Adam / Adamax bias
+// corrections are computed once per phase, not per element (the scalar rule inlined at
+// every update site cost ~1 KB of scratch per lane in this kernel)
+struct OptStep {
+  int kind;          // 0 plain SGD, 1 momentum, 2 Nesterov, 3 RMSprop, 4 RMSprop + momentum, 5 Adam,
+                     // 6 Adagrad, 7 Adamax
+  float lr, lrt;     // decayed lr; Adam / Adamax bias-corrected lr
+};
+__device__ __forceinline__ OptStep opt_step(const OptParams& p, long long it) {
+  OptStep o;
+  o.lr = p.lr / (1.f + p.decay * (float)it);
+  o.lrt = o.lr;
+  const float t = (float)(it + 1);
+  switch (p.opt) {
+    case OPT_SGD: o.kind = p.mom == 0.f ? 0 : (p.nesterov ? 2 : 1); break;
+    case OPT_RMSPROP: o.kind = p.mom > 0.f ? 4 : 3; break;
+    case OPT_ADAM: o.kind = 5; o.lrt = o.lr * sqrtf(1.f - powf(p.b2, t)) / (1.f - powf(p.b1, t)); break;
+    case OPT_ADAGRAD: o.kind = 6; break;
+    default: o.kind = 7; o.lrt = o.lr / (1.f - powf(p.b1, t)); break;
+  }
+  return o;
+}
+template <bool SGD0>
+__device__ __forceinline__ float upd(const DeepArgs& a, const Ctx& x, const OptStep& o, long long pi, float w, float g) {
+  g *= a.op.grad_scale;
+  if constexpr (SGD0) {
+    return w - o.lr * g;
+  } else {
+    const OptParams& p = a.op;
+    float* S = x.S;
+    const long long s1 = pi + p.s_plane;
+    switch (o.kind) {
+      case 0: return w - o.lr * g;
+      case 1: case 2: {
+        const float v = p.mom * S[pi] - o.lr * g;
+        S[pi] = v;
+        return o.kind == 2 ? w + p.mom * v - o.lr * g : w + v;
+      }
+      case 3: case 4: {
+        const float ms = p.rho * S[pi] + (1.f - p.rho) * g * g;
+        S[pi] = ms;
+        if (o.kind == 4) {   // tf ApplyRMSProp: epsilon inside the square root
+          const float m = p.mom * S[s1] + o.lr * g / sqrtf(ms + p.eps);
+          S[s1] = m;
+          return w - m;
+        }
+        return w - o.lr * g / (sqrtf(ms) + p.eps);
+      }
+      case 5: {
+        const float m = p.b1 * S[pi] + (1.f - p.b1) * g;
+        const float v = p.b2 * S[s1] + (1.f - p.b2) * g * g;
+        S[pi] = m;
+        S[s1] = v;
+        return w - o.lrt * m / (sqrtf(v) + p.eps);
+      }
+      case 6: {
+        const float ac = S[pi] + g * g;
+        S[pi] = ac;
+        return w - o.lr * g / (sqrtf(ac) + p.eps);
+      }
+      default: {
+        const float m = p.b1 * S[pi] + (1.f - p.b1) * g;
+        const float u = fmaxf(p.b2 * S[s1], fabsf(g));
+        S[pi] = m;
+        S[s1] = u;
+        return w - o.lrt * m / (u + p.eps);
+      }
+    }
+  }
+}
+
+// ---- C[16 rows x 16] of one wave: rows from global (loadA(k) -> this lane's float4
+//      A[row][k .. k + 3]), B^T from LDS ([16][ldb], k contiguous), over the k-chunks
+//      t = kp + KS u.  A register ring of PF chunks is issued (ring_issue) ahead of the
+//      consumer; the chunk count is padded to a multiple of PF so that the loop body has
+//      no load under a condition (k past Kx reads a clamped address and multiplies zeros)
+template <int PF, typename LA>
+__device__ __forceinline__ void ring_issue(f32x4 (&ring)[PF], LA loadA, int kp, int KS, int g) {
+#pragma unroll
+  for (int u = 0; u < PF; ++u) ring[u] = loadA(16 * (kp + KS * u) + 4 * g);
+}
+template <int PF, typename LA>
+__device__ __forceinline__ f32x4 ring_run(f32x4 (&ring)[PF], LA loadA, const float* bt, int ldb, int Kx, int kp, int KS,
+                                          int nmine, int lane) {
+  const int g = lane >> 4, c = lane & 15;
+  f32x4 acc0 = z4(), acc1 = z4();
+  for (int u0 = 0; u0 < nmine; u0 += PF) {
+#pragma unroll
+    for (int v = 0; v < PF; ++v) {
+      const int u = u0 + v;
+      const int k = 16 * (kp + KS * u) + 4 * g;
+      f32x4 av = ring[v];
+      ring[v] = loadA(16 * (kp + KS * (u + PF)) + 4 * g);   // clamped by loadA past the end
+      const bool kin = k < Kx;
+      f32x4 bv = lds4(bt + c * ldb + (kin ? k : 0));
+      if (!kin) { av = z4(); bv = z4(); }
+      if (v & 1) mma4(acc1, av, bv);
+      else mma4(acc0, av, bv);
+    }
+  }
+  return acc0 + acc1;
+}
+
+// split-K partials of waves kp > 0 summed into the kp == 0 wave of the row tile (LDS red)
+__device__ __forceinline__ f32x4 ks_reduce(const DeepArgs& a, const Ctx& x, float* red, f32x4 acc, int kp) {
+  if (a.KS == 1) return acc;
+  if (kp > 0) lds4(red + ((x.w - a.RT) * 64 + x.lane) * 4, acc);
+  lds_barrier();
+  if (kp == 0)
+    for (int p = 1; p < a.KS; ++p) acc += lds4(red + ((x.w + (p - 1) * a.RT) * 64 + x.lane) * 4);
+  lds_barrier();
+  return acc;
+}
+
+// ---- forward of hidden layer l (column tile j): Z = A_{l-1} W_l[:, J] + b -> act, dropout
+//      -> A_l[:, J] (workspace, sc1) + A_l^T stripe (LDS) + G_l (registers) [+ G_{L-2} to
+//      the workspace for the tail]
+template <int L, int l>
+__device__ __forceinline__ void fwd_phase(const DeepArgs& a, float* smem, const Ctx& x0, int s, int valid, long long it,
+                                          f32x4 (&G)[L - 1]) {
+  const Ctx x = lanes(x0);
+  const DeepLayer ly = a.ly[l];
+  if (x.j >= ly.T) return;
+  const int J0 = 16 * x.j;
+  const int rt = x.w % a.RT, kp = x.w / a.RT;
+  const int Kx = ly.Kx, nkc = (Kx + 15) >> 4;
+  const int m = 16 * rt + x.c16;   // this lane's A row
+  f32x4 acc;
+  if constexpr (l == 0) {
+    constexpr int PF = 8;
+    const int nmine = ((nkc - kp + a.KS - 1) / a.KS + PF - 1) / PF * PF;
+    const int row = x.prow[(s & 1) * DP_ROWS + m];
+    const float* xr = a.X + (long long)x.r * a.sX + (long long)row * a.ldx;
+    auto loadA = [&](int k) { return *reinterpret_cast<const f32x4*>(xr + (k < Kx ? k : 0)); };
+    f32x4 ring[PF];
+    ring_issue<PF>(ring, loadA, kp, a.KS, x.g);
+    acc = ring_run<PF>(ring, loadA, smem + ly.l_w, Kx + 4, Kx, kp, a.KS, nmine, x.lane);
+  } else {
+    constexpr int PF = 16;
+    const int nmine = ((nkc - kp + a.KS - 1) / a.KS + PF - 1) / PF * PF;
+    const DeepLayer lp = a.ly[l - 1];
+    // the W^T rows J of the image first (the staging the MFMAs wait for), then the A ring
+    float* sb = smem + a.l_stage;
+    const int q4n = Kx >> 2, tot = 16 * q4n;
+    f32x4 stg[8];   // Kx <= 1024: <= 8 float4 per thread
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int e = x.tid + NTH * u, ec = e < tot ? e : tot - 1;
+      const int c = ec / q4n, q = ec - c * q4n;
+      stg[u] = ld4(x.rs, (J0 + c) * Kx + 4 * q, ly.o_wt);
+    }
+    auto loadA = [&](int k) { return ld4(x.rs, m * Kx + (k < Kx ? k : 0), lp.o_a); };
+    f32x4 ring[PF];
+    ring_issue<PF>(ring, loadA, kp, a.KS, x.g);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int e = x.tid + NTH * u;
+      if (e < tot) {
+        const int c = e / q4n, q = e - c * q4n;
+        lds4(sb + c * (Kx + 4) + 4 * q, stg[u]);
+      }
+    }
+    lds_barrier();
+    acc = ring_run<PF>(ring, loadA, sb, Kx + 4, Kx, kp, a.KS, nmine, x.lane);
+  }
+  acc = ks_reduce(a, x, smem + a.l_red, acc, kp);
+  if (kp != 0) return;
+  // epilogue: lane (column c16, group g) holds rows 16 rt + 4 g + q
+  const int col = J0 + x.c16;
+  const float bias = smem[ly.l_b + x.c16];
+  float z[4], o[4], gg[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) z[q] = acc[q] + bias;
+  act_fg_v<4>(ly.act, z, o, gg);
+  const float scale = ly.rate > 0.f ? 1.f / (1.f - ly.rate) : 1.f;
+  const uint32_t dbase = dropout_base(a.seed, x.r, l, it);
+  f32x4 av, gv;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int mm = 16 * rt + 4 * x.g + q;
+    const bool live = mm < valid && col < ly.N;
+    const float u = (live && ly.rate > 0.f) ? dropout_u1(dbase, mm, col) : 1.f;
+    const bool keep = live && u >= ly.rate;
+    av[q] = keep ? o[q] * scale : 0.f;
+    gv[q] = keep ? gg[q] * scale : 0.f;
+  }
+  G[l] = gv;
+  const int r0 = 16 * rt + 4 * x.g;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) st1(x.rs, (r0 + q) * ly.N16 + col, ly.o_a, av[q]);
+  lds4(smem + ly.l_at + x.c16 * (a.Bp + 4) + r0, av);
+  if constexpr (l == L - 2) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) st1(x.rs, (r0 + q) * ly.N16 + col, a.o_g, gv[q]);
+  }
+}
+
+// ---- tail (row tiles j, j + nw, ...): logits = A_{L-2} W_{L-1} + b, loss / metrics,
+//      dZ_{L-1} rows, dZ_{L-2} rows = (dZ_{L-1} W_{L-1}^T) * G_{L-2}
+template <int L, bool FAST>
+__device__ __forceinline__ void tail_phase(const DeepArgs& a, float* smem, const Ctx& x0, int s, int valid) {
+  const Ctx x = lanes(x0);
+  const DeepLayer la = a.ly[L - 2], lb = a.ly[L - 1];
+  const int C = lb.N, C16 = lb.N16, NCT = C16 >> 4;
+  const int Kx = lb.Kx, nkc = Kx >> 4;   // Kx = la.N16
+  float* red = smem + a.l_stage;         // [8 waves][2 col tiles][256]
+  float* sLg = red + NWV * 2 * 256;      // [16][36] logits -> dZ_{L-1}
+  float* sY = sLg + 16 * 36;             // [16][32]
+  int* sRow = reinterpret_cast<int*>(sY + 16 * 32);
+  const float inv_valid = 1.f / (float)valid;
+  for (int rt = x.j; rt < a.RT; rt += a.nw) {
+    const int m0 = 16 * rt;
+    const int m = m0 + x.c16;
+    // ---- logits: wave w takes the k-chunks w, w + 8, ... (<= 8 of them)
+    f32x4 av[8], bv0[8], bv1[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int t = x.w + NWV * u, tc = t < nkc ? t : nkc - 1;
+      const int k = 16 * tc + 4 * x.g;
+      av[u] = ld4(x.rs, m * Kx + k, la.o_a);
+      bv0[u] = ld4(x.rs, x.c16 * Kx + k, lb.o_wt);
+      bv1[u] = ld4(x.rs, (NCT > 1 ? 16 + x.c16 : x.c16) * Kx + k, lb.o_wt);
+    }
+    {   // targets of the tile's rows (one element per thread)
+      const int row = x.tid >> 5, c = x.tid & 31;
+      const int pr = m0 + row < valid ? x.prow[(s & 1) * DP_ROWS + m0 + row] : -1;
+      const float yv = (pr >= 0 && c < a.ldy) ? a.Y[(long long)x.r * a.sY + (long long)pr * a.ldy + c] : 0.f;
+      sY[row * 32 + c] = yv;
+      if (x.tid < 16) sRow[x.tid] = m0 + x.tid < valid ? 1 : -1;
+    }
+    f32x4 acc0 = z4(), acc1 = z4();
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      if (x.w + NWV * u < nkc) {
+        mma4(acc0, av[u], bv0[u]);
+        if (NCT > 1) mma4(acc1, av[u], bv1[u]);
+      }
+    }
+    lds4(red + ((x.w * 2 + 0) * 64 + x.lane) * 4, acc0);
+    lds4(red + ((x.w * 2 + 1) * 64 + x.lane) * 4, acc1);
+    __syncthreads();
+    if (x.tid < 2 * 256) {   // every thread: one logit (2 column tiles x 16 x 16)
+      const int ct = x.tid >> 8, e = x.tid & 255, ln = e >> 2, q = e & 3;
+      float sum = 0.f;
+#pragma unroll
+      for (int ww = 0; ww < NWV; ++ww) sum += red[((ww * 2 + ct) * 64 + ln) * 4 + q];
+      const int row = 4 * (ln >> 4) + q, col = 16 * ct + (ln & 15);
+      const float b = (col < C && lb.has_bias) ? ld1(x.rs, col, a.o_bl) : 0.f;
+      sLg[row * 36 + col] = col < C ? sum + b : 0.f;
+    }
+    __syncthreads();
+    // ---- loss / metrics; sLg becomes dL/dz * (1 / valid)
+    {
+      Prob q;
+      q.N = C;
+      q.act = lb.act;
+      q.loss = a.loss;
+      q.nmet = a.nmet;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) q.met[i] = a.met[i];
+      q.Y = a.Y;
+      q.pred = nullptr;
+      q.sPred = 0;
+      q.ldp = 0;
+      q.chunk = 0;
+      q.B = a.B;
+      float sums[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      if constexpr (FAST) {
+        if (x.w == 0) {
+          if (C <= 16) loss_tile_cce<4, 16, 36, 32>(q, x.r, m0, sLg, sY, sRow, true, inv_valid, sums);
+          else loss_tile_cce<8, 16, 36, 32>(q, x.r, m0, sLg, sY, sRow, true, inv_valid, sums);
+        }
+      } else if (x.tid < 256) {
+        loss_tile_lds<16, 36, 32>(q, x.r, m0, sLg, sY, sRow, true, inv_valid, sums);
+      }
+      if (a.acc && (FAST ? x.w == 0 : x.w < 4)) {
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+          if (i < 2 + a.nmet) {
+            const float sv = row_sum<64>(sums[i]);
+            if (x.lane == 0 && sv != 0.f) atomicAdd(a.acc + (long long)x.r * a.acc_stride + i, (double)sv);
+          }
+        }
+      }
+    }
+    __syncthreads();
+    // ---- dZ_{L-1} rows out; dZ_{L-2} rows = (dZ_{L-1} . W_{L-1}^T) * G_{L-2}: wave w takes
+    //      the 16-column tiles w, w + 8, ... of layer L-2 (<= 8 of them)
+    for (int e = x.tid; e < 16 * C16; e += NTH) {
+      const int row = e / C16, c = e - row * C16;
+      st1(x.rs, (m0 + row) * C16 + c, lb.o_dz, sLg[row * 36 + c]);
+    }
+    const int nit = Kx >> 4;
+    f32x4 wb0[8], wb1[8], gq[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int it = x.w + NWV * u, itc = it < nit ? it : nit - 1;
+      const int i = 16 * itc + x.c16;
+      wb0[u] = ld4(x.rs, i * C16 + 4 * x.g, lb.o_w);
+      wb1[u] = ld4(x.rs, i * C16 + (NCT > 1 ? 16 : 0) + 4 * x.g, lb.o_w);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) gq[u][q] = ld1(x.rs, (m0 + 4 * x.g + q) * Kx + i, a.o_g);
+    }
+    const f32x4 d0 = lds4(sLg + x.c16 * 36 + 4 * x.g);
+    const f32x4 d1 = lds4(sLg + x.c16 * 36 + 16 + 4 * x.g);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int it = x.w + NWV * u;
+      if (it < nit) {
+        f32x4 c = z4();
+        mma4(c, d0, wb0[u]);
+        if (NCT > 1) mma4(c, d1, wb1[u]);
+        const int i = 16 * it + x.c16;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) st1(x.rs, (m0 + 4 * x.g + q) * Kx + i, la.o_dz, c[q] * gq[u][q]);
+      }
+    }
+    __syncthreads();   // the LDS tiles are rewritten by the next row tile
+  }
+}
+
+// ---- weight gradient of the last layer, rows J (= column tile j of layer L-2) and (on
+//      workgroup 0) its bias; images of the updated rows for the next tail
+template <int L, bool SGD0>
+__device__ __forceinline__ void dw_last(const DeepArgs& a, float* smem, const Ctx& x0, const OptStep& os) {
+  const Ctx x = lanes(x0);
+  const DeepLayer la = a.ly[L - 2], lb = a.ly[L - 1];
+  const int C = lb.N, C16 = lb.N16, NCT = C16 >> 4, ldc = C16 + 4;
+  const bool rows = x.j < la.T, bias = x.j == 0 && lb.has_bias;
+  if (!rows && !bias) return;
+  float* sd = smem + a.l_stage;   // dZ_{L-1} [Bp][C16 + 4]
+  const int q4n = C16 >> 2, tot = a.Bp * q4n;
+  for (int e = x.tid; e < tot; e += NTH) {
+    const int row = e / q4n, q = e - row * q4n;
+    lds4(sd + row * ldc + 4 * q, ld4(x.rs, row * C16 + 4 * q, lb.o_dz));
+  }
+  __syncthreads();
+  if (rows && x.w < NCT) {
+    const int ct = x.w, I0 = 16 * x.j, ldat = a.Bp + 4;
+    const float* at = smem + la.l_at;
+    f32x4 acc = z4();
+    for (int rr = 0; rr < (a.Bp >> 4); ++rr) {
+      const f32x4 av = lds4(at + x.c16 * ldat + 16 * rr + 4 * x.g);
+      f32x4 b;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) b[e] = sd[(16 * rr + 4 * x.g + e) * ldc + 16 * ct + x.c16];
+      mma4(acc, av, b);
+    }
+    float* wr = smem + lb.l_w;
+    const int c = 16 * ct + x.c16;
+    f32x4 wv;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int ip = 4 * x.g + q;
+      float wt = wr[ip * ldc + c];
+      if (I0 + ip < lb.K && c < C) {
+        wt = upd<SGD0>(a, x, os, lb.p_off + (long long)(I0 + ip) * C + c, wt, acc[q]);
+        wr[ip * ldc + c] = wt;
+        st1(x.rs, (I0 + ip) * C16 + c, lb.o_w, wt);
+      }
+      wv[q] = wt;
+    }
+    st4(x.rs, c * lb.Kx + I0 + 4 * x.g, lb.o_wt, wv);
+  }
+  if (bias && x.tid >= 448 && x.tid - 448 < C) {   // the last wave: one unit per lane
+    const int c = x.tid - 448;
+    float db = 0.f;
+    for (int row = 0; row < a.Bp; ++row) db += sd[row * ldc + c];
+    float* bl = smem + lb.l_b;
+    const float b = upd<SGD0>(a, x, os, lb.p_off + (long long)lb.K * C + c, bl[c], db);
+    bl[c] = b;
+    st1(x.rs, c, a.o_bl, b);
+  }
+  __syncthreads();   // the staging is reused by the next phase
+}
+
+// ---- column sums of dZ_l[:, J] (the bias gradient of tile j of layer l) -> b_l[J]
+template <int l, bool SGD0>
+__device__ __forceinline__ void bias_tile(const DeepArgs& a, float* smem, const Ctx& x0, long long o_dz, int N16,
+                                          const OptStep& os) {
+  const Ctx x = lanes(x0);
+  const DeepLayer ly = a.ly[l];
+  if (x.j >= ly.T || !ly.has_bias) return;
+  const int J0 = 16 * x.j, c = x.tid & 15;
+  float sm = 0.f;
+#pragma unroll
+  for (int k = 0; k < DP_ROWS / 32; ++k) {
+    const int row = (x.tid >> 4) + 32 * k;
+    const float v = ld1(x.rs, (row < a.Bp ? row : 0) * N16 + J0 + c, o_dz);
+    sm += row < a.Bp ? v : 0.f;
+  }
+  float* red = smem + a.l_red;
+  red[x.tid] = sm;
+  __syncthreads();
+  if (x.tid < 16 && J0 + x.tid < ly.N) {
+    float db = 0.f;
+    for (int k = 0; k < NTH / 16; ++k) db += red[x.tid + 16 * k];
+    float* bt = smem + ly.l_b;
+    bt[x.tid] = upd<SGD0>(a, x, os, ly.p_off + (long long)ly.K * ly.N + J0 + x.tid, bt[x.tid], db);
+  }
+  __syncthreads();
+}
+
+// ---- backward of layer l >= 1 on row tile J of W_l: one pass over dZ_l in 64-column
+//      chunks (LDS): dA_{l-1}[:, J] += dZ_chunk W_l[J, chunk]^T (waves = row tiles) and
+//      DW_l[J, chunk] = A_{l-1}[:, J]^T dZ_chunk (waves = 4 column tiles x 2 row halves),
+//      update of the chunk's masters + their W^T image segment; finally dZ_{l-1}[:, J] =
+//      dA * G_{l-1} -> workspace (l >= 2) or the LDS dZ_0^T stripe (l = 1)
+template <int L, int l, bool SGD0>
+__device__ __forceinline__ void bw_phase(const DeepArgs& a, float* smem, const Ctx& x0, const OptStep& os,
+                                         const f32x4 (&G)[L - 1]) {
+  const Ctx x = lanes(x0);
+  const DeepLayer lp = a.ly[l - 1], ly = a.ly[l];
+  bias_tile<l, SGD0>(a, smem, x, ly.o_dz, ly.N16, os);
+  if (x.j >= lp.T) return;
+  const int I0 = 16 * x.j, Bp = a.Bp, ldat = Bp + 4, ldr = ly.N16 + 4;
+  const int rt = x.w % a.RT, kp = x.w / a.RT;
+  const int f = x.w & 3, hh = x.w >> 2;
+  float* wr = smem + ly.l_w;
+  const float* at = smem + lp.l_at;
+  float* sdz = smem + a.l_stage;
+  float* spart = sdz + DP_ROWS * LDZ;   // [4][64][4] DW partials of the second row half
+  const int nch = (ly.N16 + CW - 1) / CW;
+  // chunk staging: Bp x 64 floats = Bp * 16 float4, <= 4 per thread
+  f32x4 pre[4];
+  auto load_chunk = [&](int h) {
+    const int c0 = h * CW;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = x.tid + NTH * u, row = e >> 4, q = e & 15;
+      const int cc = c0 + 4 * q < ly.N16 ? c0 + 4 * q : c0;
+      pre[u] = ld4(x.rs, (row < Bp ? row : 0) * ly.N16 + cc, ly.o_dz);
+    }
+  };
+  load_chunk(0);
+  f32x4 accB0 = z4(), accB1 = z4();
+  for (int h = 0; h < nch; ++h) {
+    const int c0 = h * CW, cw = ly.N16 - c0 < CW ? ly.N16 - c0 : CW;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = x.tid + NTH * u, row = e >> 4, q = e & 15;
+      if (row < Bp) lds4(sdz + row * LDZ + 4 * q, 4 * q < cw ? pre[u] : z4());
+    }
+    if (h + 1 < nch) load_chunk(h + 1);
+    lds_barrier();
+    // dA_{l-1}[rows of tile rt][J] over the chunk's 16-column groups t (t % KS == kp)
+#pragma unroll
+    for (int t = 0; t < CW / 16; ++t) {
+      if (t % a.KS == kp && 16 * t < cw) {
+        const f32x4 av = lds4(sdz + (16 * rt + x.c16) * LDZ + 16 * t + 4 * x.g);
+        const f32x4 bv = lds4(wr + x.c16 * ldr + c0 + 16 * t + 4 * x.g);
+        if (t & 1) mma4(accB1, av, bv);
+        else mma4(accB0, av, bv);
+      }
+    }
+    // DW_l[J][chunk column tile f] over the row half hh
+    f32x4 accW = z4();
+    if (16 * f < cw) {
+      for (int rr = hh; rr < (Bp >> 4); rr += 2) {
+        const f32x4 av = lds4(at + x.c16 * ldat + 16 * rr + 4 * x.g);
+        f32x4 b;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) b[e] = sdz[(16 * rr + 4 * x.g + e) * LDZ + 16 * f + x.c16];
+        mma4(accW, av, b);
+      }
+    }
+    lds_barrier();   // every read of the chunk and of the old masters is done
+    if (hh == 1) lds4(spart + (f * 64 + x.lane) * 4, accW);
+    lds_barrier();
+    if (hh == 0 && 16 * f < cw) {
+      accW += lds4(spart + (f * 64 + x.lane) * 4);
+      const int col = c0 + 16 * f + x.c16;
+      f32x4 wv;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int ip = 4 * x.g + q;
+        float wt = wr[ip * ldr + col];
+        if (I0 + ip < ly.K && col < ly.N) {
+          wt = upd<SGD0>(a, x, os, ly.p_off + (long long)(I0 + ip) * ly.N + col, wt, accW[q]);
+          wr[ip * ldr + col] = wt;
+        }
+        wv[q] = wt;
+      }
+      st4(x.rs, col * ly.Kx + I0 + 4 * x.g, ly.o_wt, wv);
+    }
+  }
+  f32x4 acc = ks_reduce(a, x, smem + a.l_red, accB0 + accB1, kp);
+  if (kp != 0) return;
+  const int r0 = 16 * rt + 4 * x.g;
+  f32x4 dz;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) dz[q] = acc[q] * G[l - 1][q];
+  if constexpr (l >= 2) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) st1(x.rs, (r0 + q) * lp.N16 + I0 + x.c16, lp.o_dz, dz[q]);
+  } else {
+    lds4(smem + a.l_dz0 + x.c16 * ldat + r0, dz);
+  }
+}
+
+// ---- layer-0 weight gradient of tile j for the step whose dZ_0^T stripe is in LDS:
+//      DW_0[:, J] = X^T dZ_0[:, J] (waves = 64-feature groups; the X rows of that step,
+//      float4 along the features: MFMA e of lane group g takes batch row 16 rr + 4 g + e,
+//      output tile f the features i0 + 4 m + f), bias, in-place update of W_0^T
+template <int L, bool SGD0>
+__device__ __forceinline__ void dw0_phase(const DeepArgs& a, float* smem, const Ctx& x0, int sp, const OptStep& os) {
+  const Ctx x = lanes(x0);
+  const DeepLayer l0 = a.ly[0];
+  if (x.j >= l0.T) return;
+  const int J0 = 16 * x.j, Bp = a.Bp, ldz = Bp + 4, Kx = l0.Kx, ld0 = Kx + 4;
+  float* w0t = smem + l0.l_w;
+  const float* dz0 = smem + a.l_dz0;
+  if (x.tid < 16 && l0.has_bias && J0 + x.tid < l0.N) {
+    float db = 0.f;
+    for (int row = 0; row < Bp; ++row) db += dz0[x.tid * ldz + row];
+    float* bt = smem + l0.l_b;
+    bt[x.tid] = upd<SGD0>(a, x, os, l0.p_off + (long long)l0.K * l0.N + J0 + x.tid, bt[x.tid], db);
+  }
+  const int nfg = (Kx + 63) >> 6;
+  const int* prow = x.prow + (sp & 1) * DP_ROWS;
+  const float* Xr = a.X + (long long)x.r * a.sX;
+  for (int fg = x.w; fg < nfg; fg += NWV) {
+    const int i0 = 64 * fg, ic = i0 + 4 * x.c16;
+    const bool fin = ic < Kx;
+    f32x4 acc[4] = {z4(), z4(), z4(), z4()};
+    // two passes of 4 row groups: 16 float4 of X in flight per lane
+#pragma unroll
+    for (int half = 0; half < DP_ROWS / 64; ++half) {
+      f32x4 xv[4][4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int rr = 4 * half + q;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int rw = 16 * rr + 4 * x.g + e;
+          const int row = prow[rw < Bp ? rw : 0];
+          xv[q][e] = *reinterpret_cast<const f32x4*>(Xr + (long long)row * a.ldx + (fin ? ic : 0));
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int rr = 4 * half + q;
+        if (16 * rr < Bp) {
+          const f32x4 b = lds4(dz0 + x.c16 * ldz + 16 * rr + 4 * x.g);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const f32x4 xe = fin ? xv[q][e] : z4();
+#pragma unroll
+            for (int ff = 0; ff < 4; ++ff)
+              acc[ff] = __builtin_amdgcn_mfma_f32_16x16x4f32(xe[ff], b[e], acc[ff], 0, 0, 0);
+          }
+        }
+      }
+    }
+    // lane (column c16, group g): features i0 + 16 g + 4 q + f of column J0 + c16
+    const int col = J0 + x.c16;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int ib = i0 + 16 * x.g + 4 * q;
+      if (ib >= Kx) continue;
+      f32x4 wv = lds4(w0t + x.c16 * ld0 + ib);
+#pragma unroll
+      for (int ff = 0; ff < 4; ++ff) {
+        const int i = ib + ff;
+        if (i < l0.K && col < l0.N) wv[ff] = upd<SGD0>(a, x, os, l0.p_off + (long long)i * l0.N + col, wv[ff], acc[ff][q]);
+      }
+      lds4(w0t + x.c16 * ld0 + ib, wv);
+    }
+  }
+}
+
+// dZ_0[:, J] of a two-layer stack comes from the tail (workspace): -> the LDS dZ_0^T stripe
+__device__ __forceinline__ void load_dz0(const DeepArgs& a, float* smem, const Ctx& x0) {
+  const Ctx x = lanes(x0);
+  const DeepLayer l0 = a.ly[0];
+  if (x.j >= l0.T) return;
+  const int ldz = a.Bp + 4, J0 = 16 * x.j;
+  float* dz0 = smem + a.l_dz0;
+  for (int e = x.tid; e < a.Bp * 4; e += NTH) {
+    const int row = e >> 2, q = e & 3;
+    const f32x4 v = ld4(x.rs, row * l0.N16 + J0 + 4 * q, l0.o_dz);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) dz0[(4 * q + k) * ldz + row] = v[k];
+  }
+}
+
+
+// the forward phases of layers l .. L-2 (compile-time chain: every layer index is static)
+template <int L, int l>
+__device__ __forceinline__ bool fwd_chain(const DeepArgs& a, float* smem, const Ctx& x, int s, int valid, long long it,
+                                          unsigned base, f32x4 (&G)[L - 1]) {
+  if constexpr (l <= L - 2) {
+    if (!wait_phase(a, x.r, base + l)) return false;
+    dstamp(a, s, 2 * l + 1);
+    fwd_phase<L, l>(a, smem, x, s, valid, it, G);
+    publish(a, x.r, x.j, base + l + 1);
+    dstamp(a, s, 2 * l + 2);
+    return fwd_chain<L, l + 1>(a, smem, x, s, valid, it, base, G);
+  }
+  return true;
+}
+
+// the backward phases of layers l .. 1 (BW_{L-2} also runs the last layer's update)
+template <int L, int l, bool SGD0>
+__device__ __forceinline__ bool bw_chain(const DeepArgs& a, float* smem, const Ctx& x, int s, const OptStep& os,
+                                         unsigned base, const f32x4 (&G)[L - 1]) {
+  if constexpr (l >= 1) {
+    const unsigned p = (unsigned)(L + (L - 2 - l));
+    if (!wait_phase(a, x.r, base + p)) return false;
+    dstamp(a, s, 11 + 2 * (L - 2 - l));
+    if constexpr (l == L - 2) dw_last<L, SGD0>(a, smem, x, os);
+    bw_phase<L, l, SGD0>(a, smem, x, os, G);
+    publish(a, x.r, x.j, base + p + 1);
+    dstamp(a, s, 12 + 2 * (L - 2 - l));
+    return bw_chain<L, l - 1, SGD0>(a, smem, x, s, os, base, G);
+  }
+  return true;
+}
+
+}  // namespace
+
+template <int L, bool FAST, bool SGD0>
+__global__ __launch_bounds__(512) void mlp_deep_kernel(DeepArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  if (__hip_atomic_load((gu32*)(a.err), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) return;
+  Ctx x;
+  x.r = blockIdx.x % a.R;
+  x.j = blockIdx.x / a.R;
+  x.tid = threadIdx.x;
+  x.lane = threadIdx.x & 63;
+  x.w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  x.g = x.lane >> 4;
+  x.c16 = x.lane & 15;
+  x.rs = ws_rsrc(a.ws + (long long)x.r * a.ws_stride);
+  x.P = a.P + (long long)x.r * a.sP;
+  x.S = a.S ? a.S + (long long)x.r * a.sS : nullptr;
+  x.prow = reinterpret_cast<int*>(smem + a.lds_floats - 2 * DP_ROWS);
+  if (x.tid == 0)
+    __hip_atomic_store((gu32*)(dflag(a, x.r, 0) + x.j), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+
+  // ---- prologue: the owned masters from P into LDS (zero past the true widths)
+  for (int e = x.tid; e < a.lds_floats; e += NTH) smem[e] = 0.f;
+  __syncthreads();
+  const int Bp = a.Bp;
+  {
+    const DeepLayer l0 = a.ly[0];
+    if (x.j < l0.T) {
+      const int J0 = 16 * x.j, ld0 = l0.Kx + 4;
+      for (int e = x.tid; e < 16 * l0.K; e += NTH) {
+        const int k = e >> 4, c = e & 15;
+        if (J0 + c < l0.N) smem[l0.l_w + c * ld0 + k] = x.P[l0.p_off + (long long)k * l0.N + J0 + c];
+      }
+      if (x.tid < 16 && l0.has_bias && J0 + x.tid < l0.N)
+        smem[l0.l_b + x.tid] = x.P[l0.p_off + (long long)l0.K * l0.N + J0 + x.tid];
+    }
+  }
+#pragma unroll
+  for (int l = 1; l < L; ++l) {
+    const DeepLayer ly = a.ly[l], lp = a.ly[l - 1];
+    const int ldr = ly.N16 + 4;
+    if (x.j < lp.T) {   // rows J of W_l
+      const int I0 = 16 * x.j;
+      for (int e = x.tid; e < 16 * ly.N; e += NTH) {
+        const int ip = e / ly.N, c = e - ip * ly.N;
+        if (I0 + ip < ly.K) smem[ly.l_w + ip * ldr + c] = x.P[ly.p_off + (long long)(I0 + ip) * ly.N + c];
+      }
+    }
+    if (l < L - 1) {
+      if (x.j < ly.T && x.tid < 16 && ly.has_bias && 16 * x.j + x.tid < ly.N)
+        smem[ly.l_b + x.tid] = x.P[ly.p_off + (long long)ly.K * ly.N + 16 * x.j + x.tid];
+    } else if (x.j == 0 && ly.has_bias && x.tid < ly.N) {
+      smem[ly.l_b + x.tid] = x.P[ly.p_off + (long long)ly.K * ly.N + x.tid];
+    }
+  }
+  __syncthreads();
+  // the images the other workgroups read: W_l^T segments [c][J] (l >= 1), the last layer's
+  // row-major rows and (workgroup 0) its bias
+#pragma unroll
+  for (int l = 1; l < L; ++l) {
+    const DeepLayer ly = a.ly[l], lp = a.ly[l - 1];
+    if (x.j >= lp.T) continue;
+    const int ldr = ly.N16 + 4, I0 = 16 * x.j;
+    for (int e = x.tid; e < ly.N16 * 4; e += NTH) {
+      const int c = e >> 2, q = e & 3;
+      f32x4 v;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v[k] = smem[ly.l_w + (4 * q + k) * ldr + c];
+      st4(x.rs, c * ly.Kx + I0 + 4 * q, ly.o_wt, v);
+    }
+    if (l == L - 1) {
+      for (int e = x.tid; e < 16 * ly.N16; e += NTH) {
+        const int ip = e / ly.N16, c = e - ip * ly.N16;
+        st1(x.rs, (I0 + ip) * ly.N16 + c, ly.o_w, smem[ly.l_w + ip * ldr + c]);
+      }
+    }
+  }
+  if (x.j == 0 && x.tid < a.ly[L - 1].N16) st1(x.rs, x.tid, a.o_bl, smem[a.ly[L - 1].l_b + x.tid]);
+  __syncthreads();
+  if (!wait_grid(a)) return;
+
+  constexpr int NPH = 2 * L - 2;
+  const long long s0 = ld_inv(a.ctr);
+  const int ntr = ld_inv(a.ntrain + x.r);
+  f32x4 G[L - 1];
+#pragma unroll
+  for (int l = 0; l < L - 1; ++l) G[l] = z4();
+  int last = -1;
+  OptStep lastos = opt_step(a.op, 0);
+  for (int s = 0; s < a.nsteps; ++s) {
+    const long long cnt = (long long)ntr - (s0 + s) * a.B;
+    const int valid = (int)(cnt < 0 ? 0 : (cnt > a.B ? a.B : cnt));
+    if (valid == 0) break;   // uniform over the replica: no batch left in this epoch
+    const long long it = iter_at(a.ctr, a.ntrain, a.B, x.r, s0, s);
+    const OptStep os = opt_step(a.op, it);
+    const unsigned base = (unsigned)s * NPH;
+    dstamp(a, s, 0);
+    // ---- phase 0: the previous step's layer-0 (and, L = 2, last-layer) update, forward 0
+    {
+      const Ctx y = lanes(x);
+      if (y.tid < Bp) {
+        const int* pr = a.perm + (long long)x.r * a.sPerm + (s0 + s) * a.B;
+        x.prow[(s & 1) * DP_ROWS + y.tid] = y.tid < valid ? pr[y.tid] : 0;
+      }
+    }
+    if (last >= 0) {
+      if constexpr (L == 2) {
+        if (!wait_phase(a, x.r, base)) return;
+        dw_last<L, SGD0>(a, smem, x, lastos);
+        load_dz0(a, smem, x);
+      }
+      __syncthreads();
+      dw0_phase<L, SGD0>(a, smem, x, last, lastos);
+    }
+    __syncthreads();
+    dstamp(a, s, 1);
+    fwd_phase<L, 0>(a, smem, x, s, valid, it, G);
+    publish(a, x.r, x.j, base + 1);
+    dstamp(a, s, 2);
+    if (!fwd_chain<L, 1>(a, smem, x, s, valid, it, base, G)) return;
+    if (!wait_phase(a, x.r, base + L - 1)) return;
+    dstamp(a, s, 9);
+    tail_phase<L, FAST>(a, smem, x, s, valid);
+    publish(a, x.r, x.j, base + L);
+    dstamp(a, s, 10);
+    if (!bw_chain<L, L - 2, SGD0>(a, smem, x, s, os, base, G)) return;
+    last = s;
+    lastos = os;
+  }
+  // the pending layer-0 update of the last step that ran
+  if (last >= 0) {
+    if constexpr (L == 2) {
+      if (!wait_phase(a, x.r, (unsigned)(last + 1) * NPH)) return;
+      dw_last<L, SGD0>(a, smem, x, lastos);
+      load_dz0(a, smem, x);
+    }
+    __syncthreads();
+    dw0_phase<L, SGD0>(a, smem, x, last, lastos);
+  }
+  __syncthreads();
+  // ---- epilogue: the owned masters back to P
+  {
+    const DeepLayer l0 = a.ly[0];
+    if (x.j < l0.T) {
+      const int J0 = 16 * x.j, ld0 = l0.Kx + 4;
+      for (int e = x.tid; e < 16 * l0.K; e += NTH) {
+        const int k = e >> 4, c = e & 15;
+        if (J0 + c < l0.N) x.P[l0.p_off + (long long)k * l0.N + J0 + c] = smem[l0.l_w + c * ld0 + k];
+      }
+      if (x.tid < 16 && l0.has_bias && J0 + x.tid < l0.N)
+        x.P[l0.p_off + (long long)l0.K * l0.N + J0 + x.tid] = smem[l0.l_b + x.tid];
+    }
+  }
+#pragma unroll
+  for (int l = 1; l < L; ++l) {
+    const DeepLayer ly = a.ly[l], lp = a.ly[l - 1];
+    const int ldr = ly.N16 + 4;
+    if (x.j < lp.T) {
+      const int I0 = 16 * x.j;
+      for (int e = x.tid; e < 16 * ly.N; e += NTH) {
+        const int ip = e / ly.N, c = e - ip * ly.N;
+        if (I0 + ip < ly.K) x.P[ly.p_off + (long long)(I0 + ip) * ly.N + c] = smem[ly.l_w + ip * ldr + c];
+      }
+    }
+    if (l < L - 1) {
+      if (x.j < ly.T && x.tid < 16 && ly.has_bias && 16 * x.j + x.tid < ly.N)
+        x.P[ly.p_off + (long long)ly.K * ly.N + 16 * x.j + x.tid] = smem[ly.l_b + x.tid];
+    } else if (x.j == 0 && ly.has_bias && x.tid < ly.N) {
+      x.P[ly.p_off + (long long)ly.K * ly.N + x.tid] = smem[ly.l_b + x.tid];
+    }
+  }
+}
+
+namespace {
+// dynamic LDS above the default limit: raised once per instantiation (to the largest the
+// device allows, so later launches with other layouts need no call)
+template <int L, bool F, bool SG>
+hipError_t deep_launch_one(const DeepArgs* a, hipStream_t s) {
+  static const bool done = [] {
+    int dev = 0, mx = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&mx, hipDeviceAttributeMaxSharedMemoryPerBlock, dev);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&mlp_deep_kernel<L, F, SG>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, mx);
+    return true;
+  }();
+  (void)done;
+  hipLaunchKernelGGL((mlp_deep_kernel<L, F, SG>), dim3(a->R * a->nw), dim3(NTH), sizeof(float) * (size_t)a->lds_floats,
+                     s, *a);
+  return hipGetLastError();
+}
+
+template <int L>
+hipError_t deep_launch(const DeepArgs* a, bool fast, bool sgd0, hipStream_t s) {
+  if (fast && sgd0) return deep_launch_one<L, true, true>(a, s);
+  if (fast) return deep_launch_one<L, true, false>(a, s);
+  if (sgd0) return deep_launch_one<L, false, true>(a, s);
+  return deep_launch_one<L, false, false>(a, s);
+}
+}  // namespace
+
+}  // namespace ea
+

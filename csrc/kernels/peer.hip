@@ -247,7 +247,13 @@ __global__ __launch_bounds__(256) void ps_gather_kernel(PsArgs a, float* __restr
   }
   unsigned* began = ps_ctr(a, owner, c, 0);
   unsigned* ended = ps_ctr(a, owner, c, 1);
-  __shared__ unsigned snap;
+  // pushes made INSIDE a persistent launch (persist.hip ps_push_begin / ps_push_end) bracket
+  // their slice with per-slice began / ended words in rank 0's flag area instead of these
+  // chunk counters: the consistent pull also waits until no such writer is inside any
+  // slice, and retries if one began during the copy (thread t watches slice t)
+  const unsigned* sb = reinterpret_cast<const unsigned*>(a.base[0] + PEER_FLAG_OFF) + threadIdx.x * 16;
+  const unsigned* se = sb + PEER_MAX_BLOCKS * 16;
+  __shared__ unsigned snap, ssum;
   __shared__ int state;  // 0 retry, 1 done, 2 give up
   const unsigned long long t0 = wall_clock64();
   for (;;) {
@@ -259,15 +265,30 @@ __global__ __launch_bounds__(256) void ps_gather_kernel(PsArgs a, float* __restr
         if (ps_timed_out(a, t0)) { snap = b; break; }
         __builtin_amdgcn_s_sleep(1);
       }
+      ssum = 0u;
     }
+    unsigned mb = 0u;
+    for (;;) {   // every slice quiet (one wait for the whole workgroup)
+      const unsigned e = load_flag(se);
+      mb = load_flag(sb);
+      if (__syncthreads_and(mb == e)) break;
+      if (__syncthreads_or(ps_timed_out(a, t0))) break;   // one decision for the workgroup
+      __builtin_amdgcn_s_sleep(1);
+    }
+    atomicAdd(&ssum, mb);
     __syncthreads();
+    const unsigned s0 = ssum;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
     copy_all();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // the copy's loads complete before the re-check
     __syncthreads();
+    if (threadIdx.x == 0) ssum = 0u;
+    __syncthreads();
+    atomicAdd(&ssum, load_flag(sb));
+    __syncthreads();
     if (threadIdx.x == 0) {
       const unsigned b2 = load_flag(began);
-      state = b2 == snap ? 1 : (ps_timed_out(a, t0) ? 2 : 0);
+      state = (b2 == snap && ssum == s0) ? 1 : (ps_timed_out(a, t0) ? 2 : 0);
     }
     __syncthreads();
     if (state != 0) return;

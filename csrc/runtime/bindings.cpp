@@ -82,6 +82,7 @@ static ExecCfg parse_cfg(const py::dict& d) {
   c.persist_cus = get<int>(d, "persist_cus", 0);
   c.persist_v2 = get<int>(d, "persist_v2", -1);
   c.persist_sync = get<int>(d, "persist_sync", 0);
+  c.deep = get<int>(d, "deep", -1);
   for (auto item : d["layers"].cast<py::list>()) {
     py::dict l = item.cast<py::dict>();
     LayerCfg lc;
@@ -198,6 +199,8 @@ PYBIND11_MODULE(_C, m) {
       .def("persistent", &Executor::persistent)
       .def("persist_geometry", &Executor::persist_geometry)
       .def("persist_variant", &Executor::persist_variant)
+      .def("deep_geometry", &Executor::deep_geometry)
+      .def("set_seed", &Executor::set_seed)
       .def("persist_images", &Executor::persist_images)
       .def("set_rank_exchange", [](Executor& e, std::vector<uintptr_t> bases, int world, int rank, unsigned tag0,
                                    double timeout_s) {

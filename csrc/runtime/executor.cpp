@@ -20,6 +20,7 @@ extern "C" hipError_t ea_persist_post(unsigned* flags, int nflags, long long* ct
                                       const unsigned* err, hipStream_t s);
 extern "C" hipError_t ea_persist(const ea::PersistArgs* a, hipStream_t s);
 extern "C" int ea_persist_lds_bytes();
+extern "C" hipError_t ea_deep(const ea::DeepArgs* a, hipStream_t s);
 
 namespace ea {
 
@@ -40,8 +41,11 @@ Executor::Executor(const ExecCfg& cfg) : c_(cfg) {
   rc_.on = c_.rowchain != 0 && build_rowchain();
   if (c_.rowchain == 1 && !rc_) throw std::invalid_argument("row-chain plan requested but the model is not eligible");
   tl_.on = !rc_ && c_.rowchain != 0 && c_.tail != 0 && build_tail();
-  pm_.on = c_.persist != 0 && build_persist();
-  if (c_.persist == 1 && !pm_.on) throw std::invalid_argument("persistent plan requested but the model is not eligible");
+  // deep = 2 (tests, A/B): the layer pipeline even where persist.hip's roles are eligible
+  dp_.on = c_.persist != 0 && c_.deep == 2 && build_deep();
+  pm_.on = !dp_.on && c_.persist != 0 && build_persist();
+  if (!dp_.on && !pm_.on) dp_.on = c_.persist != 0 && c_.deep != 0 && build_deep();
+  if (c_.persist == 1 && !persistent()) throw std::invalid_argument("persistent plan requested but the model is not eligible");
 }
 
 Executor::~Executor() {
@@ -52,6 +56,8 @@ Executor::~Executor() {
   if (d_pws_) (void)hipFree(d_pws_);
   if (d_pflags_) (void)hipFree(d_pflags_);
   if (d_perr_) (void)hipFree(d_perr_);
+  if (d_dws_) (void)hipFree(d_dws_);
+  if (d_dflags_) (void)hipFree(d_dflags_);
 }
 
 // Persistent plan (persist.hip): 3 Dense layers, hidden widths 64 or 128, a last layer
@@ -82,8 +88,10 @@ bool Executor::build_persist() {
   if (cap < 1) return false;
   // V2 (persist.hip l0_role_v2 / dw_role_v2): plain SGD, ReLU hidden layers, independent
   // replicas -- the step's critical path runs through the chain workgroups only
+  // (the chain's Gram correction carries layer 0's bias update -- its ones column -- so a
+  // bias-free first layer keeps the V1 roles)
   const bool v2 = c_.persist_v2 != 0 && !c_.persist_sync && c_.op.opt == OPT_SGD && c_.op.mom == 0.f &&
-                  l0.act == ACT_RELU && l1.act == ACT_RELU;
+                  l0.act == ACT_RELU && l1.act == ACT_RELU && l0.has_bias;
   const int nd = v2 ? cdiv(l1.N / 16, PM_NTU) : 0;
   // bf16 (mixed_bfloat16): the V2 roles only (bf16-rounded operands, bf16 shard and images)
   if (c_.bf16 && !v2) return false;
@@ -198,7 +206,117 @@ bool Executor::build_persist() {
   return true;
 }
 
+// Persistent layer pipeline (deep.hip): 2..DP_MAXL Dense layers, hidden widths <= 1024, a
+// last layer of <= DP_MAXC units, B <= DP_ROWS, fp32, independent replicas (fit
+// granularity).  nw = the widest hidden layer's 16-column tiles workgroups per replica,
+// at most one workgroup per CU (every one resident: they wait for each other).
+bool Executor::build_deep() {
+  const int L = (int)c_.layers.size();
+  if (L < 2 || L > DP_MAXL || c_.bf16 || c_.persist_sync) return false;
+  if (c_.B < 1 || c_.B > DP_ROWS || c_.ldy > 32 || (c_.ldx % 8) != 0) return false;
+  const LayerCfg& lastc = c_.layers[L - 1];
+  if (lastc.N > DP_MAXC) return false;
+  auto r16 = [](int n) { return (n + 15) / 16 * 16; };
+  int nw = 0;
+  for (int l = 0; l < L - 1; ++l) {
+    const int n16 = r16(c_.layers[l].N);
+    if (n16 > 1024) return false;
+    nw = std::max(nw, n16 / 16);
+    if (l > 0 && c_.layers[l].K != c_.layers[l - 1].N) return false;
+  }
+  if (lastc.K != c_.layers[L - 2].N || c_.layers[0].K > c_.ldx) return false;
+  if (nw > DP_MAXWG) return false;
+  int dev = 0, ncu = 0, lds_max = 0;
+  check(hipGetDevice(&dev), "hipGetDevice");
+  check(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev), "hipDeviceGetAttribute");
+  check(hipDeviceGetAttribute(&lds_max, hipDeviceAttributeMaxSharedMemoryPerBlock, dev), "hipDeviceGetAttribute");
+  if (const char* e = std::getenv("ELEPHAS_AMD_PERSIST_OVERSUBSCRIBE")) ncu = std::max(ncu, std::atoi(e));
+  if (c_.persist_cus > 0) ncu = std::min(ncu, c_.persist_cus);
+  if (c_.R * nw > ncu) return false;
+  DeepArgs& a = dp_.args;
+  std::memset(&a, 0, sizeof(a));
+  a.R = c_.R; a.B = c_.B; a.L = L; a.nw = nw;
+  int rt = 1;
+  while (rt * 16 < c_.B) rt *= 2;
+  a.RT = rt; a.KS = 8 / rt; a.Bp = 16 * rt;
+  // layers, LDS layout (floats; every region a multiple of 4), workspace layout (floats,
+  // 64-float aligned regions)
+  int lds = 0;
+  long long ws = 0;
+  auto take = [&](long long n) { const long long o = ws; ws += (n + 63) / 64 * 64; return o; };
+  for (int l = 0; l < L; ++l) {
+    const LayerCfg& ly = c_.layers[l];
+    DeepLayer& d = a.ly[l];
+    d.K = ly.K; d.N = ly.N; d.N16 = r16(ly.N); d.T = d.N16 / 16;
+    d.Kx = l == 0 ? (int)c_.ldx : a.ly[l - 1].N16;
+    d.act = ly.act; d.has_bias = ly.has_bias; d.rate = ly.rate; d.p_off = ly.p_off;
+  }
+  a.ly[0].l_w = lds; lds += 16 * (a.ly[0].Kx + 4);
+  for (int l = 1; l < L; ++l) { a.ly[l].l_w = lds; lds += 16 * (a.ly[l].N16 + 4); }
+  for (int l = 0; l < L - 1; ++l) { a.ly[l].l_b = lds; lds += 16; }
+  a.ly[L - 1].l_b = lds; lds += 32;
+  for (int l = 0; l < L - 1; ++l) { a.ly[l].l_at = lds; lds += 16 * (a.Bp + 4); }
+  a.l_dz0 = lds; lds += 16 * (a.Bp + 4);
+  a.l_red = lds; lds += 2048;
+  int stage = DP_ROWS * (DP_CW + 4) + 1024;                          // backward dZ chunk + DW partials
+  stage = std::max(stage, 8 * 2 * 256 + 16 * 36 + 16 * 32 + 16);     // tail tiles
+  stage = std::max(stage, a.Bp * (a.ly[L - 1].N16 + 4));             // dZ_{L-1} of the last layer's DW
+  for (int l = 1; l < L - 1; ++l) stage = std::max(stage, 16 * (a.ly[l].Kx + 4));   // W^T stripes
+  a.l_stage = lds; lds += stage;
+  lds += 2 * DP_ROWS;                                                 // batch rows of two steps (ints, last)
+  a.lds_floats = lds;
+  if ((long long)lds * 4 + 1024 > lds_max) return false;   // + the kernel's static LDS
+  for (int l = 0; l < L - 1; ++l) {
+    a.ly[l].o_a = take((long long)a.Bp * a.ly[l].N16);
+    a.ly[l].o_dz = take((long long)a.Bp * a.ly[l].N16);
+  }
+  a.ly[L - 1].o_dz = take((long long)a.Bp * a.ly[L - 1].N16);
+  a.o_g = take((long long)a.Bp * a.ly[L - 2].N16);
+  for (int l = 1; l < L; ++l) a.ly[l].o_wt = take((long long)a.ly[l].N16 * a.ly[l].Kx);
+  a.ly[L - 1].o_w = take((long long)a.ly[L - 1].Kx * a.ly[L - 1].N16);
+  a.o_bl = take(a.ly[L - 1].N16);
+  a.X = reinterpret_cast<const float*>(c_.X); a.sX = c_.sX; a.ldx = c_.ldx;
+  a.Y = reinterpret_cast<const float*>(c_.Y); a.sY = c_.sY; a.ldy = c_.ldy;
+  a.perm = reinterpret_cast<const int*>(c_.perm); a.sPerm = c_.sPerm;
+  a.ntrain = reinterpret_cast<const int*>(c_.ntrain);
+  a.P = reinterpret_cast<float*>(c_.P); a.sP = c_.sP;
+  const bool sgd0 = c_.op.opt == OPT_SGD && c_.op.mom == 0.f;
+  a.S = sgd0 ? nullptr : reinterpret_cast<float*>(c_.S); a.sS = c_.sS;
+  a.op = c_.op;
+  a.loss = c_.loss; a.nmet = c_.nmet;
+  for (int i = 0; i < 4; ++i) a.met[i] = c_.met[i];
+  a.acc = reinterpret_cast<double*>(c_.acc); a.acc_stride = c_.acc_stride;
+  a.ctr = reinterpret_cast<long long*>(c_.ctr);
+  a.seed = c_.seed;
+  a.ws_stride = ws;
+  const size_t ws_bytes = sizeof(float) * (size_t)ws * c_.R;
+  check(hipMalloc(&d_dws_, ws_bytes), "hipMalloc(layer pipeline workspace)");
+  check(hipMemset(d_dws_, 0, ws_bytes), "hipMemset(layer pipeline workspace)");
+  dp_.flag_bytes = sizeof(unsigned) * (size_t)c_.R * 2 * DP_MAXWG;
+  check(hipMalloc(&d_dflags_, dp_.flag_bytes), "hipMalloc(layer pipeline flags)");
+  check(hipMemset(d_dflags_, 0, dp_.flag_bytes), "hipMemset(layer pipeline flags)");
+  if (!d_perr_) {
+    check(hipMalloc(&d_perr_, 256), "hipMalloc(persistent error word)");
+    check(hipMemset(d_perr_, 0, 256), "hipMemset(persistent error word)");
+  }
+  a.ws = d_dws_;
+  a.flags = d_dflags_;
+  a.err = d_perr_;
+  a.timeout = std::max<long long>(1, c_.persist_timeout_ms) * 100000LL;   // s_memrealtime: 100 MHz
+  // the zeroed flags and error word are in memory before the first launch (a caller's
+  // non-blocking stream does not order after hipMemset's)
+  check(hipDeviceSynchronize(), "hipDeviceSynchronize(layer pipeline setup)");
+  return true;
+}
+
+std::vector<int> Executor::deep_geometry() const {
+  if (!dp_.on) return {};
+  const DeepArgs& a = dp_.args;
+  return {a.nw, a.R * a.nw, a.RT, a.KS, a.lds_floats * 4};
+}
+
 std::vector<int> Executor::persist_geometry() const {
+  if (dp_.on) return {0, 0, 0, 0, 0, dp_.args.nw, dp_.args.R * dp_.args.nw};
   if (!pm_.on) return {};
   const PersistArgs& a = pm_.args;
   return {a.nk0, a.nc0, a.kc0, a.cw, a.nch, a.wgs, a.R * a.wgs};
@@ -229,6 +347,7 @@ bool Executor::set_rank_exchange(const std::vector<char*>& bases, int world, int
 }
 
 std::vector<int> Executor::persist_variant() const {
+  if (dp_.on) return {3, 0, 0};
   if (!pm_.on) return {};
   return {pm_.args.v2 ? 2 : 1, pm_.args.nd, pm_.args.sync};
 }
@@ -248,6 +367,15 @@ void Executor::persist_clear_error() {
 }
 
 void Executor::run_chunk(hipStream_t s, int nsteps) const {
+  if (dp_.on) {   // one persistent launch + the post node (flag clear, counter advance)
+    DeepArgs a = dp_.args;
+    a.nsteps = nsteps;
+    check(ea_deep(&a, s), "persistent layer pipeline kernel");
+    check(ea_persist_post(d_dflags_, (int)(dp_.flag_bytes / sizeof(unsigned)), reinterpret_cast<long long*>(c_.ctr),
+                          reinterpret_cast<const int*>(c_.ntrain), c_.R, c_.B, nsteps, d_perr_, s),
+          "persistent chunk post");
+    return;
+  }
   if (pm_.on) {
     // the flags are zero at launch (setup, then the post node of every chunk: tags
     // restart at 1), and one post node clears them again and advances the counters
@@ -489,6 +617,21 @@ void Executor::run_step(hipStream_t s, int step_off) const {
     run(fwd_, s, step_off);
     run(bwd_, s, step_off);
   }
+}
+
+// A new dropout seed for every launch of every plan (a refit that reuses this executor:
+// the reference starts every fit with a fresh worker model).  Captured graphs hold the
+// old arguments and are dropped; buffers, flags and plans stay (no allocation, no sync).
+void Executor::set_seed(unsigned long long seed) {
+  c_.seed = seed;
+  for (auto* v : {&fwd_, &bwd_, &tl_.pre, &tl_.post})
+    for (auto& L : *v) L.ga.seed = seed;
+  rc_.ta_fwd.seed = rc_.ta_dw.seed = rc_.ta_grad.seed = seed;
+  rc_.rc.seed = seed;
+  tl_.rc.seed = seed;
+  pm_.args.seed = seed;
+  dp_.args.seed = seed;
+  destroy_graphs();
 }
 
 void Executor::destroy_graphs() {
@@ -944,6 +1087,7 @@ void Executor::set_stamps(uintptr_t buf) {
   rc_.ta_fwd.stamps = rc_.ta_dw.stamps = rc_.ta_grad.stamps = p;
   rc_.rc.stamps = p;
   pm_.args.stamps = p;
+  dp_.args.stamps = p;
   for (auto* v : {&tl_.pre, &tl_.post})
     for (auto& L : *v) L.ga.stamps = p;
   tl_.rc.stamps = p;
@@ -992,13 +1136,13 @@ std::vector<int> Executor::launch_cfgs() const {
 
 void Executor::train_step(hipStream_t s) {
   run_chunk(s, 1);
-  if (!pm_.on) advance(1, s);   // the persistent chunk's post node advanced the counters
+  if (!persistent()) advance(1, s);   // the persistent chunk's post node advanced the counters
 }
 
 void Executor::train_chunk(int nsteps, hipStream_t s) {
   if (nsteps <= 0) return;
   run_chunk(s, nsteps);
-  if (!pm_.on) advance(nsteps, s);
+  if (!persistent()) advance(nsteps, s);
 }
 
 void Executor::forward_backward(hipStream_t s) {
@@ -1097,7 +1241,7 @@ int Executor::capture(int nsteps, int mode, hipStream_t s) {
       // one chunk: steps at offsets 0..nsteps-1 from the counter base, then one advance
       // (the persistent plan's post node includes it)
       run_chunk(s, nsteps);
-      if (!pm_.on) advance(nsteps, s);
+      if (!persistent()) advance(nsteps, s);
     } else {
       for (int i = 0; i < nsteps; ++i) {
         if (mode == 1) forward_backward(s);

@@ -17,6 +17,9 @@
 //   persistent plan (3-layer MLPs with 64/128-wide hidden layers, fp32;
 //                   csrc/kernels/persist.hip): a whole chunk of steps in ONE launch
 //                   (+ a 1-block post kernel: flag clear and counter advance)
+//   persistent layer pipeline (2..5 Dense layers, hidden widths <= 1024, B <= 128, fp32,
+//                   e.g. Otto 93-512-512-512-9; csrc/kernels/deep.hip): the same, with
+//                   the replica's workgroups owning column / row tiles of every layer
 //
 // The step reads its batch index, dropout counter and optimizer iteration from
 // device counters, so one captured hipGraph of a step is replayed for every
@@ -77,6 +80,8 @@ struct ExecCfg {
   int persist_cus = 0;  // > 0: CUs the persistent grid may occupy (several executors side by side)
   int persist_v2 = -1;  // persistent V2 roles when eligible (plain SGD, ReLU, independent replicas); 0 off
   int persist_sync = 0;  // persistent plan as per-step synchronous DP of the R replicas (in-launch exchange)
+  int deep = -1;        // persistent layer pipeline (deep.hip) where persist.hip is not eligible: -1 when eligible, 0 off,
+                        // 2 preferred over persist.hip (tests, A/B)
   int no_reorder = 0;   // A/B: keep a DW + DX launch's problems in declaration order
   int dual = 1;         // a layer's DW and DX on different tiles in one launch (0: two launches)
 };
@@ -114,6 +119,7 @@ class Executor {
   int capture(int nsteps, int mode, hipStream_t s);
   void replay(int graph_id, hipStream_t s);
   void destroy_graphs();
+  void set_seed(unsigned long long seed);   // new dropout seed everywhere (drops captured graphs)
 
   // launches per step (a captured chunk adds one 1-block counter advance)
   int launches_per_step() const {
@@ -123,12 +129,14 @@ class Executor {
   }
   bool rowchain() const { return rc_.on; }
   bool tailchain() const { return tl_.on; }
-  bool persistent() const { return pm_.on; }
+  bool persistent() const { return pm_.on || dp_.on; }
   // persistent plan: {L0 k-chunks, L0 column blocks, k-chunk rows, block columns, chain
   // workgroups, workgroups per replica, grid}
   std::vector<int> persist_geometry() const;
   std::vector<int> persist_variant() const;   // {1 or 2, DW workgroups per replica, sync}
   bool persist_images() const { return pm_.on && pm_.args.imgs != 0; }   // epilogue writes the weight images
+  // persistent layer pipeline: {workgroups per replica, grid, row tiles, k-split, LDS bytes}
+  std::vector<int> deep_geometry() const;
   // parameter-server hook of the persistent plan (V1 roles only): every step pushes the
   // owned parameters' deltas into the server and pulls the next step's (mode 1 hogwild,
   // 2 asynchronous, 0 off); false when the plan cannot (not persistent, or V2 roles)
@@ -196,6 +204,15 @@ class Executor {
   unsigned* d_pflags_ = nullptr;   // [R][PMF_N][PM_MAXWG] flags (zero at every launch: setup, then the post kernel)
   unsigned* d_perr_ = nullptr;     // sticky error word
   bool build_persist();
+  // persistent layer pipeline (deep.hip)
+  struct Deep {
+    bool on = false;
+    DeepArgs args{};
+    size_t flag_bytes = 0;
+  } dp_;
+  float* d_dws_ = nullptr;         // its per-replica workspace (activations, gradients, weight images)
+  unsigned* d_dflags_ = nullptr;   // [R][2][DP_MAXWG] GO / phase counters
+  bool build_deep();
   void run_chunk(hipStream_t s, int nsteps) const;   // nsteps training steps (no counter advance)
   void run_step(hipStream_t s, int step_off) const;
   std::vector<std::pair<hipGraph_t, hipGraphExec_t>> graphs_;

@@ -30,6 +30,11 @@ SOURCES = [
     "kernels/flat.hip",
     "kernels/rowchain.hip",
     "kernels/persist.hip",
+    "kernels/deep.hip",
+    "kernels/deep_l2.hip",
+    "kernels/deep_l3.hip",
+    "kernels/deep_l4.hip",
+    "kernels/deep_l5.hip",
     "kernels/peer.hip",
     "kernels/shuffle.hip",
     "runtime/executor.cpp",

@@ -129,14 +129,17 @@ class PersistentPlanError(RuntimeError):
     not resident: PERR_GRID), False when a wait timed out mid-chunk (weights may be
     partially updated -- ``fit`` restores its entry snapshot and re-runs either way)."""
 
-    def __init__(self, code: int):
+    def __init__(self, code: int, rank_exchange: bool = False):
         self.code = int(code)
         self.clean = self.code == 9
+        self.rank_exchange = bool(rank_exchange)
         super().__init__(
             f"persistent step kernel: an in-launch wait timed out (code {self.code}; "
             + ("the grid was not resident, nothing was modified" if self.clean else
                "mid-chunk: weights may be partially updated")
-            + "); the trainer now runs the row-chain plan")
+            + ("); the in-launch rank exchange is attached, so this rank cannot re-plan alone: the job's "
+               "per-step sync must be restarted without it (ELEPHAS_AMD_XRANK=0)" if rank_exchange else
+               "); the trainer now runs the row-chain plan"))
 
 
 def _replica_sum(G: torch.Tensor):
@@ -309,6 +312,7 @@ class NativeTrainer(TrainerBase):
             persist_cus=self.persist_cus,
             persist_v2=0 if self.ps_hook else int(os.environ.get("ELEPHAS_AMD_PERSIST_V2", "-1")),
             persist_sync=int(self.sync) if ws is self.ws else 0,
+            deep=int(os.environ.get("ELEPHAS_AMD_DEEP", "-1")),
             rc_split=int(os.environ.get("ELEPHAS_AMD_RC_SPLIT", "0")),
             tail=int(os.environ.get("ELEPHAS_AMD_TAIL", "-1")) if ws is self.ws else 0,
             no_reorder=int(os.environ.get("ELEPHAS_AMD_NO_REORDER", "0")),
@@ -334,6 +338,7 @@ class NativeTrainer(TrainerBase):
             self.exe.destroy_graphs()
         self._graphs = {}
         self.exe = self.C.Executor(self._cfg(self.ws))
+        self._built_persist_mode = self.persist_mode
         self.GRAPH_CHUNK = self.PERSIST_CHUNK if self.exe.persistent() else type(self).GRAPH_CHUNK
         if self._ps is not None and not self.exe.set_param_server(*self._ps):
             self._ps = None   # the rebuilt plan cannot (e.g. the row-chain fallback): host-side exchange
@@ -407,6 +412,12 @@ class NativeTrainer(TrainerBase):
             return False
         self._ps = (ps, mode)
         return True
+
+    def detach_param_server(self):
+        """Back to the host-side pull / push rounds (ps_mode 0 in the launch)."""
+        if self._ps is not None:
+            self.exe.set_param_server(self._ps[0], 0)
+            self._ps = None
 
     @property
     def param_server_in_launch(self) -> bool:
@@ -507,9 +518,17 @@ class NativeTrainer(TrainerBase):
         ``flat``, zero optimizer state and iterations, a fresh dropout seed (the training
         executor is rebuilt around the same buffers; its graphs are recaptured lazily)."""
         self.seed = int(seed) if seed is not None else int(np.random.randint(1, 2**62))
-        self._build_executor()
-        self.reset_optimizer_state()
-        self.set_weights_flat(flat)
+        if self.persist_mode == self._built_persist_mode:
+            # the same plan: only the seed changes (no executor rebuild -- that allocated and
+            # zeroed the persistent workspace and synchronised the device on every fit)
+            self.exe.set_seed(self.seed)
+            self._graphs = {}
+        else:
+            self._build_executor()
+        with torch.cuda.stream(self.stream):
+            self.S.fill_(float(self.opt_hp.get("state_init", 0.0)))
+            self.ctr.zero_()
+        self.set_weights_flat(flat)   # + both weight-image parities
 
     def reset_optimizer_state(self):
         with torch.cuda.stream(self.stream):
@@ -810,19 +829,29 @@ class NativeTrainer(TrainerBase):
         first: if a persistent launch gives up (GPU shared, grid not resident -- see
         check()), the trainer re-plans onto the row chain, restores the snapshot and
         runs the whole fit again, so the caller sees a slower fit, not an exception."""
+        if self.exe.persistent():
+            self._enter()   # the snapshot orders after the caller's pending work (e.g. a weight write)
         snap = self._snapshot() if self.exe.persistent() else None
         try:
             return self._fit(epochs, verbose, allreduce)
         except PersistentPlanError:
-            if snap is None:
+            if snap is None or getattr(self, "_xr", None) is not None:
                 raise
             self._restore(snap)
             return self._fit(epochs, verbose, allreduce)
 
     def _snapshot(self):
+        """The fit-entry state, copied into buffers kept for the trainer's life (stream
+        ordered; no allocation per fit)."""
         with torch.cuda.stream(self.stream):
-            return dict(P=self.P.clone(), S=self.S.clone(), ctr=self.ctr.clone(),
-                        perm_epoch=getattr(self, "_perm_epoch", 0))
+            snap = getattr(self, "_snap", None)
+            if snap is None or snap["P"].shape != self.P.shape or snap["S"].shape != self.S.shape:
+                snap = self._snap = dict(P=torch.empty_like(self.P), S=torch.empty_like(self.S),
+                                         ctr=torch.empty_like(self.ctr))
+            snap["P"].copy_(self.P)
+            snap["S"].copy_(self.S)
+            snap["ctr"].copy_(self.ctr)
+            return dict(snap, perm_epoch=getattr(self, "_perm_epoch", 0))
 
     def _restore(self, snap):
         with torch.cuda.stream(self.stream):
@@ -932,9 +961,15 @@ class NativeTrainer(TrainerBase):
         if self.exe is not None and self.exe.persistent():
             e = self.exe.persist_error()
             if e:
+                self.exe.persist_clear_error()
+                if getattr(self, "_xr", None) is not None:
+                    # the in-launch rank exchange cannot move to another plan on this rank
+                    # alone (the other ranks keep waiting in their launches until their
+                    # exchange timeout): one clear error, no local re-plan, no fit() retry
+                    self._xr["live"] = False
+                    raise PersistentPlanError(e, rank_exchange=True)
                 _log.warning("persistent step kernel gave up (code %d%s); falling back to the row-chain plan",
                              e, ", grid not resident" if e == 9 else "")
-                self.exe.persist_clear_error()
                 self.persist_mode = 0
                 self._build_executor()
                 self._images_stale = True   # P may hold a partial chunk: images from P first
@@ -1082,8 +1117,8 @@ class NativeTrainer(TrainerBase):
 
     @property
     def persist_variant(self) -> int:
-        """2: the V2 roles (plain SGD, ReLU: L0 Gram corrections, DW workgroups), 1: V1,
-        0: not persistent."""
+        """3: the layer pipeline (deep.hip: deeper / wider stacks), 2: the V2 roles (plain
+        SGD, ReLU: L0 Gram corrections, DW workgroups), 1: V1, 0: not persistent."""
         return int(self.exe.persist_variant()[0]) if self.exe.persistent() else 0
 
     @property
@@ -1092,6 +1127,11 @@ class NativeTrainer(TrainerBase):
         return bool(self.exe.persistent())
 
     def plan_name(self) -> str:
+        if self.exe.persistent() and self.exe.persist_variant()[0] == 3:
+            nw, grid, rt, ks, lds = self.exe.deep_geometry()
+            return (f"persistent layer pipeline (deep.hip; 1 kernel + 1 post kernel per <= {self.GRAPH_CHUNK}-step "
+                    f"chunk; {nw} workgroups of 512 threads per replica owning 16-column tiles of every layer, "
+                    f"{rt} row tiles x {ks}-way k split, {lds // 1024} KB LDS; grid {grid})")
         if self.exe.persistent():
             nk0, nc0, kc0, cw, nch, wgs, grid = self.exe.persist_geometry()
             var, nd, sync = self.exe.persist_variant()

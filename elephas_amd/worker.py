@@ -401,6 +401,13 @@ class BatchedAsynchronousWorker:
             if self.frequency == "batch":
                 grp.attach(self.client)
             groups.append(grp)
+        if self.frequency == "batch" and len({bool(g.inlaunch) for g in groups}) > 1:
+            # one protocol for every writer: in-launch pushes bracket their slices with
+            # slice counters, host pushes with chunk counters, and an in-launch pull looks at
+            # the slice counters only -- so either every group exchanges inside its launch or
+            # none does
+            for g in groups:
+                g.detach()
         if self.frequency == "epoch":
             for e in range(epochs):
                 for g in groups:          # enqueue every group's epoch, then read histories
@@ -503,6 +510,13 @@ class _Group:
     def graph(self):
         return bool(self.graphs)
 
+    @property
+    def t_inlaunch(self) -> bool:
+        """The exchange runs inside the persistent launch NOW: asked of the trainer, not
+        cached at attach time (a rebuilt executor -- plan fallback, grad-scale change -- may
+        have dropped the hook, and then the host rounds must push the deltas)."""
+        return bool(getattr(self, "inlaunch", False) and getattr(self.t, "param_server_in_launch", False))
+
     def attach(self, client):
         """frequency='batch' on the persistent plan: the server's push / pull per step runs
         inside the launch (NativeTrainer.attach_param_server); the host pulls theta
@@ -517,11 +531,16 @@ class _Group:
             return
         self.inlaunch = bool(self.t.attach_param_server(ps, bool(ps.consistent)))
 
+    def detach(self):
+        if getattr(self, "inlaunch", False):
+            self.t.detach_param_server()
+        self.inlaunch = False
+
     def capture(self, worker):
         """Capture the CHUNK-round and 1-round graphs; eager launches (logged) if capture fails."""
         import torch
         from .parallel import fault
-        if getattr(self, "inlaunch", False):
+        if self.t_inlaunch:
             return   # one persistent launch per chunk, exchange inside it
         if os.environ.get("ELEPHAS_AMD_ASYNC_GRAPH", "1") == "0" or fault.injection_active():
             return
@@ -549,7 +568,7 @@ class _Group:
     def steps(self, worker, n):
         """Enqueue n pull/step/push rounds (no host synchronisation)."""
         import torch
-        if getattr(self, "inlaunch", False):
+        if self.t_inlaunch:
             # one host pull of theta into every replica's masters per persistent chunk; the
             # kernel pushes each step's delta and pulls the next step's theta itself
             while n > 0:
