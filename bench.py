@@ -194,7 +194,8 @@ def main():
             subs[name] = {"value": round(r["samples"] / r["dt_max"], 1), "ms_per_step": round(r["dt_max"] / sk * 1e3, 4),
                           "steps": sk, "workers_per_gpu": w_, "sync": r["sync"], "engine": r["engine"],
                           "scaling": "weak" if name != "strong" else "strong",
-                          "theta_equal_on_all_ranks": r["theta_equal"], "allreduce": r["path"]}
+                          "theta_equal_on_all_ranks": r["theta_equal"], "allreduce": r["path"],
+                          "rank_exchange_selftest": r["xr_selftest"]}
     provenance = None
     if gpu:
         from elephas_amd.ops import native
@@ -312,8 +313,10 @@ def measure_train(args, model, dist, rank, world, dev, gpu, W, batch_mode, steps
         init_np = init.cpu().numpy()
         t.set_weights_flat(init_np)
     xrank = False
+    xr_selftest = None
     if sync_local and world > 1:
         xrank = t.attach_rank_exchange(rank, world)   # collective: the same answer on every rank
+        xr_selftest = getattr(t, "xr_selftest", None)   # the voted numeric self-test of the path
         if not xrank:
             sync_local = False
             t, R, Bloc = make(False)
@@ -440,7 +443,7 @@ def measure_train(args, model, dist, rank, world, dev, gpu, W, batch_mode, steps
               if gpu else "torch CPU reference")
     out = dict(t=t, R=R, rows=rows, samples=samples, dt_max=dt_max, state=state, digests=digests, devices=devices,
                path=path, nbytes=nbytes, batch_mode=batch_mode, sync=sync_desc, engine=engine,
-               theta_equal=all(d == digests[0] for d in digests), W=W)
+               theta_equal=all(d == digests[0] for d in digests), W=W, xr_selftest=xr_selftest)
     return out
 
 

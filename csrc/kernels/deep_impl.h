@@ -609,8 +609,13 @@ __device__ __forceinline__ void bw_phase(const DeepArgs& a, float* smem, const C
                                          const f32x4 (&G)[L - 1]) {
   const Ctx x = lanes(x0);
   const DeepLayer lp = a.ly[l - 1], ly = a.ly[l];
-  bias_tile<l, SGD0>(a, smem, x, ly.o_dz, ly.N16, os);
-  if (x.j >= lp.T) return;
+  if (x.j >= lp.T) {   // no row tile of W_l here; maybe its bias tile (layer l wider than l - 1)
+    bias_tile<l, SGD0>(a, smem, x, ly.o_dz, ly.N16, os);
+    return;
+  }
+  // this workgroup's bias tile j of layer l: summed from the staged chunk that holds it
+  const bool btile = x.j < ly.T && ly.has_bias;
+  const int hb = (16 * x.j) / CW, cb = 16 * x.j - hb * CW;
   const int I0 = 16 * x.j, Bp = a.Bp, ldat = Bp + 4, ldr = ly.N16 + 4;
   const int rt = x.w % a.RT, kp = x.w / a.RT;
   const int f = x.w & 3, hh = x.w >> 2;
@@ -662,8 +667,22 @@ __device__ __forceinline__ void bw_phase(const DeepArgs& a, float* smem, const C
         mma4(accW, av, b);
       }
     }
+    float* bred = smem + a.l_red;
+    if (btile && h == hb && x.tid < 256) {   // bias: 16 columns x 16 row groups of Bp / 16 rows
+      const int c = x.tid & 15, rg = x.tid >> 4, rows = Bp >> 4;
+      float sm = 0.f;
+      for (int rr = 0; rr < rows; ++rr) sm += sdz[(rg * rows + rr) * LDZ + cb + c];
+      bred[x.tid] = sm;
+    }
     lds_barrier();   // every read of the chunk and of the old masters is done
     if (hh == 1) lds4(spart + (f * 64 + x.lane) * 4, accW);
+    if (btile && h == hb && x.tid < 16 && 16 * x.j + x.tid < ly.N) {
+      float db = 0.f;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) db += bred[x.tid + 16 * k];
+      float* bt = smem + ly.l_b;
+      bt[x.tid] = upd<SGD0>(a, x, os, ly.p_off + (long long)ly.K * ly.N + 16 * x.j + x.tid, bt[x.tid], db);
+    }
     lds_barrier();
     if (hh == 0 && 16 * f < cw) {
       accW += lds4(spart + (f * 64 + x.lane) * 4);

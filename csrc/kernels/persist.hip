@@ -297,6 +297,65 @@ __device__ __forceinline__ bool wait_grid(const PersistArgs& a) {
   return ok != 0;
 }
 
+// The rank part of the per-step exchange (replica 0's owning workgroup q): put this rank's
+// tile sum v into slab [tag & 1][q] of its peer-mapped buffer, raise flag q (system scope,
+// tag monotonic over the trainer's life), wait for flag q of every rank, and replace v by
+// the ranks' slabs summed in rank order -- the same bits on every rank.  false: a rank did
+// not arrive within xr_timeout (error word PERR_XRANK).  Shared by xchg_sum and the
+// numeric self-test the host runs before it trusts the path (xrank_selftest_kernel).
+template <int N>
+__device__ __forceinline__ bool xrank_sum(const PersistArgs& a, int q, unsigned tag, f32x4 (&v)[N]) {
+  const int tid = threadIdx.x;
+  const long long soff = PEER_DATA_OFF + ((long long)(tag & 1u) * a.wgs + q) * PM_XSLOT * 4;
+  int ok = 1;
+  f32x4* dst = reinterpret_cast<f32x4*>(a.xr_base[a.xr_rank] + soff);
+#pragma unroll
+  for (int u = 0; u < N; ++u) dst[u * 256 + tid] = v[u];
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0)
+    __hip_atomic_store(reinterpret_cast<unsigned*>(a.xr_base[a.xr_rank] + PEER_FLAG_OFF + (long long)q * 64), tag,
+                       __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (tid < 64) {
+    // lane k watches rank k's flag q (the rank's buffer by selects: no per-lane kernarg indexing)
+    char* b = a.xr_base[0];
+#pragma unroll
+    for (int k = 1; k < PEER_MAX_RANKS; ++k) b = (tid == k) ? a.xr_base[k] : b;
+    const unsigned* fl = reinterpret_cast<const unsigned*>(b + PEER_FLAG_OFF + (long long)q * 64);
+    const unsigned long long t0 = wall_clock64();
+    for (;;) {
+      const unsigned f = tid < a.xr_world ? __hip_atomic_load(const_cast<unsigned*>(fl), __ATOMIC_ACQUIRE,
+                                                              __HIP_MEMORY_SCOPE_SYSTEM)
+                                          : tag;
+      if (__all((int)(f - tag) >= 0)) break;   // wrap-safe: tags only grow
+      if ((long long)(wall_clock64() - t0) > a.xr_timeout) {
+        ok = 0;
+        if (tid == 0) __hip_atomic_store((gu32*)(a.err), (unsigned)PERR_XRANK, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  ok = __syncthreads_and(ok);
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  if (!ok) return false;
+#pragma unroll
+  for (int u = 0; u < N; ++u) v[u] = zero4f();
+#pragma unroll 1
+  for (int k = 0; k < a.xr_world; ++k) {   // rank order
+    char* b = a.xr_base[0];
+#pragma unroll
+    for (int kk = 1; kk < PEER_MAX_RANKS; ++kk) b = (k == kk) ? a.xr_base[kk] : b;
+    const f32x4* src = reinterpret_cast<const f32x4*>(b + soff);
+    f32x4 x[N];
+#pragma unroll
+    for (int u = 0; u < N; ++u) x[u] = __builtin_nontemporal_load(src + u * 256 + tid);
+#pragma unroll
+    for (int u = 0; u < N; ++u) v[u] += x[u];
+  }
+  return true;
+}
+
 // sync: sum the weight-gradient fragments v[0 .. N) (f32x4 per lane, lane-linear slab
 // layout) of workgroup q over the R replicas, in replica order.  Every storing wave drains
 // its sc1 stores before the flag (publish); the slabs alternate by step parity, so a
@@ -342,56 +401,9 @@ __device__ __forceinline__ bool xchg_sum(const PersistArgs& a, int r, int q, int
   // ---- across ranks: replica 0 publishes the rank's sum, reads every rank's (over xGMI
   // on a node), sums them in rank order and leaves the total in its local total slab; the
   // other replicas read that (one remote read set per workgroup and rank, not R of them)
-  const unsigned tag = a.xr_tag0 + (unsigned)i + 1u;
-  const long long soff = PEER_DATA_OFF + ((long long)(tag & 1u) * a.wgs + q) * PM_XSLOT * 4;
   const long long tslab = a.o_xt + ((long long)(i & 1) * a.wgs + q) * PM_XSLOT;   // in replica 0's workspace
-  ok = 1;
   if (r == 0) {
-    f32x4* dst = reinterpret_cast<f32x4*>(a.xr_base[a.xr_rank] + soff);
-#pragma unroll
-    for (int u = 0; u < N; ++u) dst[u * 256 + tid] = v[u];
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0)
-      __hip_atomic_store(reinterpret_cast<unsigned*>(a.xr_base[a.xr_rank] + PEER_FLAG_OFF + (long long)q * 64), tag,
-                         __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    if (tid < 64) {
-      // lane k watches rank k's flag q (the rank's buffer by selects: no per-lane kernarg indexing)
-      char* b = a.xr_base[0];
-#pragma unroll
-      for (int k = 1; k < PEER_MAX_RANKS; ++k) b = (tid == k) ? a.xr_base[k] : b;
-      const unsigned* fl = reinterpret_cast<const unsigned*>(b + PEER_FLAG_OFF + (long long)q * 64);
-      const unsigned long long t0 = wall_clock64();
-      for (;;) {
-        const unsigned f = tid < a.xr_world ? __hip_atomic_load(const_cast<unsigned*>(fl), __ATOMIC_ACQUIRE,
-                                                                __HIP_MEMORY_SCOPE_SYSTEM)
-                                            : tag;
-        if (__all((int)(f - tag) >= 0)) break;   // wrap-safe: tags only grow
-        if ((long long)(wall_clock64() - t0) > a.xr_timeout) {
-          ok = 0;
-          if (tid == 0) __hip_atomic_store((gu32*)(a.err), (unsigned)PERR_XRANK, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
-      }
-    }
-    ok = __syncthreads_and(ok);
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    if (!ok) return false;
-#pragma unroll
-    for (int u = 0; u < N; ++u) v[u] = zero4f();
-#pragma unroll 1
-    for (int k = 0; k < a.xr_world; ++k) {   // rank order
-      char* b = a.xr_base[0];
-#pragma unroll
-      for (int kk = 1; kk < PEER_MAX_RANKS; ++kk) b = (k == kk) ? a.xr_base[kk] : b;
-      const f32x4* src = reinterpret_cast<const f32x4*>(b + soff);
-      f32x4 x[N];
-#pragma unroll
-      for (int u = 0; u < N; ++u) x[u] = __builtin_nontemporal_load(src + u * 256 + tid);
-#pragma unroll
-      for (int u = 0; u < N; ++u) v[u] += x[u];
-    }
+    if (!xrank_sum<N>(a, q, a.xr_tag0 + (unsigned)i + 1u, v)) return false;
     if (a.R > 1) {   // the total for the other replicas (write-through, then the local flag)
 #pragma unroll
       for (int u = 0; u < N; ++u) stw4(all, (u * 256 + tid) * 4, (int)tslab, v[u]);
@@ -2527,4 +2539,51 @@ extern "C" hipError_t ea_persist(const PersistArgs* a, hipStream_t s) {
   if (a->H0 == 64 && a->H1 == 64) return persist_launch<64, 64>(a, s);
   if (a->H0 == 128 && a->H1 == 64) return persist_launch<128, 64>(a, s);
   return hipErrorInvalidValue;
+}
+
+namespace ea {
+namespace {
+// value of element e (of 4) of lane slot u of workgroup q in self-test step i on rank k:
+// small integers, so every partial sum is exact in fp32 whatever the order
+__device__ __forceinline__ float xr_test_value(int k, int q, int i, int u, int tid, int e) {
+  return (float)((k + 1) * ((q % 5) + i + 2) + ((u * 1024 + tid * 4 + e) % 13));
+}
+}  // namespace
+
+// Numeric self-test of the in-launch rank exchange (xrank_sum) before a trainer trusts it:
+// nsteps exchanges of known integer tiles by every owning workgroup q (the tags continue
+// the trainer's sequence); every rank checks that each exchanged element equals the exact
+// rank sum.  bad[0] += 1 per workgroup and step with a wrong element, += 1 << 16 per
+// workgroup that timed out.  corrupt != 0 (fault injection): this rank sends a wrong tile.
+__global__ __launch_bounds__(256) void xrank_selftest_kernel(PersistArgs a, int nsteps, unsigned* bad, int corrupt) {
+  constexpr int N = PM_XSLOT / 1024;
+  const int q = blockIdx.x, tid = threadIdx.x;
+  for (int i = 0; i < nsteps; ++i) {
+    f32x4 v[N];
+#pragma unroll
+    for (int u = 0; u < N; ++u)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[u][e] = xr_test_value(a.xr_rank, q, i, u, tid, e) + (corrupt ? 0.5f : 0.f);
+    if (!xrank_sum<N>(a, q, a.xr_tag0 + (unsigned)i + 1u, v)) {
+      if (tid == 0) atomicAdd(bad, 1u << 16);
+      return;
+    }
+    int wrong = 0;
+#pragma unroll
+    for (int u = 0; u < N; ++u)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float want = 0.f;
+        for (int k = 0; k < a.xr_world; ++k) want += xr_test_value(k, q, i, u, tid, e);
+        wrong |= v[u][e] != want;
+      }
+    if (__syncthreads_or(wrong) && tid == 0) atomicAdd(bad, 1u);
+  }
+}
+
+}  // namespace ea
+
+extern "C" hipError_t ea_xrank_selftest(const PersistArgs* a, int nsteps, unsigned* bad, int corrupt, hipStream_t s) {
+  hipLaunchKernelGGL(xrank_selftest_kernel, dim3(a->wgs), dim3(256), 0, s, *a, nsteps, bad, corrupt);
+  return hipGetLastError();
 }

@@ -21,6 +21,7 @@ extern "C" hipError_t ea_persist_post(unsigned* flags, int nflags, long long* ct
 extern "C" hipError_t ea_persist(const ea::PersistArgs* a, hipStream_t s);
 extern "C" int ea_persist_lds_bytes();
 extern "C" hipError_t ea_deep(const ea::DeepArgs* a, hipStream_t s);
+extern "C" hipError_t ea_xrank_selftest(const ea::PersistArgs* a, int nsteps, unsigned* bad, int corrupt, hipStream_t s);
 
 namespace ea {
 
@@ -344,6 +345,29 @@ bool Executor::set_rank_exchange(const std::vector<char*>& bases, int world, int
   a.timeout = std::max(a.timeout, a.xr_timeout);
   pm_.xr_steps = tag0;   // a rebuilt executor continues the trainer's tag sequence
   return true;
+}
+
+// Numeric self-test of the attached rank exchange (persist.hip xrank_selftest_kernel):
+// nsteps exchanges of known integer tiles on every owning workgroup, checked against the
+// exact rank sums.  Collective (every rank runs it, the tags advance on all of them).
+// Returns {workgroup-steps with a wrong element, workgroups that timed out}.
+std::vector<unsigned> Executor::rank_exchange_selftest(int nsteps, int corrupt) {
+  if (!pm_.on || pm_.args.xr_world <= 1 || nsteps <= 0) return {0u, 0u};
+  unsigned* d = nullptr;
+  check(hipMalloc(&d, sizeof(unsigned)), "hipMalloc(self-test word)");
+  check(hipMemset(d, 0, sizeof(unsigned)), "hipMemset(self-test word)");
+  check(hipDeviceSynchronize(), "hipDeviceSynchronize(self-test setup)");
+  PersistArgs a = pm_.args;
+  a.xr_tag0 = pm_.xr_steps;
+  pm_.xr_steps += (unsigned)nsteps;
+  hipError_t e = ea_xrank_selftest(&a, nsteps, d, corrupt, nullptr);
+  if (e == hipSuccess) e = hipDeviceSynchronize();
+  unsigned v = 0;
+  if (e == hipSuccess) e = hipMemcpy(&v, d, sizeof(v), hipMemcpyDeviceToHost);
+  (void)hipFree(d);
+  check(e, "rank-exchange self-test");
+  if (persist_error() == PERR_XRANK) persist_clear_error();   // the timeout is reported in the result
+  return {v & 0xFFFFu, v >> 16};
 }
 
 std::vector<int> Executor::persist_variant() const {

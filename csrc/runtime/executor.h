@@ -145,6 +145,8 @@ class Executor {
   // rank-exchange buffer (peer-mapped); false: the plan cannot (not a persistent sync plan)
   bool set_rank_exchange(const std::vector<char*>& bases, int world, int rank, unsigned tag0, double timeout_s);
   unsigned rank_exchange_steps() const { return pm_.xr_steps; }
+  // numeric self-test of the attached exchange: {wrong workgroup-steps, timed-out workgroups}
+  std::vector<unsigned> rank_exchange_selftest(int nsteps, int corrupt);
   unsigned persist_error() const;  // sticky error word (a timed-out in-launch wait), synchronous read
   void persist_clear_error();
   int rowchain_split() const { return rc_.on ? rc_.nsplitk : 0; }

@@ -393,6 +393,29 @@ class NativeTrainer(TrainerBase):
             self._xr = None
             self._build_executor()
             return False
+        # numeric self-test before the path is trusted (the first time it crosses xGMI may
+        # be a production run): known integer tiles through the very buffers, flags and tags
+        # of the exchange, checked against the exact rank sums on every rank, voted; any
+        # mismatch or timeout -> every rank detaches and keeps its own per-step exchange
+        from ..parallel import fault
+        corrupt = 0
+        try:
+            fault.maybe_inject("xrank_selftest", int(rank))
+        except fault.InjectedFault:
+            corrupt = 1   # this rank sends a wrong tile: the vote must catch it
+        try:
+            wrong, late = (int(v) for v in self.exe.rank_exchange_selftest(2, corrupt))
+        except Exception as e:  # noqa: BLE001 - voted below
+            _log.warning("rank exchange self-test failed to run: %r", e)
+            wrong, late = -1, -1
+        verdicts = gather((wrong, late))
+        self.xr_selftest = dict(votes=[list(v) for v in verdicts], ok=all(v == (0, 0) for v in verdicts))
+        if not self.xr_selftest["ok"]:
+            _log.warning("rank exchange self-test failed on some rank (%s): using the per-step all-reduce",
+                         verdicts)
+            self._xr = None
+            self._build_executor()
+            return False
         return True
 
     @property

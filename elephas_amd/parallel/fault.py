@@ -11,7 +11,9 @@ visible instead of silent:
 * ``$ELEPHAS_AMD_FAULT_INJECT`` (``rank=R,phase=P[,after=N]``) raises
   ``InjectedFault`` on rank R the (N+1)-th time phase P is reached -- the hook the
   failure tests use. Phases: ``train``, ``allreduce``, ``push``, ``pull``, ``ps_selftest`` (the
-  rank pushes a wrong delta in the device PS self-test, which must then fail).
+  rank pushes a wrong delta in the device PS self-test, which must then fail),
+  ``xrank_selftest`` (the rank sends a wrong tile in the in-launch rank-exchange self-test:
+  every rank must then detach and keep the peer all-reduce path).
 """
 from __future__ import annotations
 

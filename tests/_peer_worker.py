@@ -349,6 +349,70 @@ def sync_inlaunch(dist, rank, world):
                 steps_tagged=int(t.exe.rank_exchange_steps()))
 
 
+def xrank_selftest(dist, rank, world):
+    """The voted numeric self-test of the in-launch rank exchange (NativeTrainer
+    .attach_rank_exchange): without a fault every rank attaches and trains inside the
+    launch; with ELEPHAS_AMD_FAULT_INJECT=rank=1,phase=xrank_selftest rank 1 sends a wrong
+    tile, every rank detaches, and the per-step all-reduce path it falls back to (one
+    replica of the rank's stacked batches, gradient sum over the ranks) still trains to
+    the same weights as ONE torch model on every worker's batches."""
+    import hashlib
+    import torch
+    from elephas_amd import config
+    from elephas_amd.models import Sequential, Dense, initializers
+    from elephas_amd.models.optimizers import SGD
+    from elephas_amd.ops.native_engine import NativeTrainer
+    from elephas_amd.ops.plan import build_plan
+    from elephas_amd.ops.torch_engine import TorchTrainer
+    config.set_policy("float32")
+    initializers.set_seed(23)
+    m = Sequential()
+    m.add(Dense(128, activation="relu", input_dim=784))
+    m.add(Dense(128, activation="relu"))
+    m.add(Dense(10, activation="softmax"))
+    m.compile(SGD(0.1), "categorical_crossentropy", ["acc"])
+    R, B, steps = 2, 64, 6
+    rng = np.random.default_rng(78)
+    xs_all = [rng.random((B * steps, 784), dtype=np.float32) for _ in range(world * R)]
+    ys_all = [np.eye(10, dtype=np.float32)[rng.integers(0, 10, B * steps)] for _ in range(world * R)]
+    xs, ys = xs_all[rank * R:(rank + 1) * R], ys_all[rank * R:(rank + 1) * R]
+    ag = _allgather(dist)
+    t = NativeTrainer(m, build_plan(m), R, B, torch.device("cuda"), seed=5, sync=True, persist_cus=128)
+    w0 = t.get_weights_flat()[0].copy()
+    t.set_data(xs, ys, 0.0, shuffle=False)
+    attached = bool(t.attach_rank_exchange(rank, world, allgather=ag))
+    selftest = getattr(t, "xr_selftest", None)
+    if attached:
+        t.fit(2)
+        w = t.get_weights_flat()[0]
+    else:
+        # the fallback: one replica of the rank's R stacked batches, gradients summed over
+        # the ranks every step (gloo here; the peer all-reduce / RCCL in the bench)
+        xr = np.concatenate([np.concatenate([x[i * B:(i + 1) * B] for x in xs]) for i in range(steps)])
+        yr = np.concatenate([np.concatenate([y[i * B:(i + 1) * B] for y in ys]) for i in range(steps)])
+        f = NativeTrainer(m, build_plan(m), 1, R * B, torch.device("cuda"), seed=5)
+        f.set_grad_scale(1.0 / world)
+        f.set_data([xr], [yr], 0.0, shuffle=False)
+
+        def gloo_sum(G):
+            h = G.detach().cpu()
+            dist.all_reduce(h)
+            G.copy_(h.to(G.device))
+        for _ in range(2):
+            f.begin_epoch()
+            f.run_steps_allreduce(steps, gloo_sum)
+        w = f.get_weights_flat()[0]
+    digs = ag(hashlib.sha1(np.ascontiguousarray(w).tobytes()).hexdigest()[:16])
+    xc = np.concatenate([np.concatenate([x[i * B:(i + 1) * B] for x in xs_all]) for i in range(steps)])
+    yc = np.concatenate([np.concatenate([y[i * B:(i + 1) * B] for y in ys_all]) for i in range(steps)])
+    ref = TorchTrainer(m, build_plan(m), 1, world * R * B, torch.device("cuda"))
+    ref.set_data([xc], [yc], 0.0, shuffle=False)
+    ref.fit(2)
+    wt = ref.get_weights_flat()[0]
+    err = float(np.abs(w - wt).max() / np.abs(wt - w0).max())
+    return dict(attached=attached, selftest=selftest, same_on_all_ranks=len(set(digs)) == 1, err=err)
+
+
 def main():
     scenario = sys.argv[1]
     dist = _gloo()
@@ -365,6 +429,8 @@ def main():
         res = ps(dist, rank, world)
     elif scenario == "ps_selftest":
         res = ps_selftest(dist, rank, world)
+    elif scenario == "xrank_selftest":
+        res = xrank_selftest(dist, rank, world)
     elif scenario == "sync_inlaunch":
         res = sync_inlaunch(dist, rank, world)
     elif scenario.startswith("spark_sync_"):  # spark_sync_<fit|epoch|batch>[p]

@@ -159,3 +159,19 @@ def test_sync_inlaunch_across_ranks_matches_one_model():
         assert r["error"] == 0 and r["replicas_equal"] and r["same_on_all_ranks"], r
         assert r["err"] < 1e-3, r
         assert r["steps_tagged"] == 18, r   # 2 epochs x 9 steps ran with the exchange
+
+
+def test_rank_exchange_selftest_votes_and_falls_back():
+    """The in-launch rank exchange is trusted only after a voted numeric self-test (known
+    integer tiles through its own buffers, flags and tags, checked against the exact rank
+    sums): clean -> every rank attaches and trains inside the launch; a rank that sends a
+    wrong tile (fault injection) -> every rank detaches, and the per-step all-reduce
+    fallback still trains to the single-model result on both ranks."""
+    for r in _run("xrank_selftest"):
+        assert r["attached"] and r["selftest"]["ok"], r
+        assert all(v == [0, 0] for v in r["selftest"]["votes"]), r
+        assert r["same_on_all_ranks"] and r["err"] < 1e-3, r
+    for r in _run("xrank_selftest", env_extra={"ELEPHAS_AMD_FAULT_INJECT": "rank=1,phase=xrank_selftest"}):
+        assert not r["attached"] and r["selftest"] is not None and not r["selftest"]["ok"], r
+        assert any(v[0] > 0 for v in r["selftest"]["votes"]), r
+        assert r["same_on_all_ranks"] and r["err"] < 1e-3, r
