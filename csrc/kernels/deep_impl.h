@@ -624,9 +624,10 @@ __device__ __forceinline__ void bw_phase(const DeepArgs& a, float* smem, const C
   float* sdz = smem + a.l_stage;
   float* spart = sdz + DP_ROWS * LDZ;   // [4][64][4] DW partials of the second row half
   const int nch = (ly.N16 + CW - 1) / CW;
-  // chunk staging: Bp x 64 floats = Bp * 16 float4, <= 4 per thread
-  f32x4 pre[4];
-  auto load_chunk = [&](int h) {
+  // chunk staging: Bp x 64 floats = Bp * 16 float4, <= 4 per thread, two chunks ahead
+  // (register sets A / B alternate; the loop is unrolled by two so their indices stay static)
+  f32x4 preA[4], preB[4];
+  auto load_chunk = [&](int h, f32x4 (&pre)[4]) {
     const int c0 = h * CW;
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
@@ -635,16 +636,17 @@ __device__ __forceinline__ void bw_phase(const DeepArgs& a, float* smem, const C
       pre[u] = ld4(x.rs, (row < Bp ? row : 0) * ly.N16 + cc, ly.o_dz);
     }
   };
-  load_chunk(0);
+  load_chunk(0, preA);
+  if (nch > 1) load_chunk(1, preB);
   f32x4 accB0 = z4(), accB1 = z4();
-  for (int h = 0; h < nch; ++h) {
+  auto chunk = [&](int h, f32x4 (&pre)[4]) {
     const int c0 = h * CW, cw = ly.N16 - c0 < CW ? ly.N16 - c0 : CW;
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int e = x.tid + NTH * u, row = e >> 4, q = e & 15;
       if (row < Bp) lds4(sdz + row * LDZ + 4 * q, 4 * q < cw ? pre[u] : z4());
     }
-    if (h + 1 < nch) load_chunk(h + 1);
+    if (h + 2 < nch) load_chunk(h + 2, pre);   // two chunks in flight ahead of the consumer
     lds_barrier();
     // dA_{l-1}[rows of tile rt][J] over the chunk's 16-column groups t (t % KS == kp)
 #pragma unroll
@@ -700,6 +702,10 @@ __device__ __forceinline__ void bw_phase(const DeepArgs& a, float* smem, const C
       }
       st4(x.rs, col * ly.Kx + I0 + 4 * x.g, ly.o_wt, wv);
     }
+  };
+  for (int h = 0; h < nch; h += 2) {
+    chunk(h, preA);
+    if (h + 1 < nch) chunk(h + 1, preB);
   }
   f32x4 acc = ks_reduce(a, x, smem + a.l_red, accB0 + accB1, kp);
   if (kp != 0) return;

@@ -201,6 +201,7 @@ PYBIND11_MODULE(_C, m) {
       .def("persist_variant", &Executor::persist_variant)
       .def("deep_geometry", &Executor::deep_geometry)
       .def("set_seed", &Executor::set_seed)
+      .def("plan_reason", &Executor::plan_reason)
       .def("rank_exchange_selftest", &Executor::rank_exchange_selftest)
       .def("persist_images", &Executor::persist_images)
       .def("set_rank_exchange", [](Executor& e, std::vector<uintptr_t> bases, int world, int rank, unsigned tag0,

@@ -65,15 +65,17 @@ Executor::~Executor() {
 // of <= 16 units, fp32, B <= 64, and a grid of at most one workgroup per CU (every
 // workgroup must be resident: they wait for each other inside the launch).
 bool Executor::build_persist() {
+  auto no_pm = [&](const char* why) { why_pm_ = why; return false; };
   const int L = (int)c_.layers.size();
-  if (L != 3) return false;
+  if (L != 3) return no_pm("persist.hip: 3 Dense layers only");
   const LayerCfg &l0 = c_.layers[0], &l1 = c_.layers[1], &l2 = c_.layers[2];
   // hidden widths (64, 64), (128, 128) or (128, 64): the kernel is compiled for those shapes
-  if (!((l0.N == 64 && l1.N == 64) || (l0.N == 128 && l1.N == 128) || (l0.N == 128 && l1.N == 64))) return false;
-  if (l1.K != l0.N || l2.K != l1.N || l2.N > PM_MAXC || c_.ldy > 32) return false;
-  if (c_.B > PM_ROWS || c_.B < 1) return false;
+  if (!((l0.N == 64 && l1.N == 64) || (l0.N == 128 && l1.N == 128) || (l0.N == 128 && l1.N == 64)))
+    return no_pm("persist.hip: hidden widths (64, 64), (128, 128) or (128, 64) only");
+  if (l1.K != l0.N || l2.K != l1.N || l2.N > PM_MAXC || c_.ldy > 32) return no_pm("persist.hip: a last layer of <= 16 units");
+  if (c_.B > PM_ROWS || c_.B < 1) return no_pm("persist.hip: batch <= 64 rows per replica");
   const int nch = cdiv(c_.B, 16);
-  if (cdiv(l1.N / 16, nch) > PM_NTU) return false;
+  if (cdiv(l1.N / 16, nch) > PM_NTU) return no_pm("persist.hip: too few chain workgroups for the layer-1 tiles");
   int dev = 0, ncu = 0;
   check(hipGetDevice(&dev), "hipGetDevice");
   check(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev), "hipDeviceGetAttribute");
@@ -84,9 +86,9 @@ bool Executor::build_persist() {
   if (c_.persist_cus > 0) ncu = std::min(ncu, c_.persist_cus);  // a share of the GPU (concurrent executors)
   int lds_max = 0;
   check(hipDeviceGetAttribute(&lds_max, hipDeviceAttributeMaxSharedMemoryPerBlock, dev), "hipDeviceGetAttribute");
-  if (ea_persist_lds_bytes() > lds_max) return false;
+  if (ea_persist_lds_bytes() > lds_max) return no_pm("persist.hip: LDS");
   const int cap = std::min(ncu / c_.R - nch, PM_MAXWG);
-  if (cap < 1) return false;
+  if (cap < 1) return no_pm("persist.hip: not enough CUs for the replicas' clusters");
   // V2 (persist.hip l0_role_v2 / dw_role_v2): plain SGD, ReLU hidden layers, independent
   // replicas -- the step's critical path runs through the chain workgroups only
   // (the chain's Gram correction carries layer 0's bias update -- its ones column -- so a
@@ -95,7 +97,7 @@ bool Executor::build_persist() {
                   l0.act == ACT_RELU && l1.act == ACT_RELU && l0.has_bias;
   const int nd = v2 ? cdiv(l1.N / 16, PM_NTU) : 0;
   // bf16 (mixed_bfloat16): the V2 roles only (bf16-rounded operands, bf16 shard and images)
-  if (c_.bf16 && !v2) return false;
+  if (c_.bf16 && !v2) return no_pm("persist.hip: mixed_bfloat16 needs the V2 roles (plain SGD, ReLU, layer-0 bias)");
   // layer-0 tiles: the cheapest (kc0, cw) whose tile count fits.  V1: cost ~ the tile's
   // MFMA work (FWD reduction padded to 64) + the partials every chain workgroup sums.
   // V2: the L0 work is off the critical path; the chain's slab loads (nk0 Pold + Gram
@@ -121,7 +123,7 @@ bool Executor::build_persist() {
       if (best_cost < 0 || cost < best_cost) { best_cost = cost; best_kc = kc; best_cw = cw; }
     }
   }
-  if (best_cost < 0) return false;
+  if (best_cost < 0) return no_pm("persist.hip: no layer-0 tiling fits the CUs");
   PersistArgs& a = pm_.args;
   std::memset(&a, 0, sizeof(a));
   a.R = c_.R; a.B = c_.B;
@@ -212,28 +214,31 @@ bool Executor::build_persist() {
 // granularity).  nw = the widest hidden layer's 16-column tiles workgroups per replica,
 // at most one workgroup per CU (every one resident: they wait for each other).
 bool Executor::build_deep() {
+  auto no_dp = [&](const char* why) { why_dp_ = why; return false; };
   const int L = (int)c_.layers.size();
-  if (L < 2 || L > DP_MAXL || c_.bf16 || c_.persist_sync) return false;
-  if (c_.B < 1 || c_.B > DP_ROWS || c_.ldy > 32 || (c_.ldx % 8) != 0) return false;
+  if (L < 2 || L > DP_MAXL) return no_dp("layer pipeline: 2..5 Dense layers");
+  if (c_.bf16) return no_dp("layer pipeline: fp32 only");
+  if (c_.persist_sync) return no_dp("layer pipeline: independent replicas (fit granularity) only");
+  if (c_.B < 1 || c_.B > DP_ROWS || c_.ldy > 32 || (c_.ldx % 8) != 0) return no_dp("layer pipeline: batch <= 128 rows per replica");
   const LayerCfg& lastc = c_.layers[L - 1];
-  if (lastc.N > DP_MAXC) return false;
+  if (lastc.N > DP_MAXC) return no_dp("layer pipeline: a last layer of <= 32 units");
   auto r16 = [](int n) { return (n + 15) / 16 * 16; };
   int nw = 0;
   for (int l = 0; l < L - 1; ++l) {
     const int n16 = r16(c_.layers[l].N);
-    if (n16 > 1024) return false;
+    if (n16 > 1024) return no_dp("layer pipeline: hidden widths <= 1024");
     nw = std::max(nw, n16 / 16);
-    if (l > 0 && c_.layers[l].K != c_.layers[l - 1].N) return false;
+    if (l > 0 && c_.layers[l].K != c_.layers[l - 1].N) return no_dp("layer pipeline: a plain Dense chain");
   }
-  if (lastc.K != c_.layers[L - 2].N || c_.layers[0].K > c_.ldx) return false;
-  if (nw > DP_MAXWG) return false;
+  if (lastc.K != c_.layers[L - 2].N || c_.layers[0].K > c_.ldx) return no_dp("layer pipeline: a plain Dense chain");
+  if (nw > DP_MAXWG) return no_dp("layer pipeline: too many column tiles");
   int dev = 0, ncu = 0, lds_max = 0;
   check(hipGetDevice(&dev), "hipGetDevice");
   check(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev), "hipDeviceGetAttribute");
   check(hipDeviceGetAttribute(&lds_max, hipDeviceAttributeMaxSharedMemoryPerBlock, dev), "hipDeviceGetAttribute");
   if (const char* e = std::getenv("ELEPHAS_AMD_PERSIST_OVERSUBSCRIBE")) ncu = std::max(ncu, std::atoi(e));
   if (c_.persist_cus > 0) ncu = std::min(ncu, c_.persist_cus);
-  if (c_.R * nw > ncu) return false;
+  if (c_.R * nw > ncu) return no_dp("layer pipeline: replicas x widest-layer tiles > CUs");
   DeepArgs& a = dp_.args;
   std::memset(&a, 0, sizeof(a));
   a.R = c_.R; a.B = c_.B; a.L = L; a.nw = nw;
@@ -266,7 +271,7 @@ bool Executor::build_deep() {
   a.l_stage = lds; lds += stage;
   lds += 2 * DP_ROWS;                                                 // batch rows of two steps (ints, last)
   a.lds_floats = lds;
-  if ((long long)lds * 4 + 1024 > lds_max) return false;   // + the kernel's static LDS
+  if ((long long)lds * 4 + 1024 > lds_max) return no_dp("layer pipeline: the owned tiles exceed the LDS");   // + static LDS
   for (int l = 0; l < L - 1; ++l) {
     a.ly[l].o_a = take((long long)a.Bp * a.ly[l].N16);
     a.ly[l].o_dz = take((long long)a.Bp * a.ly[l].N16);

@@ -137,6 +137,11 @@ class Executor {
   bool persist_images() const { return pm_.on && pm_.args.imgs != 0; }   // epilogue writes the weight images
   // persistent layer pipeline: {workgroups per replica, grid, row tiles, k-split, LDS bytes}
   std::vector<int> deep_geometry() const;
+  // why this executor does not run a persistent plan ("" when it does, or was not asked to)
+  std::string plan_reason() const {
+    if (persistent() || c_.persist == 0) return "";
+    return why_pm_ + (why_dp_.empty() ? "" : "; " + why_dp_);
+  }
   // parameter-server hook of the persistent plan (V1 roles only): every step pushes the
   // owned parameters' deltas into the server and pulls the next step's (mode 1 hogwild,
   // 2 asynchronous, 0 off); false when the plan cannot (not persistent, or V2 roles)
@@ -215,6 +220,7 @@ class Executor {
   float* d_dws_ = nullptr;         // its per-replica workspace (activations, gradients, weight images)
   unsigned* d_dflags_ = nullptr;   // [R][2][DP_MAXWG] GO / phase counters
   bool build_deep();
+  std::string why_pm_, why_dp_;   // why the persistent plans were not eligible (plan_reason)
   void run_chunk(hipStream_t s, int nsteps) const;   // nsteps training steps (no counter advance)
   void run_step(hipStream_t s, int step_off) const;
   std::vector<std::pair<hipGraph_t, hipGraphExec_t>> graphs_;

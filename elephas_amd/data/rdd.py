@@ -199,6 +199,16 @@ def _owned_frozen(a):
     return out
 
 
+def _is_frozen(a) -> bool:
+    """No one can write a's bytes: a and every array it views are read-only."""
+    import numpy as np
+    while isinstance(a, np.ndarray):
+        if a.flags.writeable:
+            return False
+        a = a.base
+    return True
+
+
 def _columnar(parts) -> bool:
     return bool(parts) and all(isinstance(p, ColumnarPartition) for p in parts)
 
@@ -209,11 +219,19 @@ class RDD:
         self.ctx = ctx or SparkContext.getOrCreate()
 
     @classmethod
-    def from_arrays(cls, x, y, num_slices: int, ctx: Optional[SparkContext] = None) -> "RDD":
-        """``parallelize`` of row-aligned arrays: contiguous columnar slices (views)."""
+    def from_arrays(cls, x, y, num_slices: int, ctx: Optional[SparkContext] = None, snapshot: bool = True,
+                    part_cls=None) -> "RDD":
+        """``parallelize`` of row-aligned arrays: contiguous columnar slices.  As PySpark's
+        ``parallelize`` (which serialises the collection when the RDD is created), the RDD
+        holds a read-only snapshot of the arrays -- an edit of the caller's arrays after
+        this does not reach it -- so its partitions stay the same frozen arrays for the
+        RDD's life and the native trainer keeps their uploaded shards across fits
+        (worker._DataKey).  ``snapshot=False``: views of the caller's arrays."""
+        if snapshot:
+            x, y = _owned_frozen(x), _owned_frozen(y)
         n, k = len(x), max(1, int(num_slices))
-        return cls([ColumnarPartition(x[i * n // k:(i + 1) * n // k], y[i * n // k:(i + 1) * n // k])
-                    for i in range(k)], ctx)
+        part_cls = part_cls or ColumnarPartition
+        return cls([part_cls(x[i * n // k:(i + 1) * n // k], y[i * n // k:(i + 1) * n // k]) for i in range(k)], ctx)
 
     # ---- structure
     @property
@@ -265,29 +283,35 @@ class RDD:
     def repartition(self, numPartitions: int) -> "RDD":
         n = max(1, int(numPartitions))
         if _columnar(self._parts):
-            # round-robin over the global row order, as below, on the arrays
+            # round-robin over the global row order, as below, on the arrays: output
+            # partition i takes global rows i, i + n, ...; of input partition j (global
+            # offset o_j) that is the strided slice starting at (i - o_j) mod n -- no index
+            # arrays, one copy per output partition
             import numpy as np
-            # one gather per output partition straight from the input partitions (no
-            # concatenated copy): global row r = offset(part) + local row
+            frozen = all(_is_frozen(p.x) and _is_frozen(p.y) for p in self._parts)
+            memo = getattr(self, "_repart_memo", None)
+            if frozen and memo is not None and n in memo:
+                return memo[n]   # an RDD is immutable: the same (frozen) output partitions
             kind = type(self._parts[0]) if len({type(p) for p in self._parts}) == 1 else ColumnarPartition
-            sizes = np.array([len(p) for p in self._parts], dtype=np.int64)
-            offs = np.concatenate([[0], np.cumsum(sizes)])
-            total = int(offs[-1])
+            offs, o = [], 0
+            for p in self._parts:
+                offs.append(o)
+                o += len(p)
             out = []
             for i in range(n):
-                rows = np.arange(i, total, n, dtype=np.int64)
-                which = np.searchsorted(offs, rows, side="right") - 1
-                xs, ys = [], []
-                for j in np.unique(which):
-                    loc = rows[which == j] - offs[j]
-                    xs.append(np.asarray(self._parts[j].x)[loc])
-                    ys.append(np.asarray(self._parts[j].y)[loc])
-                x = np.concatenate(xs) if len(xs) > 1 else (xs[0] if xs else self._parts[0].x[:0].copy())
-                y = np.concatenate(ys) if len(ys) > 1 else (ys[0] if ys else self._parts[0].y[:0].copy())
+                xs = [np.asarray(p.x)[(i - oj) % n::n] for p, oj in zip(self._parts, offs)]
+                ys = [np.asarray(p.y)[(i - oj) % n::n] for p, oj in zip(self._parts, offs)]
+                x = np.concatenate(xs) if len(xs) > 1 else np.array(xs[0])
+                y = np.concatenate(ys) if len(ys) > 1 else np.array(ys[0])
                 x.setflags(write=False)
                 y.setflags(write=False)
                 out.append(kind(x, y))
-            return RDD(out, self.ctx)
+            res = RDD(out, self.ctx)
+            if frozen:
+                if memo is None:
+                    memo = self._repart_memo = {}
+                memo[n] = res
+            return res
         parts = [[] for _ in range(n)]
         for i, x in enumerate(itertools.chain.from_iterable(self._parts)):
             parts[i % n].append(x)

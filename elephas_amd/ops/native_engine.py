@@ -339,6 +339,12 @@ class NativeTrainer(TrainerBase):
         self._graphs = {}
         self.exe = self.C.Executor(self._cfg(self.ws))
         self._built_persist_mode = self.persist_mode
+        why = self.exe.plan_reason()
+        if why and why != getattr(self, "_logged_reason", None):
+            # a shape cliff: the step runs as several launches instead of one persistent
+            # launch per chunk (2-3x the step time) -- say which constraint the model misses
+            self._logged_reason = why
+            _log.info("no persistent plan for this model (%s): %s", why, self.plan_name())
         self.GRAPH_CHUNK = self.PERSIST_CHUNK if self.exe.persistent() else type(self).GRAPH_CHUNK
         if self._ps is not None and not self.exe.set_param_server(*self._ps):
             self._ps = None   # the rebuilt plan cannot (e.g. the row-chain fallback): host-side exchange
@@ -1168,6 +1174,11 @@ class NativeTrainer(TrainerBase):
         if self.exe.tailchain():
             return f"tail-chain ({self.exe.launches_per_step()} launches per step)"
         return f"grouped ({self.exe.launches_per_step()} launches per step)"
+
+    @property
+    def plan_reason(self) -> str:
+        """Why the training step does not run one of the persistent plans ('' when it does)."""
+        return str(self.exe.plan_reason())
 
     @property
     def rowchain(self) -> bool:

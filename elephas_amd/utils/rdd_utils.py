@@ -32,9 +32,8 @@ def to_labeled_point(sc, features: np.ndarray, labels: np.ndarray, categorical: 
                                for x, y in zip(features, labels)])
     lab = np.argmax(labels.reshape(len(labels), -1), axis=1) if categorical else labels.reshape(len(labels), -1)[:, 0]
     lab = lab.astype(np.float64)
-    n, k = len(features), max(1, sc.defaultParallelism)
-    return RDD([LabeledPointPartition(features[i * n // k:(i + 1) * n // k], lab[i * n // k:(i + 1) * n // k])
-                for i in range(k)], sc)
+    # a read-only snapshot, as parallelize (RDD.from_arrays)
+    return RDD.from_arrays(features, lab, sc.defaultParallelism, sc, part_cls=LabeledPointPartition)
 
 
 def from_labeled_point(rdd, categorical: bool = False, nb_classes: Optional[int] = None) -> Tuple[np.ndarray, np.ndarray]:
@@ -56,26 +55,42 @@ def encode_label(label, nb_classes: int) -> np.ndarray:
 
 
 def lp_to_simple_rdd(lp_rdd, categorical: bool = False, nb_classes: int = None):
-    from ..data.rdd import ColumnarPartition, LabeledPointPartition, RDD
+    from ..data.rdd import LabeledPointPartition
     parts = lp_rdd.partitions() if hasattr(lp_rdd, "partitions") else None
     if parts and all(isinstance(p, LabeledPointPartition) for p in parts):
-        # columnar LabeledPoints: the same (features, label) pairs as the per-row path,
-        # built as arrays; the features stay the partition's own (zero-copy) array, so
-        # they keep its dtype where the per-row path returns float64 toArray() copies
-        if categorical and not nb_classes:
-            nb_classes = int(max(int(p.y.max()) for p in parts if len(p))) + 1
-        out = []
-        for p in parts:
-            x = p.x
-            if categorical:
-                y = np.zeros((len(p), nb_classes))
-                y[np.arange(len(p)), p.y.astype(np.int64)] = 1.0
-            else:
-                y = np.asarray(p.y, dtype=np.float64)
-            out.append(ColumnarPartition(x, y))
-        return RDD(out, lp_rdd.context)
+        from ..data.rdd import _is_frozen
+        frozen = all(_is_frozen(p.x) and _is_frozen(p.y) for p in parts)
+        memo = getattr(lp_rdd, "_lp_simple_memo", None) if frozen else None
+        key = (bool(categorical), nb_classes)
+        if memo is not None and key in memo:
+            return memo[key]   # the same frozen arrays as the previous conversion of this RDD
+        res = _lp_columnar(lp_rdd, parts, categorical, nb_classes)
+        if frozen:
+            if memo is None:
+                memo = lp_rdd._lp_simple_memo = {}
+            memo[key] = res
+        return res
     if categorical:
         if not nb_classes:
             nb_classes = lp_rdd.map(lambda lp: lp.label).map(int).max() + 1
         return lp_rdd.map(lambda lp: (from_vector(lp.features), encode_label(lp.label, nb_classes)))
     return lp_rdd.map(lambda lp: (from_vector(lp.features), lp.label))
+
+
+def _lp_columnar(lp_rdd, parts, categorical, nb_classes):
+    """Columnar LabeledPoints -> (features, label) partitions as arrays: the same pairs as
+    the per-row path; the features stay the partition's own array (no copy, its dtype,
+    where the per-row path returns float64 toArray() copies)."""
+    from ..data.rdd import ColumnarPartition, RDD
+    if categorical and not nb_classes:
+        nb_classes = int(max(int(p.y.max()) for p in parts if len(p))) + 1
+    out = []
+    for p in parts:
+        if categorical:
+            y = np.zeros((len(p), nb_classes))
+            y[np.arange(len(p)), p.y.astype(np.int64)] = 1.0
+            y.setflags(write=False)
+        else:
+            y = np.asarray(p.y, dtype=np.float64)
+        out.append(ColumnarPartition(p.x, y))
+    return RDD(out, lp_rdd.context)

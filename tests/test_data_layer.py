@@ -124,7 +124,10 @@ def test_columnar_partitions_match_row_partitions():
     rows = RDD([list(p) for p in col.partitions()], sc)          # the row-wise equivalent
     assert all(isinstance(p, ColumnarPartition) for p in col.partitions())
     px, py = partition_to_numpy(col.partitions()[1])
-    assert np.shares_memory(px, x) and px.shape == (7, 4)
+    # a read-only snapshot, as PySpark's parallelize: the training path gets the RDD's own
+    # arrays back without a copy, and an edit of the caller's array does not reach them
+    assert np.shares_memory(px, col.partitions()[1].x) and px.shape == (7, 4) and not px.flags.writeable
+    assert not np.shares_memory(px, x)
     for a, b in ((col, rows), (col.repartition(5), rows.repartition(5))):
         assert a.getNumPartitions() == b.getNumPartitions()
         for pa, pb in zip(a.partitions(), b.partitions()):
@@ -160,3 +163,35 @@ def test_trainer_cache_data_key_is_exact():
     assert a != _data_key(copies, ys, 0.1, [True, True], True)  # equal bytes, other objects
     x[0, 0] = 99.0                                              # the source edit does not reach
     assert parts[0].x[0, 0] == 0.0                              # the owned partition copy
+
+
+def test_rdd_snapshot_memoized_conversions_reuse_frozen_arrays():
+    """parallelize-style snapshots make an RDD immutable, so its columnar conversions are
+    memoised: lp_to_simple_rdd and repartition of the same RDD return the very same
+    frozen arrays on every fit (the trainer cache then keeps the uploaded shards), the
+    strided repartition equals the row-wise round robin, and an edit of the caller's
+    arrays after creating the RDD does not reach it."""
+    from elephas_amd.data import SparkContext
+    from elephas_amd.data.rdd import RDD
+    from elephas_amd.utils.rdd_utils import to_labeled_point, lp_to_simple_rdd
+    from elephas_amd.worker import _data_key
+    sc = SparkContext(master="local[3]")
+    rng = np.random.default_rng(0)
+    x = rng.random((23, 5), dtype=np.float32)
+    y = rng.integers(0, 4, 23).astype(np.float64)
+    lp = to_labeled_point(sc, x, y)
+    a = lp_to_simple_rdd(lp, True, 4).repartition(2)
+    b = lp_to_simple_rdd(lp, True, 4).repartition(2)
+    assert a is b
+    xs = [p.x for p in a.partitions()]
+    ys = [p.y for p in a.partitions()]
+    assert _data_key(xs, ys, 0.1, [True, True], True) == _data_key([p.x for p in b.partitions()],
+                                                                    [p.y for p in b.partitions()], 0.1,
+                                                                    [True, True], True)
+    rows = RDD([list(p) for p in lp_to_simple_rdd(lp, True, 4).partitions()], sc).repartition(2)
+    for pa, pb in zip(a.partitions(), rows.partitions()):
+        assert len(pa) == len(pb)
+        for (xa, ya), (xb, yb) in zip(pa, pb):
+            assert np.array_equal(xa, xb) and np.array_equal(ya, yb)
+    x[0, 0] = 7.0
+    assert lp.partitions()[0].x[0, 0] != 7.0
