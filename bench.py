@@ -59,6 +59,8 @@ MODELS = {
     "otto": ([93, 512, 512, 512], 0.5, 9, 7735, 0.01),
     "wide": ([4096, 4096, 4096], 0.0, 1000, 16384, 0.01),   # 16 batches of 1024 per epoch
 }
+NAMES = {"mnist": "MNIST-MLP 784-128-128-10", "otto": "Otto-MLP 93-512-512-512-9",
+         "wide": "Wide-MLP 4096-4096-4096-1000"}
 
 
 def build_model(name):
@@ -102,6 +104,9 @@ def main():
     ap.add_argument("--steps", type=int, default=500)
     ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--model", default="mnist", choices=sorted(MODELS))
+    ap.add_argument("--dims", default=None,
+                    help="e.g. 784,256,128,10: the MNIST recipe (relu, dropout .2, SGD .1, 7500 rows per "
+                         "worker) on other Dense widths -- diagnostics for the persistent plans' shape coverage")
     ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
                     help="weak: --workers-per-gpu workers on every GPU (each GPU is one local[8] node); "
                          "strong: the reference job itself -- 8 partitions in total (examples/"
@@ -139,8 +144,13 @@ def main():
     ap.add_argument("--infer-rows", type=int, default=None, help="rows per GPU for --task predict/evaluate")
     args = ap.parse_args()
 
+    if args.dims:
+        dims = [int(v) for v in args.dims.split(",")]
+        MODELS["custom"] = (dims[:-1], 0.2, dims[-1], 7500, 0.1)
+        NAMES["custom"] = "MLP " + "-".join(map(str, dims))
+        args.model = "custom"
     if args.batch is None:
-        args.batch = {"mnist": 64, "otto": 128, "wide": 1024}[args.model]
+        args.batch = {"otto": 128, "wide": 1024}.get(args.model, 64)
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(_spawn_ranks(sys.argv[1:], args.gpus))
 
@@ -206,8 +216,7 @@ def main():
     if rank == 0:
         value = samples / dt_max
         launches = round(t.launches_for(args.steps) / args.steps, 4) if gpu else None
-        names = {"mnist": "MNIST-MLP 784-128-128-10", "otto": "Otto-MLP 93-512-512-512-9",
-                 "wide": "Wide-MLP 4096-4096-4096-1000"}
+        names = NAMES
         metric = ("samples/sec (whole node) MNIST-MLP 784-128-128-10 sync DP at 1/2/4/8 MI355X"
                   if args.model == "mnist" else f"samples/sec (whole node) {names[args.model]} sync DP")
         line = {
@@ -572,8 +581,7 @@ def bench_infer(args, model, dist, rank, world, dev):
     dt = time.perf_counter() - t0
     dt_max = max(dist.all_gather_object(dt))
     if rank == 0:
-        names = {"mnist": "MNIST-MLP 784-128-128-10", "otto": "Otto-MLP 93-512-512-512-9",
-                 "wide": "Wide-MLP 4096-4096-4096-1000"}
+        names = NAMES
         line = {
             "metric": f"samples/sec (whole node) {names[args.model]} distributed {args.task}",
             "value": round(n * args.steps / dt_max, 1), "unit": "samples/s", "n_gpus": world,

@@ -22,10 +22,32 @@ from .plan import flatten_weights, unflatten_weights
 from .trainer import TrainerBase, prepare_features, prepare_targets, split_point
 
 
+class _Bf16OperandMatmul(torch.autograd.Function):
+    """fp32 x @ w with every matrix-core operand rounded to bf16 -- x and w forward, the
+    incoming gradient and the other operand in both backward products -- and fp32
+    products / sums: the arithmetic of the native engine's mixed_bfloat16 kernels
+    (bf16 MFMA operands, fp32 accumulation, fp32 masters), as a reference for them."""
+
+    @staticmethod
+    def forward(ctx, x, w):
+        xr, wr = x.bfloat16().float(), w.bfloat16().float()
+        ctx.save_for_backward(xr, wr)
+        return xr @ wr
+
+    @staticmethod
+    def backward(ctx, g):
+        xr, wr = ctx.saved_tensors
+        gr = g.bfloat16().float()
+        return gr @ wr.t(), xr.t() @ gr
+
+
 class TorchTrainer(TrainerBase):
     def __init__(self, model, plan, R: int = 1, batch_size: int = 32, device=None, seed: Optional[int] = None,
-                 hash_dropout_seed: Optional[int] = None):
+                 hash_dropout_seed: Optional[int] = None, bf16_operands: bool = False):
         super().__init__(model, plan, R, batch_size)
+        # True: every Dense product takes bf16-rounded operands (_Bf16OperandMatmul), the
+        # fp32 reference of the mixed_bfloat16 native kernels
+        self.bf16_operands = bool(bf16_operands)
         # None: dropout masks from torch's generator; an int: the native engine's
         # counter-hash masks for that executor seed (ops/dropout_hash.py), so the two
         # engines can be compared step for step with dropout on
@@ -97,7 +119,7 @@ class TorchTrainer(TrainerBase):
         for op in self.plan.ops:
             if isinstance(op, Dense):
                 dense += 1
-                h = h @ ps[wi]
+                h = _Bf16OperandMatmul.apply(h, ps[wi]) if self.bf16_operands else h @ ps[wi]
                 wi += 1
                 if op.use_bias:
                     h = h + ps[wi]

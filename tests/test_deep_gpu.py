@@ -68,8 +68,6 @@ def test_deep_matches_fp32_reference_with_same_masks(monkeypatch, name, in_dim, 
     unequal shard sizes, partial last batches, 2 epochs, every hand-off of every step):
     2..5 layers, widths that are not multiples of 16, biases off, SGD / Nesterov / Adam."""
     from elephas_amd.models import initializers, optimizers as O
-    from elephas_amd.ops.plan import build_plan
-    from elephas_amd.ops.torch_engine import TorchTrainer
     initializers.set_seed(31)
     model = _mlp(in_dim, list(hidden), out, dropout=drop, bias=bias)
     optim = {"sgd": O.SGD(0.2), "sgd_mom": O.SGD(0.05, momentum=0.9, nesterov=True), "adam": O.Adam(0.003)}[opt]
@@ -77,15 +75,21 @@ def test_deep_matches_fp32_reference_with_same_masks(monkeypatch, name, in_dim, 
     xs, ys = _shards([3 * B, 2 * B + B // 2], in_dim, out, seed=3)
     nat = _native(model, 2, B, monkeypatch=monkeypatch)
     assert nat.persistent and nat.persist_variant == 3, nat.plan_name()
-    ref = TorchTrainer(model, build_plan(model), 2, B, torch.device("cuda"), hash_dropout_seed=12345)
+    _compare_with_torch(nat, model, xs, ys, B, adaptive=opt == "adam")
+
+
+def _compare_with_torch(nat, model, xs, ys, B, adaptive=False, epochs=2):
+    from elephas_amd.ops.plan import build_plan
+    from elephas_amd.ops.torch_engine import TorchTrainer
+    ref = TorchTrainer(model, build_plan(model), len(xs), B, torch.device("cuda"), hash_dropout_seed=12345)
     w0 = nat.get_weights_flat()[0].copy()
     for t in (nat, ref):
         t.set_data(xs, ys, 0.0, shuffle=False)
-    hn = nat.fit(2)
-    hr = ref.fit(2)
+    hn = nat.fit(epochs)
+    hr = ref.fit(epochs)
     nat.check()
     wn, wr = nat.get_weights_flat(), ref.get_weights_flat()
-    if opt == "adam":   # adaptive rule: near-zero gradients amplify fp32 rounding
+    if adaptive:   # adaptive rule: near-zero gradients amplify fp32 rounding
         err = np.abs(wn - wr).mean() / np.abs(wr - w0).mean()
         assert err < 1e-3, err
     else:
@@ -94,6 +98,28 @@ def test_deep_matches_fp32_reference_with_same_masks(monkeypatch, name, in_dim, 
     for a, b in zip(hn, hr):
         np.testing.assert_allclose(a["loss"], b["loss"], rtol=1e-4)
         np.testing.assert_allclose(a["acc"], b["acc"], atol=1e-6)
+
+
+@pytest.mark.parametrize("hidden,B,opt", [
+    ((256, 128), 64, "sgd"), ((256, 128), 128, "sgd_mom"),
+    ((128,), 64, "sgd"), ((128,), 128, "adam"),
+    ((128, 128, 128), 64, "sgd_mom"), ((128, 128, 128), 128, "sgd"),
+    ((128, 128), 128, "sgd_mom"),
+])
+def test_mnist_family_shapes_stay_persistent(monkeypatch, hidden, B, opt):
+    """The persistent plans' shape coverage at the default planning (no override): MNIST-
+    family widths other than the headline's, B 64 and 128, momentum and Adam -- 8 replicas
+    as in the reference's local[8] job -- all run one launch per chunk of steps and train
+    as fp32 torch with the same masks."""
+    from elephas_amd.models import initializers, optimizers as O
+    initializers.set_seed(17)
+    model = _mlp(784, list(hidden), 10, dropout=0.2)
+    optim = {"sgd": O.SGD(0.1), "sgd_mom": O.SGD(0.05, momentum=0.9), "adam": O.Adam(0.001)}[opt]
+    model.compile(optim, "categorical_crossentropy", ["acc"])
+    xs, ys = _shards([2 * B] * 7 + [B + B // 3], 784, 10, seed=8)
+    nat = _native(model, 8, B, deep="-1", monkeypatch=monkeypatch)
+    assert nat.persistent, (nat.plan_name(), nat.plan_reason())
+    _compare_with_torch(nat, model, xs, ys, B, adaptive=opt == "adam", epochs=1)
 
 
 def test_deep_regression_generic_loss(monkeypatch):

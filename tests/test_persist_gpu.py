@@ -16,10 +16,10 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-def _mlp(in_dim, hidden, out, act="relu", out_act="softmax", dropout=0.0):
+def _mlp(in_dim, hidden, out, act="relu", out_act="softmax", dropout=0.0, bias0=True):
     from elephas_amd.models import Sequential, Dense, Dropout, Activation
     m = Sequential()
-    m.add(Dense(hidden[0], input_dim=in_dim))
+    m.add(Dense(hidden[0], input_dim=in_dim, use_bias=bias0))
     m.add(Activation(act))
     if dropout:
         m.add(Dropout(dropout))
@@ -53,24 +53,28 @@ def _trainer(model, R, B, persist, seed=12345, rowchain=None):
 
 
 @pytest.mark.parametrize("opt,hidden", [("sgd", (64, 64)), ("sgd_mom", (64, 64)), ("adam", (64, 64)),
-                                        ("sgd", (128, 64)), ("sgd_mom", (128, 64))])
+                                        ("sgd", (128, 64)), ("sgd_mom", (128, 64)), ("sgd_nobias0", (64, 64))])
 def test_persist_matches_fp32_reference_with_same_masks(opt, hidden):
     """Persistent plan == fp32 torch autograd with the same dropout masks (2 replicas,
     3 steps per epoch, 2 epochs: every hand-off of every step is exercised); equal and
-    unequal hidden widths."""
+    unequal hidden widths; a first Dense without bias under plain SGD stays off the V2
+    roles (their Gram correction carries the b0 update)."""
     from elephas_amd.models import initializers, optimizers as O
     from elephas_amd.ops.plan import build_plan
     from elephas_amd.ops.torch_engine import TorchTrainer
     initializers.set_seed(31)
-    model = _mlp(40, list(hidden), 6, dropout=0.3)
-    optim = {"sgd": O.SGD(0.2), "sgd_mom": O.SGD(0.05, momentum=0.9, nesterov=True),
+    model = _mlp(40, list(hidden), 6, dropout=0.3, bias0=opt != "sgd_nobias0")
+    optim = {"sgd": O.SGD(0.2), "sgd_nobias0": O.SGD(0.2), "sgd_mom": O.SGD(0.05, momentum=0.9, nesterov=True),
              "adam": O.Adam(0.003)}[opt]
     model.compile(optim, "categorical_crossentropy", ["acc"])
     xs, ys = _shards([96, 96], 40, 6, seed=3)
     nat = _trainer(model, 2, 32, persist=1)
     assert nat.persistent
-    # plain SGD + ReLU takes the V2 roles (Gram-corrected layer 0, DW workgroups)
-    assert nat.persist_variant == (2 if opt == "sgd" else 1), nat.plan_name()
+    # plain SGD + ReLU (+ a layer-0 bias) takes the V2 roles (Gram-corrected layer 0, DW workgroups)
+    if opt == "sgd_nobias0":
+        assert nat.persist_variant != 2, nat.plan_name()
+    else:
+        assert nat.persist_variant == (2 if opt == "sgd" else 1), nat.plan_name()
     ref = TorchTrainer(model, build_plan(model), 2, 32, torch.device("cuda"), hash_dropout_seed=12345)
     w0 = nat.get_weights_flat()[0].copy()
     for t in (nat, ref):
@@ -435,3 +439,45 @@ def test_persist_bf16_policy_matches_rowchain_bf16():
     for a, b in zip(out["p_bf16"][1], out["rc_bf16"][1]):
         np.testing.assert_allclose(a["loss"], b["loss"], rtol=1e-2, atol=1e-2)
     np.testing.assert_allclose(out["p_bf16"][2], out["rc_bf16"][2], rtol=3e-2, atol=3e-2)
+
+
+def test_persist_bf16_pinned_to_bf16_operand_torch():
+    """The bf16 persistent instance against an fp32 torch model whose Dense products take
+    bf16-rounded operands (forward and both backward products; fp32 sums, masters and
+    update -- TorchTrainer(bf16_operands=True)) with the same dropout masks.  The bf16 row
+    chain (no Gram re-association) sits on that model within fp32 summation order and
+    bf16 rounding-boundary flips, far below the bf16-vs-fp32 gap; the persistent V2 roles
+    (whose layer 0 re-associates X_i W0_i through the Gram correction, so W0 enters the
+    products rounded one step earlier) stay well inside that gap too."""
+    from elephas_amd import config
+    from elephas_amd.models import initializers
+    from elephas_amd.models.optimizers import SGD
+    from elephas_amd.ops.plan import build_plan
+    from elephas_amd.ops.native_engine import NativeTrainer
+    from elephas_amd.ops.torch_engine import TorchTrainer
+    initializers.set_seed(15)
+    model = _mlp(784, [128, 128], 10, dropout=0.2)
+    model.compile(SGD(learning_rate=0.1), "categorical_crossentropy", ["acc"])
+    xs, ys = _shards([640] * 8, 784, 10, seed=19)
+    out = {}
+    for name, persist in (("p_bf16", 1), ("rc_bf16", 0)):
+        t = NativeTrainer(model, build_plan(model), 8, 64, torch.device("cuda"), seed=9, persist=persist,
+                          rowchain=None if persist else 1, policy="mixed_bfloat16")
+        assert t.persistent == bool(persist), t.plan_name()
+        w0 = t.get_weights_flat()
+        t.set_data(xs, ys, 0.0, shuffle=False)
+        h = t.fit(2)
+        out[name] = (t.get_weights_flat(), h)
+    config.set_policy("float32")
+    for name, b16 in (("emul", True), ("f32", False)):
+        t = TorchTrainer(model, build_plan(model), 8, 64, torch.device("cuda"), hash_dropout_seed=9, bf16_operands=b16)
+        t.set_data(xs, ys, 0.0, shuffle=False)
+        out[name] = (t.get_weights_flat(), t.fit(2))
+    dist = lambda a, b: float(np.abs(out[a][0] - out[b][0]).mean() / np.abs(out[b][0] - w0).mean())
+    gap, d_rc, d_p = dist("f32", "emul"), dist("rc_bf16", "emul"), dist("p_bf16", "emul")
+    print(f"bf16 pin: emul-vs-f32 {gap:.3e}  rowchain-vs-emul {d_rc:.3e}  persistent-vs-emul {d_p:.3e}")
+    assert d_rc <= 0.25 * gap, (d_rc, gap)
+    assert d_p <= 1.0 * gap, (d_p, gap)
+    for name in ("p_bf16", "rc_bf16"):
+        for a, b in zip(out[name][1], out["emul"][1]):
+            np.testing.assert_allclose(a["loss"], b["loss"], rtol=5e-3)
