@@ -319,7 +319,14 @@ struct DeepArgs {
   long long* ctr;
   unsigned long long seed;
   float* ws; long long ws_stride;   // per-replica workspace (floats)
-  unsigned* flags;                  // [R][2][DP_MAXWG] GO / phase counters, zero at launch
+  unsigned* flags;                  // [R][4][DP_MAXWG] GO / phase / exchange counters, zero at launch
+  // per-step synchronous replicas (sync != 0): every workgroup's weight-gradient tile goes
+  // through the exchange buffer xg -- partial tiles [R][nw][XT], then the replica sums
+  // [nw][XT]; in a tile, W_0[:, J]^T at 0 ([16][Kx0]), b_0[J] at x_b0, rows J of W_l at
+  // x_w[l] ([16][N16_l]) and b_l at x_b[l] (l >= 1)
+  int sync, XT, x_b0;
+  int x_w[DP_MAXL], x_b[DP_MAXL];
+  float* xg;
   unsigned* err;                    // sticky error word (PmErr codes)
   long long timeout;                // spin limit in s_memrealtime ticks
   long long* stamps;                // diagnostics: [block][DP_STAMP_STEPS][32] s_memrealtime (null = off)

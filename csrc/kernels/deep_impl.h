@@ -98,8 +98,9 @@ __device__ __forceinline__ void lds_barrier() {
   asm volatile("" ::: "memory");
 }
 
+// kinds: 0 GO (residency), 1 phase counter, 2 / 3 exchange (partial tile out / slice summed)
 __device__ __forceinline__ unsigned* dflag(const DeepArgs& a, int r, int kind) {
-  return a.flags + ((long long)r * 2 + kind) * DP_MAXWG;
+  return a.flags + ((long long)r * 4 + kind) * DP_MAXWG;
 }
 
 // R1 publish of phase `tag`: every storing wave drains its sc1 stores, the workgroup
@@ -175,6 +176,8 @@ __device__ __forceinline__ void dstamp(const DeepArgs& a, int s, int k) {
 struct Ctx {
   int r, j, tid, lane, w, g, c16;
   rsrc_t rs;           // the replica's workspace
+  rsrc_t xs;           // sync: the exchange buffer (partial tiles, then replica sums)
+  long long xp;        // sync: this workgroup's partial tile in it
   float* P;            // the replica's masters
   float* S;            // the replica's optimizer state (null: none)
   int* prow;           // LDS: the batch rows of two steps [2][DP_ROWS] (by step parity)
@@ -518,8 +521,9 @@ __device__ __forceinline__ void tail_phase(const DeepArgs& a, float* smem, const
 }
 
 // ---- weight gradient of the last layer, rows J (= column tile j of layer L-2) and (on
-//      workgroup 0) its bias; images of the updated rows for the next tail
-template <int L, bool SGD0>
+//      workgroup 0) its bias; images of the updated rows for the next tail (SYNC: the
+//      gradient goes to the exchange tile instead, the update comes after the replica sum)
+template <int L, bool SGD0, bool SYNC>
 __device__ __forceinline__ void dw_last(const DeepArgs& a, float* smem, const Ctx& x0, const OptStep& os) {
   const Ctx x = lanes(x0);
   const DeepLayer la = a.ly[L - 2], lb = a.ly[L - 1];
@@ -546,34 +550,43 @@ __device__ __forceinline__ void dw_last(const DeepArgs& a, float* smem, const Ct
     }
     float* wr = smem + lb.l_w;
     const int c = 16 * ct + x.c16;
-    f32x4 wv;
+    if constexpr (SYNC) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int ip = 4 * x.g + q;
-      float wt = wr[ip * ldc + c];
-      if (I0 + ip < lb.K && c < C) {
-        wt = upd<SGD0>(a, x, os, lb.p_off + (long long)(I0 + ip) * C + c, wt, acc[q]);
-        wr[ip * ldc + c] = wt;
-        st1(x.rs, (I0 + ip) * C16 + c, lb.o_w, wt);
+      for (int q = 0; q < 4; ++q) st1(x.xs, (4 * x.g + q) * C16 + c, x.xp + a.x_w[L - 1], acc[q]);
+    } else {
+      f32x4 wv;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int ip = 4 * x.g + q;
+        float wt = wr[ip * ldc + c];
+        if (I0 + ip < lb.K && c < C) {
+          wt = upd<SGD0>(a, x, os, lb.p_off + (long long)(I0 + ip) * C + c, wt, acc[q]);
+          wr[ip * ldc + c] = wt;
+          st1(x.rs, (I0 + ip) * C16 + c, lb.o_w, wt);
+        }
+        wv[q] = wt;
       }
-      wv[q] = wt;
+      st4(x.rs, c * lb.Kx + I0 + 4 * x.g, lb.o_wt, wv);
     }
-    st4(x.rs, c * lb.Kx + I0 + 4 * x.g, lb.o_wt, wv);
   }
   if (bias && x.tid >= 448 && x.tid - 448 < C) {   // the last wave: one unit per lane
     const int c = x.tid - 448;
     float db = 0.f;
     for (int row = 0; row < a.Bp; ++row) db += sd[row * ldc + c];
-    float* bl = smem + lb.l_b;
-    const float b = upd<SGD0>(a, x, os, lb.p_off + (long long)lb.K * C + c, bl[c], db);
-    bl[c] = b;
-    st1(x.rs, c, a.o_bl, b);
+    if constexpr (SYNC) {
+      st1(x.xs, c, x.xp + a.x_b[L - 1], db);
+    } else {
+      float* bl = smem + lb.l_b;
+      const float b = upd<SGD0>(a, x, os, lb.p_off + (long long)lb.K * C + c, bl[c], db);
+      bl[c] = b;
+      st1(x.rs, c, a.o_bl, b);
+    }
   }
   __syncthreads();   // the staging is reused by the next phase
 }
 
 // ---- column sums of dZ_l[:, J] (the bias gradient of tile j of layer l) -> b_l[J]
-template <int l, bool SGD0>
+template <int l, bool SGD0, bool SYNC>
 __device__ __forceinline__ void bias_tile(const DeepArgs& a, float* smem, const Ctx& x0, long long o_dz, int N16,
                                           const OptStep& os) {
   const Ctx x = lanes(x0);
@@ -593,8 +606,12 @@ __device__ __forceinline__ void bias_tile(const DeepArgs& a, float* smem, const 
   if (x.tid < 16 && J0 + x.tid < ly.N) {
     float db = 0.f;
     for (int k = 0; k < NTH / 16; ++k) db += red[x.tid + 16 * k];
-    float* bt = smem + ly.l_b;
-    bt[x.tid] = upd<SGD0>(a, x, os, ly.p_off + (long long)ly.K * ly.N + J0 + x.tid, bt[x.tid], db);
+    if constexpr (SYNC) {
+      st1(x.xs, x.tid, x.xp + a.x_b[l], db);
+    } else {
+      float* bt = smem + ly.l_b;
+      bt[x.tid] = upd<SGD0>(a, x, os, ly.p_off + (long long)ly.K * ly.N + J0 + x.tid, bt[x.tid], db);
+    }
   }
   __syncthreads();
 }
@@ -604,13 +621,13 @@ __device__ __forceinline__ void bias_tile(const DeepArgs& a, float* smem, const 
 //      DW_l[J, chunk] = A_{l-1}[:, J]^T dZ_chunk (waves = 4 column tiles x 2 row halves),
 //      update of the chunk's masters + their W^T image segment; finally dZ_{l-1}[:, J] =
 //      dA * G_{l-1} -> workspace (l >= 2) or the LDS dZ_0^T stripe (l = 1)
-template <int L, int l, bool SGD0>
+template <int L, int l, bool SGD0, bool SYNC>
 __device__ __forceinline__ void bw_phase(const DeepArgs& a, float* smem, const Ctx& x0, const OptStep& os,
                                          const f32x4 (&G)[L - 1]) {
   const Ctx x = lanes(x0);
   const DeepLayer lp = a.ly[l - 1], ly = a.ly[l];
   if (x.j >= lp.T) {   // no row tile of W_l here; maybe its bias tile (layer l wider than l - 1)
-    bias_tile<l, SGD0>(a, smem, x, ly.o_dz, ly.N16, os);
+    bias_tile<l, SGD0, SYNC>(a, smem, x, ly.o_dz, ly.N16, os);
     return;
   }
   // this workgroup's bias tile j of layer l: summed from the staged chunk that holds it
@@ -682,11 +699,20 @@ __device__ __forceinline__ void bw_phase(const DeepArgs& a, float* smem, const C
       float db = 0.f;
 #pragma unroll
       for (int k = 0; k < 16; ++k) db += bred[x.tid + 16 * k];
-      float* bt = smem + ly.l_b;
-      bt[x.tid] = upd<SGD0>(a, x, os, ly.p_off + (long long)ly.K * ly.N + 16 * x.j + x.tid, bt[x.tid], db);
+      if constexpr (SYNC) {
+        st1(x.xs, x.tid, x.xp + a.x_b[l], db);
+      } else {
+        float* bt = smem + ly.l_b;
+        bt[x.tid] = upd<SGD0>(a, x, os, ly.p_off + (long long)ly.K * ly.N + 16 * x.j + x.tid, bt[x.tid], db);
+      }
     }
     lds_barrier();
-    if (hh == 0 && 16 * f < cw) {
+    if (SYNC && hh == 0 && 16 * f < cw) {   // the gradient rows J of the chunk's column tile f
+      accW += lds4(spart + (f * 64 + x.lane) * 4);
+      const int col = c0 + 16 * f + x.c16;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) st1(x.xs, (4 * x.g + q) * ly.N16 + col, x.xp + a.x_w[l], accW[q]);
+    } else if (!SYNC && hh == 0 && 16 * f < cw) {
       accW += lds4(spart + (f * 64 + x.lane) * 4);
       const int col = c0 + 16 * f + x.c16;
       f32x4 wv;
@@ -725,7 +751,7 @@ __device__ __forceinline__ void bw_phase(const DeepArgs& a, float* smem, const C
 //      DW_0[:, J] = X^T dZ_0[:, J] (waves = 64-feature groups; the X rows of that step,
 //      float4 along the features: MFMA e of lane group g takes batch row 16 rr + 4 g + e,
 //      output tile f the features i0 + 4 m + f), bias, in-place update of W_0^T
-template <int L, bool SGD0>
+template <int L, bool SGD0, bool SYNC>
 __device__ __forceinline__ void dw0_phase(const DeepArgs& a, float* smem, const Ctx& x0, int sp, const OptStep& os) {
   const Ctx x = lanes(x0);
   const DeepLayer l0 = a.ly[0];
@@ -736,8 +762,12 @@ __device__ __forceinline__ void dw0_phase(const DeepArgs& a, float* smem, const 
   if (x.tid < 16 && l0.has_bias && J0 + x.tid < l0.N) {
     float db = 0.f;
     for (int row = 0; row < Bp; ++row) db += dz0[x.tid * ldz + row];
-    float* bt = smem + l0.l_b;
-    bt[x.tid] = upd<SGD0>(a, x, os, l0.p_off + (long long)l0.K * l0.N + J0 + x.tid, bt[x.tid], db);
+    if constexpr (SYNC) {
+      st1(x.xs, x.tid, x.xp + a.x_b0, db);
+    } else {
+      float* bt = smem + l0.l_b;
+      bt[x.tid] = upd<SGD0>(a, x, os, l0.p_off + (long long)l0.K * l0.N + J0 + x.tid, bt[x.tid], db);
+    }
   }
   const int nfg = (Kx + 63) >> 6;
   const int* prow = x.prow + (sp & 1) * DP_ROWS;
@@ -781,6 +811,10 @@ __device__ __forceinline__ void dw0_phase(const DeepArgs& a, float* smem, const 
     for (int q = 0; q < 4; ++q) {
       const int ib = i0 + 16 * x.g + 4 * q;
       if (ib >= Kx) continue;
+      if constexpr (SYNC) {   // W_0[:, J]^T gradient, [16][Kx0] in the exchange tile
+        st4(x.xs, x.c16 * Kx + ib, x.xp, f32x4{acc[0][q], acc[1][q], acc[2][q], acc[3][q]});
+        continue;
+      }
       f32x4 wv = lds4(w0t + x.c16 * ld0 + ib);
 #pragma unroll
       for (int ff = 0; ff < 4; ++ff) {
@@ -824,25 +858,153 @@ __device__ __forceinline__ bool fwd_chain(const DeepArgs& a, float* smem, const 
 }
 
 // the backward phases of layers l .. 1 (BW_{L-2} also runs the last layer's update)
-template <int L, int l, bool SGD0>
+template <int L, int l, bool SGD0, bool SYNC>
 __device__ __forceinline__ bool bw_chain(const DeepArgs& a, float* smem, const Ctx& x, int s, const OptStep& os,
                                          unsigned base, const f32x4 (&G)[L - 1]) {
   if constexpr (l >= 1) {
     const unsigned p = (unsigned)(L + (L - 2 - l));
     if (!wait_phase(a, x.r, base + p)) return false;
     dstamp(a, s, 11 + 2 * (L - 2 - l));
-    if constexpr (l == L - 2) dw_last<L, SGD0>(a, smem, x, os);
-    bw_phase<L, l, SGD0>(a, smem, x, os, G);
+    if constexpr (l == L - 2) dw_last<L, SGD0, SYNC>(a, smem, x, os);
+    bw_phase<L, l, SGD0, SYNC>(a, smem, x, os, G);
     publish(a, x.r, x.j, base + p + 1);
     dstamp(a, s, 12 + 2 * (L - 2 - l));
-    return bw_chain<L, l - 1, SGD0>(a, smem, x, s, os, base, G);
+    return bw_chain<L, l - 1, SGD0, SYNC>(a, smem, x, s, os, base, G);
   }
+  return true;
+}
+
+// ---- per-step synchronous replicas: the exchange of workgroup j's weight-gradient tile
+//      with workgroup j of every other replica (flag kinds 2 / 3, tag = step + 1)
+__device__ __forceinline__ void publish_x(const DeepArgs& a, const Ctx& x, int kind, unsigned tag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0)
+    __hip_atomic_store((gu32*)(dflag(a, x.r, kind) + x.j), tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ bool wait_x(const DeepArgs& a, int j, int kind, unsigned tag) {
+  int ok = 1;
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    const unsigned long long t0 = wall_clock64();
+    for (;;) {
+      bool all = true;
+      for (int rr = lane; rr < a.R; rr += 64)
+        all &= __hip_atomic_load((gu32*)(dflag(a, rr, kind) + j), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= tag;
+      if (__all(all)) break;
+      if ((long long)(wall_clock64() - t0) > a.timeout) {
+        ok = 0;
+        if (lane == 0) __hip_atomic_store((gu32*)(a.err), (unsigned)PERR_CHAIN_PREV, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  ok = __syncthreads_and(ok);
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  return ok != 0;
+}
+
+// the summed gradient tile (sum0) applied to the owned masters by every replica alike --
+// the same sums and the same state, so the replicas stay one model bit for bit -- with the
+// images the other workgroups read (W_l^T segments, the last layer's rows and bias)
+template <int L, bool SGD0>
+__device__ __forceinline__ void apply_sums(const DeepArgs& a, float* smem, const Ctx& x0, long long sum0,
+                                           const OptStep& os) {
+  const Ctx x = lanes(x0);
+  const DeepLayer l0 = a.ly[0];
+  if (x.j < l0.T) {
+    const int J0 = 16 * x.j, Kx = l0.Kx, ld0 = Kx + 4, q4 = Kx >> 2;
+    float* w0t = smem + l0.l_w;
+    for (int e = x.tid; e < 16 * q4; e += NTH) {
+      const int c = e / q4, k = 4 * (e - c * q4);
+      const f32x4 g = ld4(x.xs, c * Kx + k, sum0);
+      f32x4 w = lds4(w0t + c * ld0 + k);
+#pragma unroll
+      for (int ff = 0; ff < 4; ++ff)
+        if (k + ff < l0.K && J0 + c < l0.N)
+          w[ff] = upd<SGD0>(a, x, os, l0.p_off + (long long)(k + ff) * l0.N + J0 + c, w[ff], g[ff]);
+      lds4(w0t + c * ld0 + k, w);
+    }
+    if (x.tid < 16 && l0.has_bias && J0 + x.tid < l0.N) {
+      float* bt = smem + l0.l_b;
+      bt[x.tid] = upd<SGD0>(a, x, os, l0.p_off + (long long)l0.K * l0.N + J0 + x.tid, bt[x.tid],
+                            ld1(x.xs, a.x_b0 + x.tid, sum0));
+    }
+  }
+#pragma unroll
+  for (int l = 1; l < L; ++l) {
+    const DeepLayer ly = a.ly[l], lp = a.ly[l - 1];
+    if (x.j < lp.T) {   // rows J of W_l: 4-row groups q x columns c (consecutive threads, consecutive c)
+      const int I0 = 16 * x.j, N16 = ly.N16, ldr = N16 + 4;
+      float* wr = smem + ly.l_w;
+      for (int e = x.tid; e < 4 * N16; e += NTH) {
+        const int q = e / N16, c = e - q * N16;
+        f32x4 g, w;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) g[k] = ld1(x.xs, a.x_w[l] + (4 * q + k) * N16 + c, sum0);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int ip = 4 * q + k;
+          float wt = wr[ip * ldr + c];
+          if (I0 + ip < ly.K && c < ly.N) {
+            wt = upd<SGD0>(a, x, os, ly.p_off + (long long)(I0 + ip) * ly.N + c, wt, g[k]);
+            wr[ip * ldr + c] = wt;
+          }
+          w[k] = wt;
+        }
+        st4(x.rs, c * ly.Kx + I0 + 4 * q, ly.o_wt, w);
+        if (l == L - 1) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) st1(x.rs, (I0 + 4 * q + k) * N16 + c, ly.o_w, w[k]);
+        }
+      }
+    }
+    if (l < L - 1) {
+      if (x.j < ly.T && ly.has_bias && x.tid < 16 && 16 * x.j + x.tid < ly.N) {
+        float* bt = smem + ly.l_b;
+        bt[x.tid] = upd<SGD0>(a, x, os, ly.p_off + (long long)ly.K * ly.N + 16 * x.j + x.tid, bt[x.tid],
+                              ld1(x.xs, a.x_b[l] + x.tid, sum0));
+      }
+    } else if (x.j == 0 && ly.has_bias && x.tid < ly.N) {
+      float* bl = smem + ly.l_b;
+      const float b = upd<SGD0>(a, x, os, ly.p_off + (long long)ly.K * ly.N + x.tid, bl[x.tid],
+                                ld1(x.xs, a.x_b[l] + x.tid, sum0));
+      bl[x.tid] = b;
+      st1(x.rs, x.tid, a.o_bl, b);
+    }
+  }
+}
+
+// partial tile out -> all replicas' tiles out -> slice r summed in replica order -> all
+// slices summed -> the update
+template <int L, bool SGD0>
+__device__ __forceinline__ bool exchange(const DeepArgs& a, float* smem, const Ctx& x0, int s, const OptStep& os) {
+  const Ctx x = lanes(x0);
+  const unsigned tag = (unsigned)s + 1;
+  publish_x(a, x, 2, tag);
+  if (!wait_x(a, x.j, 2, tag)) return false;
+  dstamp(a, s, 25);
+  const long long sum0 = ((long long)a.R * a.nw + x.j) * a.XT;
+  const int q4 = a.XT >> 2, per = (q4 + a.R - 1) / a.R;
+  const int e1 = (x.r + 1) * per < q4 ? (x.r + 1) * per : q4;
+  for (int e = x.r * per + x.tid; e < e1; e += NTH) {
+    f32x4 v = z4();
+    for (int rr = 0; rr < a.R; ++rr) v += ld4(x.xs, 4 * e, ((long long)rr * a.nw + x.j) * a.XT);
+    st4(x.xs, 4 * e, sum0, v);
+  }
+  publish_x(a, x, 3, tag);
+  if (!wait_x(a, x.j, 3, tag)) return false;
+  dstamp(a, s, 26);
+  apply_sums<L, SGD0>(a, smem, x, sum0, os);
+  __syncthreads();
+  dstamp(a, s, 27);
   return true;
 }
 
 }  // namespace
 
-template <int L, bool FAST, bool SGD0>
+template <int L, bool FAST, bool SGD0, bool SYNC>
 __global__ __launch_bounds__(512) void mlp_deep_kernel(DeepArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   if (__hip_atomic_load((gu32*)(a.err), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) return;
@@ -855,6 +1017,8 @@ __global__ __launch_bounds__(512) void mlp_deep_kernel(DeepArgs a) {
   x.g = x.lane >> 4;
   x.c16 = x.lane & 15;
   x.rs = ws_rsrc(a.ws + (long long)x.r * a.ws_stride);
+  x.xs = ws_rsrc(SYNC ? a.xg : a.ws);
+  x.xp = SYNC ? ((long long)x.r * a.nw + x.j) * a.XT : 0;
   x.P = a.P + (long long)x.r * a.sP;
   x.S = a.S ? a.S + (long long)x.r * a.sS : nullptr;
   x.prow = reinterpret_cast<int*>(smem + a.lds_floats - 2 * DP_ROWS);
@@ -945,14 +1109,14 @@ __global__ __launch_bounds__(512) void mlp_deep_kernel(DeepArgs a) {
         x.prow[(s & 1) * DP_ROWS + y.tid] = y.tid < valid ? pr[y.tid] : 0;
       }
     }
-    if (last >= 0) {
+    if (!SYNC && last >= 0) {
       if constexpr (L == 2) {
         if (!wait_phase(a, x.r, base)) return;
-        dw_last<L, SGD0>(a, smem, x, lastos);
+        dw_last<L, SGD0, false>(a, smem, x, lastos);
         load_dz0(a, smem, x);
       }
       __syncthreads();
-      dw0_phase<L, SGD0>(a, smem, x, last, lastos);
+      dw0_phase<L, SGD0, false>(a, smem, x, last, lastos);
     }
     __syncthreads();
     dstamp(a, s, 1);
@@ -965,19 +1129,30 @@ __global__ __launch_bounds__(512) void mlp_deep_kernel(DeepArgs a) {
     tail_phase<L, FAST>(a, smem, x, s, valid);
     publish(a, x.r, x.j, base + L);
     dstamp(a, s, 10);
-    if (!bw_chain<L, L - 2, SGD0>(a, smem, x, s, os, base, G)) return;
+    if (!bw_chain<L, L - 2, SGD0, SYNC>(a, smem, x, s, os, base, G)) return;
+    if constexpr (SYNC) {   // every gradient of the step into the exchange tile, then the exchange
+      if constexpr (L == 2) {
+        if (!wait_phase(a, x.r, base + NPH)) return;
+        dw_last<L, SGD0, true>(a, smem, x, os);
+        load_dz0(a, smem, x);
+      }
+      __syncthreads();
+      dw0_phase<L, SGD0, true>(a, smem, x, s, os);
+      dstamp(a, s, 24);
+      if (!exchange<L, SGD0>(a, smem, x, s, os)) return;
+    }
     last = s;
     lastos = os;
   }
   // the pending layer-0 update of the last step that ran
-  if (last >= 0) {
+  if (!SYNC && last >= 0) {
     if constexpr (L == 2) {
       if (!wait_phase(a, x.r, (unsigned)(last + 1) * NPH)) return;
-      dw_last<L, SGD0>(a, smem, x, lastos);
+      dw_last<L, SGD0, false>(a, smem, x, lastos);
       load_dz0(a, smem, x);
     }
     __syncthreads();
-    dw0_phase<L, SGD0>(a, smem, x, last, lastos);
+    dw0_phase<L, SGD0, false>(a, smem, x, last, lastos);
   }
   __syncthreads();
   // ---- epilogue: the owned masters back to P
@@ -1016,28 +1191,33 @@ __global__ __launch_bounds__(512) void mlp_deep_kernel(DeepArgs a) {
 namespace {
 // dynamic LDS above the default limit: raised once per instantiation (to the largest the
 // device allows, so later launches with other layouts need no call)
-template <int L, bool F, bool SG>
+template <int L, bool F, bool SG, bool SY>
 hipError_t deep_launch_one(const DeepArgs* a, hipStream_t s) {
   static const bool done = [] {
     int dev = 0, mx = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&mx, hipDeviceAttributeMaxSharedMemoryPerBlock, dev);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&mlp_deep_kernel<L, F, SG>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&mlp_deep_kernel<L, F, SG, SY>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, mx);
     return true;
   }();
   (void)done;
-  hipLaunchKernelGGL((mlp_deep_kernel<L, F, SG>), dim3(a->R * a->nw), dim3(NTH), sizeof(float) * (size_t)a->lds_floats,
-                     s, *a);
+  hipLaunchKernelGGL((mlp_deep_kernel<L, F, SG, SY>), dim3(a->R * a->nw), dim3(NTH),
+                     sizeof(float) * (size_t)a->lds_floats, s, *a);
   return hipGetLastError();
+}
+
+template <int L, bool SY>
+hipError_t deep_launch_sy(const DeepArgs* a, bool fast, bool sgd0, hipStream_t s) {
+  if (fast && sgd0) return deep_launch_one<L, true, true, SY>(a, s);
+  if (fast) return deep_launch_one<L, true, false, SY>(a, s);
+  if (sgd0) return deep_launch_one<L, false, true, SY>(a, s);
+  return deep_launch_one<L, false, false, SY>(a, s);
 }
 
 template <int L>
 hipError_t deep_launch(const DeepArgs* a, bool fast, bool sgd0, hipStream_t s) {
-  if (fast && sgd0) return deep_launch_one<L, true, true>(a, s);
-  if (fast) return deep_launch_one<L, true, false>(a, s);
-  if (sgd0) return deep_launch_one<L, false, true>(a, s);
-  return deep_launch_one<L, false, false>(a, s);
+  return a->sync ? deep_launch_sy<L, true>(a, fast, sgd0, s) : deep_launch_sy<L, false>(a, fast, sgd0, s);
 }
 }  // namespace
 

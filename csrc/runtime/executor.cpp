@@ -58,6 +58,7 @@ Executor::~Executor() {
   if (d_pflags_) (void)hipFree(d_pflags_);
   if (d_perr_) (void)hipFree(d_perr_);
   if (d_dws_) (void)hipFree(d_dws_);
+  if (d_dxg_) (void)hipFree(d_dxg_);
   if (d_dflags_) (void)hipFree(d_dflags_);
 }
 
@@ -218,7 +219,6 @@ bool Executor::build_deep() {
   const int L = (int)c_.layers.size();
   if (L < 2 || L > DP_MAXL) return no_dp("layer pipeline: 2..5 Dense layers");
   if (c_.bf16) return no_dp("layer pipeline: fp32 only");
-  if (c_.persist_sync) return no_dp("layer pipeline: independent replicas (fit granularity) only");
   if (c_.B < 1 || c_.B > DP_ROWS || c_.ldy > 32 || (c_.ldx % 8) != 0) return no_dp("layer pipeline: batch <= 128 rows per replica");
   const LayerCfg& lastc = c_.layers[L - 1];
   if (lastc.N > DP_MAXC) return no_dp("layer pipeline: a last layer of <= 32 units");
@@ -295,10 +295,24 @@ bool Executor::build_deep() {
   a.ctr = reinterpret_cast<long long*>(c_.ctr);
   a.seed = c_.seed;
   a.ws_stride = ws;
+  // per-step synchronous replicas: the gradient-tile layout of the exchange buffer
+  a.sync = c_.persist_sync ? 1 : 0;
+  if (a.sync) {
+    int xt = 16 * a.ly[0].Kx;
+    a.x_b0 = xt; xt += 16;
+    for (int l = 1; l < L; ++l) {
+      a.x_w[l] = xt; xt += 16 * a.ly[l].N16;
+      a.x_b[l] = xt; xt += 32;
+    }
+    a.XT = (xt + 63) / 64 * 64;
+    const size_t xb = sizeof(float) * (size_t)a.XT * (size_t)(c_.R + 1) * (size_t)nw;
+    check(hipMalloc(&d_dxg_, xb), "hipMalloc(layer pipeline exchange buffer)");
+    a.xg = d_dxg_;
+  }
   const size_t ws_bytes = sizeof(float) * (size_t)ws * c_.R;
   check(hipMalloc(&d_dws_, ws_bytes), "hipMalloc(layer pipeline workspace)");
   check(hipMemset(d_dws_, 0, ws_bytes), "hipMemset(layer pipeline workspace)");
-  dp_.flag_bytes = sizeof(unsigned) * (size_t)c_.R * 2 * DP_MAXWG;
+  dp_.flag_bytes = sizeof(unsigned) * (size_t)c_.R * 4 * DP_MAXWG;
   check(hipMalloc(&d_dflags_, dp_.flag_bytes), "hipMalloc(layer pipeline flags)");
   check(hipMemset(d_dflags_, 0, dp_.flag_bytes), "hipMemset(layer pipeline flags)");
   if (!d_perr_) {
@@ -376,7 +390,7 @@ std::vector<unsigned> Executor::rank_exchange_selftest(int nsteps, int corrupt) 
 }
 
 std::vector<int> Executor::persist_variant() const {
-  if (dp_.on) return {3, 0, 0};
+  if (dp_.on) return {3, 0, dp_.args.sync};
   if (!pm_.on) return {};
   return {pm_.args.v2 ? 2 : 1, pm_.args.nd, pm_.args.sync};
 }

@@ -218,6 +218,7 @@ class Executor {
     size_t flag_bytes = 0;
   } dp_;
   float* d_dws_ = nullptr;         // its per-replica workspace (activations, gradients, weight images)
+  float* d_dxg_ = nullptr;         // its exchange buffer (per-step synchronous replicas)
   unsigned* d_dflags_ = nullptr;   // [R][2][DP_MAXWG] GO / phase counters
   bool build_deep();
   std::string why_pm_, why_dp_;   // why the persistent plans were not eligible (plan_reason)

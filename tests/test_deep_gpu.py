@@ -118,7 +118,7 @@ def test_mnist_family_shapes_stay_persistent(monkeypatch, hidden, B, opt):
     model.compile(optim, "categorical_crossentropy", ["acc"])
     xs, ys = _shards([2 * B] * 7 + [B + B // 3], 784, 10, seed=8)
     nat = _native(model, 8, B, deep="-1", monkeypatch=monkeypatch)
-    assert nat.persistent, (nat.plan_name(), nat.plan_reason())
+    assert nat.persistent, (nat.plan_name(), nat.plan_reason)
     _compare_with_torch(nat, model, xs, ys, B, adaptive=opt == "adam", epochs=1)
 
 
@@ -233,3 +233,55 @@ def test_deep_oversubscribed_grid_falls_back(monkeypatch):
     assert np.array_equal(t.get_weights_flat(), ref.get_weights_flat())
     for a, b in zip(h, hr):
         np.testing.assert_allclose(a["loss"], b["loss"], rtol=1e-6)
+
+
+@pytest.mark.parametrize("name,in_dim,hidden,out,B,opt", [
+    ("otto_like", 93, (256, 256, 128), 9, 128, "sgd"),
+    ("mnist_mom", 784, (128, 128), 10, 64, "sgd_mom"),
+    ("l2_adam", 40, (100,), 7, 32, "adam"),
+])
+def test_deep_sync_replicas_match_eager_exchange(monkeypatch, name, in_dim, hidden, out, B, opt):
+    """Per-step synchronous DP on the layer pipeline (every workgroup's weight-gradient tile
+    summed over the replicas inside the launch -- reduce-scatter in replica order, then
+    every replica applies the same sums): the replicas stay bit-identical, and both it and
+    the eager per-step path (forward / backward, replica sum of G, apply) equal ONE fp32
+    torch model trained on the replicas' batches stacked (no dropout: no masks to match)."""
+    from elephas_amd.models import initializers, optimizers as O
+    from elephas_amd.ops.plan import build_plan
+    from elephas_amd.ops.native_engine import NativeTrainer
+    from elephas_amd.ops.torch_engine import TorchTrainer
+    from elephas_amd import config
+    config.set_policy("float32")
+    initializers.set_seed(12)
+    model = _mlp(in_dim, list(hidden), out)
+    optim = {"sgd": O.SGD(0.05), "sgd_mom": O.SGD(0.05, momentum=0.9), "adam": O.Adam(0.002)}[opt]
+    model.compile(optim, "categorical_crossentropy", ["acc"])
+    R, steps = 4, 5
+    xs, ys = _shards([B * steps] * R, in_dim, out, seed=13)
+    monkeypatch.setenv("ELEPHAS_AMD_DEEP", "2")
+    out_w = []
+    for persist in (1, 0):
+        t = NativeTrainer(model, build_plan(model), R, B, torch.device("cuda"), seed=5, persist=persist, sync=True)
+        assert t.persistent == bool(persist)
+        if persist:
+            assert t.persist_variant == 3 and t.exe.persist_variant()[2] == 1, t.plan_name()
+        w0 = t.get_weights_flat()[0].copy()
+        t.set_data(xs, ys, 0.0, shuffle=False)
+        t.fit(2)
+        t.check()
+        out_w.append(t.get_weights_flat())
+    xc = np.concatenate([np.concatenate([x[i * B:(i + 1) * B] for x in xs]) for i in range(steps)])
+    yc = np.concatenate([np.concatenate([y[i * B:(i + 1) * B] for y in ys]) for i in range(steps)])
+    ref = TorchTrainer(model, build_plan(model), 1, R * B, torch.device("cuda"))
+    ref.set_data([xc], [yc], 0.0, shuffle=False)
+    ref.fit(2)
+    wt = ref.get_weights_flat()[0]
+    for label, w in zip(("in-launch", "eager"), out_w):
+        for r in range(1, R):
+            assert np.array_equal(w[r], w[0]), (label, r)
+        if opt == "adam":
+            err = np.abs(w[0] - wt).mean() / np.abs(wt - w0).mean()
+            assert err < 1e-3, (label, err)
+        else:
+            err = np.abs(w[0] - wt).max() / np.abs(wt - w0).max()
+            assert err < 1e-3, (label, err)

@@ -55,7 +55,7 @@ def main():
     print("plan", t.plan_name())
     geo = t.exe.deep_geometry()
     if not geo:
-        print("not on the layer pipeline:", t.plan_reason())
+        print("not on the layer pipeline:", t.plan_reason)
         return
     nw, grid, rt, ks, lds = geo
     print(f"nw {nw} grid {grid} RT {rt} KS {ks} LDS {lds} B")
