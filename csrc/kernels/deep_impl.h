@@ -61,16 +61,34 @@ constexpr int LDZ = CW + 4;     // LDS row stride of a dZ chunk
 
 __device__ __forceinline__ f32x4 z4() { return f32x4{0.f, 0.f, 0.f, 0.f}; }
 
-// ---- write-through (sc1) accesses of handed-off bytes: per-lane offset v + uniform offset
-//      s, both in floats, through a buffer resource of the replica's workspace
+// ---- accesses of handed-off bytes: per-lane offset v + uniform offset s, both in floats,
+//      through a buffer resource of the replica's workspace.  Stores are write-through (sc1,
+//      Guideline 16 R1); loads are PLAIN behind the one agent-scope acquire of every wait
+//      (wait_phase / wait_x): a replica's workgroups re-read the same activation and
+//      gradient matrices (each of the nw workgroups reads all of A_{l-1} / dZ_l).  Measured
+//      on Otto (profiles/deep_stamps_otto_r5_*): sc1 loads with no acquire 107 us per step,
+//      plain loads behind the acquire 115 us -- the acquire costs more than the L2 returns --
+//      so the loads are sc1 (DP_LOAD_AUX 16, Guideline 16's every-load-sc1 form); 0 switches
+//      to the acquire + plain-load form
+#ifndef DP_LOAD_AUX
+#define DP_LOAD_AUX 16
+#endif
 __device__ __forceinline__ rsrc_t ws_rsrc(const float* base) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), (short)0, 0x7fffffff, 0x00020000);
 }
 __device__ __forceinline__ f32x4 ld4(rsrc_t r, int v, long long s) {
-  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, v * 4, (int)s * 4, 16));
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, v * 4, (int)s * 4, DP_LOAD_AUX));
 }
 __device__ __forceinline__ float ld1(rsrc_t r, int v, long long s) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, v * 4, (int)s * 4, 16));
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, v * 4, (int)s * 4, DP_LOAD_AUX));
+}
+// after the poll: one lane's agent-scope acquire (drops this CU's stale L1 lines), its
+// vmcnt drain, then the workgroup barrier -- the other waves' plain loads come after it
+__device__ __forceinline__ void acquire_lane0() {
+  if (DP_LOAD_AUX == 0 && threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
 }
 __device__ __forceinline__ void st1(rsrc_t r, int v, long long s, float x) {
   __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, x), r, v * 4, (int)s * 4, 16);
@@ -132,6 +150,7 @@ __device__ __forceinline__ bool wait_phase(const DeepArgs& a, int r, unsigned ta
       __builtin_amdgcn_s_sleep(1);
     }
   }
+  acquire_lane0();
   ok = __syncthreads_and(ok);
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // no load moves above the poll
   return ok != 0;
@@ -316,9 +335,29 @@ __device__ __forceinline__ f32x4 ks_reduce(const DeepArgs& a, const Ctx& x, floa
 // ---- forward of hidden layer l (column tile j): Z = A_{l-1} W_l[:, J] + b -> act, dropout
 //      -> A_l[:, J] (workspace, sc1) + A_l^T stripe (LDS) + G_l (registers) [+ G_{L-2} to
 //      the workspace for the tail]
+// the W^T rows J of layer l's image (16 x Kx, <= 8 float4 per thread) into registers; for
+// l >= 2 issued BEFORE the phase's wait -- the image was rewritten in the previous step's
+// BW_l, which every workgroup published before its FWD_0 publication this step
+template <int l>
+__device__ __forceinline__ void wt_load(const DeepArgs& a, const Ctx& x0, f32x4 (&stg)[8]) {
+  const Ctx x = lanes(x0);
+  const DeepLayer ly = a.ly[l];
+  if (x.j >= ly.T) return;
+  const int Kx = ly.Kx, q4n = Kx >> 2, tot = 16 * q4n, J0 = 16 * x.j;
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const int e = x.tid + NTH * u, ec = e < tot ? e : tot - 1;
+    const int c = ec / q4n, q = ec - c * q4n;
+    stg[u] = ld4(x.rs, (J0 + c) * Kx + 4 * q, ly.o_wt);
+  }
+}
+
+// ---- forward of hidden layer l (column tile j): Z = A_{l-1} W_l[:, J] + b -> act, dropout
+//      -> A_l^T stripe (LDS) + G_l (registers), then A_l[:, J] (workspace) as 16-byte rows from
+//      the stripe [+ G_{L-2} to the workspace for the tail]
 template <int L, int l>
 __device__ __forceinline__ void fwd_phase(const DeepArgs& a, float* smem, const Ctx& x0, int s, int valid, long long it,
-                                          f32x4 (&G)[L - 1]) {
+                                          f32x4 (&G)[L - 1], f32x4 (&stg)[8]) {
   const Ctx x = lanes(x0);
   const DeepLayer ly = a.ly[l];
   if (x.j >= ly.T) return;
@@ -340,16 +379,10 @@ __device__ __forceinline__ void fwd_phase(const DeepArgs& a, float* smem, const 
     constexpr int PF = 16;
     const int nmine = ((nkc - kp + a.KS - 1) / a.KS + PF - 1) / PF * PF;
     const DeepLayer lp = a.ly[l - 1];
-    // the W^T rows J of the image first (the staging the MFMAs wait for), then the A ring
+    // the W^T rows J (l == 1: loaded here, after the wait), then the A ring
     float* sb = smem + a.l_stage;
     const int q4n = Kx >> 2, tot = 16 * q4n;
-    f32x4 stg[8];   // Kx <= 1024: <= 8 float4 per thread
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int e = x.tid + NTH * u, ec = e < tot ? e : tot - 1;
-      const int c = ec / q4n, q = ec - c * q4n;
-      stg[u] = ld4(x.rs, (J0 + c) * Kx + 4 * q, ly.o_wt);
-    }
+    if constexpr (l == 1) wt_load<l>(a, x, stg);
     auto loadA = [&](int k) { return ld4(x.rs, m * Kx + (k < Kx ? k : 0), lp.o_a); };
     f32x4 ring[PF];
     ring_issue<PF>(ring, loadA, kp, a.KS, x.g);
@@ -362,37 +395,52 @@ __device__ __forceinline__ void fwd_phase(const DeepArgs& a, float* smem, const 
       }
     }
     lds_barrier();
+    if (l == 1) dstamp(a, s, 15);
     acc = ring_run<PF>(ring, loadA, sb, Kx + 4, Kx, kp, a.KS, nmine, x.lane);
+    if (l == 1) dstamp(a, s, 16);
   }
   acc = ks_reduce(a, x, smem + a.l_red, acc, kp);
-  if (kp != 0) return;
-  // epilogue: lane (column c16, group g) holds rows 16 rt + 4 g + q
-  const int col = J0 + x.c16;
-  const float bias = smem[ly.l_b + x.c16];
-  float z[4], o[4], gg[4];
+  if (l == 1) dstamp(a, s, 17);
+  // epilogue (kp == 0 waves): lane (column c16, group g) holds rows 16 rt + 4 g + q
+  float* gst = smem + a.l_red;   // G_{L-2}^T stripe [16][Bp] for the tail (l == L-2)
+  if (kp == 0) {
+    const int col = J0 + x.c16;
+    const float bias = smem[ly.l_b + x.c16];
+    float z[4], o[4], gg[4];
 #pragma unroll
-  for (int q = 0; q < 4; ++q) z[q] = acc[q] + bias;
-  act_fg_v<4>(ly.act, z, o, gg);
-  const float scale = ly.rate > 0.f ? 1.f / (1.f - ly.rate) : 1.f;
-  const uint32_t dbase = dropout_base(a.seed, x.r, l, it);
-  f32x4 av, gv;
+    for (int q = 0; q < 4; ++q) z[q] = acc[q] + bias;
+    act_fg_v<4>(ly.act, z, o, gg);
+    const float scale = ly.rate > 0.f ? 1.f / (1.f - ly.rate) : 1.f;
+    const uint32_t dbase = dropout_base(a.seed, x.r, l, it);
+    f32x4 av, gv;
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int mm = 16 * rt + 4 * x.g + q;
-    const bool live = mm < valid && col < ly.N;
-    const float u = (live && ly.rate > 0.f) ? dropout_u1(dbase, mm, col) : 1.f;
-    const bool keep = live && u >= ly.rate;
-    av[q] = keep ? o[q] * scale : 0.f;
-    gv[q] = keep ? gg[q] * scale : 0.f;
+    for (int q = 0; q < 4; ++q) {
+      const int mm = 16 * rt + 4 * x.g + q;
+      const bool live = mm < valid && col < ly.N;
+      const float u = (live && ly.rate > 0.f) ? dropout_u1(dbase, mm, col) : 1.f;
+      const bool keep = live && u >= ly.rate;
+      av[q] = keep ? o[q] * scale : 0.f;
+      gv[q] = keep ? gg[q] * scale : 0.f;
+    }
+    G[l] = gv;
+    const int r0 = 16 * rt + 4 * x.g;
+    lds4(smem + ly.l_at + x.c16 * (a.Bp + 4) + r0, av);
+    if constexpr (l == L - 2) lds4(gst + x.c16 * a.Bp + r0, gv);
   }
-  G[l] = gv;
-  const int r0 = 16 * rt + 4 * x.g;
+  lds_barrier();
+  // A_l[:, J] (and G_{L-2}[:, J]) rows out of the stripes: one 16-byte store per 4 columns
+  const float* at = smem + ly.l_at;
+  for (int e = x.tid; e < a.Bp * 4; e += NTH) {
+    const int row = e >> 2, q = e & 3;
+    f32x4 v;
 #pragma unroll
-  for (int q = 0; q < 4; ++q) st1(x.rs, (r0 + q) * ly.N16 + col, ly.o_a, av[q]);
-  lds4(smem + ly.l_at + x.c16 * (a.Bp + 4) + r0, av);
-  if constexpr (l == L - 2) {
+    for (int k = 0; k < 4; ++k) v[k] = at[(4 * q + k) * (a.Bp + 4) + row];
+    st4(x.rs, row * ly.N16 + J0 + 4 * q, ly.o_a, v);
+    if constexpr (l == L - 2) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) st1(x.rs, (r0 + q) * ly.N16 + col, a.o_g, gv[q]);
+      for (int k = 0; k < 4; ++k) v[k] = gst[(4 * q + k) * a.Bp + row];
+      st4(x.rs, row * ly.N16 + J0 + 4 * q, a.o_g, v);
+    }
   }
 }
 
@@ -450,6 +498,7 @@ __device__ __forceinline__ void tail_phase(const DeepArgs& a, float* smem, const
       sLg[row * 36 + col] = col < C ? sum + b : 0.f;
     }
     __syncthreads();
+    if (rt == x.j) dstamp(a, s, 21);
     // ---- loss / metrics; sLg becomes dL/dz * (1 / valid)
     {
       Prob q;
@@ -485,6 +534,7 @@ __device__ __forceinline__ void tail_phase(const DeepArgs& a, float* smem, const
       }
     }
     __syncthreads();
+    if (rt == x.j) dstamp(a, s, 22);
     // ---- dZ_{L-1} rows out; dZ_{L-2} rows = (dZ_{L-1} . W_{L-1}^T) * G_{L-2}: wave w takes
     //      the 16-column tiles w, w + 8, ... of layer L-2 (<= 8 of them)
     for (int e = x.tid; e < 16 * C16; e += NTH) {
@@ -504,6 +554,8 @@ __device__ __forceinline__ void tail_phase(const DeepArgs& a, float* smem, const
     }
     const f32x4 d0 = lds4(sLg + x.c16 * 36 + 4 * x.g);
     const f32x4 d1 = lds4(sLg + x.c16 * 36 + 16 + 4 * x.g);
+    __syncthreads();   // the stage is rewritten below: the dZ_{L-2} rows [16][Kx]
+    float* sdz = red;
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const int it = x.w + NWV * u;
@@ -513,8 +565,13 @@ __device__ __forceinline__ void tail_phase(const DeepArgs& a, float* smem, const
         if (NCT > 1) mma4(c, d1, wb1[u]);
         const int i = 16 * it + x.c16;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) st1(x.rs, (m0 + 4 * x.g + q) * Kx + i, la.o_dz, c[q] * gq[u][q]);
+        for (int q = 0; q < 4; ++q) sdz[(4 * x.g + q) * Kx + i] = c[q] * gq[u][q];
       }
+    }
+    __syncthreads();
+    for (int e = x.tid; e < 4 * Kx; e += NTH) {   // 16 rows x Kx / 4 float4
+      const int row = e / (Kx >> 2), q4 = e - row * (Kx >> 2);
+      st4(x.rs, (m0 + row) * Kx + 4 * q4, la.o_dz, lds4(sdz + row * Kx + 4 * q4));
     }
     __syncthreads();   // the LDS tiles are rewritten by the next row tile
   }
@@ -623,7 +680,7 @@ __device__ __forceinline__ void bias_tile(const DeepArgs& a, float* smem, const 
 //      dA * G_{l-1} -> workspace (l >= 2) or the LDS dZ_0^T stripe (l = 1)
 template <int L, int l, bool SGD0, bool SYNC>
 __device__ __forceinline__ void bw_phase(const DeepArgs& a, float* smem, const Ctx& x0, const OptStep& os,
-                                         const f32x4 (&G)[L - 1]) {
+                                         const f32x4 (&G)[L - 1], int s) {
   const Ctx x = lanes(x0);
   const DeepLayer lp = a.ly[l - 1], ly = a.ly[l];
   if (x.j >= lp.T) {   // no row tile of W_l here; maybe its bias tile (layer l wider than l - 1)
@@ -731,19 +788,30 @@ __device__ __forceinline__ void bw_phase(const DeepArgs& a, float* smem, const C
   };
   for (int h = 0; h < nch; h += 2) {
     chunk(h, preA);
+    if (l == L - 2 && h == 0) dstamp(a, s, 18);
     if (h + 1 < nch) chunk(h + 1, preB);
   }
+  if (l == L - 2) dstamp(a, s, 19);
   f32x4 acc = ks_reduce(a, x, smem + a.l_red, accB0 + accB1, kp);
-  if (kp != 0) return;
-  const int r0 = 16 * rt + 4 * x.g;
-  f32x4 dz;
+  // dZ_{l-1}[:, J] = dA * G_{l-1} -> the LDS dZ^T stripe (l = 1: layer 0's DW operand; l >= 2:
+  // staging of the 16-byte row stores below -- BW_1 rewrites the stripe after them)
+  if (kp == 0) {
+    const int r0 = 16 * rt + 4 * x.g;
+    f32x4 dz;
 #pragma unroll
-  for (int q = 0; q < 4; ++q) dz[q] = acc[q] * G[l - 1][q];
-  if constexpr (l >= 2) {
-#pragma unroll
-    for (int q = 0; q < 4; ++q) st1(x.rs, (r0 + q) * lp.N16 + I0 + x.c16, lp.o_dz, dz[q]);
-  } else {
+    for (int q = 0; q < 4; ++q) dz[q] = acc[q] * G[l - 1][q];
     lds4(smem + a.l_dz0 + x.c16 * ldat + r0, dz);
+  }
+  if constexpr (l >= 2) {
+    lds_barrier();
+    const float* st = smem + a.l_dz0;
+    for (int e = x.tid; e < Bp * 4; e += NTH) {
+      const int row = e >> 2, q = e & 3;
+      f32x4 v;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v[k] = st[(4 * q + k) * ldat + row];
+      st4(x.rs, row * lp.N16 + I0 + 4 * q, lp.o_dz, v);
+    }
   }
 }
 
@@ -847,9 +915,11 @@ template <int L, int l>
 __device__ __forceinline__ bool fwd_chain(const DeepArgs& a, float* smem, const Ctx& x, int s, int valid, long long it,
                                           unsigned base, f32x4 (&G)[L - 1]) {
   if constexpr (l <= L - 2) {
+    f32x4 stg[8];
+    if constexpr (l >= 2) wt_load<l>(a, x, stg);   // ready since this step's FWD_0 publications
     if (!wait_phase(a, x.r, base + l)) return false;
     dstamp(a, s, 2 * l + 1);
-    fwd_phase<L, l>(a, smem, x, s, valid, it, G);
+    fwd_phase<L, l>(a, smem, x, s, valid, it, G, stg);
     publish(a, x.r, x.j, base + l + 1);
     dstamp(a, s, 2 * l + 2);
     return fwd_chain<L, l + 1>(a, smem, x, s, valid, it, base, G);
@@ -865,8 +935,11 @@ __device__ __forceinline__ bool bw_chain(const DeepArgs& a, float* smem, const C
     const unsigned p = (unsigned)(L + (L - 2 - l));
     if (!wait_phase(a, x.r, base + p)) return false;
     dstamp(a, s, 11 + 2 * (L - 2 - l));
-    if constexpr (l == L - 2) dw_last<L, SGD0, SYNC>(a, smem, x, os);
-    bw_phase<L, l, SGD0, SYNC>(a, smem, x, os, G);
+    if constexpr (l == L - 2) {
+      dw_last<L, SGD0, SYNC>(a, smem, x, os);
+      dstamp(a, s, 23);
+    }
+    bw_phase<L, l, SGD0, SYNC>(a, smem, x, os, G, s);
     publish(a, x.r, x.j, base + p + 1);
     dstamp(a, s, 12 + 2 * (L - 2 - l));
     return bw_chain<L, l - 1, SGD0, SYNC>(a, smem, x, s, os, base, G);
@@ -900,6 +973,7 @@ __device__ __forceinline__ bool wait_x(const DeepArgs& a, int j, int kind, unsig
       __builtin_amdgcn_s_sleep(1);
     }
   }
+  acquire_lane0();
   ok = __syncthreads_and(ok);
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   return ok != 0;
@@ -1120,7 +1194,10 @@ __global__ __launch_bounds__(512) void mlp_deep_kernel(DeepArgs a) {
     }
     __syncthreads();
     dstamp(a, s, 1);
-    fwd_phase<L, 0>(a, smem, x, s, valid, it, G);
+    {
+      f32x4 stg0[8];
+      fwd_phase<L, 0>(a, smem, x, s, valid, it, G, stg0);
+    }
     publish(a, x.r, x.j, base + 1);
     dstamp(a, s, 2);
     if (!fwd_chain<L, 1>(a, smem, x, s, valid, it, base, G)) return;
@@ -1189,21 +1266,20 @@ __global__ __launch_bounds__(512) void mlp_deep_kernel(DeepArgs a) {
 }
 
 namespace {
-// dynamic LDS above the default limit: raised once per instantiation (to the largest the
-// device allows, so later launches with other layouts need no call)
+// dynamic LDS above the default limit: raised per instantiation to the largest layout
+// launched so far (the kernel's own static LDS -- e.g. the __syncthreads_and word -- counts
+// against the same 160 KB, so the device maximum itself is refused)
 template <int L, bool F, bool SG, bool SY>
 hipError_t deep_launch_one(const DeepArgs* a, hipStream_t s) {
-  static const bool done = [] {
-    int dev = 0, mx = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&mx, hipDeviceAttributeMaxSharedMemoryPerBlock, dev);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&mlp_deep_kernel<L, F, SG, SY>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, mx);
-    return true;
-  }();
-  (void)done;
-  hipLaunchKernelGGL((mlp_deep_kernel<L, F, SG, SY>), dim3(a->R * a->nw), dim3(NTH),
-                     sizeof(float) * (size_t)a->lds_floats, s, *a);
+  static int set_bytes = 0;
+  const int need = (int)(sizeof(float) * (size_t)a->lds_floats);
+  if (need > set_bytes) {
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&mlp_deep_kernel<L, F, SG, SY>),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, need);
+    if (e != hipSuccess) return e;
+    set_bytes = need;
+  }
+  hipLaunchKernelGGL((mlp_deep_kernel<L, F, SG, SY>), dim3(a->R * a->nw), dim3(NTH), (size_t)need, s, *a);
   return hipGetLastError();
 }
 

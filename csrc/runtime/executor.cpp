@@ -268,6 +268,7 @@ bool Executor::build_deep() {
   stage = std::max(stage, 8 * 2 * 256 + 16 * 36 + 16 * 32 + 16);     // tail tiles
   stage = std::max(stage, a.Bp * (a.ly[L - 1].N16 + 4));             // dZ_{L-1} of the last layer's DW
   for (int l = 1; l < L - 1; ++l) stage = std::max(stage, 16 * (a.ly[l].Kx + 4));   // W^T stripes
+  stage = std::max(stage, 16 * a.ly[L - 1].Kx);                       // the tail's dZ_{L-2} rows
   a.l_stage = lds; lds += stage;
   lds += 2 * DP_ROWS;                                                 // batch rows of two steps (ints, last)
   a.lds_floats = lds;

@@ -472,7 +472,8 @@ def test_persist_bf16_pinned_to_bf16_operand_torch():
     for name, b16 in (("emul", True), ("f32", False)):
         t = TorchTrainer(model, build_plan(model), 8, 64, torch.device("cuda"), hash_dropout_seed=9, bf16_operands=b16)
         t.set_data(xs, ys, 0.0, shuffle=False)
-        out[name] = (t.get_weights_flat(), t.fit(2))
+        h = t.fit(2)
+        out[name] = (t.get_weights_flat(), h)
     dist = lambda a, b: float(np.abs(out[a][0] - out[b][0]).mean() / np.abs(out[b][0] - w0).mean())
     gap, d_rc, d_p = dist("f32", "emul"), dist("rc_bf16", "emul"), dist("p_bf16", "emul")
     print(f"bf16 pin: emul-vs-f32 {gap:.3e}  rowchain-vs-emul {d_rc:.3e}  persistent-vs-emul {d_p:.3e}")

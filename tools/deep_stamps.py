@@ -20,6 +20,9 @@ def names(L):
     for l in range(1, L - 1):
         n[2 * l + 1] = f"fwd{l}_seen"
         n[2 * l + 2] = f"fwd{l}_pub"
+    n.update({15: "fwd1_wt_staged", 16: "fwd1_ring_done", 17: "fwd1_ksred", 21: "tail_logits", 22: "tail_loss",
+              23: "dwlast_done", 18: "bw_top_chunk0", 19: "bw_top_chunks", 24: "dw0_sync", 25: "xa_seen",
+              26: "xb_seen", 27: "applied"})
     n[9] = "tail_seen"
     n[10] = "tail_pub"
     for l in range(L - 2, 0, -1):
@@ -82,13 +85,16 @@ def main():
     rep = np.arange(grid) % R
     print("us relative to the replica's median step start (stamp 0); medians over workgroups")
     starts = []
+    order = sorted(nm, key=lambda k: np.median(s[:, min(3, nst - 1), k][s[:, min(3, nst - 1), k] > 0]) if
+                   (s[:, min(3, nst - 1), k] > 0).any() else 1e30)
     for i in range(min(8, nst)):
         b = np.zeros(grid)
         for rr in range(R):
             b[rep == rr] = np.median(s[rep == rr, i, 0])
         starts.append(np.median(b))
         vals = {}
-        for k, n in sorted(nm.items()):
+        for k in order:
+            n = nm[k]
             col = s[:, i, k]
             ok = col > 0
             if ok.any():
