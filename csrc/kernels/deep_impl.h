@@ -324,6 +324,7 @@ __device__ __forceinline__ f32x4 ring_run(f32x4 (&ring)[PF], LA loadA, const flo
 // split-K partials of waves kp > 0 summed into the kp == 0 wave of the row tile (LDS red)
 __device__ __forceinline__ f32x4 ks_reduce(const DeepArgs& a, const Ctx& x, float* red, f32x4 acc, int kp) {
   if (a.KS == 1) return acc;
+  lds_barrier();   // red is the backward's bias scratch: its last readers are done
   if (kp > 0) lds4(red + ((x.w - a.RT) * 64 + x.lane) * 4, acc);
   lds_barrier();
   if (kp == 0)
@@ -355,7 +356,9 @@ __device__ __forceinline__ void wt_load(const DeepArgs& a, const Ctx& x0, f32x4 
 // ---- forward of hidden layer l (column tile j): Z = A_{l-1} W_l[:, J] + b -> act, dropout
 //      -> A_l^T stripe (LDS) + G_l (registers), then A_l[:, J] (workspace) as 16-byte rows from
 //      the stripe [+ G_{L-2} to the workspace for the tail]
-template <int L, int l>
+// STAGED (l == 1, fit granularity): the W^T rows are already in the LDS stage (LDS-DMA
+// issued at the top of the step, wt_glds)
+template <int L, int l, bool STAGED>
 __device__ __forceinline__ void fwd_phase(const DeepArgs& a, float* smem, const Ctx& x0, int s, int valid, long long it,
                                           f32x4 (&G)[L - 1], f32x4 (&stg)[8]) {
   const Ctx x = lanes(x0);
@@ -382,19 +385,21 @@ __device__ __forceinline__ void fwd_phase(const DeepArgs& a, float* smem, const 
     // the W^T rows J (l == 1: loaded here, after the wait), then the A ring
     float* sb = smem + a.l_stage;
     const int q4n = Kx >> 2, tot = 16 * q4n;
-    if constexpr (l == 1) wt_load<l>(a, x, stg);
+    if constexpr (l == 1 && !STAGED) wt_load<l>(a, x, stg);
     auto loadA = [&](int k) { return ld4(x.rs, m * Kx + (k < Kx ? k : 0), lp.o_a); };
     f32x4 ring[PF];
     ring_issue<PF>(ring, loadA, kp, a.KS, x.g);
+    if constexpr (!(l == 1 && STAGED)) {
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int e = x.tid + NTH * u;
-      if (e < tot) {
-        const int c = e / q4n, q = e - c * q4n;
-        lds4(sb + c * (Kx + 4) + 4 * q, stg[u]);
+      for (int u = 0; u < 8; ++u) {
+        const int e = x.tid + NTH * u;
+        if (e < tot) {
+          const int c = e / q4n, q = e - c * q4n;
+          lds4(sb + c * (Kx + 4) + 4 * q, stg[u]);
+        }
       }
+      lds_barrier();
     }
-    lds_barrier();
     if (l == 1) dstamp(a, s, 15);
     acc = ring_run<PF>(ring, loadA, sb, Kx + 4, Kx, kp, a.KS, nmine, x.lane);
     if (l == 1) dstamp(a, s, 16);
@@ -441,6 +446,26 @@ __device__ __forceinline__ void fwd_phase(const DeepArgs& a, float* smem, const 
       for (int k = 0; k < 4; ++k) v[k] = gst[(4 * q + k) * a.Bp + row];
       st4(x.rs, row * ly.N16 + J0 + 4 * q, a.o_g, v);
     }
+  }
+}
+
+// the W^T rows J of layer l straight into the LDS stage by LDS-DMA (global_load_lds, no
+// registers): one wave instruction per (row, 1 KB piece); complete once the issuing waves
+// drained vmcnt and met at a barrier (publish() does both before the next phase reads it)
+template <int l>
+__device__ __forceinline__ void wt_glds(const DeepArgs& a, float* smem, const Ctx& x0) {
+  const Ctx x = lanes(x0);
+  const DeepLayer ly = a.ly[l];
+  if (x.j >= ly.T) return;
+  const int Kx = ly.Kx, q4n = Kx >> 2, nck = (q4n + 63) >> 6;
+  float* sb = smem + a.l_stage;
+  const float* src = a.ws + (long long)x.r * a.ws_stride + ly.o_wt + (long long)(16 * x.j) * Kx;
+  for (int t = x.w; t < 16 * nck; t += NWV) {
+    const int c = t / nck, h = t - c * nck, piece = 64 * h + x.lane;
+    if (piece < q4n)
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + (long long)c * Kx + 4 * piece),
+                                       (__attribute__((address_space(3))) void*)(sb + c * (Kx + 4) + 256 * h), 16, 0,
+                                       DP_LOAD_AUX);
   }
 }
 
@@ -750,8 +775,8 @@ __device__ __forceinline__ void bw_phase(const DeepArgs& a, float* smem, const C
       for (int rr = 0; rr < rows; ++rr) sm += sdz[(rg * rows + rr) * LDZ + cb + c];
       bred[x.tid] = sm;
     }
-    lds_barrier();   // every read of the chunk and of the old masters is done
     if (hh == 1) lds4(spart + (f * 64 + x.lane) * 4, accW);
+    lds_barrier();   // every read of the chunk and of the old masters is done, the partials are out
     if (btile && h == hb && x.tid < 16 && 16 * x.j + x.tid < ly.N) {
       float db = 0.f;
 #pragma unroll
@@ -763,7 +788,6 @@ __device__ __forceinline__ void bw_phase(const DeepArgs& a, float* smem, const C
         bt[x.tid] = upd<SGD0>(a, x, os, ly.p_off + (long long)ly.K * ly.N + 16 * x.j + x.tid, bt[x.tid], db);
       }
     }
-    lds_barrier();
     if (SYNC && hh == 0 && 16 * f < cw) {   // the gradient rows J of the chunk's column tile f
       accW += lds4(spart + (f * 64 + x.lane) * 4);
       const int col = c0 + 16 * f + x.c16;
@@ -911,7 +935,7 @@ __device__ __forceinline__ void load_dz0(const DeepArgs& a, float* smem, const C
 
 
 // the forward phases of layers l .. L-2 (compile-time chain: every layer index is static)
-template <int L, int l>
+template <int L, int l, bool STAGED>
 __device__ __forceinline__ bool fwd_chain(const DeepArgs& a, float* smem, const Ctx& x, int s, int valid, long long it,
                                           unsigned base, f32x4 (&G)[L - 1]) {
   if constexpr (l <= L - 2) {
@@ -919,10 +943,10 @@ __device__ __forceinline__ bool fwd_chain(const DeepArgs& a, float* smem, const 
     if constexpr (l >= 2) wt_load<l>(a, x, stg);   // ready since this step's FWD_0 publications
     if (!wait_phase(a, x.r, base + l)) return false;
     dstamp(a, s, 2 * l + 1);
-    fwd_phase<L, l>(a, smem, x, s, valid, it, G, stg);
+    fwd_phase<L, l, STAGED>(a, smem, x, s, valid, it, G, stg);
     publish(a, x.r, x.j, base + l + 1);
     dstamp(a, s, 2 * l + 2);
-    return fwd_chain<L, l + 1>(a, smem, x, s, valid, it, base, G);
+    return fwd_chain<L, l + 1, STAGED>(a, smem, x, s, valid, it, base, G);
   }
   return true;
 }
@@ -1158,6 +1182,9 @@ __global__ __launch_bounds__(512) void mlp_deep_kernel(DeepArgs a) {
   if (x.j == 0 && x.tid < a.ly[L - 1].N16) st1(x.rs, x.tid, a.o_bl, smem[a.ly[L - 1].l_b + x.tid]);
   __syncthreads();
   if (!wait_grid(a)) return;
+  // the prologue's image writes are out: tag 1 (step s then publishes s * NPH + 2 ..
+  // (s + 1) * NPH + 1, so "the previous step is done" is tag base for every s)
+  publish(a, x.r, x.j, 1u);
 
   constexpr int NPH = 2 * L - 2;
   const long long s0 = ld_inv(a.ctr);
@@ -1173,7 +1200,7 @@ __global__ __launch_bounds__(512) void mlp_deep_kernel(DeepArgs a) {
     if (valid == 0) break;   // uniform over the replica: no batch left in this epoch
     const long long it = iter_at(a.ctr, a.ntrain, a.B, x.r, s0, s);
     const OptStep os = opt_step(a.op, it);
-    const unsigned base = (unsigned)s * NPH;
+    const unsigned base = (unsigned)s * NPH + 1;
     dstamp(a, s, 0);
     // ---- phase 0: the previous step's layer-0 (and, L = 2, last-layer) update, forward 0
     {
@@ -1182,6 +1209,14 @@ __global__ __launch_bounds__(512) void mlp_deep_kernel(DeepArgs a) {
         const int* pr = a.perm + (long long)x.r * a.sPerm + (s0 + s) * a.B;
         x.prow[(s & 1) * DP_ROWS + y.tid] = y.tid < valid ? pr[y.tid] : 0;
       }
+    }
+    // FWD_1's W^T rows into the LDS stage by LDS-DMA right away (fit granularity, L >= 3):
+    // every workgroup's previous step -- its BW_1 image writes included -- is published at
+    // tag base; the copies run beside DW_0 and FWD_0, which do not touch the stage
+    constexpr bool STAGED = !SYNC && L >= 3;
+    if constexpr (STAGED) {
+      if (!wait_phase(a, x.r, base)) return;
+      wt_glds<1>(a, smem, x);
     }
     if (!SYNC && last >= 0) {
       if constexpr (L == 2) {
@@ -1196,11 +1231,11 @@ __global__ __launch_bounds__(512) void mlp_deep_kernel(DeepArgs a) {
     dstamp(a, s, 1);
     {
       f32x4 stg0[8];
-      fwd_phase<L, 0>(a, smem, x, s, valid, it, G, stg0);
+      fwd_phase<L, 0, false>(a, smem, x, s, valid, it, G, stg0);
     }
     publish(a, x.r, x.j, base + 1);
     dstamp(a, s, 2);
-    if (!fwd_chain<L, 1>(a, smem, x, s, valid, it, base, G)) return;
+    if (!fwd_chain<L, 1, STAGED>(a, smem, x, s, valid, it, base, G)) return;
     if (!wait_phase(a, x.r, base + L - 1)) return;
     dstamp(a, s, 9);
     tail_phase<L, FAST>(a, smem, x, s, valid);
@@ -1224,7 +1259,7 @@ __global__ __launch_bounds__(512) void mlp_deep_kernel(DeepArgs a) {
   // the pending layer-0 update of the last step that ran
   if (!SYNC && last >= 0) {
     if constexpr (L == 2) {
-      if (!wait_phase(a, x.r, (unsigned)(last + 1) * NPH)) return;
+      if (!wait_phase(a, x.r, (unsigned)(last + 1) * NPH + 1)) return;
       dw_last<L, SGD0, false>(a, smem, x, lastos);
       load_dz0(a, smem, x);
     }
