@@ -721,7 +721,10 @@ __device__ __forceinline__ void bw_phase(const DeepArgs& a, float* smem, const C
   float* wr = smem + ly.l_w;
   const float* at = smem + lp.l_at;
   float* sdz = smem + a.l_stage;
-  float* spart = sdz + DP_ROWS * LDZ;   // [4][64][4] DW partials of the second row half
+  // [4][64][4] DW partials of the second row half, double-buffered by chunk parity (the
+  // first half's waves finish a chunk's update at the top of the NEXT chunk, beside the
+  // other waves' MFMAs); the second buffer is the dZ_0^T stripe, free until the phase's end
+  float* spbuf[2] = {sdz + DP_ROWS * LDZ, smem + a.l_dz0};
   const int nch = (ly.N16 + CW - 1) / CW;
   // chunk staging: Bp x 64 floats = Bp * 16 float4, <= 4 per thread, two chunks ahead
   // (register sets A / B alternate; the loop is unrolled by two so their indices stay static)
@@ -738,6 +741,32 @@ __device__ __forceinline__ void bw_phase(const DeepArgs& a, float* smem, const C
   load_chunk(0, preA);
   if (nch > 1) load_chunk(1, preB);
   f32x4 accB0 = z4(), accB1 = z4();
+  f32x4 accWp = z4();   // this wave's DW partial of the previous chunk (first row half: pending update)
+  // the first-half waves complete chunk hq's rows J: partial sums, update of the masters of
+  // the chunk's columns and their W^T image segment (SYNC: the gradient to the exchange tile)
+  auto finish = [&](int hq, f32x4 accq) {
+    const int c0 = hq * CW, cw = ly.N16 - c0 < CW ? ly.N16 - c0 : CW;
+    if (hh != 0 || 16 * f >= cw) return;
+    accq += lds4(spbuf[hq & 1] + (f * 64 + x.lane) * 4);
+    const int col = c0 + 16 * f + x.c16;
+    if constexpr (SYNC) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) st1(x.xs, (4 * x.g + q) * ly.N16 + col, x.xp + a.x_w[l], accq[q]);
+    } else {
+      f32x4 wv;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int ip = 4 * x.g + q;
+        float wt = wr[ip * ldr + col];
+        if (I0 + ip < ly.K && col < ly.N) {
+          wt = upd<SGD0>(a, x, os, ly.p_off + (long long)(I0 + ip) * ly.N + col, wt, accq[q]);
+          wr[ip * ldr + col] = wt;
+        }
+        wv[q] = wt;
+      }
+      st4(x.rs, col * ly.Kx + I0 + 4 * x.g, ly.o_wt, wv);
+    }
+  };
   auto chunk = [&](int h, f32x4 (&pre)[4]) {
     const int c0 = h * CW, cw = ly.N16 - c0 < CW ? ly.N16 - c0 : CW;
 #pragma unroll
@@ -747,6 +776,7 @@ __device__ __forceinline__ void bw_phase(const DeepArgs& a, float* smem, const C
     }
     if (h + 2 < nch) load_chunk(h + 2, pre);   // two chunks in flight ahead of the consumer
     lds_barrier();
+    if (h > 0) finish(h - 1, accWp);
     // dA_{l-1}[rows of tile rt][J] over the chunk's 16-column groups t (t % KS == kp)
 #pragma unroll
     for (int t = 0; t < CW / 16; ++t) {
@@ -775,8 +805,9 @@ __device__ __forceinline__ void bw_phase(const DeepArgs& a, float* smem, const C
       for (int rr = 0; rr < rows; ++rr) sm += sdz[(rg * rows + rr) * LDZ + cb + c];
       bred[x.tid] = sm;
     }
-    if (hh == 1) lds4(spart + (f * 64 + x.lane) * 4, accW);
-    lds_barrier();   // every read of the chunk and of the old masters is done, the partials are out
+    if (hh == 1) lds4(spbuf[h & 1] + (f * 64 + x.lane) * 4, accW);
+    accWp = accW;
+    lds_barrier();   // every read of the chunk is done, the partials are out
     if (btile && h == hb && x.tid < 16 && 16 * x.j + x.tid < ly.N) {
       float db = 0.f;
 #pragma unroll
@@ -788,37 +819,19 @@ __device__ __forceinline__ void bw_phase(const DeepArgs& a, float* smem, const C
         bt[x.tid] = upd<SGD0>(a, x, os, ly.p_off + (long long)ly.K * ly.N + 16 * x.j + x.tid, bt[x.tid], db);
       }
     }
-    if (SYNC && hh == 0 && 16 * f < cw) {   // the gradient rows J of the chunk's column tile f
-      accW += lds4(spart + (f * 64 + x.lane) * 4);
-      const int col = c0 + 16 * f + x.c16;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) st1(x.xs, (4 * x.g + q) * ly.N16 + col, x.xp + a.x_w[l], accW[q]);
-    } else if (!SYNC && hh == 0 && 16 * f < cw) {
-      accW += lds4(spart + (f * 64 + x.lane) * 4);
-      const int col = c0 + 16 * f + x.c16;
-      f32x4 wv;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int ip = 4 * x.g + q;
-        float wt = wr[ip * ldr + col];
-        if (I0 + ip < ly.K && col < ly.N) {
-          wt = upd<SGD0>(a, x, os, ly.p_off + (long long)(I0 + ip) * ly.N + col, wt, accW[q]);
-          wr[ip * ldr + col] = wt;
-        }
-        wv[q] = wt;
-      }
-      st4(x.rs, col * ly.Kx + I0 + 4 * x.g, ly.o_wt, wv);
-    }
   };
   for (int h = 0; h < nch; h += 2) {
     chunk(h, preA);
     if (l == L - 2 && h == 0) dstamp(a, s, 18);
     if (h + 1 < nch) chunk(h + 1, preB);
   }
+  finish(nch - 1, accWp);   // the last chunk's partials are out since its barrier
   if (l == L - 2) dstamp(a, s, 19);
   f32x4 acc = ks_reduce(a, x, smem + a.l_red, accB0 + accB1, kp);
   // dZ_{l-1}[:, J] = dA * G_{l-1} -> the LDS dZ^T stripe (l = 1: layer 0's DW operand; l >= 2:
-  // staging of the 16-byte row stores below -- BW_1 rewrites the stripe after them)
+  // staging of the 16-byte row stores below -- BW_1 rewrites the stripe after them); the
+  // stripe held the second partial buffer until the last finish
+  if (a.KS == 1) lds_barrier();
   if (kp == 0) {
     const int r0 = 16 * rt + 4 * x.g;
     f32x4 dz;
