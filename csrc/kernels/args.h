@@ -76,6 +76,7 @@ struct Prob {
   const float* bias; long long sBias;
   float* Z; long long ldz, sZ;
   void* D; long long ldd, sD;
+  int d_bf16;              // PK_PLAIN: D holds bf16 (else fp32)
   void* DT; long long lddt, sDT;
   // loss
   int loss; int nmet; int met[4];

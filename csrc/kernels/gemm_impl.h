@@ -558,16 +558,34 @@ __device__ __forceinline__ void tile_epilogue(const GA& ga, const Prob& p, const
     }
     case PK_PLAIN: {
       if constexpr (!(KM & KB(PK_PLAIN))) break;
-      float* out = reinterpret_cast<float*>(p.D) + (long long)r * p.sD;
+      // 8 contiguous columns per thread: one 32-byte (fp32) or 16-byte (bf16) store where the
+      // row segment is whole and aligned, element stores at the ragged edge
+      const bool vec = (p.ldd & 7) == 0 && (reinterpret_cast<unsigned long long>(p.D) & 15) == 0;
 #pragma unroll EUNR
       for (int ps = 0; ps < PASSES; ++ps) {
         const int row = ps * RPP + t_row, gm = m0 + row, gn0 = n0 + t_c0;
-        if (gm >= p.M) continue;
+        if (gm >= p.M || gn0 >= p.N) continue;
         float v[8];
         lds8(row, t_c0, v);
+        const long long idx = (long long)r * p.sD + (long long)gm * p.ldd + gn0;
+        if (p.d_bf16) {
+          if (vec && gn0 + 8 <= p.N) {
+            st8<__bf16>(p.D, idx, v);
+          } else {
 #pragma unroll
-        for (int q = 0; q < 8; ++q)
-          if (gn0 + q < p.N) out[(long long)gm * p.ldd + gn0 + q] = v[q];
+            for (int q = 0; q < 8; ++q)
+              if (gn0 + q < p.N) st<__bf16>(p.D, idx + q, v[q]);
+          }
+        } else {
+          float* out = reinterpret_cast<float*>(p.D);
+          if (vec && gn0 + 8 <= p.N) {
+            st8f(out + idx, v);
+          } else {
+#pragma unroll
+            for (int q = 0; q < 8; ++q)
+              if (gn0 + q < p.N) out[idx + q] = v[q];
+          }
+        }
       }
       break;
     }

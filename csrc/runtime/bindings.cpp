@@ -224,7 +224,7 @@ PYBIND11_MODULE(_C, m) {
 
   // single PLAIN GEMM (C fp32 = A . BT^T) for kernel tests / generic matmul
   m.def("gemm_nt", [](uintptr_t A, uintptr_t BT, uintptr_t C, int M, int N, int K, long long lda, long long ldb,
-                      long long ldc, int bf16, int cfg, uintptr_t s, uintptr_t stamps) {
+                      long long ldc, int bf16, int cfg, uintptr_t s, uintptr_t stamps, int out_bf16) {
     // the kernel issues unconditional 16-byte fragment loads along K: rows must be
     // 16-byte aligned and K padded to whole chunks, or it reads out of bounds
     const int epl = bf16 ? 8 : 4;
@@ -241,6 +241,7 @@ PYBIND11_MODULE(_C, m) {
     p.A = reinterpret_cast<const void*>(A); p.lda = lda;
     p.BT = reinterpret_cast<const void*>(BT); p.ldb = ldb;
     p.D = reinterpret_cast<void*>(C); p.ldd = ldc;
+    p.d_bf16 = out_bf16 ? 1 : 0;   // C holds bf16 (16-byte aligned rows for the vector stores)
     p.ones_row = -1;
     p.B = M;
     p.tiles_m = (M + ea_gemm_tile_m(cfg) - 1) / ea_gemm_tile_m(cfg);
@@ -258,7 +259,8 @@ PYBIND11_MODULE(_C, m) {
     p.ntrain = reinterpret_cast<const int*>(dctr);  // zero batch counts: the kernel reads ntrain[0]
     chk(ea_gemm_grouped(&ga, bf16, cfg, S(s)), "gemm_nt");
   }, py::arg("A"), py::arg("BT"), py::arg("C"), py::arg("M"), py::arg("N"), py::arg("K"), py::arg("lda"),
-     py::arg("ldb"), py::arg("ldc"), py::arg("bf16"), py::arg("cfg"), py::arg("stream"), py::arg("stamps") = 0);
+     py::arg("ldb"), py::arg("ldc"), py::arg("bf16"), py::arg("cfg"), py::arg("stream"), py::arg("stamps") = 0,
+     py::arg("out_bf16") = 0);
   m.def("tile_shape", [](int cfg) { return py::make_tuple(ea_gemm_tile_m(cfg), ea_gemm_tile_n(cfg)); });
 
   m.def("replica_average", [](uintptr_t P, long long sP, int R, long long n, uintptr_t out, int write_back,

@@ -50,6 +50,9 @@ Executor::Executor(const ExecCfg& cfg) : c_(cfg) {
 }
 
 Executor::~Executor() {
+  // work still in flight on any stream may use these buffers and graphs (a trainer dropped
+  // right after enqueueing): drain the device before freeing anything
+  (void)hipDeviceSynchronize();
   destroy_graphs();
   if (d_probs_) (void)hipFree(d_probs_);
   if (d_zp_) (void)hipFree(d_zp_);
@@ -679,6 +682,8 @@ void Executor::set_seed(unsigned long long seed) {
 }
 
 void Executor::destroy_graphs() {
+  if (graphs_.empty()) return;
+  (void)hipDeviceSynchronize();   // an instantiated graph may still be executing
   for (auto& g : graphs_) {
     if (g.second) (void)hipGraphExecDestroy(g.second);
     if (g.first) (void)hipGraphDestroy(g.first);

@@ -160,6 +160,17 @@ class NativeTrainer(TrainerBase):
     # launch's P / S / weight-image round trip are paid once per chunk): longer chunks
     PERSIST_CHUNK = max(1, int(os.environ.get("ELEPHAS_AMD_PERSIST_CHUNK", "128")))
 
+    def __del__(self):
+        # the trainer's tensors live in torch's caching allocator, its kernels on its own
+        # stream: a dropped trainer must not hand its memory to the next allocation while
+        # work it enqueued still runs (torch only orders reuse on the allocating stream)
+        try:
+            st = self.__dict__.get("stream")
+            if st is not None:
+                st.synchronize()
+        except Exception:  # noqa: BLE001 - interpreter shutdown, CUDA already torn down
+            pass
+
     def __init__(self, model, plan, R: int = 1, batch_size: int = 32, device=None, seed: Optional[int] = None,
                  policy: Optional[str] = None, eval_batch: int = 2048, rowchain: Optional[int] = None,
                  persist: Optional[int] = None, stream: Optional[torch.cuda.Stream] = None,

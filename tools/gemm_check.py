@@ -24,17 +24,27 @@ for (M, N, K) in [(64, 128, 784), (64, 10, 128), (785, 128, 64), (300, 200, 136)
             print(f"M={M} N={N} K={K} bf16={bf16} cfg={cfg} relerr={err:.2e}", flush=True)
             if err > 1e-2:
                 ok = False
+            if bf16 and N % 8 == 0:   # bf16 C: the fp32 result rounded once
+                Cb = torch.zeros(M, N, device=dev, dtype=torch.bfloat16)
+                C.gemm_nt(A.data_ptr(), BT.data_ptr(), Cb.data_ptr(), M, N, K, K, K, N, bf16, cfg, s, 0, 1)
+                torch.cuda.synchronize()
+                ok &= bool(torch.equal(Cb, Cm.to(torch.bfloat16)))
 # timing of the wide-MLP shapes: FWD/DX (M=batch 1024) and DW (K=batch)
 s = torch.cuda.current_stream().cuda_stream
 for (M, N, K) in [(4096, 4096, 4096), (1024, 4096, 4096), (4096, 4096, 1024), (1024, 1000, 4096)]:
     A = (torch.rand(M, K, device=dev) * 2 - 1).to(torch.bfloat16)
     BT = (torch.rand(N, K, device=dev) * 2 - 1).to(torch.bfloat16)
     Cm = torch.zeros(M, N, device=dev)
+    Cb = torch.zeros(M, N, device=dev, dtype=torch.bfloat16)
     res = []
-    for cfg in (1, 2, 4, "torch"):
+    # "4b": the 256x256 tile writing bf16 C, as hipBLASLt's bf16 matmul does (fp32 C doubles
+    # the epilogue's HBM writes)
+    for cfg in (1, 2, 4, "4b", "torch"):
         def f():
             if cfg == "torch":
                 torch.matmul(A, BT.t())
+            elif cfg == "4b":
+                C.gemm_nt(A.data_ptr(), BT.data_ptr(), Cb.data_ptr(), M, N, K, K, K, N, 1, 4, s, 0, 1)
             else:
                 C.gemm_nt(A.data_ptr(), BT.data_ptr(), Cm.data_ptr(), M, N, K, K, K, N, 1, cfg, s)
         for _ in range(3): f()

@@ -21,14 +21,16 @@ for (M, N, K) in [(4096, 4096, 4096), (4096, 4096, 1024), (4097, 4096, 1024), (1
     A = (torch.rand(M, K, device=dev) * 2 - 1).to(torch.bfloat16)
     BT = (torch.rand(N, K, device=dev) * 2 - 1).to(torch.bfloat16)
     Cm = torch.zeros(M, N, device=dev)
-    for cfg in (4, 1):
+    Cb = torch.zeros(M, N, device=dev, dtype=torch.bfloat16)
+    for cfg, ob in ((4, 0), (4, 1), (1, 0)):
+        out = Cb if ob else Cm
         tm, tn = C.tile_shape(cfg)
         nb = ((M + tm - 1) // tm) * ((N + tn - 1) // tn)
         st = torch.zeros(nb * 16, dtype=torch.int64, device=dev)
         for _ in range(3):
-            C.gemm_nt(A.data_ptr(), BT.data_ptr(), Cm.data_ptr(), M, N, K, K, K, N, 1, cfg, s, 0)
+            C.gemm_nt(A.data_ptr(), BT.data_ptr(), out.data_ptr(), M, N, K, K, K, N, 1, cfg, s, 0, ob)
         torch.cuda.synchronize()
-        C.gemm_nt(A.data_ptr(), BT.data_ptr(), Cm.data_ptr(), M, N, K, K, K, N, 1, cfg, s, st.data_ptr())
+        C.gemm_nt(A.data_ptr(), BT.data_ptr(), out.data_ptr(), M, N, K, K, K, N, 1, cfg, s, st.data_ptr(), ob)
         torch.cuda.synchronize()
         v = st.view(nb, 16).cpu().numpy().astype(np.int64)
         t0 = v[:, 0].min()
@@ -38,6 +40,6 @@ for (M, N, K) in [(4096, 4096, 4096), (4096, 4096, 1024), (4097, 4096, 1024), (1
         setup = np.median(rel[:, 1] - rel[:, 0])
         loop = np.median(rel[:, 2] - rel[:, 1])
         epi = np.median(rel[:, 4] - rel[:, 2])
-        print(f"M={M} N={N} K={K} cfg={cfg} blocks={nb}: span {span:.1f} us; per block median setup {setup:.2f} "
+        print(f"M={M} N={N} K={K} cfg={cfg}{' bf16-out' if ob else ''} blocks={nb}: span {span:.1f} us; per block median setup {setup:.2f} "
               f"main loop {loop:.2f} epilogue {epi:.2f} us; start spread {np.median(rel[:, 0]):.2f}/"
               f"{rel[:, 0].max():.2f}; stamps {np.round(med, 2)}", flush=True)
