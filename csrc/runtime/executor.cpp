@@ -705,10 +705,12 @@ int Executor::split_last(int cfg, long long N, long long K) const {
 
 int Executor::pick_cfg(long long M, long long N, long long K) const {
   if (c_.force_cfg >= 0) return (c_.force_cfg == 4 && !c_.bf16) ? 1 : c_.force_cfg;
-  // 256x256 ping-pong tiles (bf16) where they alone give every CU a workgroup
-  // (e.g. the 4096 x 4096 weight gradients of the Wide MLP: 256 tiles)
-  if (c_.bf16 && c_.big && M >= 1024 && N >= 1024 && K >= 512 &&
-      (long long)c_.R * cdiv((int)M, 256) * cdiv((int)N, 256) >= 240)
+  // 256x256 ping-pong tiles (bf16): by default where the launch holds at least two rounds
+  // of them (Wide MLP, 8 workers: 8 x 272 DW tiles, 8 x 64 FWD tiles -- 2.44 M vs 2.19 M
+  // samples/s on the THR tiles; 1 worker, one round: 1.48 M vs 1.81 M, profiles/sweep_r5.jsonl);
+  // big = 1 forces them wherever they give every CU a workgroup, 0 never
+  const long long big_tiles = (long long)c_.R * cdiv((int)M, 256) * cdiv((int)N, 256);
+  if (c_.bf16 && c_.big != 0 && M >= 1024 && N >= 1024 && K >= 512 && big_tiles >= (c_.big > 0 ? 240 : 512))
     return 4;
   if (M >= 256 && N >= c_.thr_min_n && K >= c_.thr_min_k) {
     // 128x128 tiles while they give every CU at least two workgroups (256 CUs),

@@ -313,7 +313,7 @@ class NativeTrainer(TrainerBase):
         return dict(
             R=self.R, B=ws["B"], Bp=ws["Bp"], bf16=int(self.bf16), seed=self.seed,
             force_cfg=int(os.environ.get("ELEPHAS_AMD_GEMM_CFG", "-1")),
-            big=int(os.environ.get("ELEPHAS_AMD_BIG", "0")),
+            big=int(os.environ.get("ELEPHAS_AMD_BIG", "-1")),
             rc_lean=int(os.environ.get("ELEPHAS_AMD_RC_LEAN", "1")),
             thr_min_k=int(os.environ.get("ELEPHAS_AMD_THR_MIN_K", "64")),
             thr_min_n=int(os.environ.get("ELEPHAS_AMD_THR_MIN_N", "256")),
