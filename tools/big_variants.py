@@ -1,6 +1,7 @@
-"""Schedule variants of the 8-phase 256x256 tile (gemm_big.h V): cfg 4 = V0, 5 = V1
-(A copies one phase earlier), 6 = V6 (copies in the MFMA ticks), 7 = V5 (V6 with the
-fragment-read wait behind the barrier). Checks them against torch and times all."""
+"""Schedule variants of the 8-phase 256x256 tile (gemm_big.h V): cfg 4 = the production
+schedule (V1: A copies one phase earlier), 5 = V5 (V6 with the fragment-read wait behind the
+barrier), 6 = V6 (copies in the MFMA ticks), 7 = V0 (the round-3 schedule). Checks them
+against torch and times all (one order: use tools/big_ab.py for A/B)."""
 import os
 import sys
 import time

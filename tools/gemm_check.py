@@ -47,10 +47,13 @@ for (M, N, K) in [(4096, 4096, 4096), (1024, 4096, 4096), (4096, 4096, 1024), (1
                 C.gemm_nt(A.data_ptr(), BT.data_ptr(), Cb.data_ptr(), M, N, K, K, K, N, 1, 4, s, 0, 1)
             else:
                 C.gemm_nt(A.data_ptr(), BT.data_ptr(), Cm.data_ptr(), M, N, K, K, K, N, 1, cfg, s)
-        for _ in range(3): f()
-        torch.cuda.synchronize(); t = time.time()
-        for _ in range(20): f()
-        torch.cuda.synchronize(); dt = (time.time() - t) / 20
+        # steady state: a 10-call warm-up (clocks, caches), then the best of 3 rounds of 20
+        for _ in range(10): f()
+        dt = 1e9
+        for _ in range(3):
+            torch.cuda.synchronize(); t = time.time()
+            for _ in range(20): f()
+            torch.cuda.synchronize(); dt = min(dt, (time.time() - t) / 20)
         res.append(f"{cfg}: {dt*1e6:.0f} us {2*M*N*K/dt/1e12:.0f} TF")
     print(f"M={M} N={N} K={K} bf16 random:", " | ".join(res), flush=True)
 print("OK" if ok else "FAIL")

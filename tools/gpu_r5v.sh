@@ -1,0 +1,7 @@
+#!/bin/bash
+mkdir -p gpurun_out
+. tools/gpu_step.sh
+step r5v_gemm_check 300 python tools/gemm_check.py
+step r5v_native 400 python -u -m pytest tests/test_native_gpu.py -q -x --timeout 200 --timeout-method thread
+step r5v_wide_w8 150 python bench.py --model wide --policy mixed_bfloat16 --steps 20 --warmup 5 --no-sub
+step r5v_big_ab 300 python tools/big_ab.py 4,7,5

@@ -3,7 +3,7 @@ in-kernel s_memrealtime stamps (10 ns ticks): per step, the median stamp of ever
 phase of every role relative to the chain workgroups' publication of the previous
 step's dZ_0 rows (V2: the step's true start; V1: the partials seen), and the step period.
 
-  python tools/persist_stamps.py [R] [B] [steps] [v2: 1|0|-1] [policy]
+  python tools/persist_stamps.py [R] [B] [steps] [v2: 1|0|-1] [policy] [sync]
 """
 import os
 import sys
@@ -44,7 +44,8 @@ def main():
     m.add(Dropout(0.2))
     m.add(Dense(10, activation="softmax"))
     m.compile(SGD(0.1), "categorical_crossentropy", ["acc"])
-    t = NativeTrainer(m, build_plan(m), R, B, torch.device("cuda"), seed=1, persist=1)
+    sync = len(sys.argv) > 6 and sys.argv[6] == "sync"
+    t = NativeTrainer(m, build_plan(m), R, B, torch.device("cuda"), seed=1, persist=1, sync=sync)
     rng = np.random.default_rng(0)
     xs = [rng.random((7500, 784), dtype=np.float32) for _ in range(R)]
     ys = [np.eye(10, dtype=np.float32)[rng.integers(0, 10, 7500)] for _ in range(R)]
