@@ -193,7 +193,7 @@ constexpr int PM_NTU = 2;      // layer-1 column tiles (and layer-2 row tiles) a
 // XT (sync across ranks: replica 0's workgroup q has the job-wide sum of its tile in its
 // total slab; the other replicas read it there instead of every rank's slab)
 enum PmFlag : int { PMF_PART = 0, PMF_BWD = 1, PMF_W = 2, PMF_A0 = 3, PMF_D2 = 4, PMF_GO = 5, PMF_X = 6, PMF_GR = 7,
-                    PMF_XT = 8, PMF_N = 9 };
+                    PMF_XT = 8, PMF_XS = 9, PMF_N = 10 };
 // sticky error codes: the wait that timed out (PERR_GRID: the grid was not resident --
 // nothing was modified, the chunk can be re-run on another plan)
 enum PmErr : unsigned { PERR_L0_BWD = 1, PERR_CHAIN_PART = 2, PERR_CHAIN_BWD = 3, PERR_CHAIN_PREV = 4,
@@ -220,6 +220,7 @@ struct PersistArgs {
   // sums the R slabs in replica order -- the same bits everywhere, so the replicas'
   // updates (grad_scale = 1 / R) keep their weights identical
   int sync;
+  int xchg_rs;                      // sync: reduce-scatter + all-gather of the slabs (else all-gather + sum)
   long long o_xg;                   // exchange slabs [2][wgs][PM_XSLOT] in every replica's workspace
   // sync across ranks (xr_world > 1; one node, every rank the same step sequence): after
   // the replica sum, replica 0's owning workgroup q puts the rank's sum into slab

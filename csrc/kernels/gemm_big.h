@@ -327,9 +327,7 @@ __device__ __forceinline__ void run_prob_big(const GA& ga, const Prob& p, const 
 // runs on XCD b % 8; give each XCD a contiguous run of tiles, ordered in groups of
 // 4 tile rows (column-major inside a group) so an XCD's concurrent tiles share A
 // rows and B^T columns in its L2. Bijective for any tile count.
-__device__ __forceinline__ int big_tile_of(int b, int ntiles, int tiles_m, int tiles_n) {
-  const int x = b & 7, q = ntiles >> 3, rem = ntiles & 7;
-  const int lin = (x < rem ? x * (q + 1) : rem * (q + 1) + (x - rem) * q) + (b >> 3);
+__device__ __forceinline__ int big_group_of(int lin, int tiles_m, int tiles_n) {
   constexpr int GM = 4;
   const int per_group = GM * tiles_n;
   const int grp = lin / per_group, first = grp * GM;
@@ -337,10 +335,17 @@ __device__ __forceinline__ int big_tile_of(int b, int ntiles, int tiles_m, int t
   const int in = lin - grp * per_group;
   return (first + in % gsz) * tiles_n + in / gsz;
 }
+__device__ __forceinline__ int big_tile_of(int b, int ntiles, int tiles_m, int tiles_n) {
+  const int x = b & 7, q = ntiles >> 3, rem = ntiles & 7;
+  return big_group_of((x < rem ? x * (q + 1) : rem * (q + 1) + (x - rem) * q) + (b >> 3), tiles_m, tiles_n);
+}
 
 // grid (R, total_blocks): problem by block range as gemm_grouped; the tile order
-// inside a problem is XCD-aware when the launch has one replica
-template <unsigned KM0, unsigned KM1, int V = 0>
+// inside a problem is XCD-aware when the launch has one replica.  With R = 8 every
+// replica's tiles share one XCD (x-fastest dealing); G: take them in groups of 4 tile rows
+// (column-major inside a group) so the XCD's concurrent tiles read each B^T column tile
+// once per round instead of once per pair of tile rows
+template <unsigned KM0, unsigned KM1, int V = 0, int G = 0>
 __global__ __launch_bounds__(BIG_NT) void gemm_big(GroupArgs ga) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   stamp(ga, 0);
@@ -351,6 +356,7 @@ __global__ __launch_bounds__(BIG_NT) void gemm_big(GroupArgs ga) {
   int lb = bid - p.block_begin;
   const int nt = p.tiles_m * p.tiles_n;
   if (ga.R == 1 && ga.nprob == 1) lb = big_tile_of(lb, nt, p.tiles_m, p.tiles_n);
+  else if (G) lb = big_group_of(lb, p.tiles_m, p.tiles_n);
   if (pi) run_prob_big<KM1, V>(ga, ga.p[1], r, lb, smem);
   else run_prob_big<KM0, V>(ga, ga.p[0], r, lb, smem);
   stamp(ga, 4);

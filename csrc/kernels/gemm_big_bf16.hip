@@ -1,5 +1,7 @@
 // Grouped GEMM instantiation: the 256x256 8-wave ping-pong tile (gemm_big.h), bf16,
 // one variant per kind set a launch can hold.
+#include <cstdlib>
+
 #include "gemm_big.h"
 
 namespace ea {
@@ -9,16 +11,27 @@ namespace ea {
 // 1058; 8192^3 1303 / 1284, 1270 / 1266, 1260 / 1250 -- within a few per cent of each other
 // (single-order runs, profiles/big_variants_r5.txt, mostly measure clock warm-up)
 constexpr int BIG_V = 1;
+// tile order of multi-replica launches (gemm_big G): ELEPHAS_AMD_BIG_GROUP=1 groups of 4 tile rows
+static int big_group() {
+  static const int g = [] {
+    const char* e = std::getenv("ELEPHAS_AMD_BIG_GROUP");
+    return (e && std::atoi(e) != 0) ? 1 : 0;
+  }();
+  return g;
+}
 template <unsigned KM0, unsigned KM1>
 static bool big_if(const GroupArgs& ga, hipStream_t s, hipError_t& e) {
   if (!(KM0 & KB(ga.p[0].kind))) return false;
   if (ga.nprob > 1 && !(KM1 & KB(ga.p[1].kind))) return false;
-  hipLaunchKernelGGL((gemm_big<KM0, KM1, BIG_V>), dim3(ga.R, ga.total_blocks), dim3(BIG_NT), BIG_LDS, s, ga);
+  if (big_group() && ga.R > 1)
+    hipLaunchKernelGGL((gemm_big<KM0, KM1, BIG_V, 1>), dim3(ga.R, ga.total_blocks), dim3(BIG_NT), BIG_LDS, s, ga);
+  else
+    hipLaunchKernelGGL((gemm_big<KM0, KM1, BIG_V>), dim3(ga.R, ga.total_blocks), dim3(BIG_NT), BIG_LDS, s, ga);
   e = hipGetLastError();
   return true;
 }
-template <unsigned KM0, unsigned KM1, int V = 0> static void big_attr() {
-  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_big<KM0, KM1, V>),
+template <unsigned KM0, unsigned KM1, int V = 0, int G = 0> static void big_attr() {
+  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_big<KM0, KM1, V, G>),
                             hipFuncAttributeMaxDynamicSharedMemorySize, BIG_LDS);
 }
 constexpr unsigned KM_PLAIN_ = KB(PK_PLAIN);
@@ -55,4 +68,8 @@ extern "C" void ea_gemm_init_big_bf16() {
   big_attr<KM_FWD, KM_NONE, BIG_V>();
   big_attr<KM_DW, KM_DX, BIG_V>();
   big_attr<KM_DX, KM_NONE, BIG_V>();
+  big_attr<KM_PLAIN_, KM_NONE, BIG_V, 1>();
+  big_attr<KM_FWD, KM_NONE, BIG_V, 1>();
+  big_attr<KM_DW, KM_DX, BIG_V, 1>();
+  big_attr<KM_DX, KM_NONE, BIG_V, 1>();
 }

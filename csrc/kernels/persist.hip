@@ -356,27 +356,18 @@ __device__ __forceinline__ bool xrank_sum(const PersistArgs& a, int q, unsigned 
   return true;
 }
 
-// sync: sum the weight-gradient fragments v[0 .. N) (f32x4 per lane, lane-linear slab
-// layout) of workgroup q over the R replicas, in replica order.  Every storing wave drains
-// its sc1 stores before the flag (publish); the slabs alternate by step parity, so a
-// replica running a step ahead never overwrites one a peer still reads.
-template <int N>
-__device__ __forceinline__ bool xchg_sum(const PersistArgs& a, int r, int q, int i, f32x4 (&v)[N]) {
+// lane 0..R-1 of wave 0 watches flag `kind` of workgroup q in replica lane's flag area
+// until every one reaches tag; the whole workgroup leaves together
+__device__ __forceinline__ bool wait_replicas(const PersistArgs& a, int kind, int q, unsigned tag) {
   const int tid = threadIdx.x;
-  const long long slab = a.o_xg + ((long long)(i & 1) * a.wgs + q) * PM_XSLOT;
-  const rsrc_t all = ws_rsrc(a.ws);   // every replica's workspace (offsets r * ws_stride)
-#pragma unroll
-  for (int u = 0; u < N; ++u) stw4(all, (u * 256 + tid) * 4, (int)((long long)r * a.ws_stride + slab), v[u]);
-  publish(flag_at(a, r, PMF_X) + q, (unsigned)(i + 1));
-  // one lane per replica watches that replica's flag of workgroup q
   int ok = 1;
   if (tid < 64) {
     const unsigned long long t0 = wall_clock64();
     for (;;) {
-      const unsigned f = tid < a.R ? __hip_atomic_load((gu32*)(flag_at(a, tid, PMF_X) + q), __ATOMIC_RELAXED,
+      const unsigned f = tid < a.R ? __hip_atomic_load((gu32*)(flag_at(a, tid, kind) + q), __ATOMIC_RELAXED,
                                                        __HIP_MEMORY_SCOPE_AGENT)
-                                   : (unsigned)(i + 1);
-      if (__all(f >= (unsigned)(i + 1))) break;
+                                   : tag;
+      if (__all(f >= tag)) break;
       if ((long long)(wall_clock64() - t0) > a.timeout) {
         ok = 0;
         if (tid == 0) __hip_atomic_store((gu32*)(a.err), (unsigned)PERR_XCHG, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -387,15 +378,77 @@ __device__ __forceinline__ bool xchg_sum(const PersistArgs& a, int r, int q, int
   }
   ok = __syncthreads_and(ok);
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  if (!ok) return false;
+  return ok != 0;
+}
+
+// sync: sum the weight-gradient fragments v[0 .. N) (f32x4 per lane, lane-linear slab
+// layout, E = 256 N f32x4) of workgroup q over the R replicas, in replica order, as a
+// reduce-scatter + all-gather inside the slabs (xchg_rs; else every replica sums all R
+// slabs, 4 slabs' loads in flight): every replica stores its partial slab and
+// raises PMF_X; replica r sums chunk r (f32x4 [rC, rC + C), C = ceil(E / R)) over the R
+// slabs in replica order and writes the sum over its own chunk r (only r reads that
+// chunk's partial), raises PMF_XS; then every replica reads chunk o's sum from replica o.
+// Each workgroup moves 2 slabs instead of R (the all-gather-and-sum it replaces read R),
+// and the sums are the same bits as R in-order additions everywhere.  Every storing wave
+// drains its sc1 stores before a flag (publish); the slabs alternate by step parity: a
+// replica writes step i + 2's partials only after seeing every replica's step i + 1
+// partials, which each stored after finishing its step-i reads.
+template <int N>
+__device__ __forceinline__ bool xchg_sum(const PersistArgs& a, int r, int q, int i, f32x4 (&v)[N]) {
+  const int tid = threadIdx.x;
+  const long long slab = a.o_xg + ((long long)(i & 1) * a.wgs + q) * PM_XSLOT;
+  const rsrc_t all = ws_rsrc(a.ws);   // every replica's workspace (offsets r * ws_stride)
+  if (a.R > 1) {
+    const unsigned tag = (unsigned)(i + 1);
 #pragma unroll
-  for (int u = 0; u < N; ++u) v[u] = zero4f();
-  for (int rr = 0; rr < a.R; ++rr) {
-    f32x4 x[N];
+    for (int u = 0; u < N; ++u) stw4(all, (u * 256 + tid) * 4, (int)((long long)r * a.ws_stride + slab), v[u]);
+    publish(flag_at(a, r, PMF_X) + q, tag);
+    if (!wait_replicas(a, PMF_X, q, tag)) return false;
+    if (a.xchg_rs) {
+      constexpr int E = N * 256;
+      const int C = (E + a.R - 1) / a.R;
+      const int lo = r * C, hi = lo + C < E ? lo + C : E;
+      for (int e = lo + tid; e < hi; e += 256) {
+        f32x4 s = zero4f();
+        for (int rb = 0; rb < a.R; rb += 8) {   // 8 slabs' loads in flight, summed in replica order
+          f32x4 x[8];
 #pragma unroll
-    for (int u = 0; u < N; ++u) x[u] = ldw4(all, (u * 256 + tid) * 4, (int)((long long)rr * a.ws_stride + slab));
+          for (int k = 0; k < 8; ++k) {
+            const int rr = rb + k < a.R ? rb + k : rb;
+            x[k] = ldw4(all, e * 4, (int)((long long)rr * a.ws_stride + slab));
+          }
 #pragma unroll
-    for (int u = 0; u < N; ++u) v[u] += x[u];
+          for (int k = 0; k < 8; ++k)
+            if (rb + k < a.R) s += x[k];
+        }
+        stw4(all, e * 4, (int)((long long)r * a.ws_stride + slab), s);
+      }
+      publish(flag_at(a, r, PMF_XS) + q, tag);
+      if (!wait_replicas(a, PMF_XS, q, tag)) return false;
+#pragma unroll
+      for (int u = 0; u < N; ++u) {
+        const int e = u * 256 + tid;
+        v[u] = ldw4(all, e * 4, (int)((long long)(e / C) * a.ws_stride + slab));
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < N; ++u) v[u] = zero4f();
+      for (int rb = 0; rb < a.R; rb += 4) {   // 4 slabs' loads in flight, summed in replica order
+        f32x4 x[4][N];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int rr = rb + k < a.R ? rb + k : rb;
+#pragma unroll
+          for (int u = 0; u < N; ++u) x[k][u] = ldw4(all, (u * 256 + tid) * 4, (int)((long long)rr * a.ws_stride + slab));
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          if (rb + k < a.R) {
+#pragma unroll
+            for (int u = 0; u < N; ++u) v[u] += x[k][u];
+          }
+      }
+    }
   }
   if (a.xr_world <= 1) return true;
   // ---- across ranks: replica 0 publishes the rank's sum, reads every rank's (over xGMI

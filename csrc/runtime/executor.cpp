@@ -147,6 +147,8 @@ bool Executor::build_persist() {
   }
   a.wgs = a.nk0 * a.nc0 + nch + nd_use;
   a.sync = c_.persist_sync ? 1 : 0;
+  const char* xrs = std::getenv("ELEPHAS_AMD_XCHG_RS");   // A/B: reduce-scatter exchange of the replicas
+  a.xchg_rs = (xrs && std::atoi(xrs) != 0) ? 1 : 0;
   a.bf16 = c_.bf16 ? 1 : 0;
   const char* pim = std::getenv("ELEPHAS_AMD_PERSIST_IMAGES");   // A/B: V2 epilogue writes the images too
   a.imgs = (!v2 || (pim && std::atoi(pim) != 0)) ? 1 : 0;

@@ -105,6 +105,22 @@ def main():
             jl.append([(s[chain & m & (q == nl0 + j), i - 1, ref_k][0] - b0[m][0]) / 100.0 for j in range(nch)])
         print(f"step {i} last dz0_pub(i-1) {np.round(np.median(cl), 2)}  last part_pub {np.round(np.median(pl), 2)}"
               f"  last seen {np.round(np.median(sl), 2)}  per chain j dz0_pub {np.round(np.median(jl, axis=0), 2)}")
+    if sync:
+        # the replica exchange of every owning workgroup q (absolute times, all replicas):
+        # skew = last replica's arrival - this replica's, latency = this replica's exit - last arrival
+        for role, (ka, kb) in (("l0", (7, 8)), ("chain", (24, 26))):
+            sk, lat = [], []
+            for i in range(1, min(8, nst)):
+                for qq in np.unique(q[roles[role]]):
+                    m = q == qq
+                    a_, b_ = s[m, i, ka], s[m, i, kb]
+                    if (a_ == 0).any() or (b_ == 0).any():
+                        continue
+                    sk.extend((a_.max() - a_) / 100.0)
+                    lat.extend((b_ - a_.max()) / 100.0)
+            if sk:
+                print(f"exchange {role}: wait for the last replica median {np.median(sk):.2f} us (max {np.max(sk):.2f}); "
+                      f"after the last arrival median {np.median(lat):.2f} us (min {np.min(lat):.2f})")
     # the launch's fill: step 0 relative to the earliest layer-0 start stamp of the replica
     f = {}
     for rr in range(R):
