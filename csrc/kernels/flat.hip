@@ -6,6 +6,7 @@
 //   * parameter-server updates (theta <- theta - delta; lock-free hogwild variant
 //     with fp32 global atomics) and generic axpby.
 // All loads/stores are 16-byte vectorised where the layout allows.
+#include <type_traits>
 #include "common.h"
 
 namespace ea {
@@ -213,15 +214,52 @@ static int shadow_tiles(const FlatArgs& a) {
 
 // scale * sum over R replicas of P[r][i] (fp64 accumulation; scale 1/R = the mean);
 // result written to every replica if write_back (and to out if given)
+// theta <- scale * sum_r P_r: fp64 sums in replica order; every replica's loads of a chunk of
+// 8 replicas are in flight together (the loop-carried sum otherwise serialised them: one
+// memory latency per replica); VEC: 4 elements per lane (16-byte rows, n4 = n / 4 of them)
+template <bool VEC>
 __global__ __launch_bounds__(256) void replica_average_kernel(float* P, long long sP, int R, long long n,
                                                               float* out, int write_back, double scale) {
-  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
-    double s = 0.0;
-    for (int r = 0; r < R; ++r) s += P[(long long)r * sP + i];
-    const float m = (float)(s * scale);
-    if (out) out[i] = m;
+  constexpr int W = VEC ? 4 : 1;
+  using V = typename std::conditional<VEC, float4, float>::type;
+  const long long nv = n / W;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < nv; i += (long long)gridDim.x * 256) {
+    double s[W];
+#pragma unroll
+    for (int w = 0; w < W; ++w) s[w] = 0.0;
+    for (int r0 = 0; r0 < R; r0 += 8) {
+      V x[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int r = r0 + k < R ? r0 + k : r0;
+        x[k] = reinterpret_cast<const V*>(P + (long long)r * sP)[i];
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        if (r0 + k >= R) break;
+        const float* f = reinterpret_cast<const float*>(&x[k]);
+#pragma unroll
+        for (int w = 0; w < W; ++w) s[w] += f[w];
+      }
+    }
+    V m;
+    float* mf = reinterpret_cast<float*>(&m);
+#pragma unroll
+    for (int w = 0; w < W; ++w) mf[w] = (float)(s[w] * scale);
+    if (out) reinterpret_cast<V*>(out)[i] = m;
     if (write_back)
-      for (int r = 0; r < R; ++r) P[(long long)r * sP + i] = m;
+      for (int r = 0; r < R; ++r) reinterpret_cast<V*>(P + (long long)r * sP)[i] = m;
+  }
+  if (VEC) {   // the n % 4 tail elements
+    const long long t = nv * W + (long long)blockIdx.x * 256 + threadIdx.x;
+    if (t < n) {
+      double s = 0.0;
+      for (int r = 0; r < R; ++r) s += P[(long long)r * sP + t];
+      const float m = (float)(s * scale);
+      if (out) out[t] = m;
+      if (write_back)
+        for (int r = 0; r < R; ++r) P[(long long)r * sP + t] = m;
+    }
   }
 }
 
@@ -307,7 +345,14 @@ extern "C" hipError_t ea_refresh_shadows(FlatArgs* a, int bf16, hipStream_t s) {
 
 extern "C" hipError_t ea_replica_average(float* P, long long sP, int R, long long n, float* out, int write_back,
                                          double scale, hipStream_t s) {
-  hipLaunchKernelGGL(replica_average_kernel, dim3(grid_for(n)), dim3(256), 0, s, P, sP, R, n, out, write_back, scale);
+  const bool vec = sP % 4 == 0 && (reinterpret_cast<uintptr_t>(P) & 15) == 0 &&
+                   (out == nullptr || (reinterpret_cast<uintptr_t>(out) & 15) == 0);
+  if (vec)
+    hipLaunchKernelGGL(replica_average_kernel<true>, dim3(grid_for((n + 3) / 4)), dim3(256), 0, s, P, sP, R, n, out,
+                       write_back, scale);
+  else
+    hipLaunchKernelGGL(replica_average_kernel<false>, dim3(grid_for(n)), dim3(256), 0, s, P, sP, R, n, out, write_back,
+                       scale);
   return hipGetLastError();
 }
 

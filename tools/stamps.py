@@ -19,6 +19,7 @@ ys = [np.eye(dout, dtype=np.float32)[rng.integers(0, dout, 7500)] for _ in range
 t.set_data(xs, ys, 0.1)
 t.begin_epoch()
 t.run_steps(30)
+t.begin_epoch()   # the stamped launches run step 0 of an epoch (no skipped updates)
 blocks = t.exe.launch_blocks()
 buf = torch.zeros(max(blocks) * 16, dtype=torch.int64, device="cuda")
 t.exe.set_stamps(buf.data_ptr())
