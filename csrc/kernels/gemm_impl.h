@@ -597,9 +597,20 @@ __device__ __forceinline__ void tile_epilogue(const GA& ga, const Prob& p, const
       float* __restrict__ Z = p.Z ? p.Z + (long long)r * p.sZ : nullptr;
       const float keep_scale = p.rate > 0.f ? 1.f / (1.f - p.rate) : 1.f;
       const bool drop = p.rate > 0.f && !p.eval_mode;
-      // Z rows as 32-byte pairs of 16-byte accesses where whole and aligned (the element
-      // accesses they replace made the 256x256 tile's FWD epilogue ~3/4 of its time)
+      // Z rows as 32-byte pairs of 16-byte accesses where whole and aligned (element
+      // accesses: Wide step 3.24 ms, 3.06 with these)
       const bool zvec = Z && (p.ldz & 3) == 0 && (reinterpret_cast<unsigned long long>(Z) & 15) == 0;
+      // the bias of this thread's 8 columns, the same in every pass: loaded once
+      float bia[8];
+      {
+        const int gn0 = n0 + t_c0;
+        if (bias && gn0 + 8 <= p.N && (reinterpret_cast<unsigned long long>(bias + gn0) & 15) == 0) {
+          ld8f(bias + gn0, bia);
+        } else {
+#pragma unroll
+          for (int q = 0; q < 8; ++q) bia[q] = (bias && gn0 + q < p.N) ? bias[gn0 + q] : 0.f;
+        }
+      }
 #pragma unroll EUNR
       for (int ps = 0; ps < PASSES; ++ps) {
         const int row = ps * RPP + t_row, gm = m0 + row, gn0 = n0 + t_c0;
@@ -614,15 +625,14 @@ __device__ __forceinline__ void tile_epilogue(const GA& ga, const Prob& p, const
 #pragma unroll
           for (int q = 0; q < 8; ++q) u[q] = 1.f;
         }
-        if (!fwd && zw && rv) {
+        if (fwd) {
+#pragma unroll
+          for (int q = 0; q < 8; ++q) aux[q] = bia[q];
+        } else if (zw && rv) {
           ld8f(Z + (long long)gm * p.ldz + gn0, aux);
         } else {
 #pragma unroll
-          for (int q = 0; q < 8; ++q) {  // loads first
-            const bool in = gn0 + q < p.N;
-            if (fwd) aux[q] = (bias && in) ? bias[gn0 + q] : 0.f;
-            else aux[q] = (in && rv) ? Z[(long long)gm * p.ldz + gn0 + q] : 0.f;
-          }
+          for (int q = 0; q < 8; ++q) aux[q] = (gn0 + q < p.N && rv) ? Z[(long long)gm * p.ldz + gn0 + q] : 0.f;
         }
         float av[8];
         if (fwd) {

@@ -1,0 +1,9 @@
+#!/bin/bash
+# FWD epilogue: bias of the thread's 8 columns loaded once per tile half
+mkdir -p gpurun_out
+. tools/gpu_step.sh
+step r5yx_native_tests 400 python -u -m pytest tests/test_native_gpu.py -x -q --timeout 120 --timeout-method thread
+step r5yx_wide_a 150 python bench.py --model wide --policy mixed_bfloat16 --steps 20 --warmup 5 --no-sub
+step r5yx_wide_b 150 python bench.py --model wide --policy mixed_bfloat16 --steps 20 --warmup 5 --no-sub
+step r5yx_wide_stamps 240 python tools/stamps.py 8 wide 1024 mixed_bfloat16
+step r5yx_otto 120 python bench.py --model otto --steps 200 --warmup 20 --no-sub
