@@ -705,6 +705,11 @@ int Executor::split_last(int cfg, long long N, long long K) const {
   return ks;
 }
 
+static bool big_dw_off() {
+  const char* e = std::getenv("ELEPHAS_AMD_BIG_DW");
+  return e && e[0] == '0';
+}
+
 int Executor::pick_cfg(long long M, long long N, long long K) const {
   if (c_.force_cfg >= 0) return (c_.force_cfg == 4 && !c_.bf16) ? 1 : c_.force_cfg;
   // 256x256 ping-pong tiles (bf16): by default where the launch holds at least two rounds
@@ -1033,7 +1038,12 @@ void Executor::build() {
       x.DT = reinterpret_cast<void*>(pv.dZT);
       x.lddt = c_.Bp;
       x.sDT = (long long)pv.N * c_.Bp;
-      const int cw = pick_cfg(w.M, w.N, w.K), cx = pick_cfg(x.M, x.N, x.K);
+      int cw = pick_cfg(w.M, w.N, w.K);
+      const int cx = pick_cfg(x.M, x.N, x.K);
+      // A/B: the weight-gradient products on the 128x128 tiles (two workgroups per CU, so
+      // one's update epilogue -- bandwidth-bound when every CU reaches it at once -- overlaps
+      // the other's main loop) while the input gradients keep the 256x256 tile
+      if (cw == 4 && big_dw_off()) cw = 1;
       // the shared launch's tile is the larger product's; when that tile leaves the
       // launch short of two workgroups per CU while the two products prefer different
       // tiles, each gets its own launch (Otto 512x512 layers: DW 513x512x128 on 128x64
@@ -1074,6 +1084,7 @@ void Executor::build() {
       if (xw > work) { cm = x.M; cn = x.N; ck = x.K; }
     }
     La.cfg = pick_cfg(cm, cn, ck);
+    if (La.ga.nprob == 1 && La.cfg == 4 && big_dw_off()) La.cfg = 1;   // layer 0: DW alone
     finalize(La);
     bwd_.push_back(La);
   }
