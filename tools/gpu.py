@@ -16,7 +16,14 @@ touches the GPU after it.  Steps (arguments are comma-separated, no spaces):
   pmc:NAME:CTRS:ARGS      one rocprofv3 --pmc pass (CTRS '+'-separated, within one pass's limits)
   py:SCRIPT[:ARGS]        python tools/SCRIPT ARGS (stamps.py, persist_stamps.py, gemm_check.py, ...)
 
-The profiles under profiles/ name the step that produced them (profiles/README.md).
+Any step may carry a tag and environment overrides in front of it:
+
+  [TAG/][VAR=VAL[+VAR=VAL...]@]STEP
+  e.g.  sync_rs/ELEPHAS_AMD_XCHG_RS=1@py:persist_stamps.py:8,64,8,-1,float32,sync
+
+(output in gpurun_out/TAG.txt).  The profiles under profiles/ name the step that produced
+them (profiles/README.md); tools/sessions/ keeps the earlier one-file session scripts that
+produced the older ones.
 """
 from __future__ import annotations
 
@@ -60,13 +67,31 @@ def _bench(args, env=None, tag="bench"):
     return _run(tag, [sys.executable, "bench.py"] + args + ["--out", out], 300, env=env)
 
 
+def parse_step(step: str, n: int):
+    """'[TAG/][VAR=VAL[+VAR=VAL...]@]KIND[:REST]' -> (tag, env overrides, kind, rest)."""
+    tag = None
+    head, sep, tail = step.partition("@")
+    if sep and "=" in head:
+        envspec, step = head, tail
+    else:
+        envspec = ""
+    if "/" in envspec.split("=")[0]:
+        tag, _, envspec = envspec.partition("/")
+    elif not envspec and "/" in step.split(":")[0]:
+        tag, _, step = step.partition("/")
+    env = dict(kv.split("=", 1) for kv in envspec.split("+")) if envspec else {}
+    kind, _, rest = step.partition(":")
+    return tag or f"s{n:02d}_{kind}", env, kind, rest
+
+
 def main(steps):
     os.makedirs(OUT, exist_ok=True)
     n = 0
     for step in steps:
         n += 1
-        kind, _, rest = step.partition(":")
-        tag = f"s{n:02d}_{kind}"
+        tag, extra, kind, rest = parse_step(step, n)
+        saved = {k: os.environ.get(k) for k in extra}
+        os.environ.update(extra)   # inherited by this step's child (restored below)
         if kind == "tests":
             cmd = [sys.executable, "-u", "-m", "pytest", "tests", "-m", "gpu", "-x", "-q", "--timeout", "300",
                    "--timeout-method", "thread"] + (["-k", rest] if rest else [])
@@ -109,6 +134,11 @@ def main(steps):
             rc = _run(tag, [sys.executable, os.path.join("tools", script)] + (args.split(",") if args else []), 600)
         else:
             raise SystemExit(f"unknown step {step!r}")
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
         if rc in FATAL:
             print(f"stopping: {step} ended with {rc}", flush=True)
             return rc
