@@ -127,6 +127,10 @@ def build(verbose: bool = False, force: bool = False, jobs: int = 6) -> str:
             raise RuntimeError(f"hipcc failed:\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
         return r
 
+    # a build that fails part-way may already have compiled bindings.cpp with this digest:
+    # drop the stamp first, so the next build recompiles it for whatever tree it sees
+    if cmds and os.path.exists(stamp):
+        os.remove(stamp)
     with ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
         list(ex.map(run, cmds))
     with open(stamp, "w") as f:
