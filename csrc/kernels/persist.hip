@@ -1550,17 +1550,24 @@ __device__ __forceinline__ void chain_role(const PersistArgs& a, float* smem, in
   };
   // data rows of this workgroup's targets (thread: rows tid / 32 + 8h, target column
   // tid % 32), read one step ahead so the target loads have no dependent address load
-  auto target_rows = [&](int s, int (&prow)[2]) {
+  // The permutation entries load unconditionally (index clamped into the row) and the
+  // row's validity is kept beside them: a select on the loaded value made the chain wait
+  // for this load right after the step's hand-off poll, ahead of the partial sums' loads
+  auto target_rows = [&](int s, int (&prow)[2], bool (&pok)[2]) {
     const int vs = st.valid(a, s);
-    const int* pr = a.perm + (long long)r * a.sPerm + (st.s0 + s) * a.B + m0;
+    const long long first = (long long)(st.s0 + s) * a.B + m0;
+    const int* pr = a.perm + (long long)r * a.sPerm;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int rr = (tid >> 5) + 8 * h;
-      prow[h] = (m0 + rr < vs && (tid & 31) < a.ldy) ? pr[rr] : -1;
+      const long long idx = first + rr < a.sPerm ? first + rr : a.sPerm - 1;
+      prow[h] = pr[idx];
+      pok[h] = m0 + rr < vs && (tid & 31) < a.ldy;
     }
   };
   int prow[2];
-  target_rows(0, prow);
+  bool pok[2];
+  target_rows(0, prow, pok);
   // the loss / metric sums of this workgroup's rows over the chunk (threads < 2 + nmet):
   // one fp64 atomic per value at the end of the launch instead of one per step (an
   // atomic in flight holds up the next hand-off's drain; float partials summed in fp64
@@ -1575,7 +1582,7 @@ __device__ __forceinline__ void chain_role(const PersistArgs& a, float* smem, in
     {
       const float* Yb = a.Y + (long long)r * a.sY;
 #pragma unroll
-      for (int h = 0; h < 2; ++h) yv[h] = prow[h] >= 0 ? Yb[(long long)prow[h] * a.ldy + (tid & 31)] : 0.f;
+      for (int h = 0; h < 2; ++h) yv[h] = pok[h] ? Yb[(long long)prow[h] * a.ldy + (tid & 31)] : 0.f;
     }
     pstamp(a, i, 0);
     // V1: the partials and every chain workgroup's updated W1 / W2 columns of the previous
@@ -1592,7 +1599,7 @@ __device__ __forceinline__ void chain_role(const PersistArgs& a, float* smem, in
       if (!wait_sets(a, sets, PERR_CHAIN_PART)) return;
     }
     pstamp(a, i, 1);
-    if (i + 1 < n) target_rows(i + 1, prow);
+    if (i + 1 < n) target_rows(i + 1, prow, pok);
     Staged<H0 * H1 / 1024> w1s;
     Staged<H1 / 64> w2s;
     f32x4 bvec = zero4f();
