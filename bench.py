@@ -28,6 +28,12 @@ Usage: python bench.py --gpus N --steps K --warmup W
   (N>1: launched by torch.distributed.run, or -- without WORLD_SIZE in the environment --
   bench.py starts the N ranks itself as a child torchrun job before touching the GPU)
 Prints ONE JSON line on rank 0.
+
+Deadline: ``$ELEPHAS_AMD_BENCH_DEADLINE_S`` (default 900, 0 = none) bounds every rank's
+wall time from its process start.  Past it, rank 0 prints the line it has -- the
+headline with every sub-measurement still pending recorded as ``{"error": "deadline"}``,
+or, before the headline was measured, a line with ``value`` null and ``error`` set --
+and every rank exits, so one stalled cross-rank wait cannot cost the record.
 """
 from __future__ import annotations
 
@@ -46,7 +52,10 @@ import hashlib
 import json
 import math
 import sys
+import threading
 import time
+
+_T0 = time.monotonic()   # the job-wide deadline counts from the process start
 
 import numpy as np
 
@@ -63,10 +72,65 @@ NAMES = {"mnist": "MNIST-MLP 784-128-128-10", "otto": "Otto-MLP 93-512-512-512-9
          "wide": "Wide-MLP 4096-4096-4096-1000"}
 
 
-def build_model(name):
+# rank 0's line under construction, shared with the deadline watchdog
+_REPORT = {"line": None, "subs": None, "pending": [], "printed": False, "out": None, "metric": None}
+_REPORT_LOCK = threading.Lock()
+
+
+def _emit(line, out):
+    s = json.dumps(line)
+    print(s, flush=True)
+    if out:
+        with open(out, "a") as f:
+            f.write(s + "\n")
+
+
+def _finish_report(line, out):
+    """Normal end: print the line unless the watchdog already did."""
+    with _REPORT_LOCK:
+        if _REPORT["printed"]:
+            return
+        _REPORT["printed"] = True
+    _emit(line, out)
+
+
+def _start_deadline(rank, world):
+    """Job-wide deadline (module docstring): a daemon thread that, once the process has run
+    for $ELEPHAS_AMD_BENCH_DEADLINE_S seconds, prints rank 0's line as far as it got and
+    ends the process (os._exit: the main thread may be blocked in a collective or a device
+    wait that no signal interrupts)."""
+    limit = float(os.environ.get("ELEPHAS_AMD_BENCH_DEADLINE_S", "900") or 0)
+    if limit <= 0:
+        return
+
+    def fire():
+        time.sleep(max(0.0, limit - (time.monotonic() - _T0)))
+        with _REPORT_LOCK:
+            if rank == 0 and not _REPORT["printed"]:
+                _REPORT["printed"] = True
+                line = _REPORT["line"]
+                if line is not None:
+                    for name in _REPORT["pending"]:
+                        _REPORT["subs"][name] = {"error": "deadline"}
+                    line["config"]["sub_measurements"] = _REPORT["subs"] or None
+                else:
+                    line = {"metric": _REPORT["metric"], "value": None, "unit": "samples/s", "n_gpus": world,
+                            "error": "deadline", "deadline_s": limit}
+                line["deadline_s"] = limit
+                try:
+                    _emit(line, _REPORT["out"])
+                except Exception:  # noqa: BLE001 - exiting regardless
+                    pass
+        sys.stderr.write(f"bench.py: rank {rank} reached the {limit:g} s deadline, exiting\n")
+        sys.stderr.flush()
+        os._exit(0)
+
+    threading.Thread(target=fire, name="bench-deadline", daemon=True).start()
+
+
+def build_model(name, optimizer="sgd", lr=None):
     from elephas_amd.models import Sequential, Dense, Activation, Dropout
-    from elephas_amd.models.optimizers import SGD
-    dims, drop, classes, _, lr = MODELS[name]
+    dims, drop, classes, _, lr_default = MODELS[name]
     m = Sequential()
     m.add(Dense(dims[1], input_dim=dims[0]))
     m.add(Activation("relu"))
@@ -79,8 +143,23 @@ def build_model(name):
             m.add(Dropout(drop))
     m.add(Dense(classes))
     m.add(Activation("softmax"))
-    m.compile(SGD(learning_rate=lr), "categorical_crossentropy", ["acc"])
+    m.compile(_optimizer(optimizer, lr, lr_default), "categorical_crossentropy", ["acc"])
     return m
+
+
+def _optimizer(kind, lr, lr_default):
+    """sgd: SGD at the model's rate (the reference examples'); adam: Adam at lr 0.01, the
+    Otto notebook's (examples/Spark_ML_Pipeline.ipynb:361)."""
+    from elephas_amd.models.optimizers import SGD, Adam
+    if kind == "adam":
+        return Adam(learning_rate=0.01 if lr is None else lr)
+    return SGD(learning_rate=lr_default if lr is None else lr)
+
+
+def _optimizer_desc(args):
+    if args.optimizer == "adam":
+        return "Adam(lr=%g)" % (0.01 if args.lr is None else args.lr)
+    return "SGD(lr=%g)" % (MODELS[args.model][4] if args.lr is None else args.lr)
 
 
 def _spawn_ranks(argv, n):
@@ -142,6 +221,10 @@ def main():
                     help="predict / evaluate: distributed inference of the master network "
                          "(SparkModel.predict / evaluate path, BASELINE config #5)")
     ap.add_argument("--infer-rows", type=int, default=None, help="rows per GPU for --task predict/evaluate")
+    ap.add_argument("--optimizer", default="sgd", choices=["sgd", "adam"],
+                    help="sgd (default: the reference examples' SGD at the model's rate) or adam (Adam lr 0.01, "
+                         "the Otto notebook's optimizer)")
+    ap.add_argument("--lr", type=float, default=None, help="override the optimizer's learning rate")
     args = ap.parse_args()
 
     if args.dims:
@@ -161,6 +244,10 @@ def main():
 
     dist.init_from_env()
     rank, world = dist.rank(), dist.world_size()
+    _REPORT["out"] = args.out
+    _REPORT["metric"] = ("samples/sec (whole node) MNIST-MLP 784-128-128-10 sync DP at 1/2/4/8 MI355X"
+                         if args.model == "mnist" else f"samples/sec (whole node) {NAMES[args.model]} sync DP")
+    _start_deadline(rank, world)
     if world != args.gpus:
         raise SystemExit(f"bench.py: --gpus {args.gpus} but the job has {world} rank(s)")
     gpu = torch.cuda.is_available()
@@ -172,7 +259,7 @@ def main():
     if args.dropout is not None:
         d, dr, c, r, lr = MODELS[args.model]
         MODELS[args.model] = (d, args.dropout, c, r, lr)
-    model = build_model(args.model)
+    model = build_model(args.model, args.optimizer, args.lr)
     if args.task == "fit":
         return bench_fit(args, model, dist, rank, world, dev)
     if args.task != "train":
@@ -184,28 +271,6 @@ def main():
     W = 8 // world if args.scaling == "strong" else args.workers_per_gpu
     batch_mode = args.granularity == "batch"
     m = measure_train(args, model, dist, rank, world, dev, gpu, W, batch_mode, args.steps, args.warmup)
-    # extra measurements in the same line (after the headline's timed region, never inside
-    # it), so a multi-GPU record also exercises the per-step exchange and the reference
-    # job's strong split: per-step sync DP at the same workers per GPU, and 8 // N workers
-    # per GPU (only for the default headline invocation; --no-sub skips them)
-    subs = {}
-    if (not args.no_sub and args.model == "mnist" and not batch_mode and args.scaling == "weak"
-            and args.workers_per_gpu == 8):
-        sk, sw = max(1, args.steps), max(1, args.warmup)
-        strong_w = 8 // world if 8 % world == 0 and 8 // world != W else None   # N = 1: the headline itself
-        for name, w_, bm in (("per_step_sync", W, True), ("strong", strong_w, False)):
-            if w_ is None:
-                continue
-            try:
-                r = measure_train(args, model, dist, rank, world, dev, gpu, w_, bm, sk, sw)
-            except Exception as e:  # noqa: BLE001 - an extra measurement never costs the headline line
-                subs[name] = {"error": repr(e)[:300]}
-                continue
-            subs[name] = {"value": round(r["samples"] / r["dt_max"], 1), "ms_per_step": round(r["dt_max"] / sk * 1e3, 4),
-                          "steps": sk, "workers_per_gpu": w_, "sync": r["sync"], "engine": r["engine"],
-                          "scaling": "weak" if name != "strong" else "strong",
-                          "theta_equal_on_all_ranks": r["theta_equal"], "allreduce": r["path"],
-                          "rank_exchange_selftest": r["xr_selftest"]}
     provenance = None
     if gpu:
         from elephas_amd.ops import native
@@ -213,14 +278,14 @@ def main():
     B, rows, R, samples, dt_max = args.batch, m["rows"], m["R"], m["samples"], m["dt_max"]
     batch_mode, t, state, digests = m["batch_mode"], m["t"], m["state"], m["digests"]
     devices, path, nbytes = m["devices"], m["path"], m["nbytes"]
+    subs = {}
+    line = None
     if rank == 0:
         value = samples / dt_max
         launches = round(t.launches_for(args.steps) / args.steps, 4) if gpu else None
         names = NAMES
-        metric = ("samples/sec (whole node) MNIST-MLP 784-128-128-10 sync DP at 1/2/4/8 MI355X"
-                  if args.model == "mnist" else f"samples/sec (whole node) {names[args.model]} sync DP")
         line = {
-            "metric": metric,
+            "metric": _REPORT["metric"],
             "value": round(value, 1),
             "unit": "samples/s",
             "n_gpus": world,
@@ -251,20 +316,47 @@ def main():
                 "rank_devices": devices,
                 "theta_sha1_16": digests[0],
                 "theta_equal_on_all_ranks": all(d == digests[0] for d in digests),
-                "optimizer": "SGD(lr=%g)" % MODELS[args.model][4],
+                "optimizer": _optimizer_desc(args),
                 "engine": m["engine"],
                 "launches_per_step": launches,   # kernels the timed region issued / steps
                 "native_provenance": provenance,
                 "policy": args.policy,
                 "validation_passes_timed": state["val_passes"],
-                "sub_measurements": subs or None,
+                "sub_measurements": None,
             },
         }
-        s = json.dumps(line)
-        print(s, flush=True)
-        if args.out:
-            with open(args.out, "a") as f:
-                f.write(s + "\n")
+    # extra measurements in the same line (after the headline's timed region, never inside
+    # it), so a multi-GPU record also exercises the per-step exchange and the reference
+    # job's strong split: per-step sync DP at the same workers per GPU, and 8 // N workers
+    # per GPU (only for the default headline invocation; --no-sub skips them).  The headline
+    # line exists before they start: the deadline watchdog prints it if one of them stalls.
+    todo = []
+    if (not args.no_sub and args.model == "mnist" and not batch_mode and args.scaling == "weak"
+            and args.workers_per_gpu == 8):
+        strong_w = 8 // world if 8 % world == 0 and 8 // world != W else None   # N = 1: the headline itself
+        todo = [(name, w_, bm) for name, w_, bm in (("per_step_sync", W, True), ("strong", strong_w, False))
+                if w_ is not None]
+    with _REPORT_LOCK:
+        _REPORT["line"], _REPORT["subs"], _REPORT["pending"] = line, subs, [name for name, _, _ in todo]
+    sk, sw = max(1, args.steps), max(1, args.warmup)
+    from elephas_amd.parallel import fault
+    for name, w_, bm in todo:
+        try:
+            fault.maybe_inject("bench_sub:" + name, rank)
+            r = measure_train(args, model, dist, rank, world, dev, gpu, w_, bm, sk, sw)
+            res = {"value": round(r["samples"] / r["dt_max"], 1), "ms_per_step": round(r["dt_max"] / sk * 1e3, 4),
+                   "steps": sk, "workers_per_gpu": w_, "sync": r["sync"], "engine": r["engine"],
+                   "scaling": "weak" if name != "strong" else "strong",
+                   "theta_equal_on_all_ranks": r["theta_equal"], "allreduce": r["path"],
+                   "rank_exchange_selftest": r["xr_selftest"]}
+        except Exception as e:  # noqa: BLE001 - an extra measurement never costs the headline line
+            res = {"error": repr(e)[:300]}
+        with _REPORT_LOCK:
+            subs[name] = res
+            _REPORT["pending"].remove(name)
+    if rank == 0:
+        line["config"]["sub_measurements"] = subs or None
+        _finish_report(line, args.out)
     if dist.is_initialized():
         dist.barrier()
         import torch.distributed as tdist
@@ -526,12 +618,10 @@ def bench_fit(args, model, dist, rank, world, dev):
                        "mode": "synchronous",
                        "seq_len": None, "global_batch": args.batch * parts, "parallelism": f"dp{world}",
                        "phases_ms_last_fit": {k: round(v * 1e3, 3) for k, v in sm.metrics["phases"].items()},
+                       "optimizer": _optimizer_desc(args),
                        "train_accuracy_after": round(float(acc), 4)},
         }
-        print(json.dumps(line), flush=True)
-        if args.out:
-            with open(args.out, "a") as f:
-                f.write(json.dumps(line) + "\n")
+        _finish_report(line, args.out)
     if dist.is_initialized():
         dist.barrier()
         import torch.distributed as tdist
@@ -593,10 +683,7 @@ def bench_infer(args, model, dist, rank, world, dev):
                        "parallelism": f"dp{world}", "rows_per_gpu": per, "eval_batch": bs,
                        "engine": "native HIP eval executor" if torch.cuda.is_available() else "torch CPU"},
         }
-        print(json.dumps(line), flush=True)
-        if args.out:
-            with open(args.out, "a") as f:
-                f.write(json.dumps(line) + "\n")
+        _finish_report(line, args.out)
     if dist.is_initialized():
         dist.barrier()
         import torch.distributed as tdist
@@ -721,10 +808,7 @@ def bench_async(args, model, dist, rank, world, dev):
                                     else "hipGraph per group-step (pull, refresh, train, push)" if groups[0].graph
                                     else "eager launches")},
         }
-        print(json.dumps(line), flush=True)
-        if args.out:
-            with open(args.out, "a") as f:
-                f.write(json.dumps(line) + "\n")
+        _finish_report(line, args.out)
     dist.barrier()
     client.close()
     if dist.is_initialized():

@@ -285,6 +285,7 @@ constexpr int PM_STAMP_STEPS = 8;
 // separated by per-replica all-to-all flag barriers (see deep.hip).
 constexpr int DP_MAXL = 5;      // Dense layers
 constexpr int DP_MAXWG = 64;    // workgroups per replica (one polling wave)
+constexpr int DP_MAX_DEVICES = 64;   // devices a process may launch the layer pipeline on
 constexpr int DP_ROWS = 128;    // batch rows per replica
 constexpr int DP_MAXC = 32;     // last-layer units (whole rows in one loss tile)
 constexpr int DP_CW = 64;       // dZ columns per backward chunk

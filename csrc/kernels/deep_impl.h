@@ -43,6 +43,8 @@
 // loss epilogues (loss_tile.h).  Masters are read from P at the start of the launch and
 // written back at its end; optimizer state stays in S (read-modify-write by the owner).
 #pragma once
+#include <mutex>
+
 #include "common.h"
 #include "loss_tile.h"
 
@@ -1314,18 +1316,28 @@ __global__ __launch_bounds__(512) void mlp_deep_kernel(DeepArgs a) {
 }
 
 namespace {
-// dynamic LDS above the default limit: raised per instantiation to the largest layout
-// launched so far (the kernel's own static LDS -- e.g. the __syncthreads_and word -- counts
-// against the same 160 KB, so the device maximum itself is refused)
+// dynamic LDS above the default limit: raised per instantiation and per device to the largest
+// layout launched there so far (the kernel's own static LDS -- e.g. the __syncthreads_and word
+// -- counts against the same 160 KB, so the device maximum itself is refused).  The check and
+// the raise happen under one lock, so the attribute only ever grows and no thread launches
+// a layout larger than what its device was raised to.
 template <int L, bool F, bool SG, bool SY>
 hipError_t deep_launch_one(const DeepArgs* a, hipStream_t s) {
-  static int set_bytes = 0;
+  static std::mutex mu;
+  static int set_bytes[DP_MAX_DEVICES] = {};
   const int need = (int)(sizeof(float) * (size_t)a->lds_floats);
-  if (need > set_bytes) {
-    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&mlp_deep_kernel<L, F, SG, SY>),
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, need);
-    if (e != hipSuccess) return e;
-    set_bytes = need;
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  if (dev < 0 || dev >= DP_MAX_DEVICES) return hipErrorInvalidDevice;
+  {
+    std::lock_guard<std::mutex> g(mu);
+    if (need > set_bytes[dev]) {
+      e = hipFuncSetAttribute(reinterpret_cast<const void*>(&mlp_deep_kernel<L, F, SG, SY>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, need);
+      if (e != hipSuccess) return e;
+      set_bytes[dev] = need;
+    }
   }
   hipLaunchKernelGGL((mlp_deep_kernel<L, F, SG, SY>), dim3(a->R * a->nw), dim3(NTH), (size_t)need, s, *a);
   return hipGetLastError();

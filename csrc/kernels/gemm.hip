@@ -1,6 +1,8 @@
 // Grouped GEMM dispatch: picks the tile-config translation unit (gemm_cfg*.hip,
 // gemm_f32.hip) for a launch and runs the wide-output loss rows kernel, which
 // is not a GEMM (kernel templates: gemm_impl.h).
+#include <mutex>
+
 #include "gemm_impl.h"
 
 extern "C" {
@@ -53,15 +55,21 @@ extern "C" hipError_t ea_gemm_table(const ea::TableArgs* ta, int bf16, int dw, h
   return bf16 ? ea_gemm_table_lat_bf16(ta, dw, s) : ea_gemm_table_f32(ta, dw, s);
 }
 
+// the function attributes (dynamic-LDS limits) are per device: raised once on each device a
+// process builds an executor on, under a lock (executors may be built from several threads)
 extern "C" void ea_gemm_init() {
-  static bool done = false;
-  if (done) return;
+  static std::mutex mu;
+  static bool done[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+  std::lock_guard<std::mutex> g(mu);
+  if (done[dev]) return;
   ea_gemm_init_lat_bf16();
   ea_gemm_init_thr_bf16();
   ea_gemm_init_thr64_bf16();
   ea_gemm_init_big_bf16();
   ea_gemm_init_f32();
-  done = true;
+  done[dev] = true;
 }
 
 // cfg 3: the 64x64 tile of the row-chain weight-gradient table launch (not a

@@ -224,7 +224,9 @@ bool Executor::build_deep() {
   const int L = (int)c_.layers.size();
   if (L < 2 || L > DP_MAXL) return no_dp("layer pipeline: 2..5 Dense layers");
   if (c_.bf16) return no_dp("layer pipeline: fp32 only");
-  if (c_.B < 1 || c_.B > DP_ROWS || c_.ldy > 32 || (c_.ldx % 8) != 0) return no_dp("layer pipeline: batch <= 128 rows per replica");
+  if (c_.B < 1 || c_.B > DP_ROWS) return no_dp("layer pipeline: batch <= 128 rows per replica");
+  if (c_.ldy > 32) return no_dp("layer pipeline: label rows of <= 32 columns");
+  if ((c_.ldx % 8) != 0) return no_dp("layer pipeline: a feature stride that is a multiple of 8");
   const LayerCfg& lastc = c_.layers[L - 1];
   if (lastc.N > DP_MAXC) return no_dp("layer pipeline: a last layer of <= 32 units");
   auto r16 = [](int n) { return (n + 15) / 16 * 16; };
@@ -267,7 +269,8 @@ bool Executor::build_deep() {
   for (int l = 0; l < L - 1; ++l) { a.ly[l].l_b = lds; lds += 16; }
   a.ly[L - 1].l_b = lds; lds += 32;
   for (int l = 0; l < L - 1; ++l) { a.ly[l].l_at = lds; lds += 16 * (a.Bp + 4); }
-  a.l_dz0 = lds; lds += 16 * (a.Bp + 4);
+  // the dZ_0^T stripe doubles as bw_phase's second DW-partial buffer ([4][64][4] floats)
+  a.l_dz0 = lds; lds += std::max(16 * (a.Bp + 4), 4 * 64 * 4);
   a.l_red = lds; lds += 2048;
   int stage = DP_ROWS * (DP_CW + 4) + 1024;                          // backward dZ chunk + DW partials
   stage = std::max(stage, 8 * 2 * 256 + 16 * 36 + 16 * 32 + 16);     // tail tiles

@@ -200,13 +200,19 @@ def _owned_frozen(a):
 
 
 def _is_frozen(a) -> bool:
-    """No one can write a's bytes: a and every array it views are read-only."""
+    """No one can write a's bytes through a view: a is an ndarray, it and every array it
+    views are read-only, and the chain ends at an array owning its memory (or at an
+    immutable ``bytes`` object).  Lists, tensors and arrays over mutable buffers
+    (bytearray, mmap, ...) are never frozen.  (An owning array can still be made writeable
+    again explicitly; the arrays this module freezes are its own copies.)"""
     import numpy as np
+    if not isinstance(a, np.ndarray):
+        return False
     while isinstance(a, np.ndarray):
         if a.flags.writeable:
             return False
         a = a.base
-    return True
+    return a is None or isinstance(a, bytes)
 
 
 def _columnar(parts) -> bool:
@@ -307,10 +313,8 @@ class RDD:
                 y.setflags(write=False)
                 out.append(kind(x, y))
             res = RDD(out, self.ctx)
-            if frozen:
-                if memo is None:
-                    memo = self._repart_memo = {}
-                memo[n] = res
+            if frozen:   # memoised for the last numPartitions only: one extra copy of the data at most
+                self._repart_memo = {n: res}
             return res
         parts = [[] for _ in range(n)]
         for i, x in enumerate(itertools.chain.from_iterable(self._parts)):

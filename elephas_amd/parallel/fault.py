@@ -13,7 +13,10 @@ visible instead of silent:
   failure tests use. Phases: ``train``, ``allreduce``, ``push``, ``pull``, ``ps_selftest`` (the
   rank pushes a wrong delta in the device PS self-test, which must then fail),
   ``xrank_selftest`` (the rank sends a wrong tile in the in-launch rank-exchange self-test:
-  every rank must then detach and keep the peer all-reduce path).
+  every rank must then detach and keep the peer all-reduce path), ``bench_sub:<name>``
+  (bench.py, at the start of a sub-measurement).  With ``stall=1`` the rank blocks
+  forever instead of raising -- a hung rank, which bench.py's job-wide deadline
+  (``$ELEPHAS_AMD_BENCH_DEADLINE_S``) must survive.
 """
 from __future__ import annotations
 
@@ -41,19 +44,24 @@ def _spec():
     if not raw:
         return None
     kv = dict(item.split("=", 1) for item in raw.split(",") if "=" in item)
-    return int(kv.get("rank", 0)), kv.get("phase", "train"), int(kv.get("after", 0))
+    return (int(kv.get("rank", 0)), kv.get("phase", "train"), int(kv.get("after", 0)),
+            kv.get("stall", "0") not in ("0", ""))
 
 
 def maybe_inject(phase: str, rank: int) -> None:
     spec = _spec()
     if spec is None:
         return
-    r, p, after = spec
+    r, p, after, stall = spec
     if r != rank or p != phase:
         return
     n = _counts.get(phase, 0)
     _counts[phase] = n + 1
     if n >= after:
+        if stall:
+            import time
+            while True:   # a hung rank: never returns (the caller's deadline must cope)
+                time.sleep(3600)
         raise InjectedFault(f"injected fault: rank {rank}, phase {phase}, occurrence {n}")
 
 

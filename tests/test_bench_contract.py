@@ -77,3 +77,28 @@ def test_bench_under_torchrun_prints_one_json_line():
     recs = _json_lines(r.stdout)
     assert len(recs) == 1, r.stdout[-2000:]
     _check(recs[0], 2)
+
+
+def test_bench_deadline_prints_line_when_a_rank_stalls():
+    """Job-wide deadline: rank 1 hangs at the start of the per-step-sync sub-measurement
+    (fault injection, stall=1), so rank 0 blocks in that measurement's first collective.
+    The headline line must still appear -- within the deadline, with every pending
+    sub-measurement marked {"error": "deadline"} -- and the job must end."""
+    import time
+    env = _env()
+    env["MASTER_PORT"] = str(_free_port())
+    env["ELEPHAS_AMD_BENCH_DEADLINE_S"] = "45"
+    env["ELEPHAS_AMD_FAULT_INJECT"] = "rank=1,phase=bench_sub:per_step_sync,stall=1"
+    t0 = time.monotonic()
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--steps", "2", "--warmup", "1"], cwd=ROOT,
+                       env=env, capture_output=True, text=True, timeout=300)
+    elapsed = time.monotonic() - t0
+    recs = _json_lines(r.stdout)
+    assert len(recs) == 1, (r.stdout[-2000:], r.stderr[-2000:])
+    _check(recs[0], 2)
+    subs = recs[0]["config"]["sub_measurements"]
+    assert subs["per_step_sync"] == {"error": "deadline"}, subs
+    assert subs["strong"] == {"error": "deadline"}, subs
+    assert recs[0]["deadline_s"] == 45
+    assert "deadline" in r.stderr
+    assert elapsed < 45 + 60, elapsed   # the deadline (+ process teardown), not the collective timeout

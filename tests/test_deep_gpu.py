@@ -62,6 +62,11 @@ def _native(model, R, B, seed=12345, deep="2", persist=1, monkeypatch=None):
     ("l4_nobias", 30, (96, 80, 64), 5, 48, "sgd", 0.25, False),
     ("l5", 30, (64, 64, 64, 64), 5, 16, "sgd_mom", 0.0, True),
     ("wide_b128", 93, (256, 256), 9, 128, "sgd", 0.5, True),
+    # B <= 32 with an inner hidden layer wider than 64: bw_phase's second DW-partial buffer
+    # (the dZ_0^T stripe) must hold [4][64][4] floats, more than 16 x (Bp + 4) at Bp <= 32
+    ("b32_wide", 93, (256, 256), 9, 32, "sgd", 0.5, True),
+    ("b16_wide", 40, (128, 200), 7, 16, "sgd_mom", 0.2, True),
+    ("otto_b32_adam", 93, (512, 512, 512), 9, 32, "adam", 0.5, True),
 ])
 def test_deep_matches_fp32_reference_with_same_masks(monkeypatch, name, in_dim, hidden, out, B, opt, drop, bias):
     """Layer pipeline == fp32 torch autograd with the same dropout masks (2 replicas of
@@ -288,3 +293,19 @@ def test_deep_sync_replicas_match_eager_exchange(monkeypatch, name, in_dim, hidd
         else:
             err = np.abs(w[0] - wt).max() / np.abs(wt - w0).max()
             assert err < 1e-3, (label, err)
+
+
+@pytest.mark.parametrize("opt", ["sgd", "adam"])
+def test_deep_exact_otto_matches_fp32_torch(monkeypatch, opt):
+    """The exact Otto configuration of the reference notebook on the layer pipeline
+    (93-512-512-512-9, ReLU, Dropout 0.5, 8 replicas x B 128; SGD(0.01) as bench.py's default
+    and Adam(lr 0.01) as examples/Spark_ML_Pipeline.ipynb:361) == fp32 torch autograd with the
+    same dropout masks, over 2 epochs with a short last shard."""
+    from elephas_amd.models import initializers, optimizers as O
+    initializers.set_seed(77)
+    model = _mlp(93, [512, 512, 512], 9, dropout=0.5)
+    model.compile(O.SGD(0.01) if opt == "sgd" else O.Adam(0.01), "categorical_crossentropy", ["acc"])
+    xs, ys = _shards([2 * 128] * 7 + [128 + 50], 93, 9, seed=21)
+    nat = _native(model, 8, 128, deep="-1", monkeypatch=monkeypatch)
+    assert nat.persistent and nat.persist_variant == 3, (nat.plan_name(), nat.plan_reason)
+    _compare_with_torch(nat, model, xs, ys, 128, adaptive=opt == "adam")

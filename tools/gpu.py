@@ -15,6 +15,7 @@ touches the GPU after it.  Steps (arguments are comma-separated, no spaces):
   prof:NAME:ARGS          rocprofv3 --kernel-trace --stats of bench.py ARGS -> gpurun_out/prof_NAME
   pmc:NAME:CTRS:ARGS      one rocprofv3 --pmc pass (CTRS '+'-separated, within one pass's limits)
   py:SCRIPT[:ARGS]        python tools/SCRIPT ARGS (stamps.py, persist_stamps.py, gemm_check.py, ...)
+  micro:NAME              hipcc tools/micro/NAME.hip for gfx950 and run it (120 s limit)
 
 Any step may carry a tag and environment overrides in front of it:
 
@@ -129,6 +130,12 @@ def main(steps):
                                                             sys.executable, os.path.join(ROOT, "bench.py")]
             cmd += args.split(",") if args else []
             rc = _run(tag, cmd, 120, env=dict(os.environ, TMPDIR="/tmp"), cwd="/tmp")
+        elif kind == "micro":
+            exe = os.path.join("/tmp", "micro_" + rest)
+            rc = _run(tag + "_build", ["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17",
+                                       os.path.join(ROOT, "tools", "micro", rest + ".hip"), "-o", exe], 300)
+            if rc == 0:
+                rc = _run(tag, [exe], 120)
         elif kind == "py":
             script, _, args = rest.partition(":")
             rc = _run(tag, [sys.executable, os.path.join("tools", script)] + (args.split(",") if args else []), 600)
