@@ -198,7 +198,7 @@ enum PmFlag : int { PMF_PART = 0, PMF_BWD = 1, PMF_W = 2, PMF_A0 = 3, PMF_D2 = 4
 // nothing was modified, the chunk can be re-run on another plan)
 enum PmErr : unsigned { PERR_L0_BWD = 1, PERR_CHAIN_PART = 2, PERR_CHAIN_BWD = 3, PERR_CHAIN_PREV = 4,
                         PERR_DW_A0 = 5, PERR_DW_D2 = 6, PERR_XCHG = 7, PERR_PS = 8, PERR_GRID = 9,
-                        PERR_CHAIN_GR = 10, PERR_XRANK = 11 };
+                        PERR_CHAIN_GR = 10, PERR_XRANK = 11, PERR_PLACE = 12 };
 constexpr int PM_XSLOT = 7 * 1024;   // floats of one workgroup's exchange slab (sync)
 struct PersistArgs {
   int R, B, nsteps;

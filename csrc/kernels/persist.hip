@@ -51,6 +51,19 @@
 #include "common.h"
 #include "loss_tile.h"
 
+// XCD-local instance (persist_local.hip compiles this file again with EA_PLOCAL = 1): a
+// replica's workgroups all run on ONE XCD (the host picks it only where block b -> XCD b % 8
+// puts them there -- R a multiple of 8 -- and each chain verifies it at launch, below), so
+// the intra-replica hand-offs need not leave that XCD's L2: their bytes and flags are stored
+// PLAIN (the line stays in the L2, where the consumers' sc1 loads -- which skip only the
+// CU's L1 -- find it) instead of write-through (sc1 stores drop the line, and the consumer
+// re-reads it at the cross-XCD rate).  tools/micro/xchg_floor.hip: 8-workgroup exchange of
+// 16 KB slabs 3.6 -> 2.6 us, flag round 1.5 -> 1.2 us (profiles/xchg_floor_r6.txt).  The
+// cross-replica (sync exchange) and cross-rank hand-offs stay write-through.
+#ifndef EA_PLOCAL
+#define EA_PLOCAL 0
+#endif
+
 namespace ea {
 
 namespace {
@@ -155,10 +168,16 @@ __device__ __forceinline__ f32x4 ldw4(rsrc_t r, int v, int s) {
 __device__ __forceinline__ float ldw1(rsrc_t r, int v, int s) {
   return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, v * 4, s * 4, 16));
 }
+// intra-replica hand-off stores: write-through (sc1 = aux 16), or plain in the XCD-local instance
+constexpr int ST_AUX = EA_PLOCAL ? 0 : 16;
 __device__ __forceinline__ void stw1(rsrc_t r, int v, int s, float x) {
-  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, x), r, v * 4, s * 4, 16);
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, x), r, v * 4, s * 4, ST_AUX);
 }
 __device__ __forceinline__ void stw4(rsrc_t r, int v, int s, f32x4 x) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, x), r, v * 4, s * 4, ST_AUX);
+}
+// cross-replica hand-off stores (the sync exchange slabs): always write-through
+__device__ __forceinline__ void stx4(rsrc_t r, int v, int s, f32x4 x) {
   __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, x), r, v * 4, s * 4, 16);
 }
 
@@ -167,11 +186,20 @@ __device__ __forceinline__ unsigned* flag_at(const PersistArgs& a, int r, int ki
 }
 
 // R1 publish: every storing wave drains its sc1 stores, the workgroup meets, one lane
-// raises the flag (agent-scope relaxed store = sc1)
-__device__ __forceinline__ void publish(unsigned* flag, unsigned tag) {
+// raises the flag (agent-scope relaxed store = sc1).  XCD-local instance: the flag of an
+// intra-replica hand-off is a plain store (it stays in the L2 the pollers' sc1 loads read)
+__device__ __forceinline__ void publish_x(unsigned* flag, unsigned tag) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) __hip_atomic_store((gu32*)(flag), tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void publish(unsigned* flag, unsigned tag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if constexpr (EA_PLOCAL) __builtin_amdgcn_raw_buffer_store_b32(tag, ws_rsrc(reinterpret_cast<float*>(flag)), 0, 0, 0);
+    else __hip_atomic_store((gu32*)(flag), tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
 // wave 0 polls flags[0 .. n) (lane q watches producer q) until every one reaches tag;
@@ -272,19 +300,34 @@ __device__ __forceinline__ bool wait_sets(const PersistArgs& a, const WaitSet (&
 // residency: wave 0 polls the GO flag of every workgroup of the grid (R replicas x wgs)
 // until all are raised.  A workgroup that is not resident never raises
 // it, so the waiting ones time out (PERR_GRID) before any of them modified state.
-__device__ __forceinline__ bool wait_grid(const PersistArgs& a) {
+// XCD-local instance: a GO flag carries its workgroup's XCD + 1, and a replica r whose
+// workgroups do not all share this workgroup's XCD gives up (PERR_PLACE), state intact.
+__device__ __forceinline__ unsigned xcc_id() {
+  return __builtin_amdgcn_s_getreg((20) | (0 << 6) | ((4 - 1) << 11));   // HW_REG_XCC_ID[3:0]
+}
+__device__ __forceinline__ unsigned go_value() { return EA_PLOCAL ? xcc_id() + 1u : 1u; }
+__device__ __forceinline__ bool wait_grid(const PersistArgs& a, int r) {
   int ok = 1;
   if (threadIdx.x < 64) {
     const int lane = threadIdx.x, tot = a.R * a.wgs;
+    const unsigned mine = go_value();
     const unsigned long long t0 = wall_clock64();
     for (;;) {
-      bool all = true;
+      bool all = true, away = false;
       for (int f = lane; f < tot; f += 64) {
         const int rr = f % a.R, qq = f / a.R;
-        all &= __hip_atomic_load((gu32*)(flag_at(a, rr, PMF_GO) + qq), __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_AGENT) != 0u;
+        const unsigned v = __hip_atomic_load((gu32*)(flag_at(a, rr, PMF_GO) + qq), __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
+        all &= v != 0u;
+        away |= EA_PLOCAL && rr == r && v != 0u && v != mine;
       }
-      if (__all(all)) break;
+      if (__all(all)) {
+        if (__any(away)) {
+          ok = 0;
+          if (lane == 0) __hip_atomic_store((gu32*)(a.err), (unsigned)PERR_PLACE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        break;
+      }
       if ((long long)(wall_clock64() - t0) > a.timeout) {
         ok = 0;
         if (lane == 0) __hip_atomic_store((gu32*)(a.err), (unsigned)PERR_GRID, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -401,8 +444,8 @@ __device__ __forceinline__ bool xchg_sum(const PersistArgs& a, int r, int q, int
   if (a.R > 1) {
     const unsigned tag = (unsigned)(i + 1);
 #pragma unroll
-    for (int u = 0; u < N; ++u) stw4(all, (u * 256 + tid) * 4, (int)((long long)r * a.ws_stride + slab), v[u]);
-    publish(flag_at(a, r, PMF_X) + q, tag);
+    for (int u = 0; u < N; ++u) stx4(all, (u * 256 + tid) * 4, (int)((long long)r * a.ws_stride + slab), v[u]);
+    publish_x(flag_at(a, r, PMF_X) + q, tag);
     if (!wait_replicas(a, PMF_X, q, tag)) return false;
     if (a.xchg_rs) {
       constexpr int E = N * 256;
@@ -421,9 +464,9 @@ __device__ __forceinline__ bool xchg_sum(const PersistArgs& a, int r, int q, int
           for (int k = 0; k < 8; ++k)
             if (rb + k < a.R) s += x[k];
         }
-        stw4(all, e * 4, (int)((long long)r * a.ws_stride + slab), s);
+        stx4(all, e * 4, (int)((long long)r * a.ws_stride + slab), s);
       }
-      publish(flag_at(a, r, PMF_XS) + q, tag);
+      publish_x(flag_at(a, r, PMF_XS) + q, tag);
       if (!wait_replicas(a, PMF_XS, q, tag)) return false;
 #pragma unroll
       for (int u = 0; u < N; ++u) {
@@ -459,8 +502,8 @@ __device__ __forceinline__ bool xchg_sum(const PersistArgs& a, int r, int q, int
     if (!xrank_sum<N>(a, q, a.xr_tag0 + (unsigned)i + 1u, v)) return false;
     if (a.R > 1) {   // the total for the other replicas (write-through, then the local flag)
 #pragma unroll
-      for (int u = 0; u < N; ++u) stw4(all, (u * 256 + tid) * 4, (int)tslab, v[u]);
-      publish(flag_at(a, 0, PMF_XT) + q, (unsigned)(i + 1));
+      for (int u = 0; u < N; ++u) stx4(all, (u * 256 + tid) * 4, (int)tslab, v[u]);
+      publish_x(flag_at(a, 0, PMF_XT) + q, (unsigned)(i + 1));
     }
     return true;
   }
@@ -1532,7 +1575,7 @@ __device__ __forceinline__ void chain_role(const PersistArgs& a, float* smem, in
   __syncthreads();
   // every workgroup of the grid resident before any state (metric sums, hand-offs that
   // lead to weight updates) is touched: otherwise give up with PERR_GRID, state intact
-  if (!wait_grid(a)) return;
+  if (!wait_grid(a, r)) return;
 
   const int n = a.nsteps;
   // V2: this chain's rows of step s's Gram slabs (X_s . X_{s-1}^T, one per k-chunk)
@@ -2535,7 +2578,7 @@ __global__ __launch_bounds__(256) void mlp_persist_kernel(PersistArgs a) {
   const int b = blockIdx.x;
   const int r = b % a.R, q = b / a.R;
   // residency: raise this workgroup's GO flag (the chain workgroups wait for the grid)
-  if (threadIdx.x == 0) __hip_atomic_store((gu32*)(flag_at(a, r, PMF_GO) + q), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (threadIdx.x == 0) __hip_atomic_store((gu32*)(flag_at(a, r, PMF_GO) + q), go_value(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const int nl0 = a.nk0 * a.nc0;
   if constexpr (V2) {
     static_assert(NPT == 0 && RELU, "V2: plain SGD, ReLU hidden layers");
@@ -2589,16 +2632,32 @@ hipError_t persist_launch(const PersistArgs* a, hipStream_t s) {
 
 using namespace ea;
 
+#if EA_PLOCAL
+#define EA_PERSIST_ENTRY ea_persist_local
+#else
+#define EA_PERSIST_ENTRY ea_persist
 extern "C" int ea_persist_lds_bytes() { return (int)(LDS_FLOATS * sizeof(float)); }
+#endif
 
 // grid: R * wgs workgroups of 256 threads, every one resident (the host sizes the
 // grid to at most one workgroup per CU); hidden widths (64, 64), (128, 128), (128, 64)
-extern "C" hipError_t ea_persist(const PersistArgs* a, hipStream_t s) {
+extern "C" hipError_t EA_PERSIST_ENTRY(const PersistArgs* a, hipStream_t s) {
   if (a->nsteps <= 0) return hipSuccess;
   if (a->H0 == 128 && a->H1 == 128) return persist_launch<128, 128>(a, s);
   if (a->H0 == 64 && a->H1 == 64) return persist_launch<64, 64>(a, s);
   if (a->H0 == 128 && a->H1 == 64) return persist_launch<128, 64>(a, s);
   return hipErrorInvalidValue;
+}
+
+#if !EA_PLOCAL
+// placement probe: block b stores the XCD it runs on; the host enables the XCD-local
+// instance only where the dispatch puts block b on XCD b % 8 for the whole grid
+__global__ void xcc_probe_kernel(unsigned* out) {
+  if (threadIdx.x == 0) out[blockIdx.x] = ea::xcc_id();
+}
+extern "C" hipError_t ea_xcc_probe(int nblocks, unsigned* out, hipStream_t s) {
+  hipLaunchKernelGGL(xcc_probe_kernel, dim3(nblocks), dim3(64), 0, s, out);
+  return hipGetLastError();
 }
 
 namespace ea {
@@ -2647,3 +2706,4 @@ extern "C" hipError_t ea_xrank_selftest(const PersistArgs* a, int nsteps, unsign
   hipLaunchKernelGGL(xrank_selftest_kernel, dim3(a->wgs), dim3(256), 0, s, *a, nsteps, bad, corrupt);
   return hipGetLastError();
 }
+#endif  // !EA_PLOCAL

@@ -81,6 +81,7 @@ static ExecCfg parse_cfg(const py::dict& d) {
   c.persist_timeout_ms = get<long long>(d, "persist_timeout_ms", 2000);
   c.persist_cus = get<int>(d, "persist_cus", 0);
   c.persist_v2 = get<int>(d, "persist_v2", -1);
+  c.persist_local = get<int>(d, "persist_local", -1);
   c.persist_sync = get<int>(d, "persist_sync", 0);
   c.deep = get<int>(d, "deep", -1);
   for (auto item : d["layers"].cast<py::list>()) {

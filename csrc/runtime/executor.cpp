@@ -2,6 +2,9 @@
 // See executor.h for the step structure.
 #include "executor.h"
 
+#include <map>
+#include <mutex>
+
 #include <cstdlib>
 
 #include <algorithm>
@@ -19,6 +22,8 @@ extern "C" hipError_t ea_advance(long long* ctr, const int* ntrain, int R, int B
 extern "C" hipError_t ea_persist_post(unsigned* flags, int nflags, long long* ctr, const int* ntrain, int R, int B, int n,
                                       const unsigned* err, hipStream_t s);
 extern "C" hipError_t ea_persist(const ea::PersistArgs* a, hipStream_t s);
+extern "C" hipError_t ea_persist_local(const ea::PersistArgs* a, hipStream_t s);
+extern "C" hipError_t ea_xcc_probe(int nblocks, unsigned* out, hipStream_t s);
 extern "C" int ea_persist_lds_bytes();
 extern "C" hipError_t ea_deep(const ea::DeepArgs* a, hipStream_t s);
 extern "C" hipError_t ea_xrank_selftest(const ea::PersistArgs* a, int nsteps, unsigned* bad, int corrupt, hipStream_t s);
@@ -68,6 +73,27 @@ Executor::~Executor() {
 // Persistent plan (persist.hip): 3 Dense layers, hidden widths 64 or 128, a last layer
 // of <= 16 units, fp32, B <= 64, and a grid of at most one workgroup per CU (every
 // workgroup must be resident: they wait for each other inside the launch).
+// Does the dispatch put block b of an n-block grid on XCD b % 8 (the XCD-local persistent
+// instance's assumption, persist.hip EA_PLOCAL)?  Probed once per device and grid size with
+// a tiny kernel reading HW_REG_XCC_ID; the kernel re-checks it at every launch (PERR_PLACE).
+static bool xcd_round_robin(int dev, int n) {
+  static std::mutex mu;
+  static std::map<std::pair<int, int>, bool> seen;
+  std::lock_guard<std::mutex> g(mu);
+  const auto key = std::make_pair(dev, n);
+  auto it = seen.find(key);
+  if (it != seen.end()) return it->second;
+  unsigned* d = nullptr;
+  bool ok = hipMalloc(&d, sizeof(unsigned) * (size_t)n) == hipSuccess;
+  std::vector<unsigned> h(n, 99u);
+  ok = ok && ea_xcc_probe(n, d, nullptr) == hipSuccess && hipDeviceSynchronize() == hipSuccess &&
+       hipMemcpy(h.data(), d, sizeof(unsigned) * (size_t)n, hipMemcpyDeviceToHost) == hipSuccess;
+  if (d) (void)hipFree(d);
+  for (int b = 0; ok && b < n; ++b) ok = h[b] == (unsigned)(b % 8);
+  seen[key] = ok;
+  return ok;
+}
+
 bool Executor::build_persist() {
   auto no_pm = [&](const char* why) { why_pm_ = why; return false; };
   const int L = (int)c_.layers.size();
@@ -147,6 +173,9 @@ bool Executor::build_persist() {
   }
   a.wgs = a.nk0 * a.nc0 + nch + nd_use;
   a.sync = c_.persist_sync ? 1 : 0;
+  // XCD-local instance: block b serves replica b % R, so with R a multiple of 8 every
+  // replica's cluster sits on one XCD -- if the dispatch is round-robin over the XCDs
+  pm_.local = c_.persist_local != 0 && c_.R % 8 == 0 && xcd_round_robin(dev, c_.R * a.wgs);
   const char* xrs = std::getenv("ELEPHAS_AMD_XCHG_RS");   // A/B: reduce-scatter exchange of the replicas
   a.xchg_rs = (xrs && std::atoi(xrs) != 0) ? 1 : 0;
   a.bf16 = c_.bf16 ? 1 : 0;
@@ -399,9 +428,9 @@ std::vector<unsigned> Executor::rank_exchange_selftest(int nsteps, int corrupt) 
 }
 
 std::vector<int> Executor::persist_variant() const {
-  if (dp_.on) return {3, 0, dp_.args.sync};
+  if (dp_.on) return {3, 0, dp_.args.sync, 0};
   if (!pm_.on) return {};
-  return {pm_.args.v2 ? 2 : 1, pm_.args.nd, pm_.args.sync};
+  return {pm_.args.v2 ? 2 : 1, pm_.args.nd, pm_.args.sync, pm_.local ? 1 : 0};
 }
 
 unsigned Executor::persist_error() const {
@@ -440,7 +469,7 @@ void Executor::run_chunk(hipStream_t s, int nsteps) const {
       a.xr_tag0 = pm_.xr_steps;
       pm_.xr_steps += (unsigned)nsteps;
     }
-    check(ea_persist(&a, s), "persistent step kernel");
+    check(pm_.local ? ea_persist_local(&a, s) : ea_persist(&a, s), "persistent step kernel");
     check(ea_persist_post(d_pflags_, (int)(pm_.flag_bytes / sizeof(unsigned)), reinterpret_cast<long long*>(c_.ctr),
                           reinterpret_cast<const int*>(c_.ntrain), c_.R, c_.B, nsteps, d_perr_, s),
           "persistent chunk post");

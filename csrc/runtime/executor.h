@@ -79,6 +79,7 @@ struct ExecCfg {
   long long persist_timeout_ms = 2000;  // spin limit of its in-launch waits
   int persist_cus = 0;  // > 0: CUs the persistent grid may occupy (several executors side by side)
   int persist_v2 = -1;  // persistent V2 roles when eligible (plain SGD, ReLU, independent replicas); 0 off
+  int persist_local = -1;  // XCD-local persistent instance where the placement allows (persist_local.hip); 0 off
   int persist_sync = 0;  // persistent plan as per-step synchronous DP of the R replicas (in-launch exchange)
   int deep = -1;        // persistent layer pipeline (deep.hip) where persist.hip is not eligible: -1 when eligible, 0 off,
                         // 2 preferred over persist.hip (tests, A/B)
@@ -206,6 +207,7 @@ class Executor {
     PersistArgs args{};
     size_t flag_bytes = 0;
     mutable unsigned xr_steps = 0;   // steps run with the rank exchange (its flag tags)
+    bool local = false;              // the XCD-local instance (ea_persist_local)
   } pm_;
   float* d_pws_ = nullptr;         // persistent plan: per-replica exchange workspace
   unsigned* d_pflags_ = nullptr;   // [R][PMF_N][PM_MAXWG] flags (zero at every launch: setup, then the post kernel)

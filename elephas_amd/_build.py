@@ -30,6 +30,7 @@ SOURCES = [
     "kernels/flat.hip",
     "kernels/rowchain.hip",
     "kernels/persist.hip",
+    "kernels/persist_local.hip",
     "kernels/deep.hip",
     "kernels/deep_l2.hip",
     "kernels/deep_l3.hip",

@@ -131,7 +131,7 @@ class PersistentPlanError(RuntimeError):
 
     def __init__(self, code: int, rank_exchange: bool = False):
         self.code = int(code)
-        self.clean = self.code == 9
+        self.clean = self.code in (9, 12)   # grid not resident / replica not on one XCD: nothing modified
         self.rank_exchange = bool(rank_exchange)
         super().__init__(
             f"persistent step kernel: an in-launch wait timed out (code {self.code}; "
@@ -184,6 +184,7 @@ class NativeTrainer(TrainerBase):
         # xchg_sum); otherwise forward/backward -> replica sum -> apply per step.
         self.sync = bool(sync) and R > 1
         self._grad_scale = 1.0
+        self._no_local = False   # set after a launch found a replica's workgroups on two XCDs (PERR_PLACE)
         # ps_hook: the persistent plan will push / pull a device parameter server every
         # step inside the launch (attach_param_server), so it keeps the V1 roles
         self.ps_hook = bool(ps_hook)
@@ -322,6 +323,7 @@ class NativeTrainer(TrainerBase):
             persist_timeout_ms=int(os.environ.get("ELEPHAS_AMD_PERSIST_TIMEOUT_MS", "2000")),
             persist_cus=self.persist_cus,
             persist_v2=0 if self.ps_hook else int(os.environ.get("ELEPHAS_AMD_PERSIST_V2", "-1")),
+            persist_local=0 if self._no_local else int(os.environ.get("ELEPHAS_AMD_PERSIST_LOCAL", "-1")),
             persist_sync=int(self.sync) if ws is self.ws else 0,
             deep=int(os.environ.get("ELEPHAS_AMD_DEEP", "-1")),
             rc_split=int(os.environ.get("ELEPHAS_AMD_RC_SPLIT", "0")),
@@ -1008,9 +1010,16 @@ class NativeTrainer(TrainerBase):
                     # exchange timeout): one clear error, no local re-plan, no fit() retry
                     self._xr["live"] = False
                     raise PersistentPlanError(e, rank_exchange=True)
-                _log.warning("persistent step kernel gave up (code %d%s); falling back to the row-chain plan",
-                             e, ", grid not resident" if e == 9 else "")
-                self.persist_mode = 0
+                if e == 12 and not self._no_local:
+                    # a replica's workgroups on two XCDs: the XCD-local instance's premise does
+                    # not hold on this device -- the write-through instance, same plan
+                    _log.warning("persistent step kernel: replica not on one XCD (code 12); using the "
+                                 "write-through instance")
+                    self._no_local = True
+                else:
+                    _log.warning("persistent step kernel gave up (code %d%s); falling back to the row-chain plan",
+                                 e, ", grid not resident" if e == 9 else "")
+                    self.persist_mode = 0
                 self._build_executor()
                 self._images_stale = True   # P may hold a partial chunk: images from P first
                 raise PersistentPlanError(e)
@@ -1175,9 +1184,10 @@ class NativeTrainer(TrainerBase):
                     f"{rt} row tiles x {ks}-way k split, {lds // 1024} KB LDS; grid {grid})")
         if self.exe.persistent():
             nk0, nc0, kc0, cw, nch, wgs, grid = self.exe.persist_geometry()
-            var, nd, sync = self.exe.persist_variant()
+            var, nd, sync, local = self.exe.persist_variant()[:4]
             dw = f" + {nd} weight-gradient workgroups" if var == 2 else ""
             sy = ", per-step gradient exchange of the replicas inside the launch" if sync else ""
+            sy += ", XCD-local hand-offs" if local else ""
             return (f"persistent V{var}{sy} (1 kernel + 1 post kernel per <= {self.GRAPH_CHUNK}-step chunk; per "
                     f"replica {nk0}x{nc0} layer-0 tiles of {kc0}x{cw} + {nch} row-chain workgroups{dw}; "
                     f"grid {grid})")

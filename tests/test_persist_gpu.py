@@ -484,3 +484,42 @@ def test_persist_bf16_pinned_to_bf16_operand_torch():
     print(f"bf16 pin ({nst} steps): emul-vs-f32 {gap:.3e}  rowchain-vs-emul {d_rc:.3e}  persistent-vs-emul {d_p:.3e}")
     assert d_rc <= 0.3 * gap, (d_rc, gap)
     assert d_p <= 0.8 * gap, (d_p, gap)
+
+
+@pytest.mark.parametrize("case", ["v2_fit", "v1_mom_fit", "v1_sync"])
+def test_persist_xcd_local_instance_is_bit_exact(monkeypatch, case):
+    """The XCD-local instance (persist_local.hip: intra-replica hand-offs stored plain and
+    read from the XCD's L2, the replica's cluster checked to sit on one XCD at launch) is
+    picked for 8 replicas and trains bit for bit as the write-through instance: V2 fit
+    (the headline), V1 with momentum, V1 per-step sync (whose exchange stays write-through)."""
+    from elephas_amd.models import initializers
+    from elephas_amd.models.optimizers import SGD
+    from elephas_amd.ops.plan import build_plan
+    from elephas_amd.ops.native_engine import NativeTrainer
+    from elephas_amd import config
+    config.set_policy("float32")
+    initializers.set_seed(41)
+    model = _mlp(784, [128, 128], 10, dropout=0.0 if case == "v1_sync" else 0.2)
+    model.compile(SGD(0.05, momentum=0.9) if case == "v1_mom_fit" else SGD(0.1), "categorical_crossentropy",
+                  ["acc"])
+    xs, ys = _shards([64 * 9] * 7 + [64 * 5 + 17], 784, 10, seed=19)
+    if case == "v1_sync":
+        xs, ys = _shards([64 * 9] * 8, 784, 10, seed=19)
+    out = []
+    for local in ("-1", "0"):
+        monkeypatch.setenv("ELEPHAS_AMD_PERSIST_LOCAL", local)
+        t = NativeTrainer(model, build_plan(model), 8, 64, torch.device("cuda"), seed=9, persist=1,
+                          sync=case == "v1_sync")
+        var = t.exe.persist_variant()
+        assert t.persistent and var[0] == (2 if case == "v2_fit" else 1), t.plan_name()
+        assert var[3] == (1 if local == "-1" else 0), (local, var)
+        t.set_data(xs, ys, 0.1 if case != "v1_sync" else 0.0, shuffle=case != "v1_sync")
+        torch.manual_seed(3)
+        h = t.fit(2)
+        t.check()
+        out.append((t.get_weights_flat(), h))
+    (wl, hl), (wg, hg) = out
+    assert np.array_equal(wl, wg), np.abs(wl - wg).max()
+    for a, b in zip(hl, hg):
+        for key in a:
+            np.testing.assert_array_equal(a[key], b[key])

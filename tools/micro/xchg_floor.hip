@@ -220,8 +220,127 @@ __global__ __launch_bounds__(NTH) void flagbar(unsigned* flags, int R, int st, i
   if (r == 0 && threadIdx.x == 0) out[0] = t1 - t0;
 }
 
+
+// ---- chip-wide: G groups of R = 8 workgroups exchanging at once (the persistent kernels run
+//      32 such groups, one per gradient tile), with the hand-off at device scope (sc1 stores and
+//      loads, agent-scope atomic flags: what the kernels do) or XCD-local (plain stores, which
+//      keep the line in the XCD's L2, read by the same sc1 loads -- L1 skipped, L2-served --
+//      and a plain flag store polled by the same agent-scope loads) --
+//      valid only when every member of a group runs on one XCD, which the kernel checks
+//      through HW_REG_XCC_ID (err bit 4 otherwise).
+//   LOCAL: members of group g on one XCD: b = (g % 8) + 8 * ((g / 8) * 8 + r); else b = 8 g + r
+template <bool XCDL>
+__device__ __forceinline__ void st4s(rsrc_t r, int v, f32x4 x) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, x), r, v * 4, 0, XCDL ? 0 : 16);
+}
+template <bool XCDL>
+__device__ __forceinline__ f32x4 ld4s(rsrc_t r, int v) {
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, v * 4, 0, 16));   // sc1: skips L1, L2-served
+}
+template <bool XCDL>
+__device__ __forceinline__ void flag_st(unsigned* f, unsigned tag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (XCDL) __builtin_amdgcn_raw_buffer_store_b32(tag, mk((float*)f), 0, 0, 0);
+    else __hip_atomic_store((gu32*)f, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+template <bool XCDL>
+__device__ __forceinline__ bool flag_wait(const unsigned* flags, int n, unsigned tag, unsigned* err) {
+  int ok = 1;
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    const long long t0 = __builtin_amdgcn_s_memrealtime();
+    for (;;) {
+      const unsigned v = lane < n ? __hip_atomic_load((gu32*)(const_cast<unsigned*>(flags) + lane), __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_AGENT)
+                                  : tag;
+      if (__all(v >= tag)) break;
+      if (__builtin_amdgcn_s_memrealtime() - t0 > TMO) {
+        ok = 0;
+        if (lane == 0) atomicOr(err, 1u);
+        if (lane < n && blockIdx.x < 64 && blockIdx.x % 8 == 0)
+          printf("block %d lane %d flag[%d] %u want %u xcc %u\n", blockIdx.x, lane, (int)(flags - (const unsigned*)0) & 255, v, tag, xcc_id());
+        break;
+      }
+    }
+  }
+  ok = __syncthreads_and(ok);
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  return ok != 0;
+}
+
+template <int NF4, bool XCDL, bool LOCAL>
+__global__ __launch_bounds__(NTH) void groups(float* buf, unsigned* flags, unsigned* xcc, int G, int iters, long long* out,
+                                              unsigned* err) {
+  const int b = blockIdx.x, tid = threadIdx.x;
+  constexpr int R = 8;
+  int g, r;
+  if (LOCAL) { const int k = b / 8; g = (b % 8) + 8 * (k / 8); r = k % 8; }
+  else { g = b / 8; r = b % 8; }
+  if (g >= G) return;
+  const long long slab_f = (long long)NF4 * NTH * 4;
+  float* gb = buf + (long long)g * 2 * R * slab_f;
+  unsigned* gf = flags + g * 256;
+  // membership check: every member of the group on one XCD (XCDL only)
+  if (tid == 0) __hip_atomic_store((gu32*)(xcc + g * R + r), xcc_id() + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (XCDL) {
+    __shared__ int same;
+    if (tid < 64) {
+      const long long t0 = __builtin_amdgcn_s_memrealtime();
+      unsigned v = 0;
+      for (;;) {
+        v = tid < R ? __hip_atomic_load((gu32*)(xcc + g * R + tid), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 1u;
+        if (__all(v != 0u) || __builtin_amdgcn_s_memrealtime() - t0 > TMO) break;
+      }
+      const unsigned v0 = __shfl(v, 0);
+      const bool eq = __all(tid >= R || v == v0);
+      if (tid == 0) same = eq ? 1 : 0;
+    }
+    __syncthreads();
+    if (!same) { if (tid == 0) { atomicOr(err, 16u); if (g == 0) printf("group 0 member %d: not one XCD\n", r); } return; }
+  }
+  constexpr int NV = NF4 > 0 ? NF4 : 1;
+  f32x4 v[NV];
+#pragma unroll
+  for (int u = 0; u < NV; ++u) v[u] = f32x4{1.f, (float)r, 3.f, (float)tid};
+  __syncthreads();
+  const long long t0 = __builtin_amdgcn_s_memrealtime();
+  for (int i = 0; i < iters; ++i) {
+    const unsigned tag = (unsigned)(i + 1);
+    float* par = gb + (long long)(i & 1) * R * slab_f;
+#pragma unroll
+    for (int u = 0; u < NF4; ++u) st4s<XCDL>(mk(par + r * slab_f), (u * NTH + tid) * 4, v[u]);
+    flag_st<XCDL>(gf + r, tag);
+    if (!flag_wait<XCDL>(gf, R, tag, err)) break;
+    f32x4 x[R][NV];
+#pragma unroll
+    for (int k = 0; k < R; ++k)
+#pragma unroll
+      for (int u = 0; u < NF4; ++u) x[k][u] = ld4s<XCDL>(mk(par + k * slab_f), (u * NTH + tid) * 4);
+#pragma unroll
+    for (int u = 0; u < NF4; ++u) {
+      f32x4 acc = x[0][u];
+#pragma unroll
+      for (int k = 1; k < R; ++k) acc += x[k][u];
+      v[u] = acc * 0.125f;
+    }
+    flag_st<XCDL>(gf + 64 + r, tag);
+    if (!flag_wait<XCDL>(gf + 64, R, tag, err)) break;
+  }
+  const long long t1 = __builtin_amdgcn_s_memrealtime();
+  float s = 0.f;
+#pragma unroll
+  for (int u = 0; u < NF4; ++u) s += v[u].x + v[u].w;
+  if (g == 0 && r == 0 && tid == 0) { out[0] = t1 - t0; out[1] = (long long)s; }
+}
+
 struct Dev {
   float* buf;
+  float* gbuf;
+  unsigned* gflags;
+  unsigned* xcc;
   unsigned* flags;
   long long* out;
   unsigned* err;
@@ -299,6 +418,31 @@ static void fb(Dev& d, int R, int st) {
          SLEEP ? "s_sleep1" : "spin", v[2]);
 }
 
+template <int NF4, bool XCDL, bool LOCAL>
+static void gr(Dev& d, int G) {
+  std::vector<double> v;
+  const int iters = 1000;
+  for (int rep = 0; rep < 5; ++rep) {
+    CK(hipMemset(d.gflags, 0, 32 * 256 * 4));
+    CK(hipMemset(d.xcc, 0, 32 * 8 * 4));
+    CK(hipMemset(d.err, 0, 4));
+    CK(hipDeviceSynchronize());
+    hipLaunchKernelGGL((groups<NF4, XCDL, LOCAL>), dim3(256), dim3(NTH), 0, 0, d.gbuf, d.gflags, d.xcc, G, iters, d.out, d.err);
+    CK(hipGetLastError());
+    CK(hipDeviceSynchronize());
+    long long h[2];
+    unsigned e = 0;
+    CK(hipMemcpy(h, d.out, sizeof(h), hipMemcpyDeviceToHost));
+    CK(hipMemcpy(&e, d.err, 4, hipMemcpyDeviceToHost));
+    if (e) { printf("groups G %d %s %s: error %u (16 = members not on one XCD)\n", G, XCDL ? "xcd-local" : "device", LOCAL ? "one-XCD" : "spread", e); return; }
+    if (h[0] >= TMO) { printf("groups G %d %s %s: timed out without an error word\n", G, XCDL ? "xcd-local" : "device", LOCAL ? "one-XCD" : "spread"); return; }
+    v.push_back(h[0] * 10.0 / iters);
+  }
+  std::sort(v.begin(), v.end());
+  printf("groups G %2d x R 8 %-16s members %-8s slab %6d B  round %7.0f ns (exchange + one flag-only round)\n", G,
+         XCDL ? "xcd-local (L2)" : "device (sc1)", LOCAL ? "one XCD" : "8 XCDs", NF4 * NTH * 16, v[2]);
+}
+
 int main() {
   Dev d;
   CK(hipMalloc(&d.buf, 2 * 8 * 8 * 256 * 16));
@@ -306,6 +450,26 @@ int main() {
   CK(hipMalloc(&d.flags, 4096));
   CK(hipMalloc(&d.out, 8 * 80));
   CK(hipMalloc(&d.err, 4));
+  CK(hipMalloc(&d.gbuf, 32LL * 2 * 8 * 8 * 256 * 16));
+  CK(hipMemset(d.gbuf, 0, 32LL * 2 * 8 * 8 * 256 * 16));
+  CK(hipMalloc(&d.gflags, 32 * 256 * 4));
+  CK(hipMalloc(&d.xcc, 32 * 8 * 4));
+  if (getenv("XF_DEBUG")) {
+    gr<0, true, true>(d, 1);
+    gr<4, true, false>(d, 32);
+    return 0;
+  }
+  for (int G : {1, 32}) {
+    gr<0, false, false>(d, G);
+    gr<0, false, true>(d, G);
+    gr<0, true, true>(d, G);
+    gr<4, false, false>(d, G);
+    gr<4, false, true>(d, G);
+    gr<4, true, true>(d, G);
+    gr<8, false, false>(d, G);
+    gr<8, true, true>(d, G);
+  }
+  gr<4, true, false>(d, 32);   // must report the membership error
   for (int peer : {8, 1}) {
     pp<0, false>(d, peer);
     pp<0, true>(d, peer);

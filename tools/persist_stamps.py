@@ -51,7 +51,7 @@ def main():
     ys = [np.eye(10, dtype=np.float32)[rng.integers(0, 10, 7500)] for _ in range(R)]
     t.set_data(xs, ys, 0.1)
     nk0, nc0, kc0, cw, nch, wgs, grid = t.exe.persist_geometry()
-    var, nd, sync = t.exe.persist_variant()
+    var, nd, sync = t.exe.persist_variant()[:3]
     print("plan", t.plan_name())
     st = torch.zeros(grid * 8 * 32, dtype=torch.int64, device="cuda")
     t.begin_epoch()
