@@ -291,6 +291,79 @@ __device__ __forceinline__ float upd(const DeepArgs& a, const Ctx& x, const OptS
   }
 }
 
+// The optimizer state of N elements loaded ahead of their update (upd_p): issued before the
+// phase's MFMAs, so a batch of updates waits for one global-load latency, not one per element
+// (Adam on Otto: 173 us per step before, every element's state a dependent load).  The same thread updates the same elements every
+// step, so its own earlier state stores are what it reads.
+template <int N>
+struct OptPre {
+  float s0[N], s1[N];
+};
+template <bool SGD0, int N>
+__device__ __forceinline__ void opt_pre(const DeepArgs& a, const Ctx& x, const OptStep& o, const long long (&pi)[N],
+                                        const bool (&ok)[N], OptPre<N>& p) {
+  if constexpr (!SGD0) {
+    if (o.kind == 0) return;
+    const bool two = o.kind == 4 || o.kind == 5 || o.kind == 7;
+#pragma unroll
+    for (int n = 0; n < N; ++n) p.s0[n] = ok[n] ? x.S[pi[n]] : 0.f;
+    if (two) {
+#pragma unroll
+      for (int n = 0; n < N; ++n) p.s1[n] = ok[n] ? x.S[pi[n] + a.op.s_plane] : 0.f;
+    }
+  }
+}
+// upd with the state values s0 = S[pi], s1 = S[pi + s_plane] already loaded (opt_pre)
+template <bool SGD0>
+__device__ __forceinline__ float upd_p(const DeepArgs& a, const Ctx& x, const OptStep& o, long long pi, float w, float g,
+                                       float s0, float s1) {
+  g *= a.op.grad_scale;
+  if constexpr (SGD0) {
+    return w - o.lr * g;
+  } else {
+    const OptParams& p = a.op;
+    float* S = x.S;
+    const long long i1 = pi + p.s_plane;
+    switch (o.kind) {
+      case 0: return w - o.lr * g;
+      case 1: case 2: {
+        const float v = p.mom * s0 - o.lr * g;
+        S[pi] = v;
+        return o.kind == 2 ? w + p.mom * v - o.lr * g : w + v;
+      }
+      case 3: case 4: {
+        const float ms = p.rho * s0 + (1.f - p.rho) * g * g;
+        S[pi] = ms;
+        if (o.kind == 4) {
+          const float m = p.mom * s1 + o.lr * g / sqrtf(ms + p.eps);
+          S[i1] = m;
+          return w - m;
+        }
+        return w - o.lr * g / (sqrtf(ms) + p.eps);
+      }
+      case 5: {
+        const float m = p.b1 * s0 + (1.f - p.b1) * g;
+        const float v = p.b2 * s1 + (1.f - p.b2) * g * g;
+        S[pi] = m;
+        S[i1] = v;
+        return w - o.lrt * m / (sqrtf(v) + p.eps);
+      }
+      case 6: {
+        const float ac = s0 + g * g;
+        S[pi] = ac;
+        return w - o.lr * g / (sqrtf(ac) + p.eps);
+      }
+      default: {
+        const float m = p.b1 * s0 + (1.f - p.b1) * g;
+        const float u = fmaxf(p.b2 * s1, fabsf(g));
+        S[pi] = m;
+        S[i1] = u;
+        return w - o.lrt * m / (u + p.eps);
+      }
+    }
+  }
+}
+
 // ---- C[16 rows x 16] of one wave: rows from global (loadA(k) -> this lane's float4
 //      A[row][k .. k + 3]), B^T from LDS ([16][ldb], k contiguous), over the k-chunks
 //      t = kp + KS u.  A register ring of PF chunks is issued (ring_issue) ahead of the
@@ -624,6 +697,16 @@ __device__ __forceinline__ void dw_last(const DeepArgs& a, float* smem, const Ct
   if (rows && x.w < NCT) {
     const int ct = x.w, I0 = 16 * x.j, ldat = a.Bp + 4;
     const float* at = smem + la.l_at;
+    const int c = 16 * ct + x.c16;
+    long long pi[4];
+    bool ok[4];
+    OptPre<4> pre;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      pi[q] = lb.p_off + (long long)(I0 + 4 * x.g + q) * C + c;
+      ok[q] = !SYNC && I0 + 4 * x.g + q < lb.K && c < C;
+    }
+    opt_pre<SGD0 || SYNC, 4>(a, x, os, pi, ok, pre);
     f32x4 acc = z4();
     for (int rr = 0; rr < (a.Bp >> 4); ++rr) {
       const f32x4 av = lds4(at + x.c16 * ldat + 16 * rr + 4 * x.g);
@@ -633,7 +716,6 @@ __device__ __forceinline__ void dw_last(const DeepArgs& a, float* smem, const Ct
       mma4(acc, av, b);
     }
     float* wr = smem + lb.l_w;
-    const int c = 16 * ct + x.c16;
     if constexpr (SYNC) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) st1(x.xs, (4 * x.g + q) * C16 + c, x.xp + a.x_w[L - 1], acc[q]);
@@ -643,8 +725,8 @@ __device__ __forceinline__ void dw_last(const DeepArgs& a, float* smem, const Ct
       for (int q = 0; q < 4; ++q) {
         const int ip = 4 * x.g + q;
         float wt = wr[ip * ldc + c];
-        if (I0 + ip < lb.K && c < C) {
-          wt = upd<SGD0>(a, x, os, lb.p_off + (long long)(I0 + ip) * C + c, wt, acc[q]);
+        if (ok[q]) {
+          wt = upd_p<SGD0>(a, x, os, pi[q], wt, acc[q], pre.s0[q], pre.s1[q]);
           wr[ip * ldc + c] = wt;
           st1(x.rs, (I0 + ip) * C16 + c, lb.o_w, wt);
         }
@@ -744,6 +826,22 @@ __device__ __forceinline__ void bw_phase(const DeepArgs& a, float* smem, const C
   if (nch > 1) load_chunk(1, preB);
   f32x4 accB0 = z4(), accB1 = z4();
   f32x4 accWp = z4();   // this wave's DW partial of the previous chunk (first row half: pending update)
+  // optimizer state of the elements finish(h) updates, loaded at the top of chunk h (stN), in
+  // use one chunk later (stC)
+  OptPre<4> stC, stN;
+  auto state_pre = [&](int h, OptPre<4>& st) {
+    const int c0 = h * CW, cw = ly.N16 - c0 < CW ? ly.N16 - c0 : CW;
+    if (SYNC || hh != 0 || 16 * f >= cw) return;
+    const int col = c0 + 16 * f + x.c16;
+    long long pi[4];
+    bool ok[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      pi[q] = ly.p_off + (long long)(I0 + 4 * x.g + q) * ly.N + col;
+      ok[q] = I0 + 4 * x.g + q < ly.K && col < ly.N;
+    }
+    opt_pre<SGD0 || SYNC, 4>(a, x, os, pi, ok, st);
+  };
   // the first-half waves complete chunk hq's rows J: partial sums, update of the masters of
   // the chunk's columns and their W^T image segment (SYNC: the gradient to the exchange tile)
   auto finish = [&](int hq, f32x4 accq) {
@@ -761,7 +859,7 @@ __device__ __forceinline__ void bw_phase(const DeepArgs& a, float* smem, const C
         const int ip = 4 * x.g + q;
         float wt = wr[ip * ldr + col];
         if (I0 + ip < ly.K && col < ly.N) {
-          wt = upd<SGD0>(a, x, os, ly.p_off + (long long)(I0 + ip) * ly.N + col, wt, accq[q]);
+          wt = upd_p<SGD0>(a, x, os, ly.p_off + (long long)(I0 + ip) * ly.N + col, wt, accq[q], stC.s0[q], stC.s1[q]);
           wr[ip * ldr + col] = wt;
         }
         wv[q] = wt;
@@ -777,8 +875,10 @@ __device__ __forceinline__ void bw_phase(const DeepArgs& a, float* smem, const C
       if (row < Bp) lds4(sdz + row * LDZ + 4 * q, 4 * q < cw ? pre[u] : z4());
     }
     if (h + 2 < nch) load_chunk(h + 2, pre);   // two chunks in flight ahead of the consumer
+    state_pre(h, stN);
     lds_barrier();
     if (h > 0) finish(h - 1, accWp);
+    stC = stN;
     // dA_{l-1}[rows of tile rt][J] over the chunk's 16-column groups t (t % KS == kp)
 #pragma unroll
     for (int t = 0; t < CW / 16; ++t) {
@@ -882,6 +982,20 @@ __device__ __forceinline__ void dw0_phase(const DeepArgs& a, float* smem, const 
   for (int fg = x.w; fg < nfg; fg += NWV) {
     const int i0 = 64 * fg, ic = i0 + 4 * x.c16;
     const bool fin = ic < Kx;
+    const int col = J0 + x.c16;
+    // the optimizer state of this lane's 16 elements, loaded before the X rows and the MFMAs
+    long long pi[16];
+    bool ok[16];
+    OptPre<16> pre;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int ff = 0; ff < 4; ++ff) {
+        const int i = i0 + 16 * x.g + 4 * q + ff;
+        pi[4 * q + ff] = l0.p_off + (long long)i * l0.N + col;
+        ok[4 * q + ff] = !SYNC && i < l0.K && col < l0.N;
+      }
+    opt_pre<SGD0 || SYNC, 16>(a, x, os, pi, ok, pre);
     f32x4 acc[4] = {z4(), z4(), z4(), z4()};
     // two passes of 4 row groups: 16 float4 of X in flight per lane
 #pragma unroll
@@ -913,7 +1027,6 @@ __device__ __forceinline__ void dw0_phase(const DeepArgs& a, float* smem, const 
       }
     }
     // lane (column c16, group g): features i0 + 16 g + 4 q + f of column J0 + c16
-    const int col = J0 + x.c16;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int ib = i0 + 16 * x.g + 4 * q;
@@ -925,8 +1038,8 @@ __device__ __forceinline__ void dw0_phase(const DeepArgs& a, float* smem, const 
       f32x4 wv = lds4(w0t + x.c16 * ld0 + ib);
 #pragma unroll
       for (int ff = 0; ff < 4; ++ff) {
-        const int i = ib + ff;
-        if (i < l0.K && col < l0.N) wv[ff] = upd<SGD0>(a, x, os, l0.p_off + (long long)i * l0.N + col, wv[ff], acc[ff][q]);
+        if (ok[4 * q + ff])
+          wv[ff] = upd_p<SGD0>(a, x, os, pi[4 * q + ff], wv[ff], acc[ff][q], pre.s0[4 * q + ff], pre.s1[4 * q + ff]);
       }
       lds4(w0t + x.c16 * ld0 + ib, wv);
     }
@@ -1031,12 +1144,20 @@ __device__ __forceinline__ void apply_sums(const DeepArgs& a, float* smem, const
     float* w0t = smem + l0.l_w;
     for (int e = x.tid; e < 16 * q4; e += NTH) {
       const int c = e / q4, k = 4 * (e - c * q4);
+      long long pi[4];
+      bool ok[4];
+      OptPre<4> pre;
+#pragma unroll
+      for (int ff = 0; ff < 4; ++ff) {
+        pi[ff] = l0.p_off + (long long)(k + ff) * l0.N + J0 + c;
+        ok[ff] = k + ff < l0.K && J0 + c < l0.N;
+      }
+      opt_pre<SGD0, 4>(a, x, os, pi, ok, pre);
       const f32x4 g = ld4(x.xs, c * Kx + k, sum0);
       f32x4 w = lds4(w0t + c * ld0 + k);
 #pragma unroll
       for (int ff = 0; ff < 4; ++ff)
-        if (k + ff < l0.K && J0 + c < l0.N)
-          w[ff] = upd<SGD0>(a, x, os, l0.p_off + (long long)(k + ff) * l0.N + J0 + c, w[ff], g[ff]);
+        if (ok[ff]) w[ff] = upd_p<SGD0>(a, x, os, pi[ff], w[ff], g[ff], pre.s0[ff], pre.s1[ff]);
       lds4(w0t + c * ld0 + k, w);
     }
     if (x.tid < 16 && l0.has_bias && J0 + x.tid < l0.N) {
@@ -1053,6 +1174,15 @@ __device__ __forceinline__ void apply_sums(const DeepArgs& a, float* smem, const
       float* wr = smem + ly.l_w;
       for (int e = x.tid; e < 4 * N16; e += NTH) {
         const int q = e / N16, c = e - q * N16;
+        long long pi[4];
+        bool ok[4];
+        OptPre<4> pre;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          pi[k] = ly.p_off + (long long)(I0 + 4 * q + k) * ly.N + c;
+          ok[k] = I0 + 4 * q + k < ly.K && c < ly.N;
+        }
+        opt_pre<SGD0, 4>(a, x, os, pi, ok, pre);
         f32x4 g, w;
 #pragma unroll
         for (int k = 0; k < 4; ++k) g[k] = ld1(x.xs, a.x_w[l] + (4 * q + k) * N16 + c, sum0);
@@ -1060,8 +1190,8 @@ __device__ __forceinline__ void apply_sums(const DeepArgs& a, float* smem, const
         for (int k = 0; k < 4; ++k) {
           const int ip = 4 * q + k;
           float wt = wr[ip * ldr + c];
-          if (I0 + ip < ly.K && c < ly.N) {
-            wt = upd<SGD0>(a, x, os, ly.p_off + (long long)(I0 + ip) * ly.N + c, wt, g[k]);
+          if (ok[k]) {
+            wt = upd_p<SGD0>(a, x, os, pi[k], wt, g[k], pre.s0[k], pre.s1[k]);
             wr[ip * ldr + c] = wt;
           }
           w[k] = wt;
