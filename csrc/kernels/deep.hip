@@ -3,10 +3,10 @@
 #include "args.h"
 #include <hip/hip_runtime.h>
 
-extern "C" hipError_t ea_deep_l2(const ea::DeepArgs* a, int fast, int sgd0, hipStream_t s);
-extern "C" hipError_t ea_deep_l3(const ea::DeepArgs* a, int fast, int sgd0, hipStream_t s);
-extern "C" hipError_t ea_deep_l4(const ea::DeepArgs* a, int fast, int sgd0, hipStream_t s);
-extern "C" hipError_t ea_deep_l5(const ea::DeepArgs* a, int fast, int sgd0, hipStream_t s);
+extern "C" hipError_t ea_deep_l2(const ea::DeepArgs* a, int fast, int opk, hipStream_t s);
+extern "C" hipError_t ea_deep_l3(const ea::DeepArgs* a, int fast, int opk, hipStream_t s);
+extern "C" hipError_t ea_deep_l4(const ea::DeepArgs* a, int fast, int opk, hipStream_t s);
+extern "C" hipError_t ea_deep_l5(const ea::DeepArgs* a, int fast, int opk, hipStream_t s);
 
 using namespace ea;
 
@@ -20,12 +20,14 @@ extern "C" hipError_t ea_deep(const DeepArgs* a, hipStream_t s) {
   for (int i = 0; i < a->nmet; ++i)
     fast = fast && (a->met[i] == MET_ACC_CAT || a->met[i] == MET_ACC_SPARSE || a->met[i] == LOSS_CCE ||
                     a->met[i] == LOSS_SPARSE_CCE);
-  const int sgd0 = a->op.opt == OPT_SGD && a->op.mom == 0.f;   // plain SGD: no optimizer state
+  // the kernel's optimizer instance: 0 plain SGD (no optimizer state), 1 Adam, 2 any other
+  // rule (run-time dispatch) -- deep_impl.h OPK_*
+  const int opk = (a->op.opt == OPT_SGD && a->op.mom == 0.f) ? 0 : (a->op.opt == OPT_ADAM ? 1 : 2);
   switch (a->L) {
-    case 2: return ea_deep_l2(a, fast, sgd0, s);
-    case 3: return ea_deep_l3(a, fast, sgd0, s);
-    case 4: return ea_deep_l4(a, fast, sgd0, s);
-    case 5: return ea_deep_l5(a, fast, sgd0, s);
+    case 2: return ea_deep_l2(a, fast, opk, s);
+    case 3: return ea_deep_l3(a, fast, opk, s);
+    case 4: return ea_deep_l4(a, fast, opk, s);
+    case 5: return ea_deep_l5(a, fast, opk, s);
     default: return hipErrorInvalidValue;
   }
 }

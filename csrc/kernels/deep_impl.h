@@ -223,6 +223,9 @@ __device__ __forceinline__ Ctx lanes(const Ctx& x0) {
 // per-step scalars hoisted: the decayed learning rate and the Adam / Adamax bias
 // corrections are computed once per phase, not per element (the scalar rule inlined at
 // every update site cost ~1 KB of scratch per lane in this kernel)
+// optimizer instances of the kernel: plain SGD (no state), Adam (the Otto notebook's), every
+// other rule through the run-time dispatch
+constexpr int OPK_SGD0 = 0, OPK_ADAM = 1, OPK_ANY = 2;
 struct OptStep {
   int kind;          // 0 plain SGD, 1 momentum, 2 Nesterov, 3 RMSprop, 4 RMSprop + momentum, 5 Adam,
                      // 6 Adagrad, 7 Adamax
@@ -242,11 +245,18 @@ __device__ __forceinline__ OptStep opt_step(const OptParams& p, long long it) {
   }
   return o;
 }
-template <bool SGD0>
+template <int OPK>
 __device__ __forceinline__ float upd(const DeepArgs& a, const Ctx& x, const OptStep& o, long long pi, float w, float g) {
   g *= a.op.grad_scale;
-  if constexpr (SGD0) {
+  if constexpr (OPK == OPK_SGD0) {
     return w - o.lr * g;
+  } else if constexpr (OPK == OPK_ADAM) {
+    const OptParams& p = a.op;
+    const float m = p.b1 * x.S[pi] + (1.f - p.b1) * g;
+    const float v = p.b2 * x.S[pi + p.s_plane] + (1.f - p.b2) * g * g;
+    x.S[pi] = m;
+    x.S[pi + p.s_plane] = v;
+    return w - o.lrt * m / (sqrtf(v) + p.eps);
   } else {
     const OptParams& p = a.op;
     float* S = x.S;
@@ -299,12 +309,12 @@ template <int N>
 struct OptPre {
   float s0[N], s1[N];
 };
-template <bool SGD0, int N>
+template <int OPK, int N>
 __device__ __forceinline__ void opt_pre(const DeepArgs& a, const Ctx& x, const OptStep& o, const long long (&pi)[N],
                                         const bool (&ok)[N], OptPre<N>& p) {
-  if constexpr (!SGD0) {
-    if (o.kind == 0) return;
-    const bool two = o.kind == 4 || o.kind == 5 || o.kind == 7;
+  if constexpr (OPK != OPK_SGD0) {
+    if (OPK == OPK_ANY && o.kind == 0) return;
+    const bool two = OPK == OPK_ADAM || o.kind == 4 || o.kind == 5 || o.kind == 7;
 #pragma unroll
     for (int n = 0; n < N; ++n) p.s0[n] = ok[n] ? x.S[pi[n]] : 0.f;
     if (two) {
@@ -314,12 +324,19 @@ __device__ __forceinline__ void opt_pre(const DeepArgs& a, const Ctx& x, const O
   }
 }
 // upd with the state values s0 = S[pi], s1 = S[pi + s_plane] already loaded (opt_pre)
-template <bool SGD0>
+template <int OPK>
 __device__ __forceinline__ float upd_p(const DeepArgs& a, const Ctx& x, const OptStep& o, long long pi, float w, float g,
                                        float s0, float s1) {
   g *= a.op.grad_scale;
-  if constexpr (SGD0) {
+  if constexpr (OPK == OPK_SGD0) {
     return w - o.lr * g;
+  } else if constexpr (OPK == OPK_ADAM) {   // the Adam instance: no dispatch on the rule
+    const OptParams& p = a.op;
+    const float m = p.b1 * s0 + (1.f - p.b1) * g;
+    const float v = p.b2 * s1 + (1.f - p.b2) * g * g;
+    x.S[pi] = m;
+    x.S[pi + p.s_plane] = v;
+    return w - o.lrt * m / (sqrtf(v) + p.eps);
   } else {
     const OptParams& p = a.op;
     float* S = x.S;
@@ -680,7 +697,7 @@ __device__ __forceinline__ void tail_phase(const DeepArgs& a, float* smem, const
 // ---- weight gradient of the last layer, rows J (= column tile j of layer L-2) and (on
 //      workgroup 0) its bias; images of the updated rows for the next tail (SYNC: the
 //      gradient goes to the exchange tile instead, the update comes after the replica sum)
-template <int L, bool SGD0, bool SYNC>
+template <int L, int OPK, bool SYNC>
 __device__ __forceinline__ void dw_last(const DeepArgs& a, float* smem, const Ctx& x0, const OptStep& os) {
   const Ctx x = lanes(x0);
   const DeepLayer la = a.ly[L - 2], lb = a.ly[L - 1];
@@ -706,7 +723,7 @@ __device__ __forceinline__ void dw_last(const DeepArgs& a, float* smem, const Ct
       pi[q] = lb.p_off + (long long)(I0 + 4 * x.g + q) * C + c;
       ok[q] = !SYNC && I0 + 4 * x.g + q < lb.K && c < C;
     }
-    opt_pre<SGD0 || SYNC, 4>(a, x, os, pi, ok, pre);
+    opt_pre<SYNC ? OPK_SGD0 : OPK, 4>(a, x, os, pi, ok, pre);
     f32x4 acc = z4();
     for (int rr = 0; rr < (a.Bp >> 4); ++rr) {
       const f32x4 av = lds4(at + x.c16 * ldat + 16 * rr + 4 * x.g);
@@ -726,7 +743,7 @@ __device__ __forceinline__ void dw_last(const DeepArgs& a, float* smem, const Ct
         const int ip = 4 * x.g + q;
         float wt = wr[ip * ldc + c];
         if (ok[q]) {
-          wt = upd_p<SGD0>(a, x, os, pi[q], wt, acc[q], pre.s0[q], pre.s1[q]);
+          wt = upd_p<OPK>(a, x, os, pi[q], wt, acc[q], pre.s0[q], pre.s1[q]);
           wr[ip * ldc + c] = wt;
           st1(x.rs, (I0 + ip) * C16 + c, lb.o_w, wt);
         }
@@ -743,7 +760,7 @@ __device__ __forceinline__ void dw_last(const DeepArgs& a, float* smem, const Ct
       st1(x.xs, c, x.xp + a.x_b[L - 1], db);
     } else {
       float* bl = smem + lb.l_b;
-      const float b = upd<SGD0>(a, x, os, lb.p_off + (long long)lb.K * C + c, bl[c], db);
+      const float b = upd<OPK>(a, x, os, lb.p_off + (long long)lb.K * C + c, bl[c], db);
       bl[c] = b;
       st1(x.rs, c, a.o_bl, b);
     }
@@ -752,7 +769,7 @@ __device__ __forceinline__ void dw_last(const DeepArgs& a, float* smem, const Ct
 }
 
 // ---- column sums of dZ_l[:, J] (the bias gradient of tile j of layer l) -> b_l[J]
-template <int l, bool SGD0, bool SYNC>
+template <int l, int OPK, bool SYNC>
 __device__ __forceinline__ void bias_tile(const DeepArgs& a, float* smem, const Ctx& x0, long long o_dz, int N16,
                                           const OptStep& os) {
   const Ctx x = lanes(x0);
@@ -776,7 +793,7 @@ __device__ __forceinline__ void bias_tile(const DeepArgs& a, float* smem, const 
       st1(x.xs, x.tid, x.xp + a.x_b[l], db);
     } else {
       float* bt = smem + ly.l_b;
-      bt[x.tid] = upd<SGD0>(a, x, os, ly.p_off + (long long)ly.K * ly.N + J0 + x.tid, bt[x.tid], db);
+      bt[x.tid] = upd<OPK>(a, x, os, ly.p_off + (long long)ly.K * ly.N + J0 + x.tid, bt[x.tid], db);
     }
   }
   __syncthreads();
@@ -787,13 +804,13 @@ __device__ __forceinline__ void bias_tile(const DeepArgs& a, float* smem, const 
 //      DW_l[J, chunk] = A_{l-1}[:, J]^T dZ_chunk (waves = 4 column tiles x 2 row halves),
 //      update of the chunk's masters + their W^T image segment; finally dZ_{l-1}[:, J] =
 //      dA * G_{l-1} -> workspace (l >= 2) or the LDS dZ_0^T stripe (l = 1)
-template <int L, int l, bool SGD0, bool SYNC>
+template <int L, int l, int OPK, bool SYNC>
 __device__ __forceinline__ void bw_phase(const DeepArgs& a, float* smem, const Ctx& x0, const OptStep& os,
                                          const f32x4 (&G)[L - 1], int s) {
   const Ctx x = lanes(x0);
   const DeepLayer lp = a.ly[l - 1], ly = a.ly[l];
   if (x.j >= lp.T) {   // no row tile of W_l here; maybe its bias tile (layer l wider than l - 1)
-    bias_tile<l, SGD0, SYNC>(a, smem, x, ly.o_dz, ly.N16, os);
+    bias_tile<l, OPK, SYNC>(a, smem, x, ly.o_dz, ly.N16, os);
     return;
   }
   // this workgroup's bias tile j of layer l: summed from the staged chunk that holds it
@@ -840,7 +857,7 @@ __device__ __forceinline__ void bw_phase(const DeepArgs& a, float* smem, const C
       pi[q] = ly.p_off + (long long)(I0 + 4 * x.g + q) * ly.N + col;
       ok[q] = I0 + 4 * x.g + q < ly.K && col < ly.N;
     }
-    opt_pre<SGD0 || SYNC, 4>(a, x, os, pi, ok, st);
+    opt_pre<SYNC ? OPK_SGD0 : OPK, 4>(a, x, os, pi, ok, st);
   };
   // the first-half waves complete chunk hq's rows J: partial sums, update of the masters of
   // the chunk's columns and their W^T image segment (SYNC: the gradient to the exchange tile)
@@ -859,7 +876,7 @@ __device__ __forceinline__ void bw_phase(const DeepArgs& a, float* smem, const C
         const int ip = 4 * x.g + q;
         float wt = wr[ip * ldr + col];
         if (I0 + ip < ly.K && col < ly.N) {
-          wt = upd_p<SGD0>(a, x, os, ly.p_off + (long long)(I0 + ip) * ly.N + col, wt, accq[q], stC.s0[q], stC.s1[q]);
+          wt = upd_p<OPK>(a, x, os, ly.p_off + (long long)(I0 + ip) * ly.N + col, wt, accq[q], stC.s0[q], stC.s1[q]);
           wr[ip * ldr + col] = wt;
         }
         wv[q] = wt;
@@ -918,7 +935,7 @@ __device__ __forceinline__ void bw_phase(const DeepArgs& a, float* smem, const C
         st1(x.xs, x.tid, x.xp + a.x_b[l], db);
       } else {
         float* bt = smem + ly.l_b;
-        bt[x.tid] = upd<SGD0>(a, x, os, ly.p_off + (long long)ly.K * ly.N + 16 * x.j + x.tid, bt[x.tid], db);
+        bt[x.tid] = upd<OPK>(a, x, os, ly.p_off + (long long)ly.K * ly.N + 16 * x.j + x.tid, bt[x.tid], db);
       }
     }
   };
@@ -958,7 +975,7 @@ __device__ __forceinline__ void bw_phase(const DeepArgs& a, float* smem, const C
 //      DW_0[:, J] = X^T dZ_0[:, J] (waves = 64-feature groups; the X rows of that step,
 //      float4 along the features: MFMA e of lane group g takes batch row 16 rr + 4 g + e,
 //      output tile f the features i0 + 4 m + f), bias, in-place update of W_0^T
-template <int L, bool SGD0, bool SYNC>
+template <int L, int OPK, bool SYNC>
 __device__ __forceinline__ void dw0_phase(const DeepArgs& a, float* smem, const Ctx& x0, int sp, const OptStep& os) {
   const Ctx x = lanes(x0);
   const DeepLayer l0 = a.ly[0];
@@ -973,7 +990,7 @@ __device__ __forceinline__ void dw0_phase(const DeepArgs& a, float* smem, const 
       st1(x.xs, x.tid, x.xp + a.x_b0, db);
     } else {
       float* bt = smem + l0.l_b;
-      bt[x.tid] = upd<SGD0>(a, x, os, l0.p_off + (long long)l0.K * l0.N + J0 + x.tid, bt[x.tid], db);
+      bt[x.tid] = upd<OPK>(a, x, os, l0.p_off + (long long)l0.K * l0.N + J0 + x.tid, bt[x.tid], db);
     }
   }
   const int nfg = (Kx + 63) >> 6;
@@ -983,19 +1000,6 @@ __device__ __forceinline__ void dw0_phase(const DeepArgs& a, float* smem, const 
     const int i0 = 64 * fg, ic = i0 + 4 * x.c16;
     const bool fin = ic < Kx;
     const int col = J0 + x.c16;
-    // the optimizer state of this lane's 16 elements, loaded before the X rows and the MFMAs
-    long long pi[16];
-    bool ok[16];
-    OptPre<16> pre;
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-#pragma unroll
-      for (int ff = 0; ff < 4; ++ff) {
-        const int i = i0 + 16 * x.g + 4 * q + ff;
-        pi[4 * q + ff] = l0.p_off + (long long)i * l0.N + col;
-        ok[4 * q + ff] = !SYNC && i < l0.K && col < l0.N;
-      }
-    opt_pre<SGD0 || SYNC, 16>(a, x, os, pi, ok, pre);
     f32x4 acc[4] = {z4(), z4(), z4(), z4()};
     // two passes of 4 row groups: 16 float4 of X in flight per lane
 #pragma unroll
@@ -1026,7 +1030,21 @@ __device__ __forceinline__ void dw0_phase(const DeepArgs& a, float* smem, const 
         }
       }
     }
-    // lane (column c16, group g): features i0 + 16 g + 4 q + f of column J0 + c16
+    // lane (column c16, group g): features i0 + 16 g + 4 q + f of column J0 + c16; the
+    // optimizer state of its 16 elements loaded at once (after the MFMAs: the X rows'
+    // registers are free by then)
+    long long pi[16];
+    bool ok[16];
+    OptPre<16> pre;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int ff = 0; ff < 4; ++ff) {
+        const int i = i0 + 16 * x.g + 4 * q + ff;
+        pi[4 * q + ff] = l0.p_off + (long long)i * l0.N + col;
+        ok[4 * q + ff] = !SYNC && i < l0.K && col < l0.N;
+      }
+    opt_pre<SYNC ? OPK_SGD0 : OPK, 16>(a, x, os, pi, ok, pre);
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int ib = i0 + 16 * x.g + 4 * q;
@@ -1039,7 +1057,7 @@ __device__ __forceinline__ void dw0_phase(const DeepArgs& a, float* smem, const 
 #pragma unroll
       for (int ff = 0; ff < 4; ++ff) {
         if (ok[4 * q + ff])
-          wv[ff] = upd_p<SGD0>(a, x, os, pi[4 * q + ff], wv[ff], acc[ff][q], pre.s0[4 * q + ff], pre.s1[4 * q + ff]);
+          wv[ff] = upd_p<OPK>(a, x, os, pi[4 * q + ff], wv[ff], acc[ff][q], pre.s0[4 * q + ff], pre.s1[4 * q + ff]);
       }
       lds4(w0t + x.c16 * ld0 + ib, wv);
     }
@@ -1080,7 +1098,7 @@ __device__ __forceinline__ bool fwd_chain(const DeepArgs& a, float* smem, const 
 }
 
 // the backward phases of layers l .. 1 (BW_{L-2} also runs the last layer's update)
-template <int L, int l, bool SGD0, bool SYNC>
+template <int L, int l, int OPK, bool SYNC>
 __device__ __forceinline__ bool bw_chain(const DeepArgs& a, float* smem, const Ctx& x, int s, const OptStep& os,
                                          unsigned base, const f32x4 (&G)[L - 1]) {
   if constexpr (l >= 1) {
@@ -1088,13 +1106,13 @@ __device__ __forceinline__ bool bw_chain(const DeepArgs& a, float* smem, const C
     if (!wait_phase(a, x.r, base + p)) return false;
     dstamp(a, s, 11 + 2 * (L - 2 - l));
     if constexpr (l == L - 2) {
-      dw_last<L, SGD0, SYNC>(a, smem, x, os);
+      dw_last<L, OPK, SYNC>(a, smem, x, os);
       dstamp(a, s, 23);
     }
-    bw_phase<L, l, SGD0, SYNC>(a, smem, x, os, G, s);
+    bw_phase<L, l, OPK, SYNC>(a, smem, x, os, G, s);
     publish(a, x.r, x.j, base + p + 1);
     dstamp(a, s, 12 + 2 * (L - 2 - l));
-    return bw_chain<L, l - 1, SGD0, SYNC>(a, smem, x, s, os, base, G);
+    return bw_chain<L, l - 1, OPK, SYNC>(a, smem, x, s, os, base, G);
   }
   return true;
 }
@@ -1134,7 +1152,7 @@ __device__ __forceinline__ bool wait_x(const DeepArgs& a, int j, int kind, unsig
 // the summed gradient tile (sum0) applied to the owned masters by every replica alike --
 // the same sums and the same state, so the replicas stay one model bit for bit -- with the
 // images the other workgroups read (W_l^T segments, the last layer's rows and bias)
-template <int L, bool SGD0>
+template <int L, int OPK>
 __device__ __forceinline__ void apply_sums(const DeepArgs& a, float* smem, const Ctx& x0, long long sum0,
                                            const OptStep& os) {
   const Ctx x = lanes(x0);
@@ -1152,17 +1170,17 @@ __device__ __forceinline__ void apply_sums(const DeepArgs& a, float* smem, const
         pi[ff] = l0.p_off + (long long)(k + ff) * l0.N + J0 + c;
         ok[ff] = k + ff < l0.K && J0 + c < l0.N;
       }
-      opt_pre<SGD0, 4>(a, x, os, pi, ok, pre);
+      opt_pre<OPK, 4>(a, x, os, pi, ok, pre);
       const f32x4 g = ld4(x.xs, c * Kx + k, sum0);
       f32x4 w = lds4(w0t + c * ld0 + k);
 #pragma unroll
       for (int ff = 0; ff < 4; ++ff)
-        if (ok[ff]) w[ff] = upd_p<SGD0>(a, x, os, pi[ff], w[ff], g[ff], pre.s0[ff], pre.s1[ff]);
+        if (ok[ff]) w[ff] = upd_p<OPK>(a, x, os, pi[ff], w[ff], g[ff], pre.s0[ff], pre.s1[ff]);
       lds4(w0t + c * ld0 + k, w);
     }
     if (x.tid < 16 && l0.has_bias && J0 + x.tid < l0.N) {
       float* bt = smem + l0.l_b;
-      bt[x.tid] = upd<SGD0>(a, x, os, l0.p_off + (long long)l0.K * l0.N + J0 + x.tid, bt[x.tid],
+      bt[x.tid] = upd<OPK>(a, x, os, l0.p_off + (long long)l0.K * l0.N + J0 + x.tid, bt[x.tid],
                             ld1(x.xs, a.x_b0 + x.tid, sum0));
     }
   }
@@ -1182,7 +1200,7 @@ __device__ __forceinline__ void apply_sums(const DeepArgs& a, float* smem, const
           pi[k] = ly.p_off + (long long)(I0 + 4 * q + k) * ly.N + c;
           ok[k] = I0 + 4 * q + k < ly.K && c < ly.N;
         }
-        opt_pre<SGD0, 4>(a, x, os, pi, ok, pre);
+        opt_pre<OPK, 4>(a, x, os, pi, ok, pre);
         f32x4 g, w;
 #pragma unroll
         for (int k = 0; k < 4; ++k) g[k] = ld1(x.xs, a.x_w[l] + (4 * q + k) * N16 + c, sum0);
@@ -1191,7 +1209,7 @@ __device__ __forceinline__ void apply_sums(const DeepArgs& a, float* smem, const
           const int ip = 4 * q + k;
           float wt = wr[ip * ldr + c];
           if (ok[k]) {
-            wt = upd_p<SGD0>(a, x, os, pi[k], wt, g[k], pre.s0[k], pre.s1[k]);
+            wt = upd_p<OPK>(a, x, os, pi[k], wt, g[k], pre.s0[k], pre.s1[k]);
             wr[ip * ldr + c] = wt;
           }
           w[k] = wt;
@@ -1206,12 +1224,12 @@ __device__ __forceinline__ void apply_sums(const DeepArgs& a, float* smem, const
     if (l < L - 1) {
       if (x.j < ly.T && ly.has_bias && x.tid < 16 && 16 * x.j + x.tid < ly.N) {
         float* bt = smem + ly.l_b;
-        bt[x.tid] = upd<SGD0>(a, x, os, ly.p_off + (long long)ly.K * ly.N + 16 * x.j + x.tid, bt[x.tid],
+        bt[x.tid] = upd<OPK>(a, x, os, ly.p_off + (long long)ly.K * ly.N + 16 * x.j + x.tid, bt[x.tid],
                               ld1(x.xs, a.x_b[l] + x.tid, sum0));
       }
     } else if (x.j == 0 && ly.has_bias && x.tid < ly.N) {
       float* bl = smem + ly.l_b;
-      const float b = upd<SGD0>(a, x, os, ly.p_off + (long long)ly.K * ly.N + x.tid, bl[x.tid],
+      const float b = upd<OPK>(a, x, os, ly.p_off + (long long)ly.K * ly.N + x.tid, bl[x.tid],
                                 ld1(x.xs, a.x_b[l] + x.tid, sum0));
       bl[x.tid] = b;
       st1(x.rs, x.tid, a.o_bl, b);
@@ -1221,7 +1239,7 @@ __device__ __forceinline__ void apply_sums(const DeepArgs& a, float* smem, const
 
 // partial tile out -> all replicas' tiles out -> slice r summed in replica order -> all
 // slices summed -> the update
-template <int L, bool SGD0>
+template <int L, int OPK>
 __device__ __forceinline__ bool exchange(const DeepArgs& a, float* smem, const Ctx& x0, int s, const OptStep& os) {
   const Ctx x = lanes(x0);
   const unsigned tag = (unsigned)s + 1;
@@ -1239,7 +1257,7 @@ __device__ __forceinline__ bool exchange(const DeepArgs& a, float* smem, const C
   publish_x(a, x, 3, tag);
   if (!wait_x(a, x.j, 3, tag)) return false;
   dstamp(a, s, 26);
-  apply_sums<L, SGD0>(a, smem, x, sum0, os);
+  apply_sums<L, OPK>(a, smem, x, sum0, os);
   __syncthreads();
   dstamp(a, s, 27);
   return true;
@@ -1247,7 +1265,7 @@ __device__ __forceinline__ bool exchange(const DeepArgs& a, float* smem, const C
 
 }  // namespace
 
-template <int L, bool FAST, bool SGD0, bool SYNC>
+template <int L, bool FAST, int OPK, bool SYNC>
 __global__ __launch_bounds__(512) void mlp_deep_kernel(DeepArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   if (__hip_atomic_load((gu32*)(a.err), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) return;
@@ -1366,11 +1384,11 @@ __global__ __launch_bounds__(512) void mlp_deep_kernel(DeepArgs a) {
     if (!SYNC && last >= 0) {
       if constexpr (L == 2) {
         if (!wait_phase(a, x.r, base)) return;
-        dw_last<L, SGD0, false>(a, smem, x, lastos);
+        dw_last<L, OPK, false>(a, smem, x, lastos);
         load_dz0(a, smem, x);
       }
       __syncthreads();
-      dw0_phase<L, SGD0, false>(a, smem, x, last, lastos);
+      dw0_phase<L, OPK, false>(a, smem, x, last, lastos);
     }
     __syncthreads();
     dstamp(a, s, 1);
@@ -1386,17 +1404,17 @@ __global__ __launch_bounds__(512) void mlp_deep_kernel(DeepArgs a) {
     tail_phase<L, FAST>(a, smem, x, s, valid);
     publish(a, x.r, x.j, base + L);
     dstamp(a, s, 10);
-    if (!bw_chain<L, L - 2, SGD0, SYNC>(a, smem, x, s, os, base, G)) return;
+    if (!bw_chain<L, L - 2, OPK, SYNC>(a, smem, x, s, os, base, G)) return;
     if constexpr (SYNC) {   // every gradient of the step into the exchange tile, then the exchange
       if constexpr (L == 2) {
         if (!wait_phase(a, x.r, base + NPH)) return;
-        dw_last<L, SGD0, true>(a, smem, x, os);
+        dw_last<L, OPK, true>(a, smem, x, os);
         load_dz0(a, smem, x);
       }
       __syncthreads();
-      dw0_phase<L, SGD0, true>(a, smem, x, s, os);
+      dw0_phase<L, OPK, true>(a, smem, x, s, os);
       dstamp(a, s, 24);
-      if (!exchange<L, SGD0>(a, smem, x, s, os)) return;
+      if (!exchange<L, OPK>(a, smem, x, s, os)) return;
     }
     last = s;
     lastos = os;
@@ -1405,11 +1423,11 @@ __global__ __launch_bounds__(512) void mlp_deep_kernel(DeepArgs a) {
   if (!SYNC && last >= 0) {
     if constexpr (L == 2) {
       if (!wait_phase(a, x.r, (unsigned)(last + 1) * NPH + 1)) return;
-      dw_last<L, SGD0, false>(a, smem, x, lastos);
+      dw_last<L, OPK, false>(a, smem, x, lastos);
       load_dz0(a, smem, x);
     }
     __syncthreads();
-    dw0_phase<L, SGD0, false>(a, smem, x, last, lastos);
+    dw0_phase<L, OPK, false>(a, smem, x, last, lastos);
   }
   __syncthreads();
   // ---- epilogue: the owned masters back to P
@@ -1451,7 +1469,7 @@ namespace {
 // -- counts against the same 160 KB, so the device maximum itself is refused).  The check and
 // the raise happen under one lock, so the attribute only ever grows and no thread launches
 // a layout larger than what its device was raised to.
-template <int L, bool F, bool SG, bool SY>
+template <int L, bool F, int OK, bool SY>
 hipError_t deep_launch_one(const DeepArgs* a, hipStream_t s) {
   static std::mutex mu;
   static int set_bytes[DP_MAX_DEVICES] = {};
@@ -1463,27 +1481,32 @@ hipError_t deep_launch_one(const DeepArgs* a, hipStream_t s) {
   {
     std::lock_guard<std::mutex> g(mu);
     if (need > set_bytes[dev]) {
-      e = hipFuncSetAttribute(reinterpret_cast<const void*>(&mlp_deep_kernel<L, F, SG, SY>),
+      e = hipFuncSetAttribute(reinterpret_cast<const void*>(&mlp_deep_kernel<L, F, OK, SY>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, need);
       if (e != hipSuccess) return e;
       set_bytes[dev] = need;
     }
   }
-  hipLaunchKernelGGL((mlp_deep_kernel<L, F, SG, SY>), dim3(a->R * a->nw), dim3(NTH), (size_t)need, s, *a);
+  hipLaunchKernelGGL((mlp_deep_kernel<L, F, OK, SY>), dim3(a->R * a->nw), dim3(NTH), (size_t)need, s, *a);
   return hipGetLastError();
 }
 
-template <int L, bool SY>
-hipError_t deep_launch_sy(const DeepArgs* a, bool fast, bool sgd0, hipStream_t s) {
-  if (fast && sgd0) return deep_launch_one<L, true, true, SY>(a, s);
-  if (fast) return deep_launch_one<L, true, false, SY>(a, s);
-  if (sgd0) return deep_launch_one<L, false, true, SY>(a, s);
-  return deep_launch_one<L, false, false, SY>(a, s);
+template <int L, bool F, bool SY>
+hipError_t deep_launch_f(const DeepArgs* a, int opk, hipStream_t s) {
+  if (opk == OPK_SGD0) return deep_launch_one<L, F, OPK_SGD0, SY>(a, s);
+  if (opk == OPK_ADAM) return deep_launch_one<L, F, OPK_ADAM, SY>(a, s);
+  return deep_launch_one<L, F, OPK_ANY, SY>(a, s);
 }
 
+template <int L, bool SY>
+hipError_t deep_launch_sy(const DeepArgs* a, bool fast, int opk, hipStream_t s) {
+  return fast ? deep_launch_f<L, true, SY>(a, opk, s) : deep_launch_f<L, false, SY>(a, opk, s);
+}
+
+// opk: OPK_SGD0 / OPK_ADAM / OPK_ANY (deep.hip picks it from the optimizer)
 template <int L>
-hipError_t deep_launch(const DeepArgs* a, bool fast, bool sgd0, hipStream_t s) {
-  return a->sync ? deep_launch_sy<L, true>(a, fast, sgd0, s) : deep_launch_sy<L, false>(a, fast, sgd0, s);
+hipError_t deep_launch(const DeepArgs* a, bool fast, int opk, hipStream_t s) {
+  return a->sync ? deep_launch_sy<L, true>(a, fast, opk, s) : deep_launch_sy<L, false>(a, fast, opk, s);
 }
 }  // namespace
 

@@ -1,6 +1,6 @@
 // Instances of the persistent layer-pipeline kernel for 4 Dense layers (deep_impl.h)
 #include "deep_impl.h"
 
-extern "C" hipError_t ea_deep_l4(const ea::DeepArgs* a, int fast, int sgd0, hipStream_t s) {
-  return ea::deep_launch<4>(a, fast != 0, sgd0 != 0, s);
+extern "C" hipError_t ea_deep_l4(const ea::DeepArgs* a, int fast, int opk, hipStream_t s) {
+  return ea::deep_launch<4>(a, fast != 0, opk, s);
 }

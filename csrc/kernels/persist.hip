@@ -52,14 +52,20 @@
 #include "loss_tile.h"
 
 // XCD-local instance (persist_local.hip compiles this file again with EA_PLOCAL = 1): a
-// replica's workgroups all run on ONE XCD (the host picks it only where block b -> XCD b % 8
-// puts them there -- R a multiple of 8 -- and each chain verifies it at launch, below), so
+// replica's workgroups all run on ONE XCD (the dispatch deals blocks round-robin over the 8
+// XCDs, so blocks b and b + 8 share one: the host picks this instance only for R a multiple
+// of 8, after probing that, and each chain verifies it at launch, below), so
 // the intra-replica hand-offs need not leave that XCD's L2: their bytes and flags are stored
 // PLAIN (the line stays in the L2, where the consumers' sc1 loads -- which skip only the
 // CU's L1 -- find it) instead of write-through (sc1 stores drop the line, and the consumer
 // re-reads it at the cross-XCD rate).  tools/micro/xchg_floor.hip: 8-workgroup exchange of
 // 16 KB slabs 3.6 -> 2.6 us, flag round 1.5 -> 1.2 us (profiles/xchg_floor_r6.txt).  The
 // cross-replica (sync exchange) and cross-rank hand-offs stay write-through.
+//
+// Exchange-local instance (persist_xlocal.hip, EA_PLOCAL = 2; per-step sync of 8 replicas on
+// the V1 roles): the other way round -- workgroup q of every replica on ONE XCD (blocks
+// mapped so that the 8 copies of a gradient tile share an XCD), the replica-sum exchange's
+// slabs and flags stored plain, the intra-replica hand-offs (now across XCDs) write-through.
 #ifndef EA_PLOCAL
 #define EA_PLOCAL 0
 #endif
@@ -169,16 +175,18 @@ __device__ __forceinline__ float ldw1(rsrc_t r, int v, int s) {
   return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, v * 4, s * 4, 16));
 }
 // intra-replica hand-off stores: write-through (sc1 = aux 16), or plain in the XCD-local instance
-constexpr int ST_AUX = EA_PLOCAL ? 0 : 16;
+constexpr int ST_AUX = EA_PLOCAL == 1 ? 0 : 16;
 __device__ __forceinline__ void stw1(rsrc_t r, int v, int s, float x) {
   __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, x), r, v * 4, s * 4, ST_AUX);
 }
 __device__ __forceinline__ void stw4(rsrc_t r, int v, int s, f32x4 x) {
   __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, x), r, v * 4, s * 4, ST_AUX);
 }
-// cross-replica hand-off stores (the sync exchange slabs): always write-through
+// cross-replica hand-off stores (the sync exchange slabs): write-through, or plain in the
+// exchange-local instance
+constexpr int SX_AUX = EA_PLOCAL == 2 ? 0 : 16;
 __device__ __forceinline__ void stx4(rsrc_t r, int v, int s, f32x4 x) {
-  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, x), r, v * 4, s * 4, 16);
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, x), r, v * 4, s * 4, SX_AUX);
 }
 
 __device__ __forceinline__ unsigned* flag_at(const PersistArgs& a, int r, int kind) {
@@ -191,13 +199,16 @@ __device__ __forceinline__ unsigned* flag_at(const PersistArgs& a, int r, int ki
 __device__ __forceinline__ void publish_x(unsigned* flag, unsigned tag) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (threadIdx.x == 0) __hip_atomic_store((gu32*)(flag), tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (threadIdx.x == 0) {
+    if constexpr (EA_PLOCAL == 2) __builtin_amdgcn_raw_buffer_store_b32(tag, ws_rsrc(reinterpret_cast<float*>(flag)), 0, 0, 0);
+    else __hip_atomic_store((gu32*)(flag), tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 __device__ __forceinline__ void publish(unsigned* flag, unsigned tag) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
-    if constexpr (EA_PLOCAL) __builtin_amdgcn_raw_buffer_store_b32(tag, ws_rsrc(reinterpret_cast<float*>(flag)), 0, 0, 0);
+    if constexpr (EA_PLOCAL == 1) __builtin_amdgcn_raw_buffer_store_b32(tag, ws_rsrc(reinterpret_cast<float*>(flag)), 0, 0, 0);
     else __hip_atomic_store((gu32*)(flag), tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
@@ -300,13 +311,14 @@ __device__ __forceinline__ bool wait_sets(const PersistArgs& a, const WaitSet (&
 // residency: wave 0 polls the GO flag of every workgroup of the grid (R replicas x wgs)
 // until all are raised.  A workgroup that is not resident never raises
 // it, so the waiting ones time out (PERR_GRID) before any of them modified state.
-// XCD-local instance: a GO flag carries its workgroup's XCD + 1, and a replica r whose
-// workgroups do not all share this workgroup's XCD gives up (PERR_PLACE), state intact.
+// XCD-local instances: a GO flag carries its workgroup's XCD + 1, and a workgroup whose L2
+// partners (EA_PLOCAL 1: its replica; 2: the copies of its tile q in the other replicas) do
+// not all share its XCD gives up (PERR_PLACE), state intact.
 __device__ __forceinline__ unsigned xcc_id() {
   return __builtin_amdgcn_s_getreg((20) | (0 << 6) | ((4 - 1) << 11));   // HW_REG_XCC_ID[3:0]
 }
 __device__ __forceinline__ unsigned go_value() { return EA_PLOCAL ? xcc_id() + 1u : 1u; }
-__device__ __forceinline__ bool wait_grid(const PersistArgs& a, int r) {
+__device__ __forceinline__ bool wait_grid(const PersistArgs& a, int r, int q) {
   int ok = 1;
   if (threadIdx.x < 64) {
     const int lane = threadIdx.x, tot = a.R * a.wgs;
@@ -319,7 +331,8 @@ __device__ __forceinline__ bool wait_grid(const PersistArgs& a, int r) {
         const unsigned v = __hip_atomic_load((gu32*)(flag_at(a, rr, PMF_GO) + qq), __ATOMIC_RELAXED,
                                              __HIP_MEMORY_SCOPE_AGENT);
         all &= v != 0u;
-        away |= EA_PLOCAL && rr == r && v != 0u && v != mine;
+        // the workgroups this one hands off to through the L2: its replica (1) / its tile's copies (2)
+        away |= EA_PLOCAL != 0 && (EA_PLOCAL == 1 ? rr == r : qq == q) && v != 0u && v != mine;
       }
       if (__all(all)) {
         if (__any(away)) {
@@ -1575,7 +1588,7 @@ __device__ __forceinline__ void chain_role(const PersistArgs& a, float* smem, in
   __syncthreads();
   // every workgroup of the grid resident before any state (metric sums, hand-offs that
   // lead to weight updates) is touched: otherwise give up with PERR_GRID, state intact
-  if (!wait_grid(a, r)) return;
+  if (!wait_grid(a, r, a.nk0 * a.nc0 + j)) return;   // this chain is workgroup nl0 + j of its replica
 
   const int n = a.nsteps;
   // V2: this chain's rows of step s's Gram slabs (X_s . X_{s-1}^T, one per k-chunk)
@@ -2576,7 +2589,13 @@ __global__ __launch_bounds__(256) void mlp_persist_kernel(PersistArgs a) {
   __shared__ __attribute__((aligned(16))) float smem[LDS_FLOATS];
   if (__hip_atomic_load((gu32*)(a.err), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) return;
   const int b = blockIdx.x;
+#if EA_PLOCAL == 2
+  // blocks b and b + 8 share an XCD: block b -> replica (b / 8) % 8, workgroup
+  // b % 8 + 8 ((b / 8) / 8) -- the 8 copies of workgroup q on one XCD (host: R = 8, wgs % 8 == 0)
+  const int r = (b >> 3) & 7, q = (b & 7) + 8 * (b >> 6);
+#else
   const int r = b % a.R, q = b / a.R;
+#endif
   // residency: raise this workgroup's GO flag (the chain workgroups wait for the grid)
   if (threadIdx.x == 0) __hip_atomic_store((gu32*)(flag_at(a, r, PMF_GO) + q), go_value(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const int nl0 = a.nk0 * a.nc0;
@@ -2608,6 +2627,14 @@ hipError_t persist_launch(const PersistArgs* a, hipStream_t s) {
   const bool relu = a->act0 == ACT_RELU && a->act1 == ACT_RELU;
   const bool sgd = !a->S || (a->op.opt == OPT_SGD && a->op.mom == 0.f);
   const dim3 grid(a->R * a->wgs);
+#if EA_PLOCAL == 2
+  // the exchange-local instance: V1 roles, per-step sync (the host picks it for nothing else)
+  if (a->v2 || a->ps_mode) return hipErrorInvalidValue;
+  if (fast && relu && sgd) hipLaunchKernelGGL((mlp_persist_kernel<H0, H1, true, 0, true, false>), grid, dim3(256), 0, s, *a);
+  else if (fast) hipLaunchKernelGGL((mlp_persist_kernel<H0, H1, true, -1, false, false>), grid, dim3(256), 0, s, *a);
+  else hipLaunchKernelGGL((mlp_persist_kernel<H0, H1, false, -1, false, false>), grid, dim3(256), 0, s, *a);
+  return hipGetLastError();
+#endif
   if (a->v2 && a->bf16) {   // mixed_bfloat16: bf16 shard, bf16-rounded MFMA operands, fp32 masters
     if (fast) hipLaunchKernelGGL((mlp_persist_kernel<H0, H1, true, 0, true, true, false, true>), grid, dim3(256), 0, s, *a);
     else hipLaunchKernelGGL((mlp_persist_kernel<H0, H1, false, 0, true, true, false, true>), grid, dim3(256), 0, s, *a);
@@ -2632,8 +2659,10 @@ hipError_t persist_launch(const PersistArgs* a, hipStream_t s) {
 
 using namespace ea;
 
-#if EA_PLOCAL
+#if EA_PLOCAL == 1
 #define EA_PERSIST_ENTRY ea_persist_local
+#elif EA_PLOCAL == 2
+#define EA_PERSIST_ENTRY ea_persist_xlocal
 #else
 #define EA_PERSIST_ENTRY ea_persist
 extern "C" int ea_persist_lds_bytes() { return (int)(LDS_FLOATS * sizeof(float)); }
@@ -2651,7 +2680,7 @@ extern "C" hipError_t EA_PERSIST_ENTRY(const PersistArgs* a, hipStream_t s) {
 
 #if !EA_PLOCAL
 // placement probe: block b stores the XCD it runs on; the host enables the XCD-local
-// instance only where the dispatch puts block b on XCD b % 8 for the whole grid
+// instance only where blocks b and b + 8 share an XCD across the whole grid
 __global__ void xcc_probe_kernel(unsigned* out) {
   if (threadIdx.x == 0) out[blockIdx.x] = ea::xcc_id();
 }

@@ -23,6 +23,7 @@ extern "C" hipError_t ea_persist_post(unsigned* flags, int nflags, long long* ct
                                       const unsigned* err, hipStream_t s);
 extern "C" hipError_t ea_persist(const ea::PersistArgs* a, hipStream_t s);
 extern "C" hipError_t ea_persist_local(const ea::PersistArgs* a, hipStream_t s);
+extern "C" hipError_t ea_persist_xlocal(const ea::PersistArgs* a, hipStream_t s);
 extern "C" hipError_t ea_xcc_probe(int nblocks, unsigned* out, hipStream_t s);
 extern "C" int ea_persist_lds_bytes();
 extern "C" hipError_t ea_deep(const ea::DeepArgs* a, hipStream_t s);
@@ -73,8 +74,8 @@ Executor::~Executor() {
 // Persistent plan (persist.hip): 3 Dense layers, hidden widths 64 or 128, a last layer
 // of <= 16 units, fp32, B <= 64, and a grid of at most one workgroup per CU (every
 // workgroup must be resident: they wait for each other inside the launch).
-// Does the dispatch put block b of an n-block grid on XCD b % 8 (the XCD-local persistent
-// instance's assumption, persist.hip EA_PLOCAL)?  Probed once per device and grid size with
+// Does the dispatch put blocks b and b + 8 of an n-block grid on one XCD (the XCD-local
+// persistent instance's assumption, persist.hip EA_PLOCAL)?  Probed once per device and grid size with
 // a tiny kernel reading HW_REG_XCC_ID; the kernel re-checks it at every launch (PERR_PLACE).
 static bool xcd_round_robin(int dev, int n) {
   static std::mutex mu;
@@ -89,7 +90,12 @@ static bool xcd_round_robin(int dev, int n) {
   ok = ok && ea_xcc_probe(n, d, nullptr) == hipSuccess && hipDeviceSynchronize() == hipSuccess &&
        hipMemcpy(h.data(), d, sizeof(unsigned) * (size_t)n, hipMemcpyDeviceToHost) == hipSuccess;
   if (d) (void)hipFree(d);
-  for (int b = 0; ok && b < n; ++b) ok = h[b] == (unsigned)(b % 8);
+  // the dispatch deals blocks round-robin over the 8 XCDs, starting wherever the previous
+  // dispatch stopped (tools/micro/xcc_map.hip: block 0 on XCD 6 after other launches): the
+  // premise is that blocks b and b + 8 share an XCD, and the 8 residues use 8 XCDs
+  for (int b = 0; ok && b < n; ++b) ok = h[b] == h[b % 8];
+  for (int i = 0; ok && i < 8 && i < n; ++i)
+    for (int k = 0; k < i; ++k) ok = ok && h[i] != h[k];
   seen[key] = ok;
   return ok;
 }
@@ -173,9 +179,16 @@ bool Executor::build_persist() {
   }
   a.wgs = a.nk0 * a.nc0 + nch + nd_use;
   a.sync = c_.persist_sync ? 1 : 0;
-  // XCD-local instance: block b serves replica b % R, so with R a multiple of 8 every
-  // replica's cluster sits on one XCD -- if the dispatch is round-robin over the XCDs
-  pm_.local = c_.persist_local != 0 && c_.R % 8 == 0 && xcd_round_robin(dev, c_.R * a.wgs);
+  // XCD-local instances (persist.hip EA_PLOCAL), where the dispatch deals blocks round-robin
+  // over the XCDs: fit -- block b serves replica b % R, so with R a multiple of 8 every
+  // replica's cluster sits on one XCD (intra-replica hand-offs in its L2); per-step sync of 8
+  // replicas on the V1 roles -- the 8 copies of each workgroup on one XCD (the exchange in
+  // its L2).  The PS hook's in-launch exchange keeps the write-through instance.
+  pm_.local = 0;
+  if (c_.persist_local != 0 && xcd_round_robin(dev, c_.R * a.wgs)) {
+    if (!a.sync && c_.R % 8 == 0) pm_.local = 1;
+    else if (a.sync && !v2 && c_.R == 8 && a.wgs % 8 == 0) pm_.local = 2;
+  }
   const char* xrs = std::getenv("ELEPHAS_AMD_XCHG_RS");   // A/B: reduce-scatter exchange of the replicas
   a.xchg_rs = (xrs && std::atoi(xrs) != 0) ? 1 : 0;
   a.bf16 = c_.bf16 ? 1 : 0;
@@ -430,7 +443,7 @@ std::vector<unsigned> Executor::rank_exchange_selftest(int nsteps, int corrupt) 
 std::vector<int> Executor::persist_variant() const {
   if (dp_.on) return {3, 0, dp_.args.sync, 0};
   if (!pm_.on) return {};
-  return {pm_.args.v2 ? 2 : 1, pm_.args.nd, pm_.args.sync, pm_.local ? 1 : 0};
+  return {pm_.args.v2 ? 2 : 1, pm_.args.nd, pm_.args.sync, pm_.local};
 }
 
 unsigned Executor::persist_error() const {
@@ -469,7 +482,8 @@ void Executor::run_chunk(hipStream_t s, int nsteps) const {
       a.xr_tag0 = pm_.xr_steps;
       pm_.xr_steps += (unsigned)nsteps;
     }
-    check(pm_.local ? ea_persist_local(&a, s) : ea_persist(&a, s), "persistent step kernel");
+    check(pm_.local == 1 ? ea_persist_local(&a, s) : pm_.local == 2 ? ea_persist_xlocal(&a, s) : ea_persist(&a, s),
+          "persistent step kernel");
     check(ea_persist_post(d_pflags_, (int)(pm_.flag_bytes / sizeof(unsigned)), reinterpret_cast<long long*>(c_.ctr),
                           reinterpret_cast<const int*>(c_.ntrain), c_.R, c_.B, nsteps, d_perr_, s),
           "persistent chunk post");

@@ -207,7 +207,7 @@ class Executor {
     PersistArgs args{};
     size_t flag_bytes = 0;
     mutable unsigned xr_steps = 0;   // steps run with the rank exchange (its flag tags)
-    bool local = false;              // the XCD-local instance (ea_persist_local)
+    int local = 0;                   // 1: XCD-local instance (ea_persist_local), 2: exchange-local (ea_persist_xlocal)
   } pm_;
   float* d_pws_ = nullptr;         // persistent plan: per-replica exchange workspace
   unsigned* d_pflags_ = nullptr;   // [R][PMF_N][PM_MAXWG] flags (zero at every launch: setup, then the post kernel)

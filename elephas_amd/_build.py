@@ -31,6 +31,7 @@ SOURCES = [
     "kernels/rowchain.hip",
     "kernels/persist.hip",
     "kernels/persist_local.hip",
+    "kernels/persist_xlocal.hip",
     "kernels/deep.hip",
     "kernels/deep_l2.hip",
     "kernels/deep_l3.hip",

@@ -1187,7 +1187,7 @@ class NativeTrainer(TrainerBase):
             var, nd, sync, local = self.exe.persist_variant()[:4]
             dw = f" + {nd} weight-gradient workgroups" if var == 2 else ""
             sy = ", per-step gradient exchange of the replicas inside the launch" if sync else ""
-            sy += ", XCD-local hand-offs" if local else ""
+            sy += {1: ", XCD-local hand-offs", 2: ", replica exchange in the XCD's L2"}.get(local, "")
             return (f"persistent V{var}{sy} (1 kernel + 1 post kernel per <= {self.GRAPH_CHUNK}-step chunk; per "
                     f"replica {nk0}x{nc0} layer-0 tiles of {kc0}x{cw} + {nch} row-chain workgroups{dw}; "
                     f"grid {grid})")

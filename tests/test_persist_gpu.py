@@ -491,7 +491,9 @@ def test_persist_xcd_local_instance_is_bit_exact(monkeypatch, case):
     """The XCD-local instance (persist_local.hip: intra-replica hand-offs stored plain and
     read from the XCD's L2, the replica's cluster checked to sit on one XCD at launch) is
     picked for 8 replicas and trains bit for bit as the write-through instance: V2 fit
-    (the headline), V1 with momentum, V1 per-step sync (whose exchange stays write-through)."""
+    (the headline), V1 with momentum; and the exchange-local instance (persist_xlocal.hip:
+    the 8 copies of each workgroup on one XCD, the replica-sum exchange in its L2) for V1
+    per-step sync."""
     from elephas_amd.models import initializers
     from elephas_amd.models.optimizers import SGD
     from elephas_amd.ops.plan import build_plan
@@ -512,7 +514,7 @@ def test_persist_xcd_local_instance_is_bit_exact(monkeypatch, case):
                           sync=case == "v1_sync")
         var = t.exe.persist_variant()
         assert t.persistent and var[0] == (2 if case == "v2_fit" else 1), t.plan_name()
-        assert var[3] == (1 if local == "-1" else 0), (local, var)
+        assert var[3] == ((2 if case == "v1_sync" else 1) if local == "-1" else 0), (local, var)
         t.set_data(xs, ys, 0.1 if case != "v1_sync" else 0.0, shuffle=case != "v1_sync")
         torch.manual_seed(3)
         h = t.fit(2)
