@@ -23,7 +23,7 @@ Any step may carry a tag and environment overrides in front of it:
   e.g.  sync_rs/ELEPHAS_AMD_XCHG_RS=1@py:persist_stamps.py:8,64,8,-1,float32,sync
 
 (output in gpurun_out/TAG.txt).  The profiles under profiles/ name the step that produced
-them (profiles/README.md); tools/sessions/ keeps the earlier one-file session scripts that
+them (profiles/README.md); tools/archive/sessions/ keeps the earlier one-file session scripts that
 produced the older ones.
 """
 from __future__ import annotations
