@@ -330,6 +330,20 @@ struct DeepArgs {
   int sync, XT, x_b0;
   int x_w[DP_MAXL], x_b[DP_MAXL];
   float* xg;
+  // per-step sync across ranks (xr_world > 1): after the replica reduce-scatter, replica r's
+  // slice of workgroup j's summed tile goes through every rank's peer-mapped buffer
+  // (peer_args.h): data [2 parities][nw][XT] floats at PEER_DATA_OFF, flag (j * R + r) at
+  // PEER_FLAG_OFF + 64 (j R + r); tags xr_tag0 + step + 1 (monotonic over the trainer's life)
+  char* xr_base[PEER_MAX_RANKS];
+  int xr_world, xr_rank;
+  unsigned xr_tag0;
+  long long xr_timeout;
+  // in-launch parameter-server hook (ps_mode 1 hogwild / 2 asynchronous; the kernel then runs
+  // its gradient tiles through xg as in sync, without the replica sum): after each step's
+  // update every workgroup pushes theta_new - theta_old of the parameters it owns and pulls
+  // them for the next step (slice j of the server's per-slice counters)
+  int ps_mode;
+  PsArgs ps;
   unsigned* err;                    // sticky error word (PmErr codes)
   long long timeout;                // spin limit in s_memrealtime ticks
   long long* stamps;                // diagnostics: [block][DP_STAMP_STEPS][32] s_memrealtime (null = off)

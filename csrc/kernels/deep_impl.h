@@ -1149,10 +1149,189 @@ __device__ __forceinline__ bool wait_x(const DeepArgs& a, int j, int kind, unsig
   return ok != 0;
 }
 
+// ---- rank exchange (xr_world > 1; layout args.h DeepArgs, peer_args.h): rank k's buffer by
+//      selects against the uniform bases (no per-lane indexing of the kernel arguments)
+__device__ __forceinline__ char* xr_base_of(const DeepArgs& a, int k) {
+  char* b = a.xr_base[0];
+#pragma unroll
+  for (int kk = 1; kk < PEER_MAX_RANKS; ++kk) b = (k == kk) ? a.xr_base[kk] : b;
+  return b;
+}
+// this rank's slot of flag `slot` raised to tag (every storing wave drained first, release at
+// system scope), then wave 0 waits until every rank's flag `slot` reached it (lane k watches
+// rank k; wrap-safe: tags only grow).  false: a rank did not arrive within xr_timeout
+__device__ __forceinline__ bool deep_xrank_wait(const DeepArgs& a, int slot, unsigned tag) {
+  const int tid = threadIdx.x;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0)
+    __hip_atomic_store(reinterpret_cast<unsigned*>(xr_base_of(a, a.xr_rank) + PEER_FLAG_OFF + (long long)slot * 64), tag,
+                       __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  int ok = 1;
+  if (tid < 64) {
+    const unsigned* fl = reinterpret_cast<const unsigned*>(xr_base_of(a, tid < a.xr_world ? tid : 0) + PEER_FLAG_OFF +
+                                                           (long long)slot * 64);
+    const unsigned long long t0 = wall_clock64();
+    for (;;) {
+      const unsigned f = tid < a.xr_world ? __hip_atomic_load(const_cast<unsigned*>(fl), __ATOMIC_ACQUIRE,
+                                                              __HIP_MEMORY_SCOPE_SYSTEM)
+                                          : tag;
+      if (__all((int)(f - tag) >= 0)) break;
+      if ((long long)(wall_clock64() - t0) > a.xr_timeout) {
+        ok = 0;
+        if (tid == 0) __hip_atomic_store((gu32*)(a.err), (unsigned)PERR_XRANK, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  ok = __syncthreads_and(ok);
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  return ok != 0;
+}
+
+// ---- parameter-server hook (ps_mode; server layout peer_args.h PsArgs, kernels peer.hip):
+//      theta element i lives in the shard of the rank owning its chunk, in uncached memory
+__device__ __forceinline__ float* dps_elem(const PsArgs& ps, long long i) {
+  char* b = ps.base[0];
+#pragma unroll
+  for (int rr = 1; rr < PEER_MAX_RANKS; ++rr) b = (rr < ps.world && i >= ps.shard_begin[rr]) ? ps.base[rr] : b;
+  return reinterpret_cast<float*>(b + PEER_DATA_OFF) + i;
+}
+__device__ __forceinline__ unsigned* dps_ctr(const PsArgs& ps, int slice, int which) {
+  return reinterpret_cast<unsigned*>(ps.base[0] + PEER_FLAG_OFF + (long long)which * PEER_MAX_BLOCKS * 64 +
+                                     (long long)slice * 64);
+}
+// push bracket of slice j (asynchronous mode: a puller copies a slice only while no pusher is
+// inside it); hogwild: no bracket
+__device__ __forceinline__ void dps_push_begin(const DeepArgs& a, int slice) {
+  if (a.ps_mode == 2 && threadIdx.x == 0)
+    __hip_atomic_fetch_add(dps_ctr(a.ps, slice, 0), 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_SYSTEM);
+  __syncthreads();
+}
+__device__ __forceinline__ void dps_push_end(const DeepArgs& a, int slice) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (a.ps_mode == 2 && threadIdx.x == 0)
+    __hip_atomic_fetch_add(dps_ctr(a.ps, slice, 1), 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// the masters workgroup j owns -- W_0[:, J] (transposed tile), b_0[J], rows J of W_l (l >= 1),
+// b_l[J] of the hidden layers, the last layer's bias on workgroup 0 -- from src(i) (element i
+// of the flat parameter vector) into LDS
+template <int L, typename Src>
+__device__ __forceinline__ void load_masters(const DeepArgs& a, float* smem, const Ctx& x, Src src) {
+  {
+    const DeepLayer l0 = a.ly[0];
+    if (x.j < l0.T) {
+      const int J0 = 16 * x.j, ld0 = l0.Kx + 4;
+      for (int e = x.tid; e < 16 * l0.K; e += NTH) {
+        const int k = e >> 4, c = e & 15;
+        if (J0 + c < l0.N) smem[l0.l_w + c * ld0 + k] = src(l0.p_off + (long long)k * l0.N + J0 + c);
+      }
+      if (x.tid < 16 && l0.has_bias && J0 + x.tid < l0.N)
+        smem[l0.l_b + x.tid] = src(l0.p_off + (long long)l0.K * l0.N + J0 + x.tid);
+    }
+  }
+#pragma unroll
+  for (int l = 1; l < L; ++l) {
+    const DeepLayer ly = a.ly[l], lp = a.ly[l - 1];
+    const int ldr = ly.N16 + 4;
+    if (x.j < lp.T) {   // rows J of W_l
+      const int I0 = 16 * x.j;
+      for (int e = x.tid; e < 16 * ly.N; e += NTH) {
+        const int ip = e / ly.N, c = e - ip * ly.N;
+        if (I0 + ip < ly.K) smem[ly.l_w + ip * ldr + c] = src(ly.p_off + (long long)(I0 + ip) * ly.N + c);
+      }
+    }
+    if (l < L - 1) {
+      if (x.j < ly.T && x.tid < 16 && ly.has_bias && 16 * x.j + x.tid < ly.N)
+        smem[ly.l_b + x.tid] = src(ly.p_off + (long long)ly.K * ly.N + 16 * x.j + x.tid);
+    } else if (x.j == 0 && ly.has_bias && x.tid < ly.N) {
+      smem[ly.l_b + x.tid] = src(ly.p_off + (long long)ly.K * ly.N + x.tid);
+    }
+  }
+}
+
+// the images the other workgroups read: W_l^T segments [c][J] (l >= 1), the last layer's
+// row-major rows and (workgroup 0) its bias -- from the LDS masters
+template <int L>
+__device__ __forceinline__ void write_images(const DeepArgs& a, float* smem, const Ctx& x) {
+#pragma unroll
+  for (int l = 1; l < L; ++l) {
+    const DeepLayer ly = a.ly[l], lp = a.ly[l - 1];
+    if (x.j >= lp.T) continue;
+    const int ldr = ly.N16 + 4, I0 = 16 * x.j;
+    for (int e = x.tid; e < ly.N16 * 4; e += NTH) {
+      const int c = e >> 2, q = e & 3;
+      f32x4 v;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v[k] = smem[ly.l_w + (4 * q + k) * ldr + c];
+      st4(x.rs, c * ly.Kx + I0 + 4 * q, ly.o_wt, v);
+    }
+    if (l == L - 1) {
+      for (int e = x.tid; e < 16 * ly.N16; e += NTH) {
+        const int ip = e / ly.N16, c = e - ip * ly.N16;
+        st1(x.rs, (I0 + ip) * ly.N16 + c, ly.o_w, smem[ly.l_w + ip * ldr + c]);
+      }
+    }
+  }
+  if (x.j == 0 && x.tid < a.ly[L - 1].N16) st1(x.rs, x.tid, a.o_bl, smem[a.ly[L - 1].l_b + x.tid]);
+}
+
+// the PS pull of slice j into the LDS masters: in asynchronous mode only while no pusher is
+// inside the slice (ended == began before the copy, began unchanged after it), retried
+// otherwise.  false: timed out (PERR_PS)
+template <int L>
+__device__ __forceinline__ bool pull_masters(const DeepArgs& a, float* smem, const Ctx& x) {
+  auto copy = [&]() { load_masters<L>(a, smem, x, [&](long long i) { return *dps_elem(a.ps, i); }); };
+  if (a.ps_mode != 2) {
+    copy();
+    __syncthreads();
+    return true;
+  }
+  unsigned* sh = reinterpret_cast<unsigned*>(smem + a.l_red);   // two words of scratch
+  const unsigned long long t0 = wall_clock64();
+  for (;;) {
+    if (x.tid == 0) {
+      for (;;) {
+        const unsigned e = __hip_atomic_load(dps_ctr(a.ps, x.j, 1), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+        const unsigned b = __hip_atomic_load(dps_ctr(a.ps, x.j, 0), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (b == e || (long long)(wall_clock64() - t0) > a.timeout) { sh[0] = b; break; }
+        __builtin_amdgcn_s_sleep(1);
+      }
+    }
+    __syncthreads();
+    copy();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (x.tid == 0) {
+      const unsigned b2 = __hip_atomic_load(dps_ctr(a.ps, x.j, 0), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+      const bool late = (long long)(wall_clock64() - t0) > a.timeout;
+      sh[1] = b2 == sh[0] ? 1u : (late ? 2u : 0u);
+      if (late && b2 != sh[0])
+        __hip_atomic_store((gu32*)(a.err), (unsigned)PERR_PS, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    const unsigned st = sh[1];
+    __syncthreads();
+    if (st == 1u) return true;
+    if (st == 2u) return false;
+  }
+}
+
 // the summed gradient tile (sum0) applied to the owned masters by every replica alike --
 // the same sums and the same state, so the replicas stay one model bit for bit -- with the
 // images the other workgroups read (W_l^T segments, the last layer's rows and bias)
-template <int L, int OPK>
+// PSM (parameter-server hook): every changed element's delta theta_new - theta_old is added to
+// the server (system-scope atomics), and the images wait for the pull (pull_masters)
+template <bool PSM>
+__device__ __forceinline__ void ps_add(const DeepArgs& a, long long pi, float w_old, float w_new) {
+  if constexpr (PSM) {
+    if (w_new != w_old) __hip_atomic_fetch_add(dps_elem(a.ps, pi), w_new - w_old, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+template <int L, int OPK, bool PSM = false>
 __device__ __forceinline__ void apply_sums(const DeepArgs& a, float* smem, const Ctx& x0, long long sum0,
                                            const OptStep& os) {
   const Ctx x = lanes(x0);
@@ -1175,13 +1354,19 @@ __device__ __forceinline__ void apply_sums(const DeepArgs& a, float* smem, const
       f32x4 w = lds4(w0t + c * ld0 + k);
 #pragma unroll
       for (int ff = 0; ff < 4; ++ff)
-        if (ok[ff]) w[ff] = upd_p<OPK>(a, x, os, pi[ff], w[ff], g[ff], pre.s0[ff], pre.s1[ff]);
+        if (ok[ff]) {
+          const float wn = upd_p<OPK>(a, x, os, pi[ff], w[ff], g[ff], pre.s0[ff], pre.s1[ff]);
+          ps_add<PSM>(a, pi[ff], w[ff], wn);
+          w[ff] = wn;
+        }
       lds4(w0t + c * ld0 + k, w);
     }
     if (x.tid < 16 && l0.has_bias && J0 + x.tid < l0.N) {
       float* bt = smem + l0.l_b;
-      bt[x.tid] = upd<OPK>(a, x, os, l0.p_off + (long long)l0.K * l0.N + J0 + x.tid, bt[x.tid],
-                            ld1(x.xs, a.x_b0 + x.tid, sum0));
+      const long long pb = l0.p_off + (long long)l0.K * l0.N + J0 + x.tid;
+      const float bn = upd<OPK>(a, x, os, pb, bt[x.tid], ld1(x.xs, a.x_b0 + x.tid, sum0));
+      ps_add<PSM>(a, pb, bt[x.tid], bn);
+      bt[x.tid] = bn;
     }
   }
 #pragma unroll
@@ -1209,50 +1394,90 @@ __device__ __forceinline__ void apply_sums(const DeepArgs& a, float* smem, const
           const int ip = 4 * q + k;
           float wt = wr[ip * ldr + c];
           if (ok[k]) {
-            wt = upd_p<OPK>(a, x, os, pi[k], wt, g[k], pre.s0[k], pre.s1[k]);
+            const float wn = upd_p<OPK>(a, x, os, pi[k], wt, g[k], pre.s0[k], pre.s1[k]);
+            ps_add<PSM>(a, pi[k], wt, wn);
+            wt = wn;
             wr[ip * ldr + c] = wt;
           }
           w[k] = wt;
         }
-        st4(x.rs, c * ly.Kx + I0 + 4 * q, ly.o_wt, w);
-        if (l == L - 1) {
+        if constexpr (!PSM) {
+          st4(x.rs, c * ly.Kx + I0 + 4 * q, ly.o_wt, w);
+          if (l == L - 1) {
 #pragma unroll
-          for (int k = 0; k < 4; ++k) st1(x.rs, (I0 + 4 * q + k) * N16 + c, ly.o_w, w[k]);
+            for (int k = 0; k < 4; ++k) st1(x.rs, (I0 + 4 * q + k) * N16 + c, ly.o_w, w[k]);
+          }
         }
       }
     }
     if (l < L - 1) {
       if (x.j < ly.T && ly.has_bias && x.tid < 16 && 16 * x.j + x.tid < ly.N) {
         float* bt = smem + ly.l_b;
-        bt[x.tid] = upd<OPK>(a, x, os, ly.p_off + (long long)ly.K * ly.N + 16 * x.j + x.tid, bt[x.tid],
-                              ld1(x.xs, a.x_b[l] + x.tid, sum0));
+        const long long pb = ly.p_off + (long long)ly.K * ly.N + 16 * x.j + x.tid;
+        const float bn = upd<OPK>(a, x, os, pb, bt[x.tid], ld1(x.xs, a.x_b[l] + x.tid, sum0));
+        ps_add<PSM>(a, pb, bt[x.tid], bn);
+        bt[x.tid] = bn;
       }
     } else if (x.j == 0 && ly.has_bias && x.tid < ly.N) {
       float* bl = smem + ly.l_b;
-      const float b = upd<OPK>(a, x, os, ly.p_off + (long long)ly.K * ly.N + x.tid, bl[x.tid],
-                                ld1(x.xs, a.x_b[l] + x.tid, sum0));
+      const long long pb = ly.p_off + (long long)ly.K * ly.N + x.tid;
+      const float b = upd<OPK>(a, x, os, pb, bl[x.tid], ld1(x.xs, a.x_b[l] + x.tid, sum0));
+      ps_add<PSM>(a, pb, bl[x.tid], b);
       bl[x.tid] = b;
-      st1(x.rs, x.tid, a.o_bl, b);
+      if constexpr (!PSM) st1(x.rs, x.tid, a.o_bl, b);
     }
   }
 }
 
-// partial tile out -> all replicas' tiles out -> slice r summed in replica order -> all
-// slices summed -> the update
+// partial tile out -> all replicas' tiles out -> slice r summed in replica order (-> with the
+// rank exchange: summed over the ranks in rank order, deep_xrank) -> all slices summed -> the
+// update.  Parameter-server hook (ps_mode): no replica sum -- this workgroup's own tile
+// updates its masters, the deltas go to the server, the masters come back from it.
 template <int L, int OPK>
 __device__ __forceinline__ bool exchange(const DeepArgs& a, float* smem, const Ctx& x0, int s, const OptStep& os) {
   const Ctx x = lanes(x0);
   const unsigned tag = (unsigned)s + 1;
+  if (a.ps_mode) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the tile's stores are out before any wave reads it
+    __syncthreads();
+    dps_push_begin(a, x.j);
+    apply_sums<L, OPK, true>(a, smem, x, x.xp, os);
+    dps_push_end(a, x.j);
+    if (!pull_masters<L>(a, smem, x)) return false;
+    write_images<L>(a, smem, x);
+    __syncthreads();
+    return true;
+  }
   publish_x(a, x, 2, tag);
   if (!wait_x(a, x.j, 2, tag)) return false;
   dstamp(a, s, 25);
   const long long sum0 = ((long long)a.R * a.nw + x.j) * a.XT;
   const int q4 = a.XT >> 2, per = (q4 + a.R - 1) / a.R;
-  const int e1 = (x.r + 1) * per < q4 ? (x.r + 1) * per : q4;
-  for (int e = x.r * per + x.tid; e < e1; e += NTH) {
-    f32x4 v = z4();
-    for (int rr = 0; rr < a.R; ++rr) v += ld4(x.xs, 4 * e, ((long long)rr * a.nw + x.j) * a.XT);
-    st4(x.xs, 4 * e, sum0, v);
+  const int e0 = x.r * per, e1 = (x.r + 1) * per < q4 ? (x.r + 1) * per : q4;
+  if (a.xr_world <= 1) {
+    for (int e = e0 + x.tid; e < e1; e += NTH) {
+      f32x4 v = z4();
+      for (int rr = 0; rr < a.R; ++rr) v += ld4(x.xs, 4 * e, ((long long)rr * a.nw + x.j) * a.XT);
+      st4(x.xs, 4 * e, sum0, v);
+    }
+  } else {
+    // the rank's sum of slice r into this rank's peer slot, then every rank's slot summed in
+    // rank order -- the same bits on every rank
+    const unsigned xt = a.xr_tag0 + tag;
+    const long long slot = (((long long)(xt & 1u) * a.nw + x.j) * a.XT) * 4;   // bytes past PEER_DATA_OFF
+    f32x4* mine = reinterpret_cast<f32x4*>(xr_base_of(a, a.xr_rank) + PEER_DATA_OFF + slot);
+    for (int e = e0 + x.tid; e < e1; e += NTH) {
+      f32x4 v = z4();
+      for (int rr = 0; rr < a.R; ++rr) v += ld4(x.xs, 4 * e, ((long long)rr * a.nw + x.j) * a.XT);
+      mine[e] = v;
+    }
+    if (!deep_xrank_wait(a, x.j * a.R + x.r, xt)) return false;
+    for (int e = e0 + x.tid; e < e1; e += NTH) {
+      f32x4 v = z4();
+      for (int k = 0; k < a.xr_world; ++k)
+        v += __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(xr_base_of(a, k) + PEER_DATA_OFF + slot) + e);
+      st4(x.xs, 4 * e, sum0, v);
+    }
   }
   publish_x(a, x, 3, tag);
   if (!wait_x(a, x.j, 3, tag)) return false;
@@ -1286,63 +1511,14 @@ __global__ __launch_bounds__(512) void mlp_deep_kernel(DeepArgs a) {
   if (x.tid == 0)
     __hip_atomic_store((gu32*)(dflag(a, x.r, 0) + x.j), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 
-  // ---- prologue: the owned masters from P into LDS (zero past the true widths)
+  // ---- prologue: the owned masters from P into LDS (zero past the true widths), then the
+  // images the other workgroups read
   for (int e = x.tid; e < a.lds_floats; e += NTH) smem[e] = 0.f;
   __syncthreads();
   const int Bp = a.Bp;
-  {
-    const DeepLayer l0 = a.ly[0];
-    if (x.j < l0.T) {
-      const int J0 = 16 * x.j, ld0 = l0.Kx + 4;
-      for (int e = x.tid; e < 16 * l0.K; e += NTH) {
-        const int k = e >> 4, c = e & 15;
-        if (J0 + c < l0.N) smem[l0.l_w + c * ld0 + k] = x.P[l0.p_off + (long long)k * l0.N + J0 + c];
-      }
-      if (x.tid < 16 && l0.has_bias && J0 + x.tid < l0.N)
-        smem[l0.l_b + x.tid] = x.P[l0.p_off + (long long)l0.K * l0.N + J0 + x.tid];
-    }
-  }
-#pragma unroll
-  for (int l = 1; l < L; ++l) {
-    const DeepLayer ly = a.ly[l], lp = a.ly[l - 1];
-    const int ldr = ly.N16 + 4;
-    if (x.j < lp.T) {   // rows J of W_l
-      const int I0 = 16 * x.j;
-      for (int e = x.tid; e < 16 * ly.N; e += NTH) {
-        const int ip = e / ly.N, c = e - ip * ly.N;
-        if (I0 + ip < ly.K) smem[ly.l_w + ip * ldr + c] = x.P[ly.p_off + (long long)(I0 + ip) * ly.N + c];
-      }
-    }
-    if (l < L - 1) {
-      if (x.j < ly.T && x.tid < 16 && ly.has_bias && 16 * x.j + x.tid < ly.N)
-        smem[ly.l_b + x.tid] = x.P[ly.p_off + (long long)ly.K * ly.N + 16 * x.j + x.tid];
-    } else if (x.j == 0 && ly.has_bias && x.tid < ly.N) {
-      smem[ly.l_b + x.tid] = x.P[ly.p_off + (long long)ly.K * ly.N + x.tid];
-    }
-  }
+  load_masters<L>(a, smem, x, [&](long long i) { return x.P[i]; });
   __syncthreads();
-  // the images the other workgroups read: W_l^T segments [c][J] (l >= 1), the last layer's
-  // row-major rows and (workgroup 0) its bias
-#pragma unroll
-  for (int l = 1; l < L; ++l) {
-    const DeepLayer ly = a.ly[l], lp = a.ly[l - 1];
-    if (x.j >= lp.T) continue;
-    const int ldr = ly.N16 + 4, I0 = 16 * x.j;
-    for (int e = x.tid; e < ly.N16 * 4; e += NTH) {
-      const int c = e >> 2, q = e & 3;
-      f32x4 v;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) v[k] = smem[ly.l_w + (4 * q + k) * ldr + c];
-      st4(x.rs, c * ly.Kx + I0 + 4 * q, ly.o_wt, v);
-    }
-    if (l == L - 1) {
-      for (int e = x.tid; e < 16 * ly.N16; e += NTH) {
-        const int ip = e / ly.N16, c = e - ip * ly.N16;
-        st1(x.rs, (I0 + ip) * ly.N16 + c, ly.o_w, smem[ly.l_w + ip * ldr + c]);
-      }
-    }
-  }
-  if (x.j == 0 && x.tid < a.ly[L - 1].N16) st1(x.rs, x.tid, a.o_bl, smem[a.ly[L - 1].l_b + x.tid]);
+  write_images<L>(a, smem, x);
   __syncthreads();
   if (!wait_grid(a)) return;
   // the prologue's image writes are out: tag 1 (step s then publishes s * NPH + 2 ..
@@ -1506,9 +1682,62 @@ hipError_t deep_launch_sy(const DeepArgs* a, bool fast, int opk, hipStream_t s) 
 // opk: OPK_SGD0 / OPK_ADAM / OPK_ANY (deep.hip picks it from the optimizer)
 template <int L>
 hipError_t deep_launch(const DeepArgs* a, bool fast, int opk, hipStream_t s) {
-  return a->sync ? deep_launch_sy<L, true>(a, fast, opk, s) : deep_launch_sy<L, false>(a, fast, opk, s);
+  // per-step sync and the parameter-server hook both run the gradient tiles through xg
+  return (a->sync || a->ps_mode) ? deep_launch_sy<L, true>(a, fast, opk, s) : deep_launch_sy<L, false>(a, fast, opk, s);
 }
+// value of component c of f32x4 element e of replica r's slice of tile j, self-test step i on
+// rank k: small integers, so every partial sum is exact in fp32 whatever the order
+__device__ __forceinline__ float dxr_test_value(int k, int j, int r, int i, int e, int c) {
+  return (float)((k + 1) * ((j % 7) + r + i + 2) + ((4 * e + c) % 11));
+}
+// Numeric self-test of the layer pipeline's rank exchange (deep_xrank_wait + the rank-order
+// sum of exchange()): nsteps exchanges of known integer slices by every workgroup (j, r), with
+// the tags continuing the trainer's sequence; each rank checks every summed element against
+// the exact rank sum.  bad += 1 per workgroup-step with a wrong element, += 1 << 16 per
+// workgroup that timed out.  corrupt != 0 (fault injection): this rank sends a wrong slice.
+__global__ __launch_bounds__(NTH) void deep_xrank_selftest_kernel(DeepArgs a, int nsteps, unsigned* bad, int corrupt) {
+  const int r = blockIdx.x % a.R, j = blockIdx.x / a.R, tid = threadIdx.x;
+  const int q4 = a.XT >> 2, per = (q4 + a.R - 1) / a.R;
+  const int e0 = r * per, e1 = (r + 1) * per < q4 ? (r + 1) * per : q4;
+  for (int i = 0; i < nsteps; ++i) {
+    const unsigned xt = a.xr_tag0 + (unsigned)i + 1u;
+    const long long slot = (((long long)(xt & 1u) * a.nw + j) * a.XT) * 4;
+    f32x4* mine = reinterpret_cast<f32x4*>(xr_base_of(a, a.xr_rank) + PEER_DATA_OFF + slot);
+    for (int e = e0 + tid; e < e1; e += NTH) {
+      f32x4 v;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) v[c] = dxr_test_value(a.xr_rank, j, r, i, e, c) + (corrupt ? 0.5f : 0.f);
+      mine[e] = v;
+    }
+    if (!deep_xrank_wait(a, j * a.R + r, xt)) {
+      if (tid == 0) atomicAdd(bad, 1u << 16);
+      return;
+    }
+    int wrong = 0;
+    for (int e = e0 + tid; e < e1; e += NTH) {
+      f32x4 v = z4();
+      for (int k = 0; k < a.xr_world; ++k)
+        v += __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(xr_base_of(a, k) + PEER_DATA_OFF + slot) + e);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        float want = 0.f;
+        for (int k = 0; k < a.xr_world; ++k) want += dxr_test_value(k, j, r, i, e, c);
+        wrong |= v[c] != want;
+      }
+    }
+    if (__syncthreads_or(wrong) && tid == 0) atomicAdd(bad, 1u);
+  }
+}
+
 }  // namespace
 
 }  // namespace ea
 
+#ifdef EA_DEEP_XRANK_ENTRY
+// grid R * nw workgroups (every one resident: they wait for the other ranks' flags)
+extern "C" hipError_t ea_deep_xrank_selftest(const ea::DeepArgs* a, int nsteps, unsigned* bad, int corrupt,
+                                             hipStream_t s) {
+  hipLaunchKernelGGL(ea::deep_xrank_selftest_kernel, dim3(a->R * a->nw), dim3(ea::NTH), 0, s, *a, nsteps, bad, corrupt);
+  return hipGetLastError();
+}
+#endif

@@ -25,6 +25,8 @@ extern "C" hipError_t ea_persist(const ea::PersistArgs* a, hipStream_t s);
 extern "C" hipError_t ea_persist_local(const ea::PersistArgs* a, hipStream_t s);
 extern "C" hipError_t ea_persist_xlocal(const ea::PersistArgs* a, hipStream_t s);
 extern "C" hipError_t ea_xcc_probe(int nblocks, unsigned* out, hipStream_t s);
+extern "C" hipError_t ea_deep_xrank_selftest(const ea::DeepArgs* a, int nsteps, unsigned* bad, int corrupt,
+                                             hipStream_t s);
 extern "C" int ea_persist_lds_bytes();
 extern "C" hipError_t ea_deep(const ea::DeepArgs* a, hipStream_t s);
 extern "C" hipError_t ea_xrank_selftest(const ea::PersistArgs* a, int nsteps, unsigned* bad, int corrupt, hipStream_t s);
@@ -346,9 +348,10 @@ bool Executor::build_deep() {
   a.ctr = reinterpret_cast<long long*>(c_.ctr);
   a.seed = c_.seed;
   a.ws_stride = ws;
-  // per-step synchronous replicas: the gradient-tile layout of the exchange buffer
+  // the gradient-tile layout of the exchange buffer (per-step synchronous replicas, and the
+  // parameter-server hook -- set_param_server allocates it then)
   a.sync = c_.persist_sync ? 1 : 0;
-  if (a.sync) {
+  {
     int xt = 16 * a.ly[0].Kx;
     a.x_b0 = xt; xt += 16;
     for (int l = 1; l < L; ++l) {
@@ -356,6 +359,8 @@ bool Executor::build_deep() {
       a.x_b[l] = xt; xt += 32;
     }
     a.XT = (xt + 63) / 64 * 64;
+  }
+  if (a.sync) {
     const size_t xb = sizeof(float) * (size_t)a.XT * (size_t)(c_.R + 1) * (size_t)nw;
     check(hipMalloc(&d_dxg_, xb), "hipMalloc(layer pipeline exchange buffer)");
     a.xg = d_dxg_;
@@ -383,7 +388,7 @@ bool Executor::build_deep() {
 std::vector<int> Executor::deep_geometry() const {
   if (!dp_.on) return {};
   const DeepArgs& a = dp_.args;
-  return {a.nw, a.R * a.nw, a.RT, a.KS, a.lds_floats * 4};
+  return {a.nw, a.R * a.nw, a.RT, a.KS, a.lds_floats * 4, a.XT};
 }
 
 std::vector<int> Executor::persist_geometry() const {
@@ -394,6 +399,19 @@ std::vector<int> Executor::persist_geometry() const {
 }
 
 bool Executor::set_param_server(const PsArgs& ps, int mode) {
+  if (dp_.on) {   // the layer pipeline: gradient tiles through xg, push / pull per step (deep_impl.h exchange)
+    if (dp_.args.sync || ps.nchunks <= 0 || dp_.args.nw > PEER_MAX_BLOCKS) return mode == 0;
+    DeepArgs& a = dp_.args;
+    if (!d_dxg_) {
+      const size_t xb = sizeof(float) * (size_t)a.XT * (size_t)(c_.R + 1) * (size_t)a.nw;
+      check(hipMalloc(&d_dxg_, xb), "hipMalloc(layer pipeline exchange buffer)");
+      check(hipDeviceSynchronize(), "hipDeviceSynchronize(layer pipeline exchange buffer)");
+    }
+    a.xg = d_dxg_;
+    a.ps = ps;
+    a.ps_mode = mode;
+    return true;
+  }
   if (!pm_.on || pm_.args.v2 || pm_.args.sync) return mode == 0;
   pm_.args.ps = ps;
   pm_.args.ps_mode = mode;
@@ -402,6 +420,19 @@ bool Executor::set_param_server(const PsArgs& ps, int mode) {
 
 bool Executor::set_rank_exchange(const std::vector<char*>& bases, int world, int rank, unsigned tag0,
                                  double timeout_s) {
+  if (dp_.on) {   // the layer pipeline (deep_impl.h exchange + deep_xrank_wait)
+    DeepArgs& a = dp_.args;
+    if (!a.sync || world > PEER_MAX_RANKS || (int)bases.size() != world || rank < 0 || rank >= world ||
+        a.R * a.nw > 2 * PEER_MAX_BLOCKS)
+      return world <= 1;
+    for (int k = 0; k < PEER_MAX_RANKS; ++k) a.xr_base[k] = k < world ? bases[k] : nullptr;
+    a.xr_world = world;
+    a.xr_rank = rank;
+    a.xr_timeout = (long long)(std::max(1.0, timeout_s) * 1e8);   // s_memrealtime: 100 MHz
+    a.timeout = std::max(a.timeout, a.xr_timeout);
+    dp_.xr_steps = tag0;
+    return true;
+  }
   if (!pm_.on || !pm_.args.sync || world > PEER_MAX_RANKS || (int)bases.size() != world || rank < 0 ||
       rank >= world || pm_.args.wgs > PEER_MAX_BLOCKS)
     return world <= 1;
@@ -422,15 +453,25 @@ bool Executor::set_rank_exchange(const std::vector<char*>& bases, int world, int
 // exact rank sums.  Collective (every rank runs it, the tags advance on all of them).
 // Returns {workgroup-steps with a wrong element, workgroups that timed out}.
 std::vector<unsigned> Executor::rank_exchange_selftest(int nsteps, int corrupt) {
-  if (!pm_.on || pm_.args.xr_world <= 1 || nsteps <= 0) return {0u, 0u};
+  const bool deep = dp_.on && dp_.args.xr_world > 1;
+  if (!deep && (!pm_.on || pm_.args.xr_world <= 1)) return {0u, 0u};
+  if (nsteps <= 0) return {0u, 0u};
   unsigned* d = nullptr;
   check(hipMalloc(&d, sizeof(unsigned)), "hipMalloc(self-test word)");
   check(hipMemset(d, 0, sizeof(unsigned)), "hipMemset(self-test word)");
   check(hipDeviceSynchronize(), "hipDeviceSynchronize(self-test setup)");
-  PersistArgs a = pm_.args;
-  a.xr_tag0 = pm_.xr_steps;
-  pm_.xr_steps += (unsigned)nsteps;
-  hipError_t e = ea_xrank_selftest(&a, nsteps, d, corrupt, nullptr);
+  hipError_t e;
+  if (deep) {
+    DeepArgs a = dp_.args;
+    a.xr_tag0 = dp_.xr_steps;
+    dp_.xr_steps += (unsigned)nsteps;
+    e = ea_deep_xrank_selftest(&a, nsteps, d, corrupt, nullptr);
+  } else {
+    PersistArgs a = pm_.args;
+    a.xr_tag0 = pm_.xr_steps;
+    pm_.xr_steps += (unsigned)nsteps;
+    e = ea_xrank_selftest(&a, nsteps, d, corrupt, nullptr);
+  }
   if (e == hipSuccess) e = hipDeviceSynchronize();
   unsigned v = 0;
   if (e == hipSuccess) e = hipMemcpy(&v, d, sizeof(v), hipMemcpyDeviceToHost);
@@ -464,6 +505,10 @@ void Executor::run_chunk(hipStream_t s, int nsteps) const {
   if (dp_.on) {   // one persistent launch + the post node (flag clear, counter advance)
     DeepArgs a = dp_.args;
     a.nsteps = nsteps;
+    if (a.xr_world > 1) {   // the rank exchange's flag tags continue over launches
+      a.xr_tag0 = dp_.xr_steps;
+      dp_.xr_steps += (unsigned)nsteps;
+    }
     check(ea_deep(&a, s), "persistent layer pipeline kernel");
     check(ea_persist_post(d_dflags_, (int)(dp_.flag_bytes / sizeof(unsigned)), reinterpret_cast<long long*>(c_.ctr),
                           reinterpret_cast<const int*>(c_.ntrain), c_.R, c_.B, nsteps, d_perr_, s),

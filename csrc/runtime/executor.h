@@ -150,7 +150,7 @@ class Executor {
   // per-step sync across ranks inside the launch (PersistArgs::xr_*): every rank's
   // rank-exchange buffer (peer-mapped); false: the plan cannot (not a persistent sync plan)
   bool set_rank_exchange(const std::vector<char*>& bases, int world, int rank, unsigned tag0, double timeout_s);
-  unsigned rank_exchange_steps() const { return pm_.xr_steps; }
+  unsigned rank_exchange_steps() const { return dp_.on ? dp_.xr_steps : pm_.xr_steps; }
   // numeric self-test of the attached exchange: {wrong workgroup-steps, timed-out workgroups}
   std::vector<unsigned> rank_exchange_selftest(int nsteps, int corrupt);
   unsigned persist_error() const;  // sticky error word (a timed-out in-launch wait), synchronous read
@@ -218,6 +218,7 @@ class Executor {
     bool on = false;
     DeepArgs args{};
     size_t flag_bytes = 0;
+    mutable unsigned xr_steps = 0;   // steps run with the rank exchange (its flag tags)
   } dp_;
   float* d_dws_ = nullptr;         // its per-replica workspace (activations, gradients, weight images)
   float* d_dxg_ = nullptr;         // its exchange buffer (per-step synchronous replicas)

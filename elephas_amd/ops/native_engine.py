@@ -386,9 +386,13 @@ class NativeTrainer(TrainerBase):
         buf = None
         try:
             if ok:
-                wgs = int(self.exe.persist_geometry()[5])
                 devi = self.dev.index if self.dev.index is not None else torch.cuda.current_device()
-                buf = self.C.PeerBuffer(int(rank), world, 2 * wgs * 7 * 1024 * 4, int(devi))
+                if self.exe.persist_variant()[0] == 3:   # the layer pipeline: [2][nw][XT] floats
+                    geo = self.exe.deep_geometry()
+                    nbytes = 2 * int(geo[0]) * int(geo[5]) * 4
+                else:                                    # persist.hip: [2][wgs][PM_XSLOT] floats
+                    nbytes = 2 * int(self.exe.persist_geometry()[5]) * 7 * 1024 * 4
+                buf = self.C.PeerBuffer(int(rank), world, nbytes, int(devi))
         except Exception as e:  # noqa: BLE001 - voted below
             _log.warning("rank exchange: buffer setup failed: %r", e)
             ok, buf = False, None
@@ -1177,7 +1181,7 @@ class NativeTrainer(TrainerBase):
 
     def plan_name(self) -> str:
         if self.exe.persistent() and self.exe.persist_variant()[0] == 3:
-            nw, grid, rt, ks, lds = self.exe.deep_geometry()
+            nw, grid, rt, ks, lds = self.exe.deep_geometry()[:5]
             sy = ", per-step gradient exchange of the replicas inside the launch" if self.exe.persist_variant()[2] else ""
             return (f"persistent layer pipeline{sy} (deep.hip; 1 kernel + 1 post kernel per <= {self.GRAPH_CHUNK}-step "
                     f"chunk; {nw} workgroups of 512 threads per replica owning 16-column tiles of every layer, "

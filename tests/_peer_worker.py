@@ -298,7 +298,28 @@ def step_graph(dist, rank, world):
                 error=int(ch.impl.error()))
 
 
-def sync_inlaunch(dist, rank, world):
+def _sync_model(deep, seed):
+    """The scenarios' model: the MNIST MLP (persist.hip V1 roles), or with deep=True an
+    Otto-like 93-256-256-9 stack on the layer pipeline (tanh: no ReLU kink turns fp32
+    summation noise into a different gradient between the two summation orders compared)."""
+    from elephas_amd.models import Sequential, Dense, initializers
+    from elephas_amd.models.optimizers import SGD
+    initializers.set_seed(seed)   # the same initial weights on every rank
+    m = Sequential()
+    if deep:
+        m.add(Dense(256, activation="tanh", input_dim=93))
+        m.add(Dense(256, activation="tanh"))
+        m.add(Dense(9, activation="softmax"))
+        m.compile(SGD(0.05), "categorical_crossentropy", ["acc"])
+        return m, 93, 9
+    m.add(Dense(128, activation="relu", input_dim=784))
+    m.add(Dense(128, activation="relu"))
+    m.add(Dense(10, activation="softmax"))
+    m.compile(SGD(0.1), "categorical_crossentropy", ["acc"])
+    return m, 784, 10
+
+
+def sync_inlaunch(dist, rank, world, deep=False):
     """Per-step synchronous DP across ranks inside the persistent launch: two ranks x
     two replicas (each rank's grid on half the CUs), the weight-gradient tiles summed
     over the replicas and then over the ranks by the owning workgroups.  Every replica
@@ -313,16 +334,11 @@ def sync_inlaunch(dist, rank, world):
     from elephas_amd.ops.plan import build_plan
     from elephas_amd.ops.torch_engine import TorchTrainer
     config.set_policy("float32")
-    initializers.set_seed(21)   # the same initial weights on every rank
-    m = Sequential()
-    m.add(Dense(128, activation="relu", input_dim=784))
-    m.add(Dense(128, activation="relu"))
-    m.add(Dense(10, activation="softmax"))
-    m.compile(SGD(0.1), "categorical_crossentropy", ["acc"])
+    m, d, k = _sync_model(deep, 21)
     R, B, steps = 2, 64, 9
     rng = np.random.default_rng(77)   # every rank builds every worker's shard
-    xs_all = [rng.random((B * steps, 784), dtype=np.float32) for _ in range(world * R)]
-    ys_all = [np.eye(10, dtype=np.float32)[rng.integers(0, 10, B * steps)] for _ in range(world * R)]
+    xs_all = [rng.random((B * steps, d), dtype=np.float32) for _ in range(world * R)]
+    ys_all = [np.eye(k, dtype=np.float32)[rng.integers(0, k, B * steps)] for _ in range(world * R)]
     xs, ys = xs_all[rank * R:(rank + 1) * R], ys_all[rank * R:(rank + 1) * R]
     ag = _allgather(dist)
     t = NativeTrainer(m, build_plan(m), R, B, torch.device("cuda"), seed=5, sync=True, persist_cus=128)
@@ -349,7 +365,7 @@ def sync_inlaunch(dist, rank, world):
                 steps_tagged=int(t.exe.rank_exchange_steps()))
 
 
-def xrank_selftest(dist, rank, world):
+def xrank_selftest(dist, rank, world, deep=False):
     """The voted numeric self-test of the in-launch rank exchange (NativeTrainer
     .attach_rank_exchange): without a fault every rank attaches and trains inside the
     launch; with ELEPHAS_AMD_FAULT_INJECT=rank=1,phase=xrank_selftest rank 1 sends a wrong
@@ -365,16 +381,11 @@ def xrank_selftest(dist, rank, world):
     from elephas_amd.ops.plan import build_plan
     from elephas_amd.ops.torch_engine import TorchTrainer
     config.set_policy("float32")
-    initializers.set_seed(23)
-    m = Sequential()
-    m.add(Dense(128, activation="relu", input_dim=784))
-    m.add(Dense(128, activation="relu"))
-    m.add(Dense(10, activation="softmax"))
-    m.compile(SGD(0.1), "categorical_crossentropy", ["acc"])
+    m, d, k = _sync_model(deep, 23)
     R, B, steps = 2, 64, 6
     rng = np.random.default_rng(78)
-    xs_all = [rng.random((B * steps, 784), dtype=np.float32) for _ in range(world * R)]
-    ys_all = [np.eye(10, dtype=np.float32)[rng.integers(0, 10, B * steps)] for _ in range(world * R)]
+    xs_all = [rng.random((B * steps, d), dtype=np.float32) for _ in range(world * R)]
+    ys_all = [np.eye(k, dtype=np.float32)[rng.integers(0, k, B * steps)] for _ in range(world * R)]
     xs, ys = xs_all[rank * R:(rank + 1) * R], ys_all[rank * R:(rank + 1) * R]
     ag = _allgather(dist)
     t = NativeTrainer(m, build_plan(m), R, B, torch.device("cuda"), seed=5, sync=True, persist_cus=128)
@@ -429,6 +440,10 @@ def main():
         res = ps(dist, rank, world)
     elif scenario == "ps_selftest":
         res = ps_selftest(dist, rank, world)
+    elif scenario == "xrank_selftest_deep":
+        res = xrank_selftest(dist, rank, world, deep=True)
+    elif scenario == "sync_inlaunch_deep":
+        res = sync_inlaunch(dist, rank, world, deep=True)
     elif scenario == "xrank_selftest":
         res = xrank_selftest(dist, rank, world)
     elif scenario == "sync_inlaunch":

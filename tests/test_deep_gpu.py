@@ -172,7 +172,7 @@ def test_deep_otto_shape_matches_tail_chain_plan(monkeypatch):
         assert t.persistent == (persist != 0), t.plan_name()
         if persist:
             assert t.persist_variant == 3, t.plan_name()
-            nw, grid, rt, ks, lds = t.exe.deep_geometry()
+            nw, grid, rt, ks, lds = t.exe.deep_geometry()[:5]
             assert nw == 32 and grid <= torch.cuda.get_device_properties(0).multi_processor_count
         t.set_data(xs, ys, 0.15, shuffle=True)
         torch.manual_seed(5)   # epoch shuffles draw from the global CUDA generator
@@ -309,3 +309,55 @@ def test_deep_exact_otto_matches_fp32_torch(monkeypatch, opt):
     nat = _native(model, 8, 128, deep="-1", monkeypatch=monkeypatch)
     assert nat.persistent and nat.persist_variant == 3, (nat.plan_name(), nat.plan_reason)
     _compare_with_torch(nat, model, xs, ys, 128, adaptive=opt == "adam")
+
+
+@pytest.mark.parametrize("mode", ["asynchronous", "hogwild"])
+def test_deep_async_inlaunch_single_worker_equals_plain_training(mode):
+    """The layer pipeline's in-launch parameter-server hook (frequency='batch', reference
+    worker.py:114-127): every step each workgroup pushes theta_new - theta_old of the tiles it
+    owns and pulls them back for the next step.  With ONE worker the server always returns
+    that worker's own weights, so the run equals plain layer-pipeline training on the same
+    batches, across launch boundaries (chunks of 8 steps) -- Otto-like shape, dropout."""
+    from elephas_amd.models import initializers
+    from elephas_amd.models.optimizers import SGD
+    from elephas_amd.ops.plan import build_plan, flatten_weights
+    from elephas_amd.ops.native_engine import NativeTrainer
+    from elephas_amd.parameter.client import DeviceClient
+    from elephas_amd.worker import BatchedAsynchronousWorker, _Group
+    from elephas_amd import config
+    config.set_policy("float32")
+    initializers.set_seed(43)
+    model = _mlp(93, [256, 256, 128], 9, dropout=0.3)
+    model.compile(SGD(0.05), "categorical_crossentropy", ["acc"])
+    xs, ys = _shards([128 * 20], 93, 9, seed=18)
+    init = flatten_weights(model.get_weights())
+    client = DeviceClient().connect(len(init), mode, rank=0, world=1, allgather=lambda h: [h])
+    th = torch.from_numpy(init).cuda()
+    torch.cuda.synchronize()
+    client.ps.set(th.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    t = NativeTrainer(model, build_plan(model), 1, 128, torch.device("cuda"), seed=3, ps_hook=True)
+    assert t.persistent and t.persist_variant == 3, t.plan_name()
+    t.set_data(xs, ys, 0.0, shuffle=False)
+    t.GRAPH_CHUNK = 8
+    grp = _Group(t, [True])
+    grp.attach(client)
+    assert grp.inlaunch, "the layer pipeline must take the in-launch PS hook"
+    worker = BatchedAsynchronousWorker(None, None, client, {}, "batch", None, None, None, None)
+    t.begin_epoch()
+    grp.steps(worker, 19)
+    torch.cuda.synchronize()
+    t.check()
+    got = torch.empty(len(init), dtype=torch.float32, device="cuda")
+    client.ps.pull(got.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert client.ps.error() == 0
+    ref = NativeTrainer(model, build_plan(model), 1, 128, torch.device("cuda"), seed=3, persist=1)
+    assert ref.persist_variant == 3
+    ref.set_data(xs, ys, 0.0, shuffle=False)
+    ref.begin_epoch()
+    ref.run_steps(19)
+    wr = ref.get_weights_flat()[0]
+    step = np.abs(wr - init).max()
+    err = np.abs(got.cpu().numpy() - wr).max()
+    assert err <= 1e-5 * step + 1e-7, (err, step)

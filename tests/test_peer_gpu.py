@@ -176,3 +176,32 @@ def test_rank_exchange_selftest_votes_and_falls_back():
         assert not r["attached"] and r["selftest"] is not None and not r["selftest"]["ok"], r
         assert any(v[0] > 0 for v in r["selftest"]["votes"]), r
         assert r["same_on_all_ranks"] and r["err"] < 1e-3, r
+
+
+def test_sync_inlaunch_across_ranks_layer_pipeline_matches_one_model():
+    """The layer pipeline's rank exchange (deep_impl.h exchange: the replicas' reduce-scatter
+    of every gradient tile, each slice then summed over the ranks through peer-mapped
+    buffers in rank order): an Otto-like 93-256-256-9 stack, 2 ranks x 2 replicas, stays
+    bit-identical on every replica of every rank and matches ONE fp32 torch model trained
+    on the four workers' stacked batches."""
+    for r in _run("sync_inlaunch_deep"):
+        assert r["attached"], r
+        assert "layer pipeline" in r["plan"], r
+        assert r["error"] == 0 and r["replicas_equal"] and r["same_on_all_ranks"], r
+        assert r["err"] < 1e-3, r
+        assert r["steps_tagged"] == 18 + 2, r
+
+
+def test_rank_exchange_selftest_layer_pipeline_votes_and_falls_back():
+    """The layer pipeline's rank exchange is voted in by its own numeric self-test
+    (deep_xrank_selftest_kernel: known integer slices through the same buffers, flags and
+    tags): clean -> attached and trained inside the launch; a corrupting rank (fault
+    injection phase=xrank_selftest) -> every rank detaches and the per-step all-reduce
+    fallback still reaches the one-model result."""
+    for r in _run("xrank_selftest_deep"):
+        assert r["attached"] and r["selftest"]["ok"], r
+        assert r["same_on_all_ranks"] and r["err"] < 1e-3, r
+    for r in _run("xrank_selftest_deep", env_extra={"ELEPHAS_AMD_FAULT_INJECT": "rank=1,phase=xrank_selftest"}):
+        assert not r["attached"] and not r["selftest"]["ok"], r
+        assert any(v[0] > 0 for v in r["selftest"]["votes"]), r
+        assert r["same_on_all_ranks"] and r["err"] < 1e-3, r

@@ -482,8 +482,9 @@ def test_persist_bf16_pinned_to_bf16_operand_torch():
     dist = lambda a, b: float(np.abs(out[a] - out[b]).mean() / np.abs(out[b] - w0).mean())
     gap, d_rc, d_p = dist("f32", "emul"), dist("rc_bf16", "emul"), dist("p_bf16", "emul")
     print(f"bf16 pin ({nst} steps): emul-vs-f32 {gap:.3e}  rowchain-vs-emul {d_rc:.3e}  persistent-vs-emul {d_p:.3e}")
-    assert d_rc <= 0.3 * gap, (d_rc, gap)
-    assert d_p <= 0.8 * gap, (d_p, gap)
+    # measured (round 5): row chain 0.5 % of the gap, persistent V2 6 %
+    assert d_rc <= 0.05 * gap, (d_rc, gap)
+    assert d_p <= 0.2 * gap, (d_p, gap)
 
 
 @pytest.mark.parametrize("case", ["v2_fit", "v1_mom_fit", "v1_sync"])

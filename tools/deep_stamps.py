@@ -60,7 +60,7 @@ def main():
     if not geo:
         print("not on the layer pipeline:", t.plan_reason)
         return
-    nw, grid, rt, ks, lds = geo
+    nw, grid, rt, ks, lds = geo[:5]
     print(f"nw {nw} grid {grid} RT {rt} KS {ks} LDS {lds} B")
     rng = np.random.default_rng(0)
     rows = B * 64
