@@ -7,12 +7,17 @@ extern "C" hipError_t ea_deep_l2(const ea::DeepArgs* a, int fast, int opk, hipSt
 extern "C" hipError_t ea_deep_l3(const ea::DeepArgs* a, int fast, int opk, hipStream_t s);
 extern "C" hipError_t ea_deep_l4(const ea::DeepArgs* a, int fast, int opk, hipStream_t s);
 extern "C" hipError_t ea_deep_l5(const ea::DeepArgs* a, int fast, int opk, hipStream_t s);
+extern "C" hipError_t ea_deep_l2_local(const ea::DeepArgs* a, int fast, int opk, hipStream_t s);
+extern "C" hipError_t ea_deep_l3_local(const ea::DeepArgs* a, int fast, int opk, hipStream_t s);
+extern "C" hipError_t ea_deep_l4_local(const ea::DeepArgs* a, int fast, int opk, hipStream_t s);
+extern "C" hipError_t ea_deep_l5_local(const ea::DeepArgs* a, int fast, int opk, hipStream_t s);
 
 using namespace ea;
 
 // grid: R * nw workgroups of 512 threads, every one resident (the host sizes the grid to
 // at most one workgroup per CU); dynamic LDS a->lds_floats floats
-extern "C" hipError_t ea_deep(const DeepArgs* a, hipStream_t s) {
+// local != 0: the XCD-local instances (deep_l*_local.hip; the host checked R % 8 == 0, fit)
+extern "C" hipError_t ea_deep(const DeepArgs* a, int local, hipStream_t s) {
   if (a->nsteps <= 0) return hipSuccess;
   // softmax + (sparse) categorical cross-entropy with accuracy / CCE metrics: the quad-per-row
   // loss tile; everything else the generic one
@@ -24,10 +29,10 @@ extern "C" hipError_t ea_deep(const DeepArgs* a, hipStream_t s) {
   // rule (run-time dispatch) -- deep_impl.h OPK_*
   const int opk = (a->op.opt == OPT_SGD && a->op.mom == 0.f) ? 0 : (a->op.opt == OPT_ADAM ? 1 : 2);
   switch (a->L) {
-    case 2: return ea_deep_l2(a, fast, opk, s);
-    case 3: return ea_deep_l3(a, fast, opk, s);
-    case 4: return ea_deep_l4(a, fast, opk, s);
-    case 5: return ea_deep_l5(a, fast, opk, s);
+    case 2: return local ? ea_deep_l2_local(a, fast, opk, s) : ea_deep_l2(a, fast, opk, s);
+    case 3: return local ? ea_deep_l3_local(a, fast, opk, s) : ea_deep_l3(a, fast, opk, s);
+    case 4: return local ? ea_deep_l4_local(a, fast, opk, s) : ea_deep_l4(a, fast, opk, s);
+    case 5: return local ? ea_deep_l5_local(a, fast, opk, s) : ea_deep_l5(a, fast, opk, s);
     default: return hipErrorInvalidValue;
   }
 }

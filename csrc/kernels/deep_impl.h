@@ -75,6 +75,15 @@ __device__ __forceinline__ f32x4 z4() { return f32x4{0.f, 0.f, 0.f, 0.f}; }
 #ifndef DP_LOAD_AUX
 #define DP_LOAD_AUX 16
 #endif
+// XCD-local instance (deep_l{2..5}_local.hip compile this file again with EA_DLOCAL = 1; fit
+// granularity only): block b serves replica b % R, so with R a multiple of 8 a replica's
+// workgroups share one XCD (the dispatch deals blocks round-robin over the 8 XCDs; checked
+// at launch, PERR_PLACE) and its hand-offs stay in that XCD's L2: stores and phase flags
+// plain (the line stays in the L2, where the sc1 loads find it) instead of write-through
+// (persist.hip has the measurements)
+#ifndef EA_DLOCAL
+#define EA_DLOCAL 0
+#endif
 __device__ __forceinline__ rsrc_t ws_rsrc(const float* base) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), (short)0, 0x7fffffff, 0x00020000);
 }
@@ -92,11 +101,12 @@ __device__ __forceinline__ void acquire_lane0() {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
 }
+constexpr int DP_ST_AUX = EA_DLOCAL ? 0 : 16;   // sc1 (write-through) / plain in the XCD-local instance
 __device__ __forceinline__ void st1(rsrc_t r, int v, long long s, float x) {
-  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, x), r, v * 4, (int)s * 4, 16);
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, x), r, v * 4, (int)s * 4, DP_ST_AUX);
 }
 __device__ __forceinline__ void st4(rsrc_t r, int v, long long s, f32x4 x) {
-  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, x), r, v * 4, (int)s * 4, 16);
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, x), r, v * 4, (int)s * 4, DP_ST_AUX);
 }
 __device__ __forceinline__ f32x4 lds4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
 __device__ __forceinline__ void lds4(float* p, f32x4 v) { *reinterpret_cast<f32x4*>(p) = v; }
@@ -128,7 +138,10 @@ __device__ __forceinline__ unsigned* dflag(const DeepArgs& a, int r, int kind) {
 __device__ __forceinline__ void publish(const DeepArgs& a, int r, int j, unsigned tag) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (threadIdx.x == 0) __hip_atomic_store((gu32*)(dflag(a, r, 1) + j), tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (threadIdx.x == 0) {
+    if constexpr (EA_DLOCAL) __builtin_amdgcn_raw_buffer_store_b32(tag, ws_rsrc(reinterpret_cast<float*>(dflag(a, r, 1) + j)), 0, 0, 0);
+    else __hip_atomic_store((gu32*)(dflag(a, r, 1) + j), tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
 // wave 0 polls the phase counters of the replica's nw workgroups (lane q watches q) until
@@ -159,17 +172,33 @@ __device__ __forceinline__ bool wait_phase(const DeepArgs& a, int r, unsigned ta
 }
 
 // residency: every workgroup of the grid raised its GO flag (a workgroup that is not
-// resident never does: the others time out before touching any state)
-__device__ __forceinline__ bool wait_grid(const DeepArgs& a) {
+// resident never does: the others time out before touching any state).  The GO value is the
+// workgroup's XCD + 1 in the XCD-local instance, where a replica r whose workgroups do not
+// all share this one's XCD gives up (PERR_PLACE), state intact
+__device__ __forceinline__ unsigned dxcc_go() {
+  return EA_DLOCAL ? __builtin_amdgcn_s_getreg((20) | (0 << 6) | ((4 - 1) << 11)) + 1u : 1u;   // HW_REG_XCC_ID
+}
+__device__ __forceinline__ bool wait_grid(const DeepArgs& a, int r) {
   int ok = 1;
   if (threadIdx.x < 64) {
     const int lane = threadIdx.x, tot = a.R * a.nw;
+    const unsigned mine = dxcc_go();
     const unsigned long long t0 = wall_clock64();
     for (;;) {
-      bool all = true;
-      for (int f = lane; f < tot; f += 64)
-        all &= __hip_atomic_load((gu32*)(dflag(a, f % a.R, 0) + f / a.R), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
-      if (__all(all)) break;
+      bool all = true, away = false;
+      for (int f = lane; f < tot; f += 64) {
+        const unsigned v = __hip_atomic_load((gu32*)(dflag(a, f % a.R, 0) + f / a.R), __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
+        all &= v != 0u;
+        away |= EA_DLOCAL && f % a.R == r && v != 0u && v != mine;
+      }
+      if (__all(all)) {
+        if (__any(away)) {
+          ok = 0;
+          if (lane == 0) __hip_atomic_store((gu32*)(a.err), (unsigned)PERR_PLACE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        break;
+      }
       if ((long long)(wall_clock64() - t0) > a.timeout) {
         ok = 0;
         if (lane == 0) __hip_atomic_store((gu32*)(a.err), (unsigned)PERR_GRID, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1509,7 +1538,7 @@ __global__ __launch_bounds__(512) void mlp_deep_kernel(DeepArgs a) {
   x.S = a.S ? a.S + (long long)x.r * a.sS : nullptr;
   x.prow = reinterpret_cast<int*>(smem + a.lds_floats - 2 * DP_ROWS);
   if (x.tid == 0)
-    __hip_atomic_store((gu32*)(dflag(a, x.r, 0) + x.j), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store((gu32*)(dflag(a, x.r, 0) + x.j), dxcc_go(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 
   // ---- prologue: the owned masters from P into LDS (zero past the true widths), then the
   // images the other workgroups read
@@ -1520,7 +1549,7 @@ __global__ __launch_bounds__(512) void mlp_deep_kernel(DeepArgs a) {
   __syncthreads();
   write_images<L>(a, smem, x);
   __syncthreads();
-  if (!wait_grid(a)) return;
+  if (!wait_grid(a, x.r)) return;
   // the prologue's image writes are out: tag 1 (step s then publishes s * NPH + 2 ..
   // (s + 1) * NPH + 1, so "the previous step is done" is tag base for every s)
   publish(a, x.r, x.j, 1u);
@@ -1682,8 +1711,14 @@ hipError_t deep_launch_sy(const DeepArgs* a, bool fast, int opk, hipStream_t s) 
 // opk: OPK_SGD0 / OPK_ADAM / OPK_ANY (deep.hip picks it from the optimizer)
 template <int L>
 hipError_t deep_launch(const DeepArgs* a, bool fast, int opk, hipStream_t s) {
-  // per-step sync and the parameter-server hook both run the gradient tiles through xg
+  // per-step sync and the parameter-server hook both run the gradient tiles through xg (the
+  // XCD-local instance has neither: fit granularity only)
+#if EA_DLOCAL
+  if (a->sync || a->ps_mode) return hipErrorInvalidValue;
+  return deep_launch_sy<L, false>(a, fast, opk, s);
+#else
   return (a->sync || a->ps_mode) ? deep_launch_sy<L, true>(a, fast, opk, s) : deep_launch_sy<L, false>(a, fast, opk, s);
+#endif
 }
 // value of component c of f32x4 element e of replica r's slice of tile j, self-test step i on
 // rank k: small integers, so every partial sum is exact in fp32 whatever the order

@@ -28,7 +28,7 @@ extern "C" hipError_t ea_xcc_probe(int nblocks, unsigned* out, hipStream_t s);
 extern "C" hipError_t ea_deep_xrank_selftest(const ea::DeepArgs* a, int nsteps, unsigned* bad, int corrupt,
                                              hipStream_t s);
 extern "C" int ea_persist_lds_bytes();
-extern "C" hipError_t ea_deep(const ea::DeepArgs* a, hipStream_t s);
+extern "C" hipError_t ea_deep(const ea::DeepArgs* a, int local, hipStream_t s);
 extern "C" hipError_t ea_xrank_selftest(const ea::PersistArgs* a, int nsteps, unsigned* bad, int corrupt, hipStream_t s);
 
 namespace ea {
@@ -365,6 +365,8 @@ bool Executor::build_deep() {
     check(hipMalloc(&d_dxg_, xb), "hipMalloc(layer pipeline exchange buffer)");
     a.xg = d_dxg_;
   }
+  // the XCD-local instances (deep_l*_local.hip): fit granularity, R a multiple of 8
+  dp_.local = c_.persist_local != 0 && !a.sync && c_.R % 8 == 0 && xcd_round_robin(dev, c_.R * nw);
   const size_t ws_bytes = sizeof(float) * (size_t)ws * c_.R;
   check(hipMalloc(&d_dws_, ws_bytes), "hipMalloc(layer pipeline workspace)");
   check(hipMemset(d_dws_, 0, ws_bytes), "hipMemset(layer pipeline workspace)");
@@ -410,6 +412,7 @@ bool Executor::set_param_server(const PsArgs& ps, int mode) {
     a.xg = d_dxg_;
     a.ps = ps;
     a.ps_mode = mode;
+    if (mode) dp_.local = false;   // the hook runs on the write-through instances
     return true;
   }
   if (!pm_.on || pm_.args.v2 || pm_.args.sync) return mode == 0;
@@ -482,7 +485,7 @@ std::vector<unsigned> Executor::rank_exchange_selftest(int nsteps, int corrupt) 
 }
 
 std::vector<int> Executor::persist_variant() const {
-  if (dp_.on) return {3, 0, dp_.args.sync, 0};
+  if (dp_.on) return {3, 0, dp_.args.sync, dp_.local && !dp_.args.ps_mode ? 1 : 0};
   if (!pm_.on) return {};
   return {pm_.args.v2 ? 2 : 1, pm_.args.nd, pm_.args.sync, pm_.local};
 }
@@ -509,7 +512,7 @@ void Executor::run_chunk(hipStream_t s, int nsteps) const {
       a.xr_tag0 = dp_.xr_steps;
       dp_.xr_steps += (unsigned)nsteps;
     }
-    check(ea_deep(&a, s), "persistent layer pipeline kernel");
+    check(ea_deep(&a, dp_.local && !a.sync && !a.ps_mode ? 1 : 0, s), "persistent layer pipeline kernel");
     check(ea_persist_post(d_dflags_, (int)(dp_.flag_bytes / sizeof(unsigned)), reinterpret_cast<long long*>(c_.ctr),
                           reinterpret_cast<const int*>(c_.ntrain), c_.R, c_.B, nsteps, d_perr_, s),
           "persistent chunk post");

@@ -219,6 +219,7 @@ class Executor {
     DeepArgs args{};
     size_t flag_bytes = 0;
     mutable unsigned xr_steps = 0;   // steps run with the rank exchange (its flag tags)
+    bool local = false;              // the XCD-local instances (deep_l*_local.hip)
   } dp_;
   float* d_dws_ = nullptr;         // its per-replica workspace (activations, gradients, weight images)
   float* d_dxg_ = nullptr;         // its exchange buffer (per-step synchronous replicas)

@@ -37,6 +37,10 @@ SOURCES = [
     "kernels/deep_l3.hip",
     "kernels/deep_l4.hip",
     "kernels/deep_l5.hip",
+    "kernels/deep_l2_local.hip",
+    "kernels/deep_l3_local.hip",
+    "kernels/deep_l4_local.hip",
+    "kernels/deep_l5_local.hip",
     "kernels/peer.hip",
     "kernels/shuffle.hip",
     "runtime/executor.cpp",

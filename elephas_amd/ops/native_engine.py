@@ -1183,6 +1183,7 @@ class NativeTrainer(TrainerBase):
         if self.exe.persistent() and self.exe.persist_variant()[0] == 3:
             nw, grid, rt, ks, lds = self.exe.deep_geometry()[:5]
             sy = ", per-step gradient exchange of the replicas inside the launch" if self.exe.persist_variant()[2] else ""
+            sy += ", XCD-local hand-offs" if self.exe.persist_variant()[3] else ""
             return (f"persistent layer pipeline{sy} (deep.hip; 1 kernel + 1 post kernel per <= {self.GRAPH_CHUNK}-step "
                     f"chunk; {nw} workgroups of 512 threads per replica owning 16-column tiles of every layer, "
                     f"{rt} row tiles x {ks}-way k split, {lds // 1024} KB LDS; grid {grid})")

@@ -361,3 +361,31 @@ def test_deep_async_inlaunch_single_worker_equals_plain_training(mode):
     step = np.abs(wr - init).max()
     err = np.abs(got.cpu().numpy() - wr).max()
     assert err <= 1e-5 * step + 1e-7, (err, step)
+
+
+@pytest.mark.parametrize("opt", ["sgd", "adam"])
+def test_deep_xcd_local_instance_is_bit_exact(monkeypatch, opt):
+    """The layer pipeline's XCD-local instance (deep_l*_local.hip: a replica's hand-offs
+    stored plain and read from its XCD's L2, placement checked at launch) is picked for the
+    Otto job's 8 replicas and trains bit for bit as the write-through instance."""
+    from elephas_amd.models import initializers, optimizers as O
+    initializers.set_seed(52)
+    model = _mlp(93, [512, 512, 512], 9, dropout=0.5)
+    model.compile(O.SGD(0.01) if opt == "sgd" else O.Adam(0.01), "categorical_crossentropy", ["acc"])
+    xs, ys = _shards([128 * 3] * 7 + [128 + 40], 93, 9, seed=23)
+    out = []
+    for local in ("-1", "0"):
+        monkeypatch.setenv("ELEPHAS_AMD_PERSIST_LOCAL", local)
+        t = _native(model, 8, 128, deep="-1", monkeypatch=monkeypatch)
+        var = t.exe.persist_variant()
+        assert t.persistent and var[0] == 3 and var[3] == (1 if local == "-1" else 0), (local, var, t.plan_name())
+        t.set_data(xs, ys, 0.15, shuffle=True)
+        torch.manual_seed(2)
+        h = t.fit(2)
+        t.check()
+        out.append((t.get_weights_flat(), h))
+    (wl, hl), (wg, hg) = out
+    assert np.array_equal(wl, wg), np.abs(wl - wg).max()
+    for a, b in zip(hl, hg):
+        for key in a:
+            np.testing.assert_array_equal(a[key], b[key])
