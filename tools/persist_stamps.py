@@ -66,11 +66,16 @@ def main():
     t.check()
     s = st.view(grid, 8, 32).cpu().numpy().astype(np.int64)
     nl0 = nk0 * nc0
-    q = np.arange(grid) // R
+    bidx = np.arange(grid)
+    if t.exe.persist_variant()[3] == 2:   # exchange-local instance: the 8 copies of workgroup q on one XCD
+        q = (bidx & 7) + 8 * (bidx >> 6)
+        rep = (bidx >> 3) & 7
+    else:
+        q = bidx // R
+        rep = bidx % R
     roles = {"l0": q < nl0, "chain": (q >= nl0) & (q < nl0 + nch), "dw": q >= nl0 + nch}
     chain = roles["chain"]
     ref_k = 6   # chain: dZ_0 rows published (end of a step)
-    rep = np.arange(grid) % R
     print("ticks of 10 ns -> us; per step, medians relative to the same replica's chains' dZ_0 "
           "publication of the previous step (replicas run unsynchronised)")
 
