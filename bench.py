@@ -438,9 +438,12 @@ def measure_train(args, model, dist, rank, world, dev, gpu, W, batch_mode, steps
 
     state = {"step_in_epoch": steps_per_epoch, "epochs": 0, "val_passes": 0}
 
-    def run(k):
+    def run(k, then_average=False):
         """k optimizer steps with epoch rollover (the epoch-end validation pass of the
-        reference's Keras fit runs at every epoch boundary); returns rows per worker."""
+        reference's Keras fit runs at every epoch boundary); returns rows per worker.
+        then_average: the reference's averaging follows the last step (fit granularity) --
+        on the persistent plan it runs fused into the last launch's end
+        (NativeTrainer.run_steps_and_average)."""
         done_rows = 0
         while k > 0:
             if state["step_in_epoch"] >= steps_per_epoch:
@@ -459,6 +462,10 @@ def measure_train(args, model, dist, rank, world, dev, gpu, W, batch_mode, steps
                     t.run_steps_allreduce_overlap(n, dist.all_reduce_sum_)
                 elif batch_mode and world > 1 and not sync_local:
                     t.run_steps_allreduce(n, allreduce_grads, use_graph=not args.no_graph)
+                elif then_average and not batch_mode and n == k:
+                    t.run_steps_and_average(n, dist.all_reduce_sum_ if world > 1 else None, R * world,
+                                            use_graph=not args.no_graph)
+                    state["averaged"] = True
                 else:
                     t.run_steps(n, use_graph=not args.no_graph)
             else:
@@ -472,8 +479,9 @@ def measure_train(args, model, dist, rank, world, dev, gpu, W, batch_mode, steps
 
     def average():
         """Reference sync mode: theta <- mean_i theta_i over all workers of the job
-        (device replica mean -> RCCL all-reduce -> write-back into every replica)."""
-        if batch_mode:
+        (device replica mean -> RCCL all-reduce -> write-back into every replica); already
+        done if run() fused it into its last launch."""
+        if batch_mode or state.pop("averaged", False):
             return
         if gpu:
             t.average_replicas(dist.all_reduce_sum_ if world > 1 else None, R * world)
@@ -494,11 +502,11 @@ def measure_train(args, model, dist, rank, world, dev, gpu, W, batch_mode, steps
         t.prepare_graphs(allreduce_path=batch_mode and world > 1 and not args.overlap and not sync_local)
     if gpu and args.validation_split > 0:
         t._eval_exe()   # the epoch-end validation executor exists before the timed region
-    run(warmup)
+    run(warmup, then_average=True)
     average()
     sync()
     t0 = time.perf_counter()
-    rows_done = run(steps)
+    rows_done = run(steps, then_average=True)
     average()
     sync()
     dt = time.perf_counter() - t0

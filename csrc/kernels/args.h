@@ -193,12 +193,12 @@ constexpr int PM_NTU = 2;      // layer-1 column tiles (and layer-2 row tiles) a
 // XT (sync across ranks: replica 0's workgroup q has the job-wide sum of its tile in its
 // total slab; the other replicas read it there instead of every rank's slab)
 enum PmFlag : int { PMF_PART = 0, PMF_BWD = 1, PMF_W = 2, PMF_A0 = 3, PMF_D2 = 4, PMF_GO = 5, PMF_X = 6, PMF_GR = 7,
-                    PMF_XT = 8, PMF_XS = 9, PMF_N = 10 };
+                    PMF_XT = 8, PMF_XS = 9, PMF_AVG = 10, PMF_N = 11 };
 // sticky error codes: the wait that timed out (PERR_GRID: the grid was not resident --
 // nothing was modified, the chunk can be re-run on another plan)
 enum PmErr : unsigned { PERR_L0_BWD = 1, PERR_CHAIN_PART = 2, PERR_CHAIN_BWD = 3, PERR_CHAIN_PREV = 4,
                         PERR_DW_A0 = 5, PERR_DW_D2 = 6, PERR_XCHG = 7, PERR_PS = 8, PERR_GRID = 9,
-                        PERR_CHAIN_GR = 10, PERR_XRANK = 11, PERR_PLACE = 12 };
+                        PERR_CHAIN_GR = 10, PERR_XRANK = 11, PERR_PLACE = 12, PERR_AVG = 13 };
 constexpr int PM_XSLOT = 7 * 1024;   // floats of one workgroup's exchange slab (sync)
 struct PersistArgs {
   int R, B, nsteps;
@@ -271,6 +271,15 @@ struct PersistArgs {
   unsigned* err;                    // sticky error word (a timed-out wait), read by the host
   long long timeout;                // spin limit in s_memrealtime ticks (100 MHz)
   long long* stamps;                // diagnostics: [block][PM_STAMP_STEPS][32] s_memrealtime (null = off)
+  // fused replica averaging at the end of the launch (the reference's fit-end average,
+  // spark_model.py:221-227, when the host asks for it right after this chunk): every
+  // workgroup's masters reach P write-through, a grid barrier (counter flag_at(0, PMF_AVG)),
+  // then workgroup b averages its slice of the avg_n parameters over the R replicas (fp64 in
+  // replica order, * avg_scale) into avg_out (if set) and every replica's P (if avg_p)
+  int avg_end, avg_p;
+  long long avg_n;
+  double avg_scale;
+  float* avg_out;
 };
 constexpr int PM_STAMP_STEPS = 8;
 

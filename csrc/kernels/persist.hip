@@ -184,6 +184,11 @@ __device__ __forceinline__ void stw4(rsrc_t r, int v, int s, f32x4 x) {
 }
 // cross-replica hand-off stores (the sync exchange slabs): write-through, or plain in the
 // exchange-local instance
+// a master written back to P at the end of the launch: write-through, so the fused averaging's
+// readers on other XCDs find it (4-byte agent-scope store = sc1)
+__device__ __forceinline__ void pst(float* p, float v) {
+  __hip_atomic_store((gu32*)(reinterpret_cast<unsigned*>(p)), __builtin_bit_cast(unsigned, v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 constexpr int SX_AUX = EA_PLOCAL == 2 ? 0 : 16;
 __device__ __forceinline__ void stx4(rsrc_t r, int v, int s, f32x4 x) {
   __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, x), r, v * 4, s * 4, SX_AUX);
@@ -1048,7 +1053,7 @@ __device__ __forceinline__ void l0_role(const PersistArgs& a, float* smem, int r
   for (int e = tid; e < kreal * cw; e += 256) {
     const int k = e / cw, nn = e - k * cw;
     const float v = sW[k * WS + nn];
-    P[a.p_off0 + (long long)(k0 + k) * H0 + n0 + nn] = v;
+    pst(P + (a.p_off0 + (long long)(k0 + k) * H0 + n0 + nn), v);
 #pragma unroll
     for (int par = 0; par < 2; ++par) {
       Wsh[par * a.wsh_par + (long long)(k0 + k) * a.Np[0] + n0 + nn] = v;
@@ -1071,7 +1076,7 @@ __device__ __forceinline__ void l0_role(const PersistArgs& a, float* smem, int r
   }
   if (bown) {
     const long long pi = a.p_off0 + (long long)a.K0 * H0 + n0 + tid;
-    P[pi] = bw;
+    pst(P + (pi), bw);
     if (np > 0) S[pi] = bs0;
     if (np > 1) S[a.op.s_plane + pi] = bs1;
   }
@@ -1385,7 +1390,7 @@ __device__ __forceinline__ void l0_role_v2(const PersistArgs& a, float* smem, in
   for (int e = tid; e < kreal * CW; e += 256) {
     const int k = e / CW, nn = e - k * CW;
     const float v = sW[k * WS + nn];
-    P[a.p_off0 + (long long)(k0 + k) * H0 + n0 + nn] = v;
+    pst(P + (a.p_off0 + (long long)(k0 + k) * H0 + n0 + nn), v);
     if (a.imgs) {
 #pragma unroll
       for (int par = 0; par < 2; ++par) {
@@ -1394,7 +1399,7 @@ __device__ __forceinline__ void l0_role_v2(const PersistArgs& a, float* smem, in
       }
     }
   }
-  if (bown) P[a.p_off0 + (long long)a.K0 * H0 + n0 + tid] = bw;
+  if (bown) pst(P + (a.p_off0 + (long long)a.K0 * H0 + n0 + tid), bw);
 }
 
 // ============================================================== chain (rows)
@@ -2190,7 +2195,7 @@ __device__ __forceinline__ void chain_role(const PersistArgs& a, float* smem, in
     for (int qq = 0; qq < 4; ++qq) {
       const int k = rt * 16 + 4 * g + qq, nn = (j + a.nch * c) * 16 + i16;
       const long long pi = a.p_off1 + (long long)k * H1 + nn;
-      P[pi] = wm[4 * u + qq];
+      pst(P + (pi), wm[4 * u + qq]);
       if (np > 0) S[pi] = ws0[4 * u + qq];
       if (np > 1) S[a.op.s_plane + pi] = ws1[4 * u + qq];
 #pragma unroll
@@ -2205,7 +2210,7 @@ __device__ __forceinline__ void chain_role(const PersistArgs& a, float* smem, in
     for (int qq = 0; qq < 4; ++qq) {
       const int k = (j + a.nch * w) * 16 + 4 * g + qq;
       const long long pi = a.p_off2 + (long long)k * C + i16;
-      P[pi] = wm[4 * TU + qq];
+      pst(P + (pi), wm[4 * TU + qq]);
       if (np > 0) S[pi] = ws0[4 * TU + qq];
       if (np > 1) S[a.op.s_plane + pi] = ws1[4 * TU + qq];
 #pragma unroll
@@ -2217,7 +2222,7 @@ __device__ __forceinline__ void chain_role(const PersistArgs& a, float* smem, in
   }
   if (b1own || b2own) {
     const long long pi = b1own ? a.p_off1 + (long long)H0 * H1 + b1n : a.p_off2 + (long long)H1 * C + lane;
-    P[pi] = bm;
+    pst(P + (pi), bm);
     if (np > 0) S[pi] = bst0;
     if (np > 1) S[a.op.s_plane + pi] = bst1;
   }
@@ -2557,7 +2562,7 @@ __device__ __forceinline__ void dw_role_v2(const PersistArgs& a, float* smem, in
 #pragma unroll
     for (int qq = 0; qq < 4; ++qq) {
       const int k = rt * 16 + 4 * g + qq, nn = (d + nd * c) * 16 + i16;
-      P[a.p_off1 + (long long)k * H1 + nn] = wm[4 * u + qq];
+      pst(P + (a.p_off1 + (long long)k * H1 + nn), wm[4 * u + qq]);
       if (!a.imgs) continue;
 #pragma unroll
       for (int par = 0; par < 2; ++par) {
@@ -2570,7 +2575,7 @@ __device__ __forceinline__ void dw_role_v2(const PersistArgs& a, float* smem, in
 #pragma unroll
     for (int qq = 0; qq < 4; ++qq) {
       const int k = (d + nd * w) * 16 + 4 * g + qq;
-      P[a.p_off2 + (long long)k * C + i16] = wm[4 * TU + qq];
+      pst(P + (a.p_off2 + (long long)k * C + i16), wm[4 * TU + qq]);
       if (!a.imgs) continue;
 #pragma unroll
       for (int par = 0; par < 2; ++par) {
@@ -2579,10 +2584,47 @@ __device__ __forceinline__ void dw_role_v2(const PersistArgs& a, float* smem, in
       }
     }
   }
-  if (b1own || b2own) P[b1own ? a.p_off1 + (long long)H0 * H1 + b1n : a.p_off2 + (long long)H1 * C + lane] = bm;
+  if (b1own || b2own) pst(P + (b1own ? a.p_off1 + (long long)H0 * H1 + b1n : a.p_off2 + (long long)H1 * C + lane), bm);
 }
 
 }  // namespace
+
+// ---- fused replica averaging (PersistArgs::avg_end): after every role's epilogue -- its
+//      masters in P, stored write-through and drained -- each workgroup arrives at the grid
+//      counter, waits for all R x wgs, then averages its slice of the parameters over the R
+//      replicas: fp64 sums in replica order (the replica_average kernel's numerics), scaled,
+//      into avg_out and / or every replica's P.  A launch whose error word is set skips it.
+__device__ __forceinline__ void grid_average(const PersistArgs& a, int b) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  unsigned* ctr = flag_at(a, 0, PMF_AVG);
+  const unsigned tot = (unsigned)(a.R * a.wgs);
+  if (threadIdx.x == 0) __hip_atomic_fetch_add((gu32*)ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (!wait_all(a, ctr, 1, tot, PERR_AVG)) return;
+  if (__hip_atomic_load((gu32*)(a.err), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) return;
+  // element-wise (P's replica stride need not keep 16-byte alignment): 8 replicas' loads in
+  // flight per element; sc1 -- this XCD's L2 never held the other replicas' lines
+  const long long n = a.avg_n, lo = n * b / tot, hi = n * (b + 1) / tot;
+  const rsrc_t pr = ws_rsrc(a.P);
+  for (long long i = lo + threadIdx.x; i < hi; i += 256) {
+    double sm = 0.0;
+    for (int r0 = 0; r0 < a.R; r0 += 8) {
+      float x[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int r = r0 + k < a.R ? r0 + k : r0;
+        x[k] = ldw1(pr, (int)i, (int)((long long)r * a.sP));
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        if (r0 + k < a.R) sm += x[k];
+    }
+    const float m = (float)(sm * a.avg_scale);
+    if (a.avg_out) a.avg_out[i] = m;
+    if (a.avg_p)
+      for (int r = 0; r < a.R; ++r) a.P[(long long)r * a.sP + i] = m;
+  }
+}
 
 template <int H0, int H1, bool FAST, int NPT, bool RELU, bool V2, bool PS = false, bool BF = false>
 __global__ __launch_bounds__(256) void mlp_persist_kernel(PersistArgs a) {
@@ -2614,6 +2656,7 @@ __global__ __launch_bounds__(256) void mlp_persist_kernel(PersistArgs a) {
     if (q < nl0) l0_role<H0, NPT, PS>(a, smem, r, q / a.nc0, q - (q / a.nc0) * a.nc0, q);
     else chain_role<H0, H1, FAST, NPT, RELU, false, PS>(a, smem, r, q - nl0);
   }
+  if (a.avg_end) grid_average(a, b);
 }
 
 // the instances of one hidden width: the specialised MNIST-style one (relu, softmax +

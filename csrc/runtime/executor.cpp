@@ -526,6 +526,13 @@ void Executor::run_chunk(hipStream_t s, int nsteps) const {
     // but the step loop ran 2-3 % slower: profiles/persist_exit_ab_r3.txt)
     PersistArgs a = pm_.args;
     a.nsteps = nsteps;
+    if (pm_.avg) {   // train_chunk_avg: this launch ends with the fused replica averaging
+      a.avg_end = 1;
+      a.avg_p = pm_.avg->avg_p;
+      a.avg_n = pm_.avg->avg_n;
+      a.avg_scale = pm_.avg->avg_scale;
+      a.avg_out = pm_.avg->avg_out;
+    }
     if (a.xr_world > 1) {   // the rank exchange's flag tags continue over launches
       a.xr_tag0 = pm_.xr_steps;
       pm_.xr_steps += (unsigned)nsteps;
@@ -1301,6 +1308,28 @@ void Executor::train_chunk(int nsteps, hipStream_t s) {
   if (nsteps <= 0) return;
   run_chunk(s, nsteps);
   if (!persistent()) advance(nsteps, s);
+}
+
+bool Executor::train_chunk_avg(int nsteps, hipStream_t s, float* out, int write_p, double scale) {
+  // fit granularity on persist.hip only (per-step sync replicas are one model already; the
+  // PS hook's masters belong to the server)
+  if (nsteps <= 0 || !pm_.on || pm_.args.sync || pm_.args.ps_mode || c_.nparams <= 0 ||
+      (long long)c_.R * c_.sP > 0x7fffffffLL / 4)   // buffer offsets of the averaging's loads
+    return false;
+  PersistArgs avg{};
+  avg.avg_p = write_p;
+  avg.avg_n = c_.nparams;
+  avg.avg_scale = scale;
+  avg.avg_out = out;
+  pm_.avg = &avg;
+  try {
+    run_chunk(s, nsteps);
+  } catch (...) {
+    pm_.avg = nullptr;
+    throw;
+  }
+  pm_.avg = nullptr;
+  return true;
 }
 
 void Executor::forward_backward(hipStream_t s) {

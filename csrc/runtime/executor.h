@@ -105,6 +105,11 @@ class Executor {
   // nsteps fused-update steps (+ one counter advance): ONE launch on the persistent
   // plan whatever nsteps is (no graph needed: memset + kernel + advance)
   void train_chunk(int nsteps, hipStream_t s);
+  // the same, on the persistent replica-cluster plan with the replica averaging fused into the
+  // launch's end (persist.hip grid_average): scale * sum_r P_r -> out (if not null) and every
+  // replica's P (if write_p).  false (nothing launched): the plan cannot -- the caller runs
+  // train_chunk and its own averaging
+  bool train_chunk_avg(int nsteps, hipStream_t s, float* out, int write_p, double scale);
   void forward_backward(hipStream_t s);    // gradient path: writes G (no update)
   void apply(hipStream_t s);               // gradient path: optimizer apply + advance
   void eval_chunk(long long chunk, const EvalSource& src, hipStream_t s);
@@ -208,6 +213,7 @@ class Executor {
     size_t flag_bytes = 0;
     mutable unsigned xr_steps = 0;   // steps run with the rank exchange (its flag tags)
     int local = 0;                   // 1: XCD-local instance (ea_persist_local), 2: exchange-local (ea_persist_xlocal)
+    mutable PersistArgs* avg = nullptr;   // train_chunk_avg: the averaging fields of the next launch
   } pm_;
   float* d_pws_ = nullptr;         // persistent plan: per-replica exchange workspace
   unsigned* d_pflags_ = nullptr;   // [R][PMF_N][PM_MAXWG] flags (zero at every launch: setup, then the post kernel)

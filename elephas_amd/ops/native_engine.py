@@ -185,6 +185,7 @@ class NativeTrainer(TrainerBase):
         self.sync = bool(sync) and R > 1
         self._grad_scale = 1.0
         self._no_local = False   # set after a launch found a replica's workgroups on two XCDs (PERR_PLACE)
+        self._fused_done = False  # the last _run_steps ended with the fused replica averaging
         # ps_hook: the persistent plan will push / pull a device parameter server every
         # step inside the launch (attach_param_server), so it keeps the V1 roles
         self.ps_hook = bool(ps_hook)
@@ -708,6 +709,46 @@ class NativeTrainer(TrainerBase):
         ev.record(self.stream)
         _PERSIST_LAST[self.dev.index] = (self.s, ev)
 
+    def run_steps_and_average(self, nsteps: int, allreduce=None, n_total: Optional[int] = None,
+                              use_graph: bool = True):
+        """run_steps(nsteps) then average_replicas(allreduce, n_total) -- the reference's
+        train-then-average (spark_model.py:217-228) -- with the averaging fused into the end
+        of the last persistent launch where the plan allows it (persist.hip grid_average:
+        one launch fewer per fit, ~10 us at the bench's 20-step shape): the replica mean
+        (world 1) or the replica sum for the caller's all-reduce lands in the same buffer
+        average_replicas fills.  Returns that buffer, as average_replicas does."""
+        fusable = (nsteps > 0 and self.exe.persistent() and not self.sync and self._ps is None
+                   and getattr(self, "_xr", None) is None and self.exe.persist_variant()[0] in (1, 2)
+                   and os.environ.get("ELEPHAS_AMD_FUSED_AVG", "1") != "0")
+        if not fusable:
+            self.run_steps(nsteps, use_graph=use_graph)
+            return self.average_replicas(allreduce, n_total)
+        n_total = int(n_total or self.R)
+        avg = getattr(self, "_avg_buf", None)
+        if avg is None or avg.numel() != self.n:
+            with torch.cuda.stream(self.stream):
+                avg = self._avg_buf = torch.empty(self.n, dtype=torch.float32, device=self.dev)
+        fused = (avg.data_ptr(), 1, 1.0 / n_total) if allreduce is None else (avg.data_ptr(), 0, 1.0)
+        if self.persist_cus:
+            self._run_steps(nsteps, use_graph, fused)
+        else:
+            with _persist_lock(self.dev.index):
+                self._persist_fence()
+                try:
+                    self._run_steps(nsteps, use_graph, fused)
+                finally:
+                    self._persist_mark()
+        if not self._fused_done:   # the plan declined (train_chunk_avg false): the separate kernel
+            return self.average_replicas(allreduce, n_total)
+        with torch.cuda.stream(self.stream):
+            if allreduce is not None:
+                allreduce(avg)
+                avg.mul_(1.0 / n_total)
+                self.P.copy_(avg.expand_as(self.P))
+            self._images_stale = True
+        self._exit()
+        return avg
+
     def run_steps(self, nsteps: int, use_graph: bool = True):
         """Launch nsteps fused training steps on self.stream (asynchronous)."""
         if nsteps <= 0:
@@ -733,7 +774,8 @@ class NativeTrainer(TrainerBase):
     def _sync_in_launch(self) -> bool:
         return bool(self.exe.persistent() and self.exe.persist_variant()[2] and getattr(self, "_sync_equal", False))
 
-    def _run_steps(self, nsteps: int, use_graph: bool):
+    def _run_steps(self, nsteps: int, use_graph: bool, fused_avg=None):
+        self._fused_done = False
         if self.exe.persistent():
             # one persistent launch per chunk of up to PERSIST_CHUNK steps, a remainder
             # included (the kernel takes its step count at launch): a chunk is two
@@ -745,7 +787,12 @@ class NativeTrainer(TrainerBase):
                 self._images_stale = True   # the kernel updates the masters only (V2)
             while nsteps > 0:
                 n = min(nsteps, self.GRAPH_CHUNK)
-                self.exe.train_chunk(n, self.s)
+                if fused_avg is not None and n == nsteps:   # the last chunk ends with the averaging
+                    self._fused_done = bool(self.exe.train_chunk_avg(n, self.s, *fused_avg))
+                    if not self._fused_done:
+                        self.exe.train_chunk(n, self.s)
+                else:
+                    self.exe.train_chunk(n, self.s)
                 nsteps -= n
             return
         self._ensure_images()

@@ -528,3 +528,41 @@ def test_persist_xcd_local_instance_is_bit_exact(monkeypatch, case):
     for a, b in zip(hl, hg):
         for key in a:
             np.testing.assert_array_equal(a[key], b[key])
+
+
+@pytest.mark.parametrize("v2,allreduce", [("1", False), ("0", False), ("1", True)])
+def test_fused_average_equals_separate_kernel(monkeypatch, v2, allreduce):
+    """run_steps_and_average (the replica averaging fused into the last persistent launch:
+    grid barrier, then every workgroup averages its slice of the parameters over the replicas
+    in fp64, replica order) == run_steps + the replica_average kernel, bit for bit -- the
+    world-1 mean written into every replica, and the replica-sum form an all-reduce follows
+    (identity here) -- on V2 and V1, over a chunk boundary."""
+    from elephas_amd.models import initializers
+    from elephas_amd.models.optimizers import SGD
+    initializers.set_seed(61)
+    model = _mlp(784, [128, 128], 10, dropout=0.2)
+    model.compile(SGD(0.1), "categorical_crossentropy", ["acc"])
+    xs, ys = _shards([64 * 12] * 8, 784, 10, seed=29)
+    monkeypatch.setenv("ELEPHAS_AMD_PERSIST_V2", v2)
+    out = []
+    for fused in (True, False):
+        t = _trainer(model, 8, 64, persist=1, seed=4)
+        assert t.persist_variant == (2 if v2 == "1" else 1), t.plan_name()
+        t.set_data(xs, ys, 0.0, shuffle=False)
+        t.GRAPH_CHUNK = 6
+        t.begin_epoch()
+        ar = (lambda g: None) if allreduce else None
+        if fused:
+            avg = t.run_steps_and_average(10, ar, 8)
+            assert t._fused_done, "the persistent plan must fuse the averaging"
+        else:
+            t.run_steps(10)
+            avg = t.average_replicas(ar, 8)
+        torch.cuda.synchronize()
+        t.check()
+        out.append((t.get_weights_flat(), avg.cpu().numpy().copy()))
+    (wf, af), (ws, as_) = out
+    assert np.array_equal(af, as_), np.abs(af - as_).max()
+    assert np.array_equal(wf, ws), np.abs(wf - ws).max()
+    for r in range(1, 8):
+        assert np.array_equal(wf[r], wf[0])

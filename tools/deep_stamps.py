@@ -3,7 +3,7 @@ s_memrealtime stamps (10 ns ticks): per step, the median (over the replica's wor
 of every phase's start / publication relative to the replica's median step start, and
 the step period.
 
-  python tools/deep_stamps.py [dims] [R] [B] [steps] [dropout]
+  python tools/deep_stamps.py [dims] [R] [B] [steps] [dropout] [sgd|adam]
   e.g. python tools/deep_stamps.py 93,512,512,512,9 8 128 8 0.5     (Otto, the default)
 """
 import os
@@ -37,10 +37,11 @@ def main():
     B = int(sys.argv[3]) if len(sys.argv) > 3 else 128
     nst = int(sys.argv[4]) if len(sys.argv) > 4 else 8
     drop = float(sys.argv[5]) if len(sys.argv) > 5 else 0.5
+    opt = sys.argv[6] if len(sys.argv) > 6 else "sgd"
     os.environ.setdefault("ELEPHAS_AMD_DEEP", "2")
     from elephas_amd import config
     from elephas_amd.models import Sequential, Dense, Dropout
-    from elephas_amd.models.optimizers import SGD
+    from elephas_amd.models.optimizers import SGD, Adam
     from elephas_amd.ops.plan import build_plan
     from elephas_amd.ops.native_engine import NativeTrainer
     config.set_policy("float32")
@@ -53,7 +54,7 @@ def main():
         if drop:
             m.add(Dropout(drop))
     m.add(Dense(dims[-1], activation="softmax"))
-    m.compile(SGD(0.01), "categorical_crossentropy", ["acc"])
+    m.compile(Adam(0.01) if opt == "adam" else SGD(0.01), "categorical_crossentropy", ["acc"])
     t = NativeTrainer(m, build_plan(m), R, B, torch.device("cuda"), seed=1, persist=1)
     print("plan", t.plan_name())
     geo = t.exe.deep_geometry()
