@@ -733,6 +733,14 @@ __device__ __forceinline__ void dw_last(const DeepArgs& a, float* smem, const Ct
   const int C = lb.N, C16 = lb.N16, NCT = C16 >> 4, ldc = C16 + 4;
   const bool rows = x.j < la.T, bias = x.j == 0 && lb.has_bias;
   if (!rows && !bias) return;
+  // the bias element's optimizer state, loaded before the dZ staging (the last wave: one unit per lane)
+  const bool bl_ok = !SYNC && bias && x.tid >= 448 && x.tid - 448 < C;
+  OptPre<1> bpre;
+  {
+    const long long pb[1] = {lb.p_off + (long long)lb.K * C + (x.tid >= 448 ? x.tid - 448 : 0)};
+    const bool okb[1] = {bl_ok};
+    opt_pre<SYNC ? OPK_SGD0 : OPK, 1>(a, x, os, pb, okb, bpre);
+  }
   float* sd = smem + a.l_stage;   // dZ_{L-1} [Bp][C16 + 4]
   const int q4n = C16 >> 2, tot = a.Bp * q4n;
   for (int e = x.tid; e < tot; e += NTH) {
@@ -789,7 +797,7 @@ __device__ __forceinline__ void dw_last(const DeepArgs& a, float* smem, const Ct
       st1(x.xs, c, x.xp + a.x_b[L - 1], db);
     } else {
       float* bl = smem + lb.l_b;
-      const float b = upd<OPK>(a, x, os, lb.p_off + (long long)lb.K * C + c, bl[c], db);
+      const float b = upd_p<OPK>(a, x, os, lb.p_off + (long long)lb.K * C + c, bl[c], db, bpre.s0[0], bpre.s1[0]);
       bl[c] = b;
       st1(x.rs, c, a.o_bl, b);
     }
@@ -805,6 +813,12 @@ __device__ __forceinline__ void bias_tile(const DeepArgs& a, float* smem, const 
   const DeepLayer ly = a.ly[l];
   if (x.j >= ly.T || !ly.has_bias) return;
   const int J0 = 16 * x.j, c = x.tid & 15;
+  OptPre<1> bpre;   // the bias element's optimizer state, ahead of the column sums
+  {
+    const long long pb[1] = {ly.p_off + (long long)ly.K * ly.N + J0 + c};
+    const bool okb[1] = {!SYNC && x.tid < 16 && J0 + x.tid < ly.N};
+    opt_pre<SYNC ? OPK_SGD0 : OPK, 1>(a, x, os, pb, okb, bpre);
+  }
   float sm = 0.f;
 #pragma unroll
   for (int k = 0; k < DP_ROWS / 32; ++k) {
@@ -822,7 +836,8 @@ __device__ __forceinline__ void bias_tile(const DeepArgs& a, float* smem, const 
       st1(x.xs, x.tid, x.xp + a.x_b[l], db);
     } else {
       float* bt = smem + ly.l_b;
-      bt[x.tid] = upd<OPK>(a, x, os, ly.p_off + (long long)ly.K * ly.N + J0 + x.tid, bt[x.tid], db);
+      bt[x.tid] = upd_p<OPK>(a, x, os, ly.p_off + (long long)ly.K * ly.N + J0 + x.tid, bt[x.tid], db, bpre.s0[0],
+                             bpre.s1[0]);
     }
   }
   __syncthreads();
@@ -845,6 +860,7 @@ __device__ __forceinline__ void bw_phase(const DeepArgs& a, float* smem, const C
   // this workgroup's bias tile j of layer l: summed from the staged chunk that holds it
   const bool btile = x.j < ly.T && ly.has_bias;
   const int hb = (16 * x.j) / CW, cb = 16 * x.j - hb * CW;
+
   const int I0 = 16 * x.j, Bp = a.Bp, ldat = Bp + 4, ldr = ly.N16 + 4;
   const int rt = x.w % a.RT, kp = x.w / a.RT;
   const int f = x.w & 3, hh = x.w >> 2;
@@ -1013,13 +1029,17 @@ __device__ __forceinline__ void dw0_phase(const DeepArgs& a, float* smem, const 
   float* w0t = smem + l0.l_w;
   const float* dz0 = smem + a.l_dz0;
   if (x.tid < 16 && l0.has_bias && J0 + x.tid < l0.N) {
+    OptPre<1> bpre;   // the state load overlaps the column sum
+    const long long pb[1] = {l0.p_off + (long long)l0.K * l0.N + J0 + x.tid};
+    const bool okb[1] = {!SYNC};
+    opt_pre<SYNC ? OPK_SGD0 : OPK, 1>(a, x, os, pb, okb, bpre);
     float db = 0.f;
     for (int row = 0; row < Bp; ++row) db += dz0[x.tid * ldz + row];
     if constexpr (SYNC) {
       st1(x.xs, x.tid, x.xp + a.x_b0, db);
     } else {
       float* bt = smem + l0.l_b;
-      bt[x.tid] = upd<OPK>(a, x, os, l0.p_off + (long long)l0.K * l0.N + J0 + x.tid, bt[x.tid], db);
+      bt[x.tid] = upd_p<OPK>(a, x, os, pb[0], bt[x.tid], db, bpre.s0[0], bpre.s1[0]);
     }
   }
   const int nfg = (Kx + 63) >> 6;
