@@ -184,10 +184,14 @@ __device__ __forceinline__ void stw4(rsrc_t r, int v, int s, f32x4 x) {
 }
 // cross-replica hand-off stores (the sync exchange slabs): write-through, or plain in the
 // exchange-local instance
-// a master written back to P at the end of the launch: write-through, so the fused averaging's
-// readers on other XCDs find it (4-byte agent-scope store = sc1)
-__device__ __forceinline__ void pst(float* p, float v) {
-  __hip_atomic_store((gu32*)(reinterpret_cast<unsigned*>(p)), __builtin_bit_cast(unsigned, v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+// a master written back to P at the end of the launch: plain -- or, when the launch ends with the
+// fused averaging, write-through (4-byte agent-scope store = sc1) so its readers on other XCDs
+// find it.  (Measured: the 4-byte write-through epilogue costs more than the launch the fused
+// averaging saves -- 20.0 vs 19.3 us per step at the bench's 20-step shape -- so the bench
+// keeps the separate replica_average kernel; ELEPHAS_AMD_FUSED_AVG=1 selects this path)
+__device__ __forceinline__ void pst(const PersistArgs& a, float* p, float v) {
+  if (a.avg_end) __hip_atomic_store((gu32*)(reinterpret_cast<unsigned*>(p)), __builtin_bit_cast(unsigned, v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else *p = v;
 }
 constexpr int SX_AUX = EA_PLOCAL == 2 ? 0 : 16;
 __device__ __forceinline__ void stx4(rsrc_t r, int v, int s, f32x4 x) {
@@ -1053,7 +1057,7 @@ __device__ __forceinline__ void l0_role(const PersistArgs& a, float* smem, int r
   for (int e = tid; e < kreal * cw; e += 256) {
     const int k = e / cw, nn = e - k * cw;
     const float v = sW[k * WS + nn];
-    pst(P + (a.p_off0 + (long long)(k0 + k) * H0 + n0 + nn), v);
+    pst(a, P + (a.p_off0 + (long long)(k0 + k) * H0 + n0 + nn), v);
 #pragma unroll
     for (int par = 0; par < 2; ++par) {
       Wsh[par * a.wsh_par + (long long)(k0 + k) * a.Np[0] + n0 + nn] = v;
@@ -1076,7 +1080,7 @@ __device__ __forceinline__ void l0_role(const PersistArgs& a, float* smem, int r
   }
   if (bown) {
     const long long pi = a.p_off0 + (long long)a.K0 * H0 + n0 + tid;
-    pst(P + (pi), bw);
+    pst(a, P + (pi), bw);
     if (np > 0) S[pi] = bs0;
     if (np > 1) S[a.op.s_plane + pi] = bs1;
   }
@@ -1390,7 +1394,7 @@ __device__ __forceinline__ void l0_role_v2(const PersistArgs& a, float* smem, in
   for (int e = tid; e < kreal * CW; e += 256) {
     const int k = e / CW, nn = e - k * CW;
     const float v = sW[k * WS + nn];
-    pst(P + (a.p_off0 + (long long)(k0 + k) * H0 + n0 + nn), v);
+    pst(a, P + (a.p_off0 + (long long)(k0 + k) * H0 + n0 + nn), v);
     if (a.imgs) {
 #pragma unroll
       for (int par = 0; par < 2; ++par) {
@@ -1399,7 +1403,7 @@ __device__ __forceinline__ void l0_role_v2(const PersistArgs& a, float* smem, in
       }
     }
   }
-  if (bown) pst(P + (a.p_off0 + (long long)a.K0 * H0 + n0 + tid), bw);
+  if (bown) pst(a, P + (a.p_off0 + (long long)a.K0 * H0 + n0 + tid), bw);
 }
 
 // ============================================================== chain (rows)
@@ -2195,7 +2199,7 @@ __device__ __forceinline__ void chain_role(const PersistArgs& a, float* smem, in
     for (int qq = 0; qq < 4; ++qq) {
       const int k = rt * 16 + 4 * g + qq, nn = (j + a.nch * c) * 16 + i16;
       const long long pi = a.p_off1 + (long long)k * H1 + nn;
-      pst(P + (pi), wm[4 * u + qq]);
+      pst(a, P + (pi), wm[4 * u + qq]);
       if (np > 0) S[pi] = ws0[4 * u + qq];
       if (np > 1) S[a.op.s_plane + pi] = ws1[4 * u + qq];
 #pragma unroll
@@ -2210,7 +2214,7 @@ __device__ __forceinline__ void chain_role(const PersistArgs& a, float* smem, in
     for (int qq = 0; qq < 4; ++qq) {
       const int k = (j + a.nch * w) * 16 + 4 * g + qq;
       const long long pi = a.p_off2 + (long long)k * C + i16;
-      pst(P + (pi), wm[4 * TU + qq]);
+      pst(a, P + (pi), wm[4 * TU + qq]);
       if (np > 0) S[pi] = ws0[4 * TU + qq];
       if (np > 1) S[a.op.s_plane + pi] = ws1[4 * TU + qq];
 #pragma unroll
@@ -2222,7 +2226,7 @@ __device__ __forceinline__ void chain_role(const PersistArgs& a, float* smem, in
   }
   if (b1own || b2own) {
     const long long pi = b1own ? a.p_off1 + (long long)H0 * H1 + b1n : a.p_off2 + (long long)H1 * C + lane;
-    pst(P + (pi), bm);
+    pst(a, P + (pi), bm);
     if (np > 0) S[pi] = bst0;
     if (np > 1) S[a.op.s_plane + pi] = bst1;
   }
@@ -2562,7 +2566,7 @@ __device__ __forceinline__ void dw_role_v2(const PersistArgs& a, float* smem, in
 #pragma unroll
     for (int qq = 0; qq < 4; ++qq) {
       const int k = rt * 16 + 4 * g + qq, nn = (d + nd * c) * 16 + i16;
-      pst(P + (a.p_off1 + (long long)k * H1 + nn), wm[4 * u + qq]);
+      pst(a, P + (a.p_off1 + (long long)k * H1 + nn), wm[4 * u + qq]);
       if (!a.imgs) continue;
 #pragma unroll
       for (int par = 0; par < 2; ++par) {
@@ -2575,7 +2579,7 @@ __device__ __forceinline__ void dw_role_v2(const PersistArgs& a, float* smem, in
 #pragma unroll
     for (int qq = 0; qq < 4; ++qq) {
       const int k = (d + nd * w) * 16 + 4 * g + qq;
-      pst(P + (a.p_off2 + (long long)k * C + i16), wm[4 * TU + qq]);
+      pst(a, P + (a.p_off2 + (long long)k * C + i16), wm[4 * TU + qq]);
       if (!a.imgs) continue;
 #pragma unroll
       for (int par = 0; par < 2; ++par) {
@@ -2584,7 +2588,7 @@ __device__ __forceinline__ void dw_role_v2(const PersistArgs& a, float* smem, in
       }
     }
   }
-  if (b1own || b2own) pst(P + (b1own ? a.p_off1 + (long long)H0 * H1 + b1n : a.p_off2 + (long long)H1 * C + lane), bm);
+  if (b1own || b2own) pst(a, P + (b1own ? a.p_off1 + (long long)H0 * H1 + b1n : a.p_off2 + (long long)H1 * C + lane), bm);
 }
 
 }  // namespace

@@ -472,7 +472,11 @@ class NativeTrainer(TrainerBase):
 
     def _eval_exe(self):
         if self.exe_eval is None:
-            with torch.cuda.device(self.dev):
+            # the workspace's zero fill on the executor stream: the eval kernels run there, and a
+            # fill on another stream could land after the first validation pass's writes (its
+            # padded columns must be zero; reused allocator memory is not) -- seen as a wrong
+            # first-epoch val_loss now and then on the Otto shape in a long test process
+            with torch.cuda.device(self.dev), torch.cuda.stream(self.stream):
                 self.ws_eval = self._alloc_workspace(self.eval_B)
             self.exe_eval = self.C.Executor(self._cfg(self.ws_eval))
         return self.exe_eval
@@ -713,13 +717,14 @@ class NativeTrainer(TrainerBase):
                               use_graph: bool = True):
         """run_steps(nsteps) then average_replicas(allreduce, n_total) -- the reference's
         train-then-average (spark_model.py:217-228) -- with the averaging fused into the end
-        of the last persistent launch where the plan allows it (persist.hip grid_average:
-        one launch fewer per fit, ~10 us at the bench's 20-step shape): the replica mean
-        (world 1) or the replica sum for the caller's all-reduce lands in the same buffer
-        average_replicas fills.  Returns that buffer, as average_replicas does."""
+        of the last persistent launch where the plan allows it and ELEPHAS_AMD_FUSED_AVG=1
+        (persist.hip grid_average: one launch fewer per fit; measured slower at the bench's
+        20-step shape -- the write-through epilogue it needs costs more -- so off by default):
+        the replica mean (world 1) or the replica sum for the caller's all-reduce lands in the
+        same buffer average_replicas fills.  Returns that buffer, as average_replicas does."""
         fusable = (nsteps > 0 and self.exe.persistent() and not self.sync and self._ps is None
                    and getattr(self, "_xr", None) is None and self.exe.persist_variant()[0] in (1, 2)
-                   and os.environ.get("ELEPHAS_AMD_FUSED_AVG", "1") != "0")
+                   and os.environ.get("ELEPHAS_AMD_FUSED_AVG", "0") == "1")
         if not fusable:
             self.run_steps(nsteps, use_graph=use_graph)
             return self.average_replicas(allreduce, n_total)
@@ -1086,7 +1091,7 @@ class NativeTrainer(TrainerBase):
             n2 = max(need, 2 * cap["n"] if cap else 0)
             with torch.cuda.device(self.dev):
                 cap = self._ebuf = dict(n=n2, X=None, Y=None, pred=None, host=None)
-        with torch.cuda.device(self.dev):
+        with torch.cuda.device(self.dev), torch.cuda.stream(self.stream):   # fills ordered before the eval kernels
             if cap["X"] is None:
                 cap["X"] = torch.zeros(cap["n"], self.Kp0, dtype=self.T, device=self.dev)
             if with_y and cap["Y"] is None:

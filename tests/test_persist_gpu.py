@@ -544,6 +544,7 @@ def test_fused_average_equals_separate_kernel(monkeypatch, v2, allreduce):
     model.compile(SGD(0.1), "categorical_crossentropy", ["acc"])
     xs, ys = _shards([64 * 12] * 8, 784, 10, seed=29)
     monkeypatch.setenv("ELEPHAS_AMD_PERSIST_V2", v2)
+    monkeypatch.setenv("ELEPHAS_AMD_FUSED_AVG", "1")
     out = []
     for fused in (True, False):
         t = _trainer(model, 8, 64, persist=1, seed=4)

@@ -32,7 +32,8 @@ def names(L):
 
 
 def main():
-    dims = [int(v) for v in (sys.argv[1] if len(sys.argv) > 1 else "93,512,512,512,9").split(",")]
+    # dims as 93,512,512,512,9 or 93-512-512-512-9 (tools/gpu.py py: steps split on commas)
+    dims = [int(v) for v in (sys.argv[1] if len(sys.argv) > 1 else "93,512,512,512,9").replace("-", ",").split(",")]
     R = int(sys.argv[2]) if len(sys.argv) > 2 else 8
     B = int(sys.argv[3]) if len(sys.argv) > 3 else 128
     nst = int(sys.argv[4]) if len(sys.argv) > 4 else 8

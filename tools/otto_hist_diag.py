@@ -21,7 +21,9 @@ def main():
     xs, ys = _shards([1000] * 7 + [450], 93, 9, seed=11)
     out = {}
     os.environ["ELEPHAS_AMD_DEEP"] = "-1"
-    for name, persist, local in (("deep_local", -1, "-1"), ("deep_wt", -1, "0"), ("tail", 0, "0")):
+    reps = int(sys.argv[1]) if len(sys.argv) > 1 else 1
+    runs = [(f"deep_local{i}", -1, "-1") for i in range(reps)] + [(f"deep_wt{i}", -1, "0") for i in range(reps)]
+    for name, persist, local in runs + [("tail", 0, "0")]:
         os.environ["ELEPHAS_AMD_PERSIST_LOCAL"] = local
         t = _native(model, 8, 128, seed=7, persist=persist)
         print(name, t.plan_name()[:90])
@@ -30,7 +32,7 @@ def main():
         h = t.fit(2)
         t.check()
         out[name] = (t.get_weights_flat(), h)
-    for name in ("deep_local", "deep_wt"):
+    for name, _, _ in runs:
         w, h = out[name]
         wr, hr = out["tail"]
         print(name, "weights max diff", float(np.abs(w - wr).max()))
@@ -39,6 +41,7 @@ def main():
                 d = np.abs(np.asarray(a[key]) - np.asarray(b[key]))
                 if d.max() > 5e-4:
                     print(f"  replica {r} {key}: {a[key]} vs {b[key]}")
+        print(f"  {name}: per-replica loss epoch 1", [round(float(hh['loss'][0]), 4) for hh in h])
 
 
 if __name__ == "__main__":
