@@ -620,6 +620,8 @@ class NativeTrainer(TrainerBase):
         n, k = x.shape
         if n == 0:
             return
+        if stream is None:
+            self._enter()   # after the caller's pending work on dst (e.g. its zero fill)
         s = int((stream or self.stream).cuda_stream)
         if dst.shape[-1] < k or dst.stride(-1) != 1:
             raise ValueError("destination rows too narrow")
