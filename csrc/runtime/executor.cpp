@@ -440,6 +440,9 @@ bool Executor::set_rank_exchange(const std::vector<char*>& bases, int world, int
       rank >= world || pm_.args.wgs > PEER_MAX_BLOCKS)
     return world <= 1;
   PersistArgs& a = pm_.args;
+  // the exchange-local instance's replica exchange was only validated on one rank (the
+  // 2-process tests cannot hold 8 replicas per rank on one GPU): across ranks, write-through
+  if (world > 1 && pm_.local == 2) pm_.local = 0;
   for (int k = 0; k < PEER_MAX_RANKS; ++k) a.xr_base[k] = k < world ? bases[k] : nullptr;
   a.xr_world = world;
   a.xr_rank = rank;
