@@ -755,89 +755,70 @@ __device__ __forceinline__ void tile_epilogue(const GA& ga, const Prob& p, const
       const long long wpar = ((iter + 1) & 1);
       const int krows = p.ones_row >= 0 ? p.ones_row : p.M;
       const int np = S ? opt_planes(p.op) : 0;
-      // passes in groups of GP: the master / state loads of a group's passes are issued
-      // together before its updates (a pass's loads would otherwise wait behind the previous
-      // pass's stores to the same array -- one memory round trip per pass, 8 per tile)
-      constexpr int GP = EUNR > 1 ? 4 : 1;   // the 256x256 tile (rolled passes) has no registers to spare
-#pragma unroll EUNR > 1 ? PASSES / GP : 1
-      for (int pg = 0; pg < PASSES; pg += GP) {
-        float w[GP][8], s0[GP][8], s1[GP][8];
-        bool vec[GP], live[GP];
+#pragma unroll EUNR
+      for (int ps = 0; ps < PASSES; ++ps) {
+        const int row = ps * RPP + t_row, gm = m0 + row, gn0 = n0 + t_c0;
+        if (gm >= p.M || gn0 >= p.N) continue;
+        float v[8];
+        lds8(row, t_c0, v);
+        const long long pidx = p.p_off + (long long)gm * p.N + gn0;
+        if (!upd) {
+          // the raw gradient: the apply kernel (flat.hip) multiplies by grad_scale once
+          // (scaling here too squared it: 1 / world^2 on the multi-rank per-step path)
 #pragma unroll
-        for (int gi = 0; gi < GP; ++gi) {
-          const int ps = pg + gi, row = ps * RPP + t_row, gm = m0 + row, gn0 = n0 + t_c0;
-          live[gi] = ps < PASSES && gm < p.M && gn0 < p.N;
-          vec[gi] = false;
-          zero8(w[gi]);
-          zero8(s0[gi]);
-          zero8(s1[gi]);
-          if (!live[gi] || !upd) continue;
-          const long long pidx = p.p_off + (long long)gm * p.N + gn0;
-          // whole 16-byte-aligned chunks (the common case) move as float4 pairs
-          vec[gi] = gn0 + 8 <= p.N && (pidx & 3) == 0 && (p.op.s_plane & 3) == 0;
-          if (DW_PF && pf_vec[DW_PF ? (ps < PFP ? ps : 0) : 0]) {
+          for (int q = 0; q < 8; ++q)
+            if (gn0 + q < p.N) G[pidx + q] = valid > 0 ? v[q] : 0.f;
+          continue;
+        }
+        float w[8], s0[8], s1[8];
+        // whole 16-byte-aligned chunks (the common case) move as float4 pairs
+        const bool vec = gn0 + 8 <= p.N && (pidx & 3) == 0 && (p.op.s_plane & 3) == 0;
+        if (DW_PF && pf_vec[DW_PF ? ps : 0]) {
 #pragma unroll
-            for (int q = 0; q < 8; ++q) {
-              w[gi][q] = pf_w[DW_PF ? (ps < PFP ? ps : 0) : 0][q];
-              s0[gi][q] = pf_s0[DW_PF ? (ps < PFP ? ps : 0) : 0][q];
-              s1[gi][q] = pf_s1[DW_PF ? (ps < PFP ? ps : 0) : 0][q];
-            }
-          } else if (vec[gi]) {
-            ld8f(P + pidx, w[gi]);
-            if (np > 0) ld8f(S + pidx, s0[gi]);
-            if (np > 1) ld8f(S + p.op.s_plane + pidx, s1[gi]);
-          } else {
+          for (int q = 0; q < 8; ++q) {
+            w[q] = pf_w[DW_PF ? ps : 0][q];
+            s0[q] = pf_s0[DW_PF ? ps : 0][q];
+            s1[q] = pf_s1[DW_PF ? ps : 0][q];
+          }
+        } else if (vec) {
+          ld8f(P + pidx, w);
+          if (np > 0) ld8f(S + pidx, s0); else zero8(s0);
+          if (np > 1) ld8f(S + p.op.s_plane + pidx, s1); else zero8(s1);
+        } else {
 #pragma unroll
-            for (int q = 0; q < 8; ++q) {
-              const bool in = gn0 + q < p.N;
-              w[gi][q] = in ? P[pidx + q] : 0.f;
-              s0[gi][q] = (in && np > 0) ? S[pidx + q] : 0.f;
-              s1[gi][q] = (in && np > 1) ? S[p.op.s_plane + pidx + q] : 0.f;
+          for (int q = 0; q < 8; ++q) {  // loads first
+            const bool in = gn0 + q < p.N;
+            w[q] = in ? P[pidx + q] : 0.f;
+            s0[q] = (in && np > 0) ? S[pidx + q] : 0.f;
+            s1[q] = (in && np > 1) ? S[p.op.s_plane + pidx + q] : 0.f;
+          }
+        }
+        {
+          float gq[8];
+#pragma unroll
+          for (int q = 0; q < 8; ++q) gq[q] = v[q] * p.op.grad_scale;
+          opt_update_v<8>(p.op, w, gq, s0, s1, iter);  // lanes past N are discarded below
+        }
+        if (ps == 0) stamp(ga, 5);
+        if (vec) {
+          st8f(P + pidx, w);
+          if (np > 0) st8f(S + pidx, s0);
+          if (np > 1) st8f(S + p.op.s_plane + pidx, s1);
+        } else {
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            if (gn0 + q < p.N) {
+              P[pidx + q] = w[q];
+              if (np > 0) S[pidx + q] = s0[q];
+              if (np > 1) S[p.op.s_plane + pidx + q] = s1[q];
+            } else {
+              w[q] = 0.f;
             }
           }
         }
-#pragma unroll
-        for (int gi = 0; gi < GP; ++gi) {
-          const int ps = pg + gi, row = ps * RPP + t_row, gm = m0 + row, gn0 = n0 + t_c0;
-          if (!live[gi]) continue;
-          float v[8];
-          lds8(row, t_c0, v);
-          const long long pidx = p.p_off + (long long)gm * p.N + gn0;
-          if (!upd) {
-            // the raw gradient: the apply kernel (flat.hip) multiplies by grad_scale once
-            // (scaling here too squared it: 1 / world^2 on the multi-rank per-step path)
-#pragma unroll
-            for (int q = 0; q < 8; ++q)
-              if (gn0 + q < p.N) G[pidx + q] = valid > 0 ? v[q] : 0.f;
-            continue;
-          }
-          {
-            float gq[8];
-#pragma unroll
-            for (int q = 0; q < 8; ++q) gq[q] = v[q] * p.op.grad_scale;
-            opt_update_v<8>(p.op, w[gi], gq, s0[gi], s1[gi], iter);  // lanes past N are discarded below
-          }
-          if (ps == 0) stamp(ga, 5);
-          if (vec[gi]) {
-            st8f(P + pidx, w[gi]);
-            if (np > 0) st8f(S + pidx, s0[gi]);
-            if (np > 1) st8f(S + p.op.s_plane + pidx, s1[gi]);
-          } else {
-#pragma unroll
-            for (int q = 0; q < 8; ++q) {
-              if (gn0 + q < p.N) {
-                P[pidx + q] = w[gi][q];
-                if (np > 0) S[pidx + q] = s0[gi][q];
-                if (np > 1) S[p.op.s_plane + pidx + q] = s1[gi][q];
-              } else {
-                w[gi][q] = 0.f;
-              }
-            }
-          }
-          if (p.Wsh && gm < krows)
-            st8<T>(p.Wsh, (long long)r * p.sWsh + wpar * p.wsh_par + (long long)gm * p.ldwsh + gn0, w[gi]);
-          sts8(row, t_c0, w[gi]);
-        }
+        if (p.Wsh && gm < krows)
+          st8<T>(p.Wsh, (long long)r * p.sWsh + wpar * p.wsh_par + (long long)gm * p.ldwsh + gn0, w);
+        sts8(row, t_c0, w);
       }
       stamp(ga, 6);
       if (upd && p.WTsh) {
