@@ -55,6 +55,7 @@ namespace {
 using gu32 = __attribute__((address_space(1))) unsigned;
 using rsrc_t = __amdgpu_buffer_rsrc_t;
 typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
+typedef __attribute__((ext_vector_type(2))) unsigned u32x2;
 
 constexpr int NWV = 8;          // waves per workgroup
 constexpr int NTH = NWV * 64;   // threads per workgroup
@@ -107,6 +108,10 @@ __device__ __forceinline__ void st1(rsrc_t r, int v, long long s, float x) {
 }
 __device__ __forceinline__ void st4(rsrc_t r, int v, long long s, f32x4 x) {
   __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, x), r, v * 4, (int)s * 4, DP_ST_AUX);
+}
+__device__ __forceinline__ void st2(rsrc_t r, int v, long long s, float x0, float x1) {
+  const u32x2 u = {__builtin_bit_cast(unsigned, x0), __builtin_bit_cast(unsigned, x1)};
+  __builtin_amdgcn_raw_buffer_store_b64(u, r, v * 4, (int)s * 4, DP_ST_AUX);
 }
 __device__ __forceinline__ f32x4 lds4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
 __device__ __forceinline__ void lds4(float* p, f32x4 v) { *reinterpret_cast<f32x4*>(p) = v; }
@@ -867,9 +872,13 @@ __device__ __forceinline__ void bw_phase(const DeepArgs& a, float* smem, const C
   float* wr = smem + ly.l_w;
   const float* at = smem + lp.l_at;
   float* sdz = smem + a.l_stage;
-  // [4][64][4] DW partials of the second row half, double-buffered by chunk parity (the
-  // first half's waves finish a chunk's update at the top of the NEXT chunk, beside the
-  // other waves' MFMAs); the second buffer is the dZ_0^T stripe, free until the phase's end
+  // [4][64][4] DW partials, double-buffered by chunk parity: both row halves finish a chunk's
+  // update at the top of the NEXT chunk, beside the MFMAs, each for 2 of a lane's 4 rows
+  // (half hh: rows 4 g + 2 hh + {0, 1}) -- slots {0, 1} hold the second half's partials of
+  // the first half's rows, slots {2, 3} the first half's of the second's.  (One half doing
+  // all 4 put the whole update on that half's path to every chunk barrier: Adam on Otto
+  // spent +7 us per 512-wide layer there.)  The second buffer is the dZ_0^T stripe, free
+  // until the phase's end.
   float* spbuf[2] = {sdz + DP_ROWS * LDZ, smem + a.l_dz0};
   const int nch = (ly.N16 + CW - 1) / CW;
   // chunk staging: Bp x 64 floats = Bp * 16 float4, <= 4 per thread, two chunks ahead
@@ -890,43 +899,47 @@ __device__ __forceinline__ void bw_phase(const DeepArgs& a, float* smem, const C
   f32x4 accWp = z4();   // this wave's DW partial of the previous chunk (first row half: pending update)
   // optimizer state of the elements finish(h) updates, loaded at the top of chunk h (stN), in
   // use one chunk later (stC)
-  OptPre<4> stC, stN;
-  auto state_pre = [&](int h, OptPre<4>& st) {
+  const int q0 = 2 * hh;   // this half's rows of a lane: 4 g + q0 + {0, 1}
+  OptPre<2> stC, stN;
+  auto state_pre = [&](int h, OptPre<2>& st) {
     const int c0 = h * CW, cw = ly.N16 - c0 < CW ? ly.N16 - c0 : CW;
-    if (SYNC || hh != 0 || 16 * f >= cw) return;
+    if (SYNC || 16 * f >= cw) return;
     const int col = c0 + 16 * f + x.c16;
-    long long pi[4];
-    bool ok[4];
+    long long pi[2];
+    bool ok[2];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      pi[q] = ly.p_off + (long long)(I0 + 4 * x.g + q) * ly.N + col;
-      ok[q] = I0 + 4 * x.g + q < ly.K && col < ly.N;
+    for (int q = 0; q < 2; ++q) {
+      pi[q] = ly.p_off + (long long)(I0 + 4 * x.g + q0 + q) * ly.N + col;
+      ok[q] = I0 + 4 * x.g + q0 + q < ly.K && col < ly.N;
     }
-    opt_pre<SYNC ? OPK_SGD0 : OPK, 4>(a, x, os, pi, ok, st);
+    opt_pre<SYNC ? OPK_SGD0 : OPK, 2>(a, x, os, pi, ok, st);
   };
   // the first-half waves complete chunk hq's rows J: partial sums, update of the masters of
   // the chunk's columns and their W^T image segment (SYNC: the gradient to the exchange tile)
   auto finish = [&](int hq, f32x4 accq) {
     const int c0 = hq * CW, cw = ly.N16 - c0 < CW ? ly.N16 - c0 : CW;
-    if (hh != 0 || 16 * f >= cw) return;
-    accq += lds4(spbuf[hq & 1] + (f * 64 + x.lane) * 4);
+    if (16 * f >= cw) return;
+    const f32x4 other = lds4(spbuf[hq & 1] + (f * 64 + x.lane) * 4);
+    float gq[2];
+    gq[0] = (hh ? accq[2] : accq[0]) + (hh ? other[2] : other[0]);
+    gq[1] = (hh ? accq[3] : accq[1]) + (hh ? other[3] : other[1]);
     const int col = c0 + 16 * f + x.c16;
     if constexpr (SYNC) {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) st1(x.xs, (4 * x.g + q) * ly.N16 + col, x.xp + a.x_w[l], accq[q]);
+      for (int q = 0; q < 2; ++q) st1(x.xs, (4 * x.g + q0 + q) * ly.N16 + col, x.xp + a.x_w[l], gq[q]);
     } else {
-      f32x4 wv;
+      float wv[2];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int ip = 4 * x.g + q;
+      for (int q = 0; q < 2; ++q) {
+        const int ip = 4 * x.g + q0 + q;
         float wt = wr[ip * ldr + col];
         if (I0 + ip < ly.K && col < ly.N) {
-          wt = upd_p<OPK>(a, x, os, ly.p_off + (long long)(I0 + ip) * ly.N + col, wt, accq[q], stC.s0[q], stC.s1[q]);
+          wt = upd_p<OPK>(a, x, os, ly.p_off + (long long)(I0 + ip) * ly.N + col, wt, gq[q], stC.s0[q], stC.s1[q]);
           wr[ip * ldr + col] = wt;
         }
         wv[q] = wt;
       }
-      st4(x.rs, col * ly.Kx + I0 + 4 * x.g, ly.o_wt, wv);
+      st2(x.rs, col * ly.Kx + I0 + 4 * x.g + q0, ly.o_wt, wv[0], wv[1]);
     }
   };
   auto chunk = [&](int h, f32x4 (&pre)[4]) {
@@ -969,7 +982,11 @@ __device__ __forceinline__ void bw_phase(const DeepArgs& a, float* smem, const C
       for (int rr = 0; rr < rows; ++rr) sm += sdz[(rg * rows + rr) * LDZ + cb + c];
       bred[x.tid] = sm;
     }
-    if (hh == 1) lds4(spbuf[h & 1] + (f * 64 + x.lane) * 4, accW);
+    {   // the other half's rows of this lane: half 1 -> slots 0, 1; half 0 -> slots 2, 3
+      float* sp = spbuf[h & 1] + (f * 64 + x.lane) * 4 + (hh ? 0 : 2);
+      sp[0] = hh ? accW[0] : accW[2];
+      sp[1] = hh ? accW[1] : accW[3];
+    }
     accWp = accW;
     lds_barrier();   // every read of the chunk is done, the partials are out
     if (btile && h == hb && x.tid < 16 && 16 * x.j + x.tid < ly.N) {
@@ -1045,6 +1062,16 @@ __device__ __forceinline__ void dw0_phase(const DeepArgs& a, float* smem, const 
   const int nfg = (Kx + 63) >> 6;
   const int* prow = x.prow + (sp & 1) * DP_ROWS;
   const float* Xr = a.X + (long long)x.r * a.sX;
+  // A stateful rule on a narrow input layer (Otto: 93 features = 2 of the 8 waves) updates
+  // through the LDS: the MFMA waves park their sums in the dead dZ_0 stripe + reduction
+  // buffer and all 8 waves run the update (the state loads and the Adam math of 16 elements
+  // per lane of 2 waves were 5.3 of the 22 us Adam added per Otto step)
+  // (L >= 3 only: a two-layer stack keeps the one-wave-per-feature-group update -- with the
+  // LDS path compiled in, its Adam kernel's results varied run to run on the GPU)
+  constexpr bool STATEFUL = !SYNC && OPK != OPK_SGD0 && L >= 3;
+  const int scr_n = (16 * ldz > 1024 ? 16 * ldz : 1024) + 2048;   // l_dz0 + l_red (executor.cpp)
+  const bool spread = STATEFUL && nfg <= NWV && 16 * Kx <= scr_n && !(OPK == OPK_ANY && os.kind == 0);
+  f32x4 keep[4] = {z4(), z4(), z4(), z4()};
   for (int fg = x.w; fg < nfg; fg += NWV) {
     const int i0 = 64 * fg, ic = i0 + 4 * x.c16;
     const bool fin = ic < Kx;
@@ -1079,6 +1106,11 @@ __device__ __forceinline__ void dw0_phase(const DeepArgs& a, float* smem, const 
         }
       }
     }
+    if (spread) {
+#pragma unroll
+      for (int ff = 0; ff < 4; ++ff) keep[ff] = acc[ff];
+      continue;
+    }
     // lane (column c16, group g): features i0 + 16 g + 4 q + f of column J0 + c16; the
     // optimizer state of its 16 elements loaded at once (after the MFMAs: the X rows'
     // registers are free by then)
@@ -1109,6 +1141,41 @@ __device__ __forceinline__ void dw0_phase(const DeepArgs& a, float* smem, const 
           wv[ff] = upd_p<OPK>(a, x, os, pi[4 * q + ff], wv[ff], acc[ff][q], pre.s0[4 * q + ff], pre.s1[4 * q + ff]);
       }
       lds4(w0t + x.c16 * ld0 + ib, wv);
+    }
+  }
+  if constexpr (STATEFUL) {
+    if (!spread) return;
+    float* scr = smem + a.l_dz0;   // [Kx][16]: feature-major, a column's 16 lanes contiguous
+    __syncthreads();               // every dZ_0 read (the MFMAs, the bias sums) is done
+    if (x.w < nfg) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int ff = 0; ff < 4; ++ff) {
+          const int i = 64 * x.w + 16 * x.g + 4 * q + ff;
+          if (i < Kx) scr[i * 16 + x.c16] = keep[ff][q];
+        }
+    }
+    __syncthreads();
+    constexpr int PE = 4;
+    for (int e0 = 0; e0 < 16 * l0.K; e0 += PE * NTH) {
+      long long pi[PE];
+      bool ok[PE];
+      OptPre<PE> pre;
+#pragma unroll
+      for (int u = 0; u < PE; ++u) {
+        const int e = e0 + u * NTH + x.tid, i = e >> 4, c = e & 15;
+        pi[u] = l0.p_off + (long long)i * l0.N + J0 + c;
+        ok[u] = e < 16 * l0.K && J0 + c < l0.N;
+      }
+      opt_pre<OPK, PE>(a, x, os, pi, ok, pre);
+#pragma unroll
+      for (int u = 0; u < PE; ++u) {
+        if (!ok[u]) continue;
+        const int e = e0 + u * NTH + x.tid, i = e >> 4, c = e & 15;
+        float* w = w0t + c * ld0 + i;
+        *w = upd_p<OPK>(a, x, os, pi[u], *w, scr[e], pre.s0[u], pre.s1[u]);
+      }
     }
   }
 }

@@ -96,10 +96,10 @@ def _compare_with_torch(nat, model, xs, ys, B, adaptive=False, epochs=2):
     wn, wr = nat.get_weights_flat(), ref.get_weights_flat()
     if adaptive:   # adaptive rule: near-zero gradients amplify fp32 rounding
         err = np.abs(wn - wr).mean() / np.abs(wr - w0).mean()
-        assert err < 1e-3, err
+        assert err < 1e-3, (err, nat.plan_name())
     else:
         err = np.abs(wn - wr).max() / np.abs(wr - w0).max()
-        assert err < 1e-4, err
+        assert err < 1e-4, (err, nat.plan_name())
     for a, b in zip(hn, hr):
         np.testing.assert_allclose(a["loss"], b["loss"], rtol=1e-4)
         np.testing.assert_allclose(a["acc"], b["acc"], atol=1e-6)
