@@ -218,12 +218,12 @@ static int shadow_tiles(const FlatArgs& a) {
 // 8 replicas are in flight together (the loop-carried sum otherwise serialised them: one
 // memory latency per replica); VEC: 4 elements per lane (16-byte rows, n4 = n / 4 of them)
 template <bool VEC>
-__global__ __launch_bounds__(256) void replica_average_kernel(float* P, long long sP, int R, long long n,
-                                                              float* out, int write_back, double scale) {
+__device__ __forceinline__ void replica_average_blocks(float* P, long long sP, int R, long long n, float* out,
+                                                       int write_back, double scale, int blk, int nblk) {
   constexpr int W = VEC ? 4 : 1;
   using V = typename std::conditional<VEC, float4, float>::type;
   const long long nv = n / W;
-  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < nv; i += (long long)gridDim.x * 256) {
+  for (long long i = (long long)blk * 256 + threadIdx.x; i < nv; i += (long long)nblk * 256) {
     double s[W];
 #pragma unroll
     for (int w = 0; w < W; ++w) s[w] = 0.0;
@@ -251,7 +251,7 @@ __global__ __launch_bounds__(256) void replica_average_kernel(float* P, long lon
       for (int r = 0; r < R; ++r) reinterpret_cast<V*>(P + (long long)r * sP)[i] = m;
   }
   if (VEC) {   // the n % 4 tail elements
-    const long long t = nv * W + (long long)blockIdx.x * 256 + threadIdx.x;
+    const long long t = nv * W + (long long)blk * 256 + threadIdx.x;
     if (t < n) {
       double s = 0.0;
       for (int r = 0; r < R; ++r) s += P[(long long)r * sP + t];
@@ -261,6 +261,38 @@ __global__ __launch_bounds__(256) void replica_average_kernel(float* P, long lon
         for (int r = 0; r < R; ++r) P[(long long)r * sP + t] = m;
     }
   }
+}
+template <bool VEC>
+__global__ __launch_bounds__(256) void replica_average_kernel(float* P, long long sP, int R, long long n,
+                                                              float* out, int write_back, double scale) {
+  replica_average_blocks<VEC>(P, sP, R, n, out, write_back, scale, blockIdx.x, gridDim.x);
+}
+
+// The post node of a persistent chunk that ends a fit (train-then-average, reference
+// spark_model.py:217-228) with the replica averaging in the same launch: the last block
+// clears the flags and advances the counters (persist_post_kernel), the others average.
+// One kernel boundary fewer than post + replica_average (measured at the MNIST bench's
+// 20-step shape: the post node 4.8 us, then 7.6 us to the average kernel's start).
+template <bool VEC>
+__global__ __launch_bounds__(256) void persist_post_average_kernel(unsigned* flags, int nflags, long long* ctr,
+                                                                   const int* ntrain, int R, int B, int n,
+                                                                   const unsigned* err, float* P, long long sP,
+                                                                   long long np, float* out, int write_back,
+                                                                   double scale) {
+  if (blockIdx.x == gridDim.x - 1) {
+    for (int e = threadIdx.x; e < nflags; e += 256) flags[e] = 0u;
+    if (*err != 0u) return;
+    const long long s0 = ctr[0];
+    for (int r = threadIdx.x; r < R; r += 256) {
+      const long long nb = ((long long)ntrain[r] + B - 1) / B;
+      const long long d = nb - s0;
+      ctr[2 + r] += d < 0 ? 0 : (d > n ? n : d);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) ctr[0] = s0 + n;
+    return;
+  }
+  replica_average_blocks<VEC>(P, sP, R, np, out, write_back, scale, blockIdx.x, gridDim.x - 1);
 }
 
 // y = alpha*x + beta*y   (vectorised, n multiple handled with tail)
@@ -326,6 +358,21 @@ extern "C" hipError_t ea_apply_update(FlatArgs* a, int bf16, hipStream_t s) {
 extern "C" hipError_t ea_persist_post(unsigned* flags, int nflags, long long* ctr, const int* ntrain, int R, int B, int n,
                                       const unsigned* err, hipStream_t s) {
   hipLaunchKernelGGL(persist_post_kernel, dim3(1), dim3(256), 0, s, flags, nflags, ctr, ntrain, R, B, n, err);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t ea_persist_post_average(unsigned* flags, int nflags, long long* ctr, const int* ntrain, int R,
+                                              int B, int n, const unsigned* err, float* P, long long sP, long long np,
+                                              float* out, int write_back, double scale, hipStream_t s) {
+  const bool vec = sP % 4 == 0 && (reinterpret_cast<uintptr_t>(P) & 15) == 0 &&
+                   (out == nullptr || (reinterpret_cast<uintptr_t>(out) & 15) == 0);
+  const int g = grid_for(vec ? (np + 3) / 4 : np) + 1;
+  if (vec)
+    hipLaunchKernelGGL(persist_post_average_kernel<true>, dim3(g), dim3(256), 0, s, flags, nflags, ctr, ntrain, R, B,
+                       n, err, P, sP, np, out, write_back, scale);
+  else
+    hipLaunchKernelGGL(persist_post_average_kernel<false>, dim3(g), dim3(256), 0, s, flags, nflags, ctr, ntrain, R, B,
+                       n, err, P, sP, np, out, write_back, scale);
   return hipGetLastError();
 }
 

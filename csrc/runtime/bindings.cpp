@@ -170,8 +170,8 @@ PYBIND11_MODULE(_C, m) {
       .def(py::init([](py::dict cfg) { return new Executor(parse_cfg(cfg)); }))
       .def("train_step", [](Executor& e, uintptr_t s) { e.train_step(S(s)); })
       .def("train_chunk", [](Executor& e, int n, uintptr_t s) { e.train_chunk(n, S(s)); })
-      .def("train_chunk_avg", [](Executor& e, int n, uintptr_t s, uintptr_t out, int write_p, double scale) {
-        return e.train_chunk_avg(n, S(s), reinterpret_cast<float*>(out), write_p, scale);
+      .def("train_chunk_avg", [](Executor& e, int n, uintptr_t s, uintptr_t out, int write_p, double scale, int mode) {
+        return e.train_chunk_avg(n, S(s), reinterpret_cast<float*>(out), write_p, scale, mode);
       })
       .def("forward_backward", [](Executor& e, uintptr_t s) { e.forward_backward(S(s)); })
       .def("apply", [](Executor& e, uintptr_t s) { e.apply(S(s)); })

@@ -19,6 +19,9 @@ extern "C" hipError_t ea_rowchain(const ea::RcArgs* a, int bf16, int nbw, hipStr
 extern "C" hipError_t ea_apply_update(ea::FlatArgs* a, int bf16, hipStream_t s);
 extern "C" hipError_t ea_refresh_shadows(ea::FlatArgs* a, int bf16, hipStream_t s);
 extern "C" hipError_t ea_advance(long long* ctr, const int* ntrain, int R, int B, int n, hipStream_t s);
+extern "C" hipError_t ea_persist_post_average(unsigned* flags, int nflags, long long* ctr, const int* ntrain, int R,
+                                              int B, int n, const unsigned* err, float* P, long long sP, long long np,
+                                              float* out, int write_back, double scale, hipStream_t s);
 extern "C" hipError_t ea_persist_post(unsigned* flags, int nflags, long long* ctr, const int* ntrain, int R, int B, int n,
                                       const unsigned* err, hipStream_t s);
 extern "C" hipError_t ea_persist(const ea::PersistArgs* a, hipStream_t s);
@@ -516,9 +519,7 @@ void Executor::run_chunk(hipStream_t s, int nsteps) const {
       dp_.xr_steps += (unsigned)nsteps;
     }
     check(ea_deep(&a, dp_.local && !a.sync && !a.ps_mode ? 1 : 0, s), "persistent layer pipeline kernel");
-    check(ea_persist_post(d_dflags_, (int)(dp_.flag_bytes / sizeof(unsigned)), reinterpret_cast<long long*>(c_.ctr),
-                          reinterpret_cast<const int*>(c_.ntrain), c_.R, c_.B, nsteps, d_perr_, s),
-          "persistent chunk post");
+    chunk_post(d_dflags_, dp_.flag_bytes, nsteps, s);
     return;
   }
   if (pm_.on) {
@@ -542,12 +543,26 @@ void Executor::run_chunk(hipStream_t s, int nsteps) const {
     }
     check(pm_.local == 1 ? ea_persist_local(&a, s) : pm_.local == 2 ? ea_persist_xlocal(&a, s) : ea_persist(&a, s),
           "persistent step kernel");
-    check(ea_persist_post(d_pflags_, (int)(pm_.flag_bytes / sizeof(unsigned)), reinterpret_cast<long long*>(c_.ctr),
-                          reinterpret_cast<const int*>(c_.ntrain), c_.R, c_.B, nsteps, d_perr_, s),
-          "persistent chunk post");
+    chunk_post(d_pflags_, pm_.flag_bytes, nsteps, s);
     return;
   }
   for (int i = 0; i < nsteps; ++i) run_step(s, i);
+}
+
+// the post node of a persistent chunk: flag clear + counter advance, and (train_chunk_avg
+// mode 2) the replica averaging in the same launch
+void Executor::chunk_post(unsigned* flags, size_t flag_bytes, int nsteps, hipStream_t s) const {
+  const int nflags = (int)(flag_bytes / sizeof(unsigned));
+  long long* ctr = reinterpret_cast<long long*>(c_.ctr);
+  const int* ntrain = reinterpret_cast<const int*>(c_.ntrain);
+  if (post_avg_) {
+    check(ea_persist_post_average(flags, nflags, ctr, ntrain, c_.R, c_.B, nsteps, d_perr_,
+                                  reinterpret_cast<float*>(c_.P), c_.sP, c_.nparams, post_avg_->out,
+                                  post_avg_->write_p, post_avg_->scale, s),
+          "persistent chunk post + replica average");
+    return;
+  }
+  check(ea_persist_post(flags, nflags, ctr, ntrain, c_.R, c_.B, nsteps, d_perr_, s), "persistent chunk post");
 }
 
 // Row-chain plan (rowchain.hip): 2 <= L <= RC_MAXL Dense layers, every layer but
@@ -1313,7 +1328,21 @@ void Executor::train_chunk(int nsteps, hipStream_t s) {
   if (!persistent()) advance(nsteps, s);
 }
 
-bool Executor::train_chunk_avg(int nsteps, hipStream_t s, float* out, int write_p, double scale) {
+bool Executor::train_chunk_avg(int nsteps, hipStream_t s, float* out, int write_p, double scale, int mode) {
+  if (mode == 2) {   // the averaging in the chunk's post node: any persistent fit-granularity plan
+    const bool ok = (pm_.on && !pm_.args.sync && !pm_.args.ps_mode) || (dp_.on && !dp_.args.sync && !dp_.args.ps_mode);
+    if (nsteps <= 0 || !ok || c_.nparams <= 0 || c_.P == 0) return false;
+    const PostAvg pa{out, write_p, scale};
+    post_avg_ = &pa;
+    try {
+      run_chunk(s, nsteps);
+    } catch (...) {
+      post_avg_ = nullptr;
+      throw;
+    }
+    post_avg_ = nullptr;
+    return true;
+  }
   // fit granularity on persist.hip only (per-step sync replicas are one model already; the
   // PS hook's masters belong to the server)
   if (nsteps <= 0 || !pm_.on || pm_.args.sync || pm_.args.ps_mode || c_.nparams <= 0 ||

@@ -109,7 +109,10 @@ class Executor {
   // launch's end (persist.hip grid_average): scale * sum_r P_r -> out (if not null) and every
   // replica's P (if write_p).  false (nothing launched): the plan cannot -- the caller runs
   // train_chunk and its own averaging
-  bool train_chunk_avg(int nsteps, hipStream_t s, float* out, int write_p, double scale);
+  // mode 1: inside the kernel (persist.hip grid_average, V1 / V2 roles only); mode 2: in the
+  // chunk's post node (persist_post_average_kernel: one launch with the flag clear and the
+  // counter advance; V1 / V2 roles and the layer pipeline)
+  bool train_chunk_avg(int nsteps, hipStream_t s, float* out, int write_p, double scale, int mode = 1);
   void forward_backward(hipStream_t s);    // gradient path: writes G (no update)
   void apply(hipStream_t s);               // gradient path: optimizer apply + advance
   void eval_chunk(long long chunk, const EvalSource& src, hipStream_t s);
@@ -218,6 +221,13 @@ class Executor {
   float* d_pws_ = nullptr;         // persistent plan: per-replica exchange workspace
   unsigned* d_pflags_ = nullptr;   // [R][PMF_N][PM_MAXWG] flags (zero at every launch: setup, then the post kernel)
   unsigned* d_perr_ = nullptr;     // sticky error word
+  struct PostAvg {
+    float* out;
+    int write_p;
+    double scale;
+  };
+  mutable const PostAvg* post_avg_ = nullptr;   // train_chunk_avg mode 2: the next chunk's post node averages
+  void chunk_post(unsigned* flags, size_t flag_bytes, int nsteps, hipStream_t s) const;
   bool build_persist();
   // persistent layer pipeline (deep.hip)
   struct Deep {

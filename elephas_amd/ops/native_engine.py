@@ -718,15 +718,19 @@ class NativeTrainer(TrainerBase):
     def run_steps_and_average(self, nsteps: int, allreduce=None, n_total: Optional[int] = None,
                               use_graph: bool = True):
         """run_steps(nsteps) then average_replicas(allreduce, n_total) -- the reference's
-        train-then-average (spark_model.py:217-228) -- with the averaging fused into the end
-        of the last persistent launch where the plan allows it and ELEPHAS_AMD_FUSED_AVG=1
-        (persist.hip grid_average: one launch fewer per fit; measured slower at the bench's
-        20-step shape -- the write-through epilogue it needs costs more -- so off by default):
-        the replica mean (world 1) or the replica sum for the caller's all-reduce lands in the
-        same buffer average_replicas fills.  Returns that buffer, as average_replicas does."""
+        train-then-average (spark_model.py:217-228) -- on a persistent plan with the averaging
+        in the last chunk's post node (mode 2: one launch does the flag clear, the counter
+        advance and the averaging -- one kernel boundary fewer than post + replica_average),
+        or with ELEPHAS_AMD_FUSED_AVG=1 inside the last launch itself (mode 1, persist.hip
+        grid_average; measured slower at the bench's 20-step shape -- the write-through
+        epilogue it needs costs more).  The replica mean (world 1) or the replica sum for the
+        caller's all-reduce lands in the same buffer average_replicas fills.  Returns that
+        buffer, as average_replicas does."""
+        mode = 1 if os.environ.get("ELEPHAS_AMD_FUSED_AVG", "0") == "1" else 2
         fusable = (nsteps > 0 and self.exe.persistent() and not self.sync and self._ps is None
-                   and getattr(self, "_xr", None) is None and self.exe.persist_variant()[0] in (1, 2)
-                   and os.environ.get("ELEPHAS_AMD_FUSED_AVG", "0") == "1")
+                   and getattr(self, "_xr", None) is None
+                   and (mode == 2 or self.exe.persist_variant()[0] in (1, 2))
+                   and os.environ.get("ELEPHAS_AMD_FUSED_AVG", "") != "0")
         if not fusable:
             self.run_steps(nsteps, use_graph=use_graph)
             return self.average_replicas(allreduce, n_total)
@@ -735,7 +739,7 @@ class NativeTrainer(TrainerBase):
         if avg is None or avg.numel() != self.n:
             with torch.cuda.stream(self.stream):
                 avg = self._avg_buf = torch.empty(self.n, dtype=torch.float32, device=self.dev)
-        fused = (avg.data_ptr(), 1, 1.0 / n_total) if allreduce is None else (avg.data_ptr(), 0, 1.0)
+        fused = (avg.data_ptr(), 1, 1.0 / n_total, mode) if allreduce is None else (avg.data_ptr(), 0, 1.0, mode)
         if self.persist_cus:
             self._run_steps(nsteps, use_graph, fused)
         else:

@@ -389,3 +389,37 @@ def test_deep_xcd_local_instance_is_bit_exact(monkeypatch, opt):
     for a, b in zip(hl, hg):
         for key in a:
             np.testing.assert_array_equal(a[key], b[key])
+
+
+def test_deep_post_node_average_equals_separate_kernel(monkeypatch):
+    """The layer pipeline's fit-granularity chunk with the replica averaging in its post node
+    (run_steps_and_average, default mode) == run_steps + the replica_average kernel, bit for
+    bit, over a chunk boundary; the mean is in every replica afterwards."""
+    from elephas_amd.models import initializers
+    from elephas_amd.models.optimizers import SGD
+    initializers.set_seed(19)
+    model = _mlp(93, [256, 256], 9, dropout=0.5)
+    model.compile(SGD(0.05), "categorical_crossentropy", ["acc"])
+    xs, ys = _shards([128 * 9] * 8, 93, 9, seed=23)
+    monkeypatch.delenv("ELEPHAS_AMD_FUSED_AVG", raising=False)
+    out = []
+    for fused in (True, False):
+        t = _native(model, 8, 128, seed=6, deep="-1", monkeypatch=monkeypatch)
+        assert t.persistent and t.persist_variant == 3, t.plan_name()
+        t.set_data(xs, ys, 0.0, shuffle=False)
+        t.GRAPH_CHUNK = 4
+        t.begin_epoch()
+        if fused:
+            avg = t.run_steps_and_average(7, None, 8)
+            assert t._fused_done, "the layer pipeline must average in its post node"
+        else:
+            t.run_steps(7)
+            avg = t.average_replicas(None, 8)
+        torch.cuda.synchronize()
+        t.check()
+        out.append((t.get_weights_flat(), avg.cpu().numpy().copy()))
+    (wf, af), (ws, as_) = out
+    assert np.array_equal(af, as_), np.abs(af - as_).max()
+    assert np.array_equal(wf, ws), np.abs(wf - ws).max()
+    for r in range(1, 8):
+        assert np.array_equal(wf[r], wf[0])

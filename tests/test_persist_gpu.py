@@ -530,13 +530,15 @@ def test_persist_xcd_local_instance_is_bit_exact(monkeypatch, case):
             np.testing.assert_array_equal(a[key], b[key])
 
 
+@pytest.mark.parametrize("mode", ["1", "2"])
 @pytest.mark.parametrize("v2,allreduce", [("1", False), ("0", False), ("1", True)])
-def test_fused_average_equals_separate_kernel(monkeypatch, v2, allreduce):
-    """run_steps_and_average (the replica averaging fused into the last persistent launch:
-    grid barrier, then every workgroup averages its slice of the parameters over the replicas
-    in fp64, replica order) == run_steps + the replica_average kernel, bit for bit -- the
+def test_fused_average_equals_separate_kernel(monkeypatch, v2, allreduce, mode):
+    """run_steps_and_average == run_steps + the replica_average kernel, bit for bit -- the
     world-1 mean written into every replica, and the replica-sum form an all-reduce follows
-    (identity here) -- on V2 and V1, over a chunk boundary."""
+    (identity here) -- on V2 and V1, over a chunk boundary.  Mode 1 (ELEPHAS_AMD_FUSED_AVG=1):
+    the averaging fused into the last persistent launch (grid barrier, then every workgroup
+    averages its slice in fp64, replica order); mode 2 (the default): in the chunk's post
+    node, one launch with the flag clear and the counter advance."""
     from elephas_amd.models import initializers
     from elephas_amd.models.optimizers import SGD
     initializers.set_seed(61)
@@ -544,7 +546,10 @@ def test_fused_average_equals_separate_kernel(monkeypatch, v2, allreduce):
     model.compile(SGD(0.1), "categorical_crossentropy", ["acc"])
     xs, ys = _shards([64 * 12] * 8, 784, 10, seed=29)
     monkeypatch.setenv("ELEPHAS_AMD_PERSIST_V2", v2)
-    monkeypatch.setenv("ELEPHAS_AMD_FUSED_AVG", "1")
+    if mode == "1":
+        monkeypatch.setenv("ELEPHAS_AMD_FUSED_AVG", "1")
+    else:
+        monkeypatch.delenv("ELEPHAS_AMD_FUSED_AVG", raising=False)
     out = []
     for fused in (True, False):
         t = _trainer(model, 8, 64, persist=1, seed=4)
