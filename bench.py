@@ -521,6 +521,14 @@ def measure_train(args, model, dist, rank, world, dev, gpu, W, batch_mode, steps
     average()
     sync()
     dt = time.perf_counter() - t0
+    # diagnostics only (stderr; the reported line keeps the first timed region): the same
+    # region timed again ELEPHAS_AMD_BENCH_REPEAT - 1 more times
+    for _ in range(int(os.environ.get("ELEPHAS_AMD_BENCH_REPEAT", "1")) - 1):
+        ta = time.perf_counter()
+        run(steps, then_average=True)
+        average()
+        sync()
+        print(f"bench repeat: {(time.perf_counter() - ta) * 1e6:.1f} us (first {dt * 1e6:.1f})", file=sys.stderr)
 
     dts = dist.all_gather_object(dt)
     dt_max = max(dts)
