@@ -549,7 +549,8 @@ def measure_train(args, model, dist, rank, world, dev, gpu, W, batch_mode, steps
     from elephas_amd.parallel import p2p
     nbytes = (t.G.numel() if batch_mode and gpu else theta.size) * 4
     if xrank:
-        path = "in-launch rank exchange: per-step weight-gradient tiles through peer-mapped buffers (persist.hip)"
+        kern = "deep_impl.h" if t.persist_variant == 3 else "persist.hip"
+        path = f"in-launch rank exchange: per-step weight-gradient tiles through peer-mapped buffers ({kern})"
     elif channel is not None:
         path = "peer-memory kernel captured in the step's hipGraph (dedicated channel)"
     elif gpu and world > 1 and not batch_mode:
