@@ -295,6 +295,31 @@ __global__ __launch_bounds__(256) void persist_post_average_kernel(unsigned* fla
   replica_average_blocks<VEC>(P, sP, R, np, out, write_back, scale, blockIdx.x, gridDim.x - 1);
 }
 
+// C[m][n] = sum over the ks split-K slabs S[k][m][n] (fp32, slab order): the reduction
+// step of the split-K GEMM entry (gemm_nt splitk > 1); VEC: 4 columns per lane
+template <bool VEC>
+__global__ __launch_bounds__(256) void sum_slabs_kernel(const float* S, int ks, long long slab, int M, int N,
+                                                        float* C, long long ldc) {
+  constexpr int W = VEC ? 4 : 1;
+  const int nw = N / W;
+  const long long tot = (long long)M * nw;
+  for (long long e = (long long)blockIdx.x * 256 + threadIdx.x; e < tot; e += (long long)gridDim.x * 256) {
+    const int m = (int)(e / nw), c = (int)(e - (long long)m * nw) * W;
+    if constexpr (VEC) {
+      float4 acc = *reinterpret_cast<const float4*>(S + (long long)m * N + c);
+      for (int k = 1; k < ks; ++k) {
+        const float4 v = *reinterpret_cast<const float4*>(S + k * slab + (long long)m * N + c);
+        acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+      }
+      *reinterpret_cast<float4*>(C + (long long)m * ldc + c) = acc;
+    } else {
+      float acc = S[(long long)m * N + c];
+      for (int k = 1; k < ks; ++k) acc += S[k * slab + (long long)m * N + c];
+      C[(long long)m * ldc + c] = acc;
+    }
+  }
+}
+
 // y = alpha*x + beta*y   (vectorised, n multiple handled with tail)
 __global__ __launch_bounds__(256) void axpby_kernel(const float* x, float* y, long long n, float alpha, float beta) {
   const long long n4 = n / 4;
@@ -400,6 +425,17 @@ extern "C" hipError_t ea_replica_average(float* P, long long sP, int R, long lon
   else
     hipLaunchKernelGGL(replica_average_kernel<false>, dim3(grid_for(n)), dim3(256), 0, s, P, sP, R, n, out, write_back,
                        scale);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t ea_sum_slabs(const float* S, int ks, int M, int N, float* C, long long ldc, hipStream_t s) {
+  const long long slab = (long long)M * N;
+  const bool vec = N % 4 == 0 && ldc % 4 == 0 && (reinterpret_cast<uintptr_t>(S) & 15) == 0 &&
+                   (reinterpret_cast<uintptr_t>(C) & 15) == 0;
+  if (vec)
+    hipLaunchKernelGGL(sum_slabs_kernel<true>, dim3(grid_for(slab / 4)), dim3(256), 0, s, S, ks, slab, M, N, C, ldc);
+  else
+    hipLaunchKernelGGL(sum_slabs_kernel<false>, dim3(grid_for(slab)), dim3(256), 0, s, S, ks, slab, M, N, C, ldc);
   return hipGetLastError();
 }
 

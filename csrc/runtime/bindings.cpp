@@ -24,6 +24,7 @@ extern "C" void ea_gemm_init();
 extern "C" hipError_t ea_replica_average(float* P, long long sP, int R, long long n, float* out, int write_back,
                                          double scale, hipStream_t s);
 extern "C" hipError_t ea_axpby(const float* x, float* y, long long n, float alpha, float beta, hipStream_t s);
+extern "C" hipError_t ea_sum_slabs(const float* S, int ks, int M, int N, float* C, long long ldc, hipStream_t s);
 extern "C" hipError_t ea_ps_sub(float* p, const float* d, long long n, float scale, int atomic, hipStream_t s);
 extern "C" hipError_t ea_poison_lds(unsigned pattern, hipStream_t s);
 extern "C" hipError_t ea_sub(const float* a, const float* b, float* out, long long n, hipStream_t s);
@@ -227,8 +228,11 @@ PYBIND11_MODULE(_C, m) {
       .def("grad_launch", [](Executor& e, int idx, uintptr_t s) { e.grad_launch(idx, S(s)); });
 
   // single PLAIN GEMM (C fp32 = A . BT^T) for kernel tests / generic matmul
+  // splitk > 1 (fp32 C only): the reduction split over splitk workgroup slabs (PK_PARTIAL, the
+  // Wide model's last-layer form), then one slab-sum launch -- for grids too small to fill the
+  // 256 CUs (1024 x 1000 x 4096: 64 tiles of 128 x 128)
   m.def("gemm_nt", [](uintptr_t A, uintptr_t BT, uintptr_t C, int M, int N, int K, long long lda, long long ldb,
-                      long long ldc, int bf16, int cfg, uintptr_t s, uintptr_t stamps, int out_bf16) {
+                      long long ldc, int bf16, int cfg, uintptr_t s, uintptr_t stamps, int out_bf16, int splitk) {
     // the kernel issues unconditional 16-byte fragment loads along K: rows must be
     // 16-byte aligned and K padded to whole chunks, or it reads out of bounds
     const int epl = bf16 ? 8 : 4;
@@ -254,6 +258,25 @@ PYBIND11_MODULE(_C, m) {
     ga.R = 1;
     ga.total_blocks = p.tiles_m * p.tiles_n;
     ga.stamps = reinterpret_cast<long long*>(stamps);  // diagnostics (null = off)
+    static float* slabs = nullptr;
+    static size_t slab_cap = 0;
+    if (splitk > 1) {
+      if (out_bf16 || splitk > 16) throw std::invalid_argument("gemm_nt: splitk needs fp32 C and <= 16 slabs");
+      const size_t need = (size_t)splitk * M * N;
+      if (need > slab_cap) {
+        if (slabs) chk(hipFree(slabs), "hipFree");
+        chk(hipMalloc(&slabs, need * sizeof(float)), "hipMalloc(split-K slabs)");
+        slab_cap = need;
+      }
+      p.kind = PK_PARTIAL;
+      p.tiles_k = splitk;
+      p.kchunk = ((K + splitk - 1) / splitk + 63) / 64 * 64;
+      p.D = slabs;
+      p.ldd = N;
+      p.sPart = (long long)M * N;
+      p.sD = (long long)splitk * M * N;
+      ga.total_blocks *= splitk;
+    }
     static long long* dctr = nullptr;
     if (!dctr) {
       chk(hipMalloc(&dctr, 64 * sizeof(long long)), "hipMalloc");
@@ -262,9 +285,10 @@ PYBIND11_MODULE(_C, m) {
     ga.ctr = dctr;
     p.ntrain = reinterpret_cast<const int*>(dctr);  // zero batch counts: the kernel reads ntrain[0]
     chk(ea_gemm_grouped(&ga, bf16, cfg, S(s)), "gemm_nt");
+    if (splitk > 1) chk(ea_sum_slabs(slabs, splitk, M, N, reinterpret_cast<float*>(C), ldc, S(s)), "gemm_nt slab sum");
   }, py::arg("A"), py::arg("BT"), py::arg("C"), py::arg("M"), py::arg("N"), py::arg("K"), py::arg("lda"),
      py::arg("ldb"), py::arg("ldc"), py::arg("bf16"), py::arg("cfg"), py::arg("stream"), py::arg("stamps") = 0,
-     py::arg("out_bf16") = 0);
+     py::arg("out_bf16") = 0, py::arg("splitk") = 1);
   m.def("tile_shape", [](int cfg) { return py::make_tuple(ea_gemm_tile_m(cfg), ea_gemm_tile_n(cfg)); });
 
   m.def("replica_average", [](uintptr_t P, long long sP, int R, long long n, uintptr_t out, int write_back,

@@ -29,6 +29,20 @@ for (M, N, K) in [(64, 128, 784), (64, 10, 128), (785, 128, 64), (300, 200, 136)
                 C.gemm_nt(A.data_ptr(), BT.data_ptr(), Cb.data_ptr(), M, N, K, K, K, N, bf16, cfg, s, 0, 1)
                 torch.cuda.synchronize()
                 ok &= bool(torch.equal(Cb, Cm.to(torch.bfloat16)))
+# split-K entry (PK_PARTIAL slabs + one slab-sum launch): numerics
+for (M, N, K, ks) in [(1024, 1000, 4096, 4), (300, 200, 136, 2), (513, 770, 1000, 3)]:
+    A = torch.randn(M, K, device=dev).to(torch.bfloat16)
+    BT = torch.randn(N, K, device=dev).to(torch.bfloat16)
+    for cfg in (1, 2):
+        Cm = torch.zeros(M, N, device=dev)
+        s = torch.cuda.current_stream().cuda_stream
+        C.gemm_nt(A.data_ptr(), BT.data_ptr(), Cm.data_ptr(), M, N, K, K, K, N, 1, cfg, s, 0, 0, ks)
+        torch.cuda.synchronize()
+        ref = A.float() @ BT.float().t()
+        err = (Cm - ref).abs().max().item() / (ref.abs().max().item() + 1e-6)
+        print(f"M={M} N={N} K={K} bf16=1 cfg={cfg} splitk={ks} relerr={err:.2e}", flush=True)
+        if err > 1e-2:
+            ok = False
 # timing of the wide-MLP shapes: FWD/DX (M=batch 1024) and DW (K=batch)
 s = torch.cuda.current_stream().cuda_stream
 for (M, N, K) in [(4096, 4096, 4096), (1024, 4096, 4096), (4096, 4096, 1024), (1024, 1000, 4096)]:
@@ -39,10 +53,14 @@ for (M, N, K) in [(4096, 4096, 4096), (1024, 4096, 4096), (4096, 4096, 1024), (1
     res = []
     # "4b": the 256x256 tile writing bf16 C, as hipBLASLt's bf16 matmul does (fp32 C doubles
     # the epilogue's HBM writes)
-    for cfg in (1, 2, 4, "4b", "torch"):
+    # "2k4" / "1k2": the split-K entry (4 / 2 slabs on the 128x64 / 128x128 tile, + slab sum)
+    for cfg in (1, 2, 4, "4b", "2k4", "2k2", "1k2", "torch"):
         def f():
             if cfg == "torch":
                 torch.matmul(A, BT.t())
+            elif isinstance(cfg, str) and "k" in cfg:
+                c, ks = (int(v) for v in cfg.split("k"))
+                C.gemm_nt(A.data_ptr(), BT.data_ptr(), Cm.data_ptr(), M, N, K, K, K, N, 1, c, s, 0, 0, ks)
             elif cfg == "4b":
                 C.gemm_nt(A.data_ptr(), BT.data_ptr(), Cb.data_ptr(), M, N, K, K, K, N, 1, 4, s, 0, 1)
             else:
