@@ -325,6 +325,26 @@ def test_plain_gemm_matches_torch_fp32(M, N, K, bf16, cfg):
     assert err < (1e-4 if not bf16 else 1e-3), err
 
 
+@pytest.mark.parametrize("cfg", [1, 2])
+@pytest.mark.parametrize("M,N,K,ks", [(1024, 1000, 4096, 4), (300, 200, 136, 2), (513, 770, 1000, 3), (64, 10, 128, 5)])
+def test_plain_gemm_split_k_matches_torch_fp32(M, N, K, ks, cfg):
+    """The GEMM entry with the reduction split over workgroup slabs (PK_PARTIAL) and one
+    slab-sum launch -- including more slabs than 64-wide K chunks (empty slabs) -- vs. a
+    torch fp32 matmul, bf16 operands."""
+    from elephas_amd.ops import native
+    C = native.require()
+    torch.manual_seed(1)
+    A = torch.randn(M, K, device="cuda").to(torch.bfloat16)
+    BT = torch.randn(N, K, device="cuda").to(torch.bfloat16)
+    out = torch.full((M, N), float("nan"), device="cuda")
+    C.gemm_nt(A.data_ptr(), BT.data_ptr(), out.data_ptr(), M, N, K, K, K, N, 1, cfg,
+              torch.cuda.current_stream().cuda_stream, 0, 0, ks)
+    torch.cuda.synchronize()
+    ref = A.float() @ BT.float().t()
+    err = (out - ref).abs().max().item() / ref.abs().max().item()
+    assert err < 1e-3, err
+
+
 def test_plain_gemm_rejects_misaligned_shapes():
     from elephas_amd.ops import native
     C = native.require()
