@@ -58,8 +58,8 @@ __global__ __launch_bounds__(64) void advance_kernel(long long* ctr, const int* 
 // After a persistent chunk (persist.hip): clear the launch's flag block for the next
 // launch and advance the step counters -- one node instead of a flag memset ahead of
 // the next launch plus advance_kernel (one block; the flag block is a few thousand words)
-__global__ __launch_bounds__(256) void persist_post_kernel(unsigned* flags, int nflags, long long* ctr, const int* ntrain,
-                                                           int R, int B, int n, const unsigned* err) {
+__device__ __forceinline__ void persist_post_block(unsigned* flags, int nflags, long long* ctr, const int* ntrain,
+                                                   int R, int B, int n, const unsigned* err) {
   for (int e = threadIdx.x; e < nflags; e += 256) flags[e] = 0u;
   // a launch that gave up (sticky error word) did not run its steps: the counters stay
   // (the host re-plans and re-runs them, native_engine.py NativeTrainer.check)
@@ -72,6 +72,10 @@ __global__ __launch_bounds__(256) void persist_post_kernel(unsigned* flags, int 
   }
   __syncthreads();
   if (threadIdx.x == 0) ctr[0] = s0 + n;
+}
+__global__ __launch_bounds__(256) void persist_post_kernel(unsigned* flags, int nflags, long long* ctr, const int* ntrain,
+                                                           int R, int B, int n, const unsigned* err) {
+  persist_post_block(flags, nflags, ctr, ntrain, R, B, n, err);
 }
 
 // grid: total_blocks over R*n elements
@@ -280,16 +284,7 @@ __global__ __launch_bounds__(256) void persist_post_average_kernel(unsigned* fla
                                                                    long long np, float* out, int write_back,
                                                                    double scale) {
   if (blockIdx.x == gridDim.x - 1) {
-    for (int e = threadIdx.x; e < nflags; e += 256) flags[e] = 0u;
-    if (*err != 0u) return;
-    const long long s0 = ctr[0];
-    for (int r = threadIdx.x; r < R; r += 256) {
-      const long long nb = ((long long)ntrain[r] + B - 1) / B;
-      const long long d = nb - s0;
-      ctr[2 + r] += d < 0 ? 0 : (d > n ? n : d);
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) ctr[0] = s0 + n;
+    persist_post_block(flags, nflags, ctr, ntrain, R, B, n, err);
     return;
   }
   replica_average_blocks<VEC>(P, sP, R, np, out, write_back, scale, blockIdx.x, gridDim.x - 1);
