@@ -497,8 +497,11 @@ class NativeTrainer(TrainerBase):
         if flat.ndim == 1:
             flat = np.broadcast_to(flat, (self.R, flat.size))
         self._enter()
+        # pinned staging (the caching host allocator keeps it until the copy has run): no
+        # pageable-memory DMA, see _host
+        src = torch.from_numpy(np.array(flat, dtype=np.float32, copy=True)).pin_memory()
         with torch.cuda.stream(self.stream):
-            self.P.copy_(torch.from_numpy(np.array(flat, dtype=np.float32, copy=True)).to(self.dev))
+            self.P.copy_(src, non_blocking=True)
             self.exe.refresh_shadows(True, self.s)
         self._exit()
         self._images_stale = False
@@ -599,9 +602,10 @@ class NativeTrainer(TrainerBase):
         it = torch.from_numpy(np.array(np.broadcast_to(np.asarray(iterations, np.int64), (self.R,)),
                                        dtype=np.int64))
         self._enter()
+        st, it = st.pin_memory(), it.pin_memory()   # pinned staging, as set_weights_flat
         with torch.cuda.stream(self.stream):
-            self.S.copy_(st.to(self.dev))
-            self.ctr[2:].copy_(it.to(self.dev))
+            self.S.copy_(st, non_blocking=True)
+            self.ctr[2:].copy_(it, non_blocking=True)
             self.exe.refresh_shadows(True, self.s)
         self._exit()
 
@@ -1051,10 +1055,15 @@ class NativeTrainer(TrainerBase):
         return self._host(self.acc_val)
 
     def _host(self, t: torch.Tensor) -> np.ndarray:
-        """Device -> host read ordered after everything queued on the executor stream."""
+        """Device -> host read ordered after everything queued on the executor stream, through
+        a pinned staging tensor on that stream (no pageable-memory DMA: every intermittent
+        illegal-address error of the long GPU test runs surfaced at a pageable copy)."""
+        out = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+        with torch.cuda.stream(self.stream):
+            out.copy_(t.detach(), non_blocking=True)
         self.stream.synchronize()
         self.check()
-        return t.detach().cpu().numpy().copy()
+        return out.numpy().copy()
 
     def check(self):
         """Raise PersistentPlanError if a persistent-plan launch gave up waiting inside the
