@@ -669,9 +669,10 @@ class NativeTrainer(TrainerBase):
         # in-launch gradient exchange needs every replica to run the same steps
         self._sync_equal = len(set(nt)) == 1
         with torch.cuda.stream(self.stream):
-            self.ntrain.copy_(torch.tensor(nt, dtype=torch.int32))
-            self.vstart.copy_(torch.tensor(vs, dtype=torch.int32))
-            self.vcount.copy_(torch.tensor(vc, dtype=torch.int32))
+            # (pinned staging, as set_weights_flat)
+            self.ntrain.copy_(torch.tensor(nt, dtype=torch.int32).pin_memory(), non_blocking=True)
+            self.vstart.copy_(torch.tensor(vs, dtype=torch.int32).pin_memory(), non_blocking=True)
+            self.vcount.copy_(torch.tensor(vc, dtype=torch.int32).pin_memory(), non_blocking=True)
         self.shuffle = shuffle
         if rebuild:
             self._build_executor()
