@@ -29,6 +29,23 @@ def _fresh_names():
     yield
 
 
+@pytest.fixture(autouse=True)
+def _gpu_isolation(request):
+    """After every GPU test: a device synchronisation (an asynchronous device error is charged
+    to the test that caused it, as a teardown error, not to whichever later test first
+    touches the device) and a garbage collection (the test's trainers -- executors, loaders,
+    streams -- are destroyed at the boundary, not inside a later test)."""
+    yield
+    if request.node.get_closest_marker("gpu") is None:
+        return
+    import gc
+    import torch
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+        gc.collect()
+        torch.cuda.synchronize()
+
+
 @pytest.fixture
 def classification_model():
     from elephas_amd.models import Sequential, Dense, Activation, Dropout
